@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""Benchmark: cas_ids/s + hashed GB/s (whole node) on MI355X — BASELINE.json's metric.
+
+Workload (one "step"): every rank hashes its resident batch of sampled-path files
+(BASELINE configs 3/4: 57,344 gathered bytes per file, 57,352-B BLAKE3 message, 30 %
+duplicate content) with K1 and groups the cas keys into Objects — locally on one GPU,
+by key-range all-to-all over RCCL on several.  Inputs are synthesized on the device
+before the timed region (data: synthetic) and are resident in HBM when it starts.
+Weak scaling: FILES_PER_GPU (default 1.25M = 71.7 GB/GPU) per rank per step, so one step
+at 8 GPUs is the 10M-file headline job.
+
+Output: ONE JSON line on rank 0 (driver contract), with
+  roofline      — K1 (sd_cas_sampled_kernel), timed by HIP events on its own stream:
+                  algorithmic message bytes / kernel time vs the 8 TB/s HBM peak, plus the
+                  int32 VALU view (spec ops per compression) in "valu";
+  cpu_baseline  — the oracle's AVX-512 16-lane CPU path (oracle/cas_fast.c) on a bounded
+                  sample of the SAME files on the host cores (rank 0, N=1 only); the sample's
+                  keys are also checked against the GPU's.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+MSG_BYTES = 57352            # le64(size) || 57,344 sampled bytes
+COMPRESSIONS = 953           # 897 chunk blocks + 56 parents per sampled message
+SPEC_OPS = 792               # int32 ops per compression (7 rounds x 8 G x 14 + 8)
+HW_OPS = 680                 # VALU instructions per compression as compiled (add3/alignbit)
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # 256 CUs x 4 SIMD32 x 32 lanes x 2.4 GHz = 78.6
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--files-per-gpu", type=int, default=1_250_000)
+    ap.add_argument("--dup-permille", type=int, default=300)
+    ap.add_argument("--seed", type=int, default=0x5DCA50004)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from spacedrive_amd import CasEngine
+    from spacedrive_amd.shard import HipShardOps, sharded_group
+
+    eng = CasEngine(local)
+    F = args.files_per_gpu
+    file0 = rank * F
+    dev = torch.device("cuda", local)
+    content = torch.empty((F, 57344), dtype=torch.uint8, device=dev)
+    sizes = torch.empty(F, dtype=torch.int64, device=dev)
+    keys = torch.empty(F, dtype=torch.int64, device=dev)
+    rep = torch.empty(F, dtype=torch.int32, device=dev)
+    eng.synth_sampled(args.seed, file0, F, content, sizes, 57344, dup_permille=args.dup_permille)
+    torch.cuda.synchronize()
+    ops = HipShardOps(eng)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+
+    def step(i: int, timed: bool):
+        if timed:
+            ev[i][0].record()
+        eng.hash_sampled(content, sizes, keys)            # K1 on torch's current stream
+        if timed:
+            ev[i][1].record()
+        if world == 1:
+            return eng.group(keys, rep, want_objects=False)  # K4 + K5, stays async
+        return sharded_group(keys, file0, ops)
+
+    for i in range(args.warmup):
+        step(i, False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        res = step(i, True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    km = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(km, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    kern_ms = float(km.item())
+
+    # objects (for the record) — outside the timed region
+    if world == 1:
+        objects = eng.group(keys, rep)
+    else:
+        objects = res.objects
+
+    files_total = world * F * args.steps
+    value = files_total / dt
+    gbs = files_total * MSG_BYTES / dt / 1e9
+    achieved = F * MSG_BYTES / (kern_ms / 1e3) / 1e9  # per-GPU kernel GB/s
+    valu = F * COMPRESSIONS * SPEC_OPS / (kern_ms / 1e3) / 1e12
+    valu_hw = F * COMPRESSIONS * HW_OPS / (kern_ms / 1e3) / 1e12
+
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_sampled_kernel.json")
+    if os.path.exists(pmc):
+        with open(pmc) as fh:
+            traffic = json.load(fh).get("hbm_bytes_per_launch_per_file")
+            if traffic is not None:
+                traffic = traffic * F
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(content, sizes, keys, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "cas_ids/sec + hashed GB/s (whole node), 10M files at 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "cas_ids/s",
+            "hashed_gb_per_s": gbs,
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (on-device splitmix64 content, 30% duplicates), resident in HBM",
+            "config": {
+                "workload": "sampled-path cas_id (57,352-B BLAKE3 message/file) + Object grouping; "
+                            f"{F} files/GPU/step ({world * F} per step at n_gpus={world})",
+                "files_per_gpu": F,
+                "dup_permille": args.dup_permille,
+                "parallelism": f"shard-by-file x{world}" + (" + RCCL key-range all-to-all" if world > 1 else ""),
+                "objects": objects,
+            },
+            "roofline": {
+                "kernel": "sd_cas_sampled_kernel",
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel_ms": kern_ms,
+                "algorithmic_bytes_per_launch": F * MSG_BYTES,
+                "valu": {"achieved_spec_tops": valu, "achieved_hw_tops": valu_hw,
+                         "peak_tops": VALU_PEAK_TOPS, "frac_spec": valu / VALU_PEAK_TOPS,
+                         "frac_hw": valu_hw / VALU_PEAK_TOPS},
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(content, sizes, keys, seconds: float):
+    """Oracle AVX-512 path on the host cores over a bounded sample of the same files."""
+    import numpy as np
+
+    from oracle.pyoracle import Oracle
+    orc = Oracle()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    m = min(content.shape[0], 16 * 4096)
+    host = content[:m].cpu().numpy()
+    hs = sizes[:m].cpu().numpy().view(np.uint64)
+    gk = keys[:m].cpu().numpy().view(np.uint64)
+    # calibrate, then hash whole passes over the sample for ~`seconds`
+    t0 = time.perf_counter()
+    k = orc.fast_cas_keys_strided(host.reshape(-1), 57344, 57344, hs, threads)
+    one = time.perf_counter() - t0
+    parity = bool((k == gk).all())
+    reps = max(1, int(seconds / max(one, 1e-3)))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        orc.fast_cas_keys_strided(host.reshape(-1), 57344, 57344, hs, threads)
+    dt = time.perf_counter() - t0
+    files = reps * m
+    return {"value": files / dt, "unit": "cas_ids/s", "hashed_gb_per_s": files * MSG_BYTES / dt / 1e9,
+            "cores": threads, "kind": "port",
+            "simd": "avx512 16-lane" if orc.has_simd() else "scalar",
+            "sample": f"{reps} passes over the first {m} files of the bench batch (hashing only, "
+                      f"messages pre-gathered in DRAM), {dt:.1f}s",
+            "parity_vs_gpu": parity}
+
+
+if __name__ == "__main__":
+    main()

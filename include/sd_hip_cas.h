@@ -1,0 +1,155 @@
+/*
+ * sd_hip_cas.h — C ABI of the MI355X (gfx950) content-identification engine.
+ *
+ * Drop-in boundary for the north-star path of annihilatorrrr/spacedrive:
+ *   generate_cas_id   core/src/object/cas.rs:23-62
+ *   (its batch caller) core/src/object/file_identifier/mod.rs:78-86, 98-350
+ *   file_checksum     core/src/object/validation/hash.rs:11-25
+ * Plain C: pointers + sizes, no C++ or torch types.  The Rust-side binding
+ * (`sd-hip-cas` crate, extern "C" block + safe `generate_cas_ids`) is shown in
+ * INTEGRATION.md.
+ *
+ * Conventions
+ *   - Every function returns an int status: SD_CAS_OK (0) or a negative SD_CAS_E*.
+ *     The message of the last failure on a context is sd_cas_last_error(ctx).
+ *   - A "cas key" is the big-endian u64 of BLAKE3(le64(size) || content)[0..8]:
+ *     sd_cas_key_to_hex(key) is exactly the 16-char cas_id String of cas.rs:61, and
+ *     numeric key order equals the string order of cas_ids.
+ *   - "content" is what generate_cas_id feeds after the size prefix: the whole file
+ *     when size <= SD_CAS_MINIMUM_FILE_SIZE (cas.rs:27-29), otherwise the 57,344
+ *     gathered bytes header || 4 samples || footer (cas.rs:31-58).
+ *   - *_dev functions take device pointers already resident in HBM and a hipStream_t
+ *     passed as void* (NULL = the context's own stream); they enqueue and return
+ *     without synchronising unless stated.  Host-buffer functions are blocking.
+ *   - Contexts are not thread-safe; use one per (thread, device).
+ */
+#ifndef SD_HIP_CAS_H
+#define SD_HIP_CAS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SD_CAS_ABI_VERSION 1
+
+/* core/src/object/cas.rs:10-15 */
+#define SD_CAS_SAMPLE_COUNT 4u
+#define SD_CAS_SAMPLE_SIZE (1024u * 10u)
+#define SD_CAS_HEADER_OR_FOOTER_SIZE (1024u * 8u)
+#define SD_CAS_MINIMUM_FILE_SIZE (1024u * 100u)
+#define SD_CAS_SAMPLED_CONTENT_LEN (2u * SD_CAS_HEADER_OR_FOOTER_SIZE + SD_CAS_SAMPLE_COUNT * SD_CAS_SAMPLE_SIZE)
+/* file_identifier/mod.rs:34 */
+#define SD_CAS_CHUNK_SIZE 100u
+/* largest content the packed kernel takes (128 BLAKE3 chunks incl. the size prefix) */
+#define SD_CAS_MAX_PACKED_CONTENT_LEN (128u * 1024u - 8u)
+
+#define SD_CAS_OK 0
+#define SD_CAS_EINVAL (-1)  /* bad argument (null pointer, misaligned, too large) */
+#define SD_CAS_EHIP (-2)    /* HIP runtime / kernel launch failure: batch-level */
+#define SD_CAS_EIO (-3)     /* file I/O failure (per-file status carries -errno) */
+#define SD_CAS_ENOMEM (-4)  /* device or pinned allocation failed */
+#define SD_CAS_ENODEV (-5)  /* no gfx950 device at this ordinal */
+
+typedef struct sd_cas_ctx sd_cas_ctx;
+
+int sd_cas_abi_version(void);
+
+/* ---- context / memory --------------------------------------------------------------- */
+int sd_cas_ctx_create(int device, sd_cas_ctx** out);
+void sd_cas_ctx_destroy(sd_cas_ctx* ctx);
+const char* sd_cas_last_error(const sd_cas_ctx* ctx);
+/* the context's compute stream (hipStream_t) */
+void* sd_cas_ctx_stream(sd_cas_ctx* ctx);
+int sd_cas_synchronize(sd_cas_ctx* ctx);
+/* page-locked host staging for the gather (replaces the per-file Box<[u8]> of cas.rs:32) */
+int sd_cas_alloc_pinned(sd_cas_ctx* ctx, size_t bytes, void** out);
+int sd_cas_free_pinned(sd_cas_ctx* ctx, void* p);
+
+/* ---- cas_id: host buffers (blocking) --------------------------------------------------
+ * Batched generate_cas_id (cas.rs:23) over already-gathered content:
+ *   bufs[i] / buf_lens[i] = content of file i, sizes[i] = fs::metadata().len()
+ *   (file_identifier/mod.rs:78-79).  out_keys[i] = cas key.
+ * Staged through pinned memory and hipMemcpyAsync on a side stream, then hashed.
+ * A sampled file (size > SD_CAS_MINIMUM_FILE_SIZE) must have buf_len == 57,344. */
+int sd_cas_generate_cas_ids(sd_cas_ctx* ctx, const uint8_t* const* bufs, const uint64_t* buf_lens,
+                            const uint64_t* sizes, size_t n, uint64_t* out_keys);
+
+/* Same, gathering each file from its path with pread at the cas.rs:27-58 offsets.
+ * status[i] = 0, or -errno for a file that failed to open/read (a short read of a sampled
+ * file is -EIO == tokio's UnexpectedEof); such files get out_keys[i] = 0 and are to be
+ * dropped from the step like mod.rs:125-141 does.  Returns SD_CAS_OK unless the batch
+ * itself failed. */
+int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* ctx, const char* const* paths,
+                                       const uint64_t* sizes, size_t n, uint64_t* out_keys,
+                                       int32_t* status);
+
+/* 16 lowercase hex chars + NUL: the cas_id String of cas.rs:61 */
+void sd_cas_key_to_hex(uint64_t key, char out[17]);
+
+/* ---- cas_id: device-resident batches (async on stream) --------------------------------
+ * K1 sampled path: n contents of exactly 57,344 B at d_content + i*stride
+ * (stride >= 57,344, multiple of 16; d_content 16-B aligned). */
+int sd_cas_hash_sampled_dev(sd_cas_ctx* ctx, const void* d_content, uint64_t stride,
+                            const uint64_t* d_sizes, size_t n, uint64_t* d_keys, void* stream);
+
+/* K2 packed path: content i at d_arena + d_offs[i] (16-B aligned), d_lens[i] bytes
+ * (<= SD_CAS_MAX_PACKED_CONTENT_LEN); the arena must be readable up to the 16-B round-up
+ * of every content end.  Files are visited longest-first via an on-device length sort
+ * (workspace in ctx). */
+int sd_cas_hash_packed_dev(sd_cas_ctx* ctx, const void* d_arena, const uint64_t* d_offs,
+                           const uint32_t* d_lens, const uint64_t* d_sizes, size_t n,
+                           uint64_t* d_keys, void* stream);
+
+/* ---- Object grouping (file_identifier/mod.rs:98-350) ----------------------------------
+ * Canonical: d_rep[i] = min{ j : key[j] == key[i] } (the file whose Object file i links
+ * to); *out_objects = number of Objects (= distinct keys).  Blocks until done when
+ * out_objects != NULL.  n < 2^32. */
+int sd_cas_group_dev(sd_cas_ctx* ctx, const uint64_t* d_keys, size_t n, uint32_t* d_rep,
+                     uint64_t* out_objects, void* stream);
+/* Same on already-sorted pairs (keys ascending, vals = file idx, stable). */
+int sd_cas_group_sorted_dev(sd_cas_ctx* ctx, const uint64_t* d_sorted_keys,
+                            const uint32_t* d_sorted_vals, size_t n, uint32_t* d_rep,
+                            uint64_t* out_objects, void* stream);
+/* Reference chunk replay (identifier_job_step over CHUNK_SIZE rows, HashMap order :=
+ * ascending idx): d_rep_chunked[i] = i if file i creates a new Object, else the file
+ * whose Object it links to; *out_created / *out_linked = the summed per-step
+ * (total_created, total_linked) of mod.rs:349.  Blocking. */
+int sd_cas_group_chunked_dev(sd_cas_ctx* ctx, const uint32_t* d_rep, size_t n, uint32_t chunk,
+                             uint32_t* d_rep_chunked, uint64_t* out_created,
+                             uint64_t* out_linked, void* stream);
+/* Stable LSD radix sort of (u64 key, u32 val) on bits [begin_bit, end_bit).
+ * d_vals_in == NULL sorts the identity 0..n-1. */
+int sd_cas_sort_pairs_dev(sd_cas_ctx* ctx, const uint64_t* d_keys_in, const uint32_t* d_vals_in,
+                          size_t n, uint64_t* d_keys_out, uint32_t* d_vals_out, int begin_bit,
+                          int end_bit, void* stream);
+
+/* ---- file_checksum (validation/hash.rs:11-25) ------------------------------------------
+ * Full BLAKE3 digest (32 B) of a device buffer (16-B aligned, readable to the 16-B round-up
+ * of len).  Blocking. */
+int sd_cas_checksum_dev(sd_cas_ctx* ctx, const void* d_data, uint64_t len, uint8_t out[32],
+                        void* stream);
+/* file_checksum(path): streams the file through pinned staging in 64 MiB segments, one
+ * BLAKE3 subtree per segment on the GPU; out_hex = 64 lowercase hex + NUL.
+ * Returns SD_CAS_EIO with *err_no set on an I/O error. */
+int sd_cas_file_checksum(sd_cas_ctx* ctx, const char* path, char out_hex[65], int* err_no);
+
+/* ---- synthetic inputs (benchmarks / tests; same generator as oracle/cas_ref.c) ------- */
+int sd_cas_synth_sampled_dev(sd_cas_ctx* ctx, uint64_t seed, uint64_t file0, size_t n,
+                             uint32_t dup_permille, void* d_content, uint64_t stride,
+                             uint64_t* d_sizes, void* stream);
+/* whole-file path: fills d_sizes/d_lens, d_offs (16-B aligned packing) and the arena;
+ * *out_arena_bytes = bytes used.  Pass d_arena == NULL to only size it (blocking). */
+int sd_cas_synth_small_dev(sd_cas_ctx* ctx, uint64_t seed, uint64_t file0, size_t n,
+                           uint32_t dup_permille, uint64_t* d_sizes, uint32_t* d_lens,
+                           uint64_t* d_offs, void* d_arena, uint64_t* out_arena_bytes,
+                           void* stream);
+int sd_cas_synth_roots_dev(sd_cas_ctx* ctx, uint64_t seed, uint64_t file0, size_t n,
+                           uint32_t dup_permille, uint64_t* d_roots, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SD_HIP_CAS_H */

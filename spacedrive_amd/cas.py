@@ -1,0 +1,326 @@
+"""Host-side mirror of the reference's content-identification interface, over the C ABI.
+
+Reference (annihilatorrrr/spacedrive, Rust) → here:
+
+* ``generate_cas_id(path, size) -> String``        core/src/object/cas.rs:23-62
+  → :func:`generate_cas_id` (a one-file batch) and :meth:`CasEngine.generate_cas_ids`
+  (the batched drop-in the north star asks for: ``generate_cas_ids(&[(buf, size)])``).
+* ``file_checksum(path) -> String``                  core/src/object/validation/hash.rs:11-25
+  → :func:`file_checksum`.
+* ``FileMetadata::new`` + ``identifier_job_step``    core/src/object/file_identifier/mod.rs:55-350
+  → :func:`identifier_job_step` (cas_ids, Object links, ``(total_created, total_linked)``).
+
+Errors follow the reference: an I/O failure on one file is an ``OSError`` for the
+single-file call (``io::Error`` in Rust) and a per-file drop in the batch
+(mod.rs:125-141); a GPU failure is a batch-level :class:`CasError`.
+
+Device arrays are torch tensors used as plain HBM buffers (u64 values are stored in
+int64 tensors bit-for-bit); all computation happens in libsd_hip_cas.so.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _native
+from ._native import CasError
+
+# core/src/object/cas.rs:10-15 and file_identifier/mod.rs:34
+SAMPLE_COUNT = 4
+SAMPLE_SIZE = 1024 * 10
+HEADER_OR_FOOTER_SIZE = 1024 * 8
+MINIMUM_FILE_SIZE = 1024 * 100
+SAMPLED_CONTENT_LEN = 2 * HEADER_OR_FOOTER_SIZE + SAMPLE_COUNT * SAMPLE_SIZE  # 57,344
+CHUNK_SIZE = 100
+MAX_PACKED_CONTENT_LEN = 128 * 1024 - 8
+
+
+def key_to_cas_id(key: int) -> str:
+    """cas.rs:61 ``hasher.finalize().to_hex()[..16]`` from the big-endian u64 key."""
+    return f"{int(key) & 0xFFFFFFFFFFFFFFFF:016x}"
+
+
+def cas_id_to_key(cas_id: str) -> int:
+    return int(cas_id, 16)
+
+
+def _ptr(t) -> int:
+    return int(t.data_ptr())
+
+
+def _stream(stream: Optional[int]) -> int:
+    """Device calls default to torch's current stream so they order with tensor ops."""
+    if stream is not None:
+        return stream
+    import torch
+    return int(torch.cuda.current_stream().cuda_stream)
+
+
+def _np_ptr(a: np.ndarray) -> int:
+    return int(a.ctypes.data)
+
+
+class CasEngine:
+    """One context on one gfx950 device (one per thread/device, like the C ABI)."""
+
+    def __init__(self, device: int = 0):
+        self.L = _native.lib()
+        h = ctypes.c_void_p()
+        rc = self.L.sd_cas_ctx_create(int(device), ctypes.byref(h))
+        if rc != 0:
+            raise CasError(rc, f"sd_cas_ctx_create(device={device}) failed "
+                               "(needs a gfx950 / MI355X device)")
+        self.h = h
+        self.device = device
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            self.L.sd_cas_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- helpers --------------------------------------------------------------------
+    def _check(self, rc: int, what: str) -> None:
+        if rc != 0:
+            msg = self.L.sd_cas_last_error(self.h)
+            raise CasError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+    @property
+    def stream(self) -> int:
+        return int(self.L.sd_cas_ctx_stream(self.h) or 0)
+
+    def synchronize(self) -> None:
+        self._check(self.L.sd_cas_synchronize(self.h), "synchronize")
+
+    # ---- host batches (blocking) -------------------------------------------------------
+    def generate_cas_keys(self, items: Sequence[tuple[bytes, int]]) -> np.ndarray:
+        """Batched ``generate_cas_id`` over already-gathered content: items = (buf, size)."""
+        n = len(items)
+        if n == 0:
+            return np.zeros(0, dtype=np.uint64)
+        bufs = [bytes(b) for b, _ in items]
+        ptrs = (ctypes.c_char_p * n)(*bufs)
+        lens = np.array([len(b) for b in bufs], dtype=np.uint64)
+        sizes = np.array([int(s) for _, s in items], dtype=np.uint64)
+        keys = np.zeros(n, dtype=np.uint64)
+        rc = self.L.sd_cas_generate_cas_ids(self.h, ctypes.cast(ptrs, ctypes.c_void_p),
+                                            _np_ptr(lens), _np_ptr(sizes), n, _np_ptr(keys))
+        self._check(rc, "generate_cas_ids")
+        return keys
+
+    def generate_cas_ids(self, items: Sequence[tuple[bytes, int]]) -> list[str]:
+        return [key_to_cas_id(k) for k in self.generate_cas_keys(items)]
+
+    def generate_cas_keys_from_paths(self, paths: Sequence[str], sizes: Sequence[int]):
+        """Gather (pread at the cas.rs:27-58 offsets) + hash. Returns (keys, errno array)."""
+        n = len(paths)
+        enc = [os.fsencode(p) for p in paths]
+        parr = (ctypes.c_char_p * n)(*enc)
+        sz = np.array([int(s) for s in sizes], dtype=np.uint64)
+        keys = np.zeros(n, dtype=np.uint64)
+        status = np.zeros(n, dtype=np.int32)
+        if n:
+            rc = self.L.sd_cas_generate_cas_ids_from_paths(
+                self.h, ctypes.cast(parr, ctypes.c_void_p), _np_ptr(sz), n, _np_ptr(keys),
+                _np_ptr(status))
+            self._check(rc, "generate_cas_ids_from_paths")
+        return keys, -status
+
+    def file_checksum(self, path: str) -> str:
+        out = ctypes.create_string_buffer(65)
+        err = ctypes.c_int(0)
+        rc = self.L.sd_cas_file_checksum(self.h, os.fsencode(path), out, ctypes.byref(err))
+        if rc == -3 and err.value:
+            raise OSError(err.value, os.strerror(err.value), path)
+        self._check(rc, "file_checksum")
+        return out.value.decode()
+
+    # ---- device-resident (torch tensors as HBM buffers) ----------------------------------
+    def hash_sampled(self, content, sizes, keys, stride: Optional[int] = None,
+                     n: Optional[int] = None, stream: Optional[int] = None) -> None:
+        """K1: content uint8 [n, stride] (or flat), sizes/keys int64 [n]."""
+        n = int(sizes.numel()) if n is None else n
+        stride = int(content.shape[-1]) if stride is None and content.dim() == 2 else stride
+        self._check(self.L.sd_cas_hash_sampled_dev(self.h, _ptr(content), int(stride), _ptr(sizes),
+                                                   n, _ptr(keys), _stream(stream)), "hash_sampled")
+
+    def hash_packed(self, arena, offs, lens, sizes, keys, stream: Optional[int] = None) -> None:
+        n = int(sizes.numel())
+        self._check(self.L.sd_cas_hash_packed_dev(self.h, _ptr(arena), _ptr(offs), _ptr(lens),
+                                                  _ptr(sizes), n, _ptr(keys), _stream(stream)),
+                    "hash_packed")
+
+    def group(self, keys, rep, stream: Optional[int] = None, want_objects: bool = True) -> Optional[int]:
+        n = int(keys.numel())
+        obj = ctypes.c_uint64(0)
+        self._check(self.L.sd_cas_group_dev(self.h, _ptr(keys), n, _ptr(rep),
+                                            ctypes.byref(obj) if want_objects else None, _stream(stream)),
+                    "group")
+        return int(obj.value) if want_objects else None
+
+    def group_sorted(self, skeys, svals, rep, stream: Optional[int] = None) -> int:
+        n = int(skeys.numel())
+        obj = ctypes.c_uint64(0)
+        self._check(self.L.sd_cas_group_sorted_dev(self.h, _ptr(skeys), _ptr(svals), n, _ptr(rep),
+                                                   ctypes.byref(obj), _stream(stream)), "group_sorted")
+        return int(obj.value)
+
+    def group_chunked(self, rep, rep_chunked, chunk: int = CHUNK_SIZE,
+                      stream: Optional[int] = None) -> tuple[int, int]:
+        n = int(rep.numel())
+        c = ctypes.c_uint64(0)
+        ln = ctypes.c_uint64(0)
+        self._check(self.L.sd_cas_group_chunked_dev(self.h, _ptr(rep), n, int(chunk),
+                                                     _ptr(rep_chunked), ctypes.byref(c),
+                                                     ctypes.byref(ln), _stream(stream)), "group_chunked")
+        return int(c.value), int(ln.value)
+
+    def sort_pairs(self, keys_in, vals_in, keys_out, vals_out, begin_bit: int = 0,
+                   end_bit: int = 64, stream: Optional[int] = None) -> None:
+        n = int(keys_in.numel())
+        self._check(self.L.sd_cas_sort_pairs_dev(
+            self.h, _ptr(keys_in), _ptr(vals_in) if vals_in is not None else None, n,
+            _ptr(keys_out), _ptr(vals_out), begin_bit, end_bit, _stream(stream)), "sort_pairs")
+
+    def checksum_dev(self, data, length: Optional[int] = None, stream: Optional[int] = None) -> str:
+        length = int(data.numel() * data.element_size()) if length is None else length
+        out = ctypes.create_string_buffer(32)
+        self._check(self.L.sd_cas_checksum_dev(self.h, _ptr(data), int(length), out, _stream(stream)),
+                    "checksum")
+        return out.raw.hex()
+
+    def synth_sampled(self, seed: int, file0: int, n: int, content, sizes, stride: int,
+                      dup_permille: int = 0, stream: Optional[int] = None) -> None:
+        self._check(self.L.sd_cas_synth_sampled_dev(self.h, seed, file0, n, dup_permille,
+                                                    _ptr(content), stride, _ptr(sizes), _stream(stream)),
+                    "synth_sampled")
+
+    def synth_small(self, seed: int, file0: int, n: int, sizes, lens, offs, arena=None,
+                    dup_permille: int = 0, stream: Optional[int] = None) -> int:
+        out = ctypes.c_uint64(0)
+        self._check(self.L.sd_cas_synth_small_dev(self.h, seed, file0, n, dup_permille,
+                                                  _ptr(sizes), _ptr(lens), _ptr(offs),
+                                                  _ptr(arena) if arena is not None else None,
+                                                  ctypes.byref(out), _stream(stream)), "synth_small")
+        return int(out.value)
+
+    def synth_roots(self, seed: int, file0: int, n: int, roots, dup_permille: int = 0,
+                    stream: Optional[int] = None) -> None:
+        self._check(self.L.sd_cas_synth_roots_dev(self.h, seed, file0, n, dup_permille,
+                                                  _ptr(roots), _stream(stream)), "synth_roots")
+
+
+_DEFAULT: dict[int, CasEngine] = {}
+
+
+def engine(device: int = 0) -> CasEngine:
+    if device not in _DEFAULT:
+        _DEFAULT[device] = CasEngine(device)
+    return _DEFAULT[device]
+
+
+# ---- reference-shaped free functions -----------------------------------------------------
+def generate_cas_id(path: str, size: int) -> str:
+    """``generate_cas_id(path, size)`` (cas.rs:23): a one-file batch on the GPU.
+    Raises OSError like the reference's io::Error."""
+    keys, errs = engine().generate_cas_keys_from_paths([path], [size])
+    if errs[0]:
+        raise OSError(int(errs[0]), os.strerror(int(errs[0])), path)
+    return key_to_cas_id(keys[0])
+
+
+def generate_cas_ids(items: Sequence[tuple[bytes, int]]) -> list[str]:
+    """North-star drop-in: ``generate_cas_ids(&[(buf, size)]) -> Vec<CasId>``."""
+    return engine().generate_cas_ids(items)
+
+
+def file_checksum(path: str) -> str:
+    """``file_checksum(path)`` (validation/hash.rs:11): full 64-hex BLAKE3 digest."""
+    return engine().file_checksum(path)
+
+
+@dataclass
+class FileMetadata:
+    """file_identifier/mod.rs:48-53 (kind is out of scope: sd-file-ext)."""
+    cas_id: Optional[str]
+    size: int
+
+
+@dataclass
+class StepResult:
+    """What identifier_job_step (mod.rs:98-350) decides for one batch of file_paths."""
+    metadata: dict = field(default_factory=dict)   # idx -> FileMetadata (errors dropped)
+    object_of: dict = field(default_factory=dict)  # idx -> idx of the file owning its Object
+    total_created: int = 0
+    total_linked: int = 0
+    errors: dict = field(default_factory=dict)     # idx -> errno (logged + dropped, :125-141)
+
+
+def identifier_job_step(paths: Sequence[str], chunk: int = CHUNK_SIZE,
+                        eng: Optional[CasEngine] = None) -> StepResult:
+    """Run the file identifier over ``paths`` (ascending file_path.id order) on a fresh
+    library, CHUNK_SIZE rows per step, as mod.rs:98-350 would: cas_ids from the GPU,
+    Objects from the GPU grouping in its chunk-replay form (HashMap order := ascending
+    idx).  Empty files get no cas_id and their own Object (mod.rs:78-86,
+    :246-311).  Returns the per-file decisions and the summed (created, linked)."""
+    import torch
+
+    eng = eng or engine()
+    res = StepResult()
+    sizes = []
+    for i, p in enumerate(paths):
+        try:
+            sizes.append(os.stat(p).st_size)  # fs::metadata (mod.rs:63)
+        except OSError as e:
+            res.errors[i] = e.errno
+            sizes.append(-1)
+    live = [i for i in range(len(paths)) if sizes[i] > 0]
+    keys, errs = eng.generate_cas_keys_from_paths([paths[i] for i in live], [sizes[i] for i in live])
+    for j, i in enumerate(live):
+        if errs[j]:
+            res.errors[i] = int(errs[j])
+    for i in range(len(paths)):
+        if i in res.errors:
+            continue
+        res.metadata[i] = FileMetadata(None if sizes[i] == 0 else None, sizes[i])
+    ok = [j for j, i in enumerate(live) if not errs[j]]
+    for j in ok:
+        res.metadata[live[j]].cas_id = key_to_cas_id(keys[j])
+    # rows that survive into the step, in id order (errors are dropped from the chunk but
+    # still occupy their row of the 100-row query, so chunk membership uses the row index)
+    rows = sorted(res.metadata)
+    hashed = [i for i in rows if res.metadata[i].cas_id is not None]
+    if hashed:
+        dev = torch.device("cuda", eng.device)
+        # key per hashed file; rows without cas are not grouped (each gets its own Object)
+        k = torch.tensor(np.array([cas_id_to_key(res.metadata[i].cas_id) for i in hashed],
+                                  dtype=np.uint64).view(np.int64), device=dev)
+        rep = torch.empty(len(hashed), dtype=torch.int32, device=dev)
+        eng.group(k, rep)
+        rep = rep.cpu().numpy().astype(np.int64)
+        canon = {hashed[a]: hashed[int(rep[a])] for a in range(len(hashed))}
+    else:
+        canon = {}
+    for i in rows:
+        if i in canon and canon[i] // chunk != i // chunk:
+            res.object_of[i] = canon[i]
+            res.total_linked += 1
+        else:
+            res.object_of[i] = i
+            res.total_created += 1
+    return res

@@ -1,0 +1,179 @@
+// checksum.hip — full-content BLAKE3 of one large file on gfx950 (K3, validator path).
+//
+// Replaces file_checksum (core/src/object/validation/hash.rs:11-25), which feeds the whole
+// file through ONE blake3::Hasher on one thread, 1 MiB at a time, and returns the full
+// 64-hex digest.  Here the file is hashed tree-parallel:
+//   sd_b3_chunk_groups: one lane per 1 KiB chunk, 256 chunks per workgroup; chunk CVs
+//     go to LDS and the workgroup pair-and-promotes them to ONE subtree CV (8 levels).
+//   sd_b3_reduce_cvs: the same pair-and-promote over 256 CVs at a time, repeated until
+//     one CV remains; only the very last parent carries ROOT.
+// Level-wise pair-and-promote over aligned groups of 2^k equals BLAKE3's left-balanced
+// tree (checked by the oracle's third formulation, blake3_levelwise).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "blake3_device.hpp"
+#include "sd_checksum.h"
+
+namespace sdcas {
+
+constexpr int GROUP = 256;  // chunks (or CVs) reduced per workgroup
+
+// CV (or ROOT digest) of one chunk of `clen` <= 1024 bytes at global chunk index `ctr`.
+__device__ __forceinline__ void chunk_cv(const uint4* __restrict__ q, uint32_t clen, uint64_t ctr,
+                                         bool root, uint32_t (&cv)[8]) {
+  const uint32_t nblk = clen == 0 ? 1u : (clen + 63u) >> 6;
+  set_iv(cv);
+  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+  uint4 a0, a1, a2, a3;
+  auto load = [&](uint32_t b) {
+    const uint32_t o = b << 6;
+    a0 = (o < clen) ? q[4 * b] : z;
+    a1 = (o + 16u < clen) ? q[4 * b + 1] : z;
+    a2 = (o + 32u < clen) ? q[4 * b + 2] : z;
+    a3 = (o + 48u < clen) ? q[4 * b + 3] : z;
+  };
+  load(0);
+  for (uint32_t b = 0; b < nblk; ++b) {
+    uint32_t m[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                      a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+    const uint32_t rem = clen - (b << 6);
+    const uint32_t blen = clen == 0 ? 0u : (rem < 64u ? rem : 64u);
+    if (blen < 64u) {
+#pragma unroll
+      for (int w = 0; w < 16; ++w) {
+        const int vb = (int)blen - 4 * w;
+        m[w] &= vb >= 4 ? 0xFFFFFFFFu : (vb <= 0 ? 0u : ((1u << (8 * vb)) - 1u));
+      }
+    }
+    if (b + 1 < nblk) load(b + 1);
+    uint32_t flags = (b == 0 ? (uint32_t)CHUNK_START : 0u) | (b + 1 == nblk ? (uint32_t)CHUNK_END : 0u);
+    if (root && b + 1 == nblk) flags |= ROOT;
+    compress(cv, m, (uint32_t)ctr, (uint32_t)(ctr >> 32), blen, flags);
+  }
+}
+
+// Pair-and-promote `count` (<= 256) CVs held in LDS cv[GROUP][8] down to one (in cv[0]).
+// `root_last`: the final parent carries ROOT (only when this is the whole tree's top).
+__device__ __forceinline__ void lds_reduce(uint32_t (*cvs)[8], uint32_t count, bool root_last) {
+  const uint32_t t = threadIdx.x;
+  while (count > 1) {
+    const uint32_t pairs = count >> 1;
+    uint32_t out[8];
+    if (t < pairs) {
+      uint32_t l[8], r[8];
+#pragma unroll
+      for (int w = 0; w < 8; ++w) { l[w] = cvs[2 * t][w]; r[w] = cvs[2 * t + 1][w]; }
+      parent(out, l, r, (root_last && count == 2) ? (uint32_t)ROOT : 0u);
+    }
+    uint32_t promoted[8];
+    const bool odd = count & 1u;
+    if (odd && t == pairs) {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) promoted[w] = cvs[count - 1][w];
+    }
+    __syncthreads();
+    if (t < pairs) {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) cvs[t][w] = out[w];
+    }
+    if (odd && t == pairs) {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) cvs[t][w] = promoted[w];
+    }
+    __syncthreads();
+    count = pairs + (odd ? 1u : 0u);
+  }
+}
+
+// One workgroup = chunks [g*256, g*256+256) of the buffer (global chunk index chunk0 + ...).
+// out[g] = subtree CV; when nchunks_total == 1 the single chunk is the root (digest).
+extern "C" __global__ void __launch_bounds__(GROUP)
+sd_b3_chunk_groups(const uint8_t* __restrict__ data, uint64_t len, uint64_t chunk0,
+                   uint32_t* __restrict__ out, int root_if_single_group) {
+  __shared__ uint32_t cvs[GROUP][8];
+  const uint64_t nchunks = len == 0 ? 1 : (len + 1023) >> 10;
+  const uint64_t first = (uint64_t)blockIdx.x * GROUP;
+  const uint32_t count = (uint32_t)min((uint64_t)GROUP, nchunks - first);
+  const uint32_t t = threadIdx.x;
+  const bool whole_tree = root_if_single_group && nchunks <= (uint64_t)GROUP;
+  if (t < count) {
+    const uint64_t c = first + t;
+    const uint64_t off = c << 10;
+    const uint32_t clen = (uint32_t)min((uint64_t)1024, len - off);
+    uint32_t cv[8];
+    chunk_cv(reinterpret_cast<const uint4*>(data + off), clen, chunk0 + c,
+             whole_tree && nchunks == 1, cv);
+#pragma unroll
+    for (int w = 0; w < 8; ++w) cvs[t][w] = cv[w];
+  }
+  __syncthreads();
+  lds_reduce(cvs, count, whole_tree);
+  if (t < 8) out[(uint64_t)blockIdx.x * 8 + t] = cvs[0][t];
+}
+
+// Reduce groups of 256 CVs: in[cnt][8] -> out[ceil(cnt/256)][8].
+extern "C" __global__ void __launch_bounds__(GROUP)
+sd_b3_reduce_cvs(const uint32_t* __restrict__ in, uint64_t cnt, uint32_t* __restrict__ out,
+                 int root_if_single_group) {
+  __shared__ uint32_t cvs[GROUP][8];
+  const uint64_t first = (uint64_t)blockIdx.x * GROUP;
+  const uint32_t count = (uint32_t)min((uint64_t)GROUP, cnt - first);
+  const uint32_t t = threadIdx.x;
+  if (t < count) {
+#pragma unroll
+    for (int w = 0; w < 8; ++w) cvs[t][w] = in[(first + t) * 8 + w];
+  }
+  __syncthreads();
+  lds_reduce(cvs, count, root_if_single_group && cnt <= (uint64_t)GROUP);
+  if (t < 8) out[(uint64_t)blockIdx.x * 8 + t] = cvs[0][t];
+}
+
+size_t checksum_workspace_bytes(uint64_t len) {
+  const uint64_t nchunks = len == 0 ? 1 : (len + 1023) >> 10;
+  const uint64_t g = (nchunks + GROUP - 1) / GROUP;
+  return 2 * ((g * 32 + 255) / 256 * 256) + 512;
+}
+
+// Reduce `cnt` CVs at d_cvs (ping-pong with `tmp`) to one; result in *result (device).
+static hipError_t reduce_to_one(uint32_t* a, uint32_t* b, uint64_t cnt, bool root,
+                                uint32_t** result, hipStream_t s) {
+  while (cnt > 1) {
+    const uint64_t g = (cnt + GROUP - 1) / GROUP;
+    sd_b3_reduce_cvs<<<(uint32_t)g, GROUP, 0, s>>>(a, cnt, b, root ? 1 : 0);
+    uint32_t* t = a; a = b; b = t;
+    cnt = g;
+  }
+  *result = a;
+  return hipGetLastError();
+}
+
+hipError_t checksum_device(const uint8_t* data, uint64_t len, uint64_t chunk0, bool root,
+                           uint32_t* d_out8, void* ws, hipStream_t s) {
+  const uint64_t nchunks = len == 0 ? 1 : (len + 1023) >> 10;
+  const uint64_t g = (nchunks + GROUP - 1) / GROUP;
+  if (g >= (1ull << 31)) return hipErrorInvalidValue;
+  uint32_t* a = (uint32_t*)ws;
+  uint32_t* b = (uint32_t*)((char*)ws + (g * 32 + 255) / 256 * 256);
+  sd_b3_chunk_groups<<<(uint32_t)g, GROUP, 0, s>>>(data, len, chunk0, a, root ? 1 : 0);
+  uint32_t* res;
+  hipError_t e = reduce_to_one(a, b, g, root, &res, s);
+  if (e != hipSuccess) return e;
+  return hipMemcpyAsync(d_out8, res, 32, hipMemcpyDeviceToDevice, s);
+}
+
+hipError_t reduce_cvs_device(const uint32_t* d_cvs, uint64_t cnt, uint32_t* d_out8, void* ws,
+                             hipStream_t s) {
+  if (cnt == 0) return hipErrorInvalidValue;
+  const uint64_t g = (cnt + GROUP - 1) / GROUP;
+  uint32_t* a = (uint32_t*)ws;
+  uint32_t* b = (uint32_t*)((char*)ws + (g * 32 + 255) / 256 * 256);
+  if (cnt == 1) return hipMemcpyAsync(d_out8, d_cvs, 32, hipMemcpyDeviceToDevice, s);
+  sd_b3_reduce_cvs<<<(uint32_t)g, GROUP, 0, s>>>(d_cvs, cnt, a, 1);
+  uint32_t* res;
+  hipError_t e = reduce_to_one(a, b, g, true, &res, s);
+  if (e != hipSuccess) return e;
+  return hipMemcpyAsync(d_out8, res, 32, hipMemcpyDeviceToDevice, s);
+}
+
+}  // namespace sdcas

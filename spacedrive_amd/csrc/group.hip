@@ -1,0 +1,395 @@
+// group.hip — Object grouping on gfx950: LSD radix sort of (cas key, file idx) pairs and
+// segmented run-length grouping (K4 + K5).
+//
+// Replaces the grouping logic of core/src/object/file_identifier/mod.rs:98-350
+// (unique_cas_ids HashSet :149-154, the SQL `cas_id IN (...)` lookup :181-198, the
+// linear `find` over existing Objects :214-224, one new Object per remaining file
+// :246-311).  Canonical contract: rep(f) = min{ g : key(g) == key(f) },
+// objects = #distinct keys.  LSD radix sort is stable and the values enter in ascending
+// idx order, so the head of every equal-key run carries the minimum idx.
+//
+// Sort pass = upsweep (per-tile digit histogram in LDS) -> exclusive scan over the
+// digit-major [digit][tile] table -> downsweep (stable wave-level ranking with 8 ballots
+// per item, tile-local digit offsets in LDS, scatter).  All integer/byte work bound by
+// HBM; nothing here is reshaped into a GEMM.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sd_group.h"
+
+namespace sdcas {
+
+constexpr int RADIX = 256;
+constexpr int SORT_THREADS = 256;
+constexpr int SORT_ROUNDS = 16;  // items per thread per tile
+constexpr int TILE = SORT_THREADS * SORT_ROUNDS;  // 4096 keys per tile
+
+__device__ __forceinline__ uint32_t digit_of(uint64_t k, uint32_t shift, uint32_t mask) {
+  return (uint32_t)(k >> shift) & mask;
+}
+
+// hist[d * ntiles + tile] = #keys of `tile` with digit d
+extern "C" __global__ void __launch_bounds__(SORT_THREADS)
+sd_radix_upsweep(const uint64_t* __restrict__ keys, uint64_t n, uint32_t shift, uint32_t mask,
+                 uint32_t* __restrict__ hist, uint32_t ntiles) {
+  __shared__ uint32_t cnt[RADIX];
+  const uint32_t t = threadIdx.x;
+  cnt[t] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * TILE;
+#pragma unroll 4
+  for (int r = 0; r < SORT_ROUNDS; ++r) {
+    const uint64_t i = base + (uint64_t)r * SORT_THREADS + t;
+    if (i < n) atomicAdd(&cnt[digit_of(keys[i], shift, mask)], 1u);
+  }
+  __syncthreads();
+  hist[(uint64_t)t * ntiles + blockIdx.x] = cnt[t];
+}
+
+// Stable scatter of one tile.  offs = exclusive-scanned hist (same layout).
+template <bool HAS_VALS>
+__device__ __forceinline__ void downsweep_body(const uint64_t* __restrict__ keys_in,
+                                               const uint32_t* __restrict__ vals_in,
+                                               uint64_t* __restrict__ keys_out,
+                                               uint32_t* __restrict__ vals_out, uint64_t n,
+                                               uint32_t shift, uint32_t mask,
+                                               const uint32_t* __restrict__ offs,
+                                               uint32_t ntiles) {
+  __shared__ uint32_t run[RADIX];        // per-digit running count within this tile
+  __shared__ uint32_t wcnt[4][RADIX];    // per-wave digit counts of the current round
+  __shared__ uint32_t gbase[RADIX];      // global offset of this tile's digit d
+  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+  run[t] = 0;
+  wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
+  gbase[t] = offs[(uint64_t)t * ntiles + blockIdx.x];
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * TILE;
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int r = 0; r < SORT_ROUNDS; ++r) {
+    const uint64_t i = base + (uint64_t)r * SORT_THREADS + t;
+    const bool valid = i < n;
+    const uint64_t k = valid ? keys_in[i] : 0ull;
+    const uint32_t v = (HAS_VALS && valid) ? vals_in[i] : (uint32_t)i;
+    const uint32_t d = digit_of(k, shift, mask);
+    // lanes of this wave holding the same digit
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const uint64_t bal = __ballot((d >> b) & 1u);
+      peers &= ((d >> b) & 1u) ? bal : ~bal;
+    }
+    const uint32_t rank_in_wave = __popcll(peers & lt_mask);
+    if (valid && rank_in_wave == 0) wcnt[w][d] = (uint32_t)__popcll(peers);
+    __syncthreads();
+    uint32_t pos = 0;
+    if (valid) {
+      uint32_t before = run[d];
+      for (uint32_t ww = 0; ww < w; ++ww) before += wcnt[ww][d];
+      pos = gbase[d] + before + rank_in_wave;
+    }
+    __syncthreads();
+    run[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
+    wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
+    if (valid) {
+      keys_out[pos] = k;
+      vals_out[pos] = v;
+    }
+    __syncthreads();
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(SORT_THREADS)
+sd_radix_downsweep(const uint64_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
+                   uint64_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out, uint64_t n,
+                   uint32_t shift, uint32_t mask, const uint32_t* __restrict__ offs,
+                   uint32_t ntiles) {
+  downsweep_body<true>(keys_in, vals_in, keys_out, vals_out, n, shift, mask, offs, ntiles);
+}
+
+// first pass: values are the identity (file idx) — no value read
+extern "C" __global__ void __launch_bounds__(SORT_THREADS)
+sd_radix_downsweep_iota(const uint64_t* __restrict__ keys_in, uint64_t* __restrict__ keys_out,
+                        uint32_t* __restrict__ vals_out, uint64_t n, uint32_t shift,
+                        uint32_t mask, const uint32_t* __restrict__ offs, uint32_t ntiles) {
+  downsweep_body<false>(keys_in, nullptr, keys_out, vals_out, n, shift, mask, offs, ntiles);
+}
+
+// ---- device-wide exclusive scan (u32, sum) over m <= SCAN_TILE^2 elements ----------
+constexpr int SCAN_THREADS = 256;
+constexpr int SCAN_ITEMS = 16;
+constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;  // 4096
+
+__device__ __forceinline__ uint32_t block_exclusive_sum(uint32_t x, uint32_t* total) {
+  __shared__ uint32_t wsum[SCAN_THREADS / 64];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  uint32_t inc = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= (uint32_t)o) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t wpre = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_THREADS / 64; ++i) {
+    const uint32_t s = wsum[i];
+    if ((uint32_t)i < w) wpre += s;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return wpre + inc - x;
+}
+
+// per-tile sums
+extern "C" __global__ void __launch_bounds__(SCAN_THREADS)
+sd_scan_reduce(const uint32_t* __restrict__ in, uint64_t m, uint32_t* __restrict__ partial) {
+  const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) s += (base + k < m) ? in[base + k] : 0u;
+  uint32_t tot;
+  (void)block_exclusive_sum(s, &tot);
+  if (threadIdx.x == 0) partial[blockIdx.x] = tot;
+}
+
+// exclusive scan of a tile (blocked per thread), seeded with tile_offset[blockIdx] (or 0)
+extern "C" __global__ void __launch_bounds__(SCAN_THREADS)
+sd_scan_tiles(const uint32_t* __restrict__ in, uint64_t m, uint32_t* __restrict__ out,
+              const uint32_t* __restrict__ tile_offset) {
+  const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+  uint32_t v[SCAN_ITEMS];
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) { v[k] = (base + k < m) ? in[base + k] : 0u; s += v[k]; }
+  uint32_t tot;
+  uint32_t run = block_exclusive_sum(s, &tot) + (tile_offset ? tile_offset[blockIdx.x] : 0u);
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    if (base + k < m) out[base + k] = run;
+    run += v[k];
+  }
+}
+
+// ---- grouping over the sorted pairs -------------------------------------------------
+// head position scan: hp[i] = max{ j <= i : key[j] != key[j-1] or j == 0 }.
+// Done per tile with a block max-scan, then the cross-tile carry is resolved by the
+// tiny per-tile "last head" array (sd_group_carry), then applied in sd_group_emit.
+__device__ __forceinline__ uint32_t block_inclusive_max(uint32_t x, uint32_t* total) {
+  __shared__ uint32_t wmax[SCAN_THREADS / 64];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  uint32_t inc = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= (uint32_t)o) inc = max(inc, y);
+  }
+  if (lane == 63) wmax[w] = inc;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_THREADS / 64; ++i) {
+    const uint32_t s = wmax[i];
+    if ((uint32_t)i < w) pre = max(pre, s);
+    tot = max(tot, s);
+  }
+  __syncthreads();
+  *total = tot;
+  return max(pre, inc);
+}
+
+// +1-encoded head positions (0 = no head seen in this prefix of the tile)
+extern "C" __global__ void __launch_bounds__(SCAN_THREADS)
+sd_group_tile_heads(const uint64_t* __restrict__ skeys, uint64_t n,
+                    uint32_t* __restrict__ tile_last_head, uint32_t* __restrict__ tile_heads) {
+  const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+  uint32_t hmax = 0, hcnt = 0;
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const uint64_t i = base + k;
+    if (i < n && (i == 0 || skeys[i] != skeys[i - 1])) { hmax = (uint32_t)i + 1u; ++hcnt; }
+  }
+  uint32_t tmax, tsum;
+  (void)block_inclusive_max(hmax, &tmax);
+  (void)block_exclusive_sum(hcnt, &tsum);
+  if (threadIdx.x == 0) { tile_last_head[blockIdx.x] = tmax; tile_heads[blockIdx.x] = tsum; }
+}
+
+// carry[t] = max(tile_last_head[0..t-1]) (single block, sequential over <= ~64k tiles)
+extern "C" __global__ void __launch_bounds__(SCAN_THREADS)
+sd_group_carry(const uint32_t* __restrict__ tile_last_head, uint32_t ntiles,
+               uint32_t* __restrict__ carry, const uint32_t* __restrict__ tile_heads,
+               uint64_t* __restrict__ objects) {
+  // chunked sequential scan: each thread owns a contiguous slice
+  const uint32_t per = (ntiles + SCAN_THREADS - 1) / SCAN_THREADS;
+  const uint32_t lo = threadIdx.x * per, hi = min(ntiles, lo + per);
+  uint32_t m = 0, s = 0;
+  for (uint32_t t = lo; t < hi; ++t) { m = max(m, tile_last_head[t]); s += tile_heads[t]; }
+  uint32_t tot;
+  const uint32_t pre = block_inclusive_max(m, &tot);
+  // exclusive max for my slice start: inclusive of previous threads
+  __shared__ uint32_t incl[SCAN_THREADS];
+  incl[threadIdx.x] = pre;
+  __syncthreads();
+  uint32_t run = threadIdx.x ? incl[threadIdx.x - 1] : 0u;
+  for (uint32_t t = lo; t < hi; ++t) { carry[t] = run; run = max(run, tile_last_head[t]); }
+  uint32_t stot;
+  (void)block_exclusive_sum(s, &stot);
+  if (threadIdx.x == 0) *objects = stot;
+}
+
+// rep[vals[i]] = vals[head(i)]
+extern "C" __global__ void __launch_bounds__(SCAN_THREADS)
+sd_group_emit(const uint64_t* __restrict__ skeys, const uint32_t* __restrict__ svals,
+              uint64_t n, const uint32_t* __restrict__ carry, uint32_t* __restrict__ rep) {
+  const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+  uint32_t hm[SCAN_ITEMS];
+  uint32_t run = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const uint64_t i = base + k;
+    if (i < n && (i == 0 || skeys[i] != skeys[i - 1])) run = (uint32_t)i + 1u;
+    hm[k] = run;
+  }
+  uint32_t tot;
+  const uint32_t incl = block_inclusive_max(run, &tot);
+  // exclusive prefix max from earlier threads of this block, and from earlier tiles
+  __shared__ uint32_t inc_s[SCAN_THREADS];
+  inc_s[threadIdx.x] = incl;
+  __syncthreads();
+  uint32_t prev = threadIdx.x ? inc_s[threadIdx.x - 1] : 0u;
+  prev = max(prev, carry[blockIdx.x]);
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const uint64_t i = base + k;
+    if (i < n) {
+      const uint32_t h = max(prev, hm[k]) - 1u;  // always >= 1 because i==0 is a head
+      rep[svals[i]] = svals[h];
+    }
+  }
+}
+
+// chunk-of-`chunk` reference emulation (mod.rs:202-311):
+// rep_c[i] = i if canonical rep is in i's own chunk, else canonical rep.
+extern "C" __global__ void __launch_bounds__(256)
+sd_group_chunked(const uint32_t* __restrict__ rep, uint64_t n, uint32_t chunk,
+                 uint32_t* __restrict__ rep_chunked, unsigned long long* __restrict__ created) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool own = false;
+  if (i < n) {
+    const uint32_t r = rep[i];
+    own = (r / chunk) == ((uint32_t)i / chunk);
+    rep_chunked[i] = own ? (uint32_t)i : r;
+  }
+  const uint64_t b = __ballot(own);
+  if ((threadIdx.x & 63u) == 0 && b) atomicAdd(created, (unsigned long long)__popcll(b));
+}
+
+}  // namespace sdcas
+
+// ---- host launchers ----------------------------------------------------------------
+namespace sdcas {
+
+static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+static inline uint32_t tiles_of(uint64_t n, uint64_t tile) { return (uint32_t)((n + tile - 1) / tile); }
+
+size_t sort_workspace_bytes(uint64_t n) {
+  const uint64_t nt = tiles_of(n ? n : 1, TILE);
+  const uint64_t m = (uint64_t)RADIX * nt;
+  return align_up(n * 8, 256) + align_up(n * 4, 256) + 2 * align_up(m * 4, 256) +
+         align_up(tiles_of(m, SCAN_TILE) * 4 + 4, 256) + 256;
+}
+
+size_t group_workspace_bytes(uint64_t n) {
+  const uint64_t ng = tiles_of(n ? n : 1, SCAN_TILE);
+  return sort_workspace_bytes(n) + align_up(n * 8, 256) + align_up(n * 4, 256) +
+         3 * align_up(ng * 4, 256) + 256;
+}
+
+static hipError_t exclusive_scan_u32(const uint32_t* in, uint32_t* out, uint64_t m,
+                                     uint32_t* partial, hipStream_t s) {
+  const uint32_t nt = tiles_of(m, SCAN_TILE);
+  if (nt <= 1) {
+    sd_scan_tiles<<<1, SCAN_THREADS, 0, s>>>(in, m, out, nullptr);
+    return hipGetLastError();
+  }
+  if (nt > (uint32_t)SCAN_TILE) return hipErrorInvalidValue;
+  sd_scan_reduce<<<nt, SCAN_THREADS, 0, s>>>(in, m, partial);
+  sd_scan_tiles<<<1, SCAN_THREADS, 0, s>>>(partial, nt, partial, nullptr);
+  sd_scan_tiles<<<nt, SCAN_THREADS, 0, s>>>(in, m, out, partial);
+  return hipGetLastError();
+}
+
+hipError_t radix_sort_pairs(const uint64_t* keys_in, const uint32_t* vals_in, uint64_t* keys_out,
+                            uint32_t* vals_out, uint64_t n, int begin_bit, int end_bit, void* ws,
+                            hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (n >= (1ull << 32) || begin_bit < 0 || end_bit > 64 || end_bit <= begin_bit)
+    return hipErrorInvalidValue;
+  const uint32_t nt = tiles_of(n, TILE);
+  const uint64_t m = (uint64_t)RADIX * nt;
+  char* p = (char*)ws;
+  uint64_t* kalt = (uint64_t*)p; p += align_up(n * 8, 256);
+  uint32_t* valt = (uint32_t*)p; p += align_up(n * 4, 256);
+  uint32_t* hist = (uint32_t*)p; p += align_up(m * 4, 256);
+  uint32_t* offs = (uint32_t*)p; p += align_up(m * 4, 256);
+  uint32_t* partial = (uint32_t*)p;
+  const int passes = (end_bit - begin_bit + 7) / 8;
+  const uint64_t* ksrc = keys_in;
+  const uint32_t* vsrc = vals_in;
+  for (int i = 0; i < passes; ++i) {
+    const uint32_t shift = (uint32_t)(begin_bit + 8 * i);
+    const int bits = (end_bit - (int)shift) < 8 ? (end_bit - (int)shift) : 8;
+    const uint32_t mask = (1u << bits) - 1u;
+    const bool to_out = ((passes - 1 - i) % 2) == 0;
+    uint64_t* kdst = to_out ? keys_out : kalt;
+    uint32_t* vdst = to_out ? vals_out : valt;
+    sd_radix_upsweep<<<nt, SORT_THREADS, 0, s>>>(ksrc, n, shift, mask, hist, nt);
+    hipError_t e = exclusive_scan_u32(hist, offs, m, partial, s);
+    if (e != hipSuccess) return e;
+    if (vsrc)
+      sd_radix_downsweep<<<nt, SORT_THREADS, 0, s>>>(ksrc, vsrc, kdst, vdst, n, shift, mask, offs, nt);
+    else
+      sd_radix_downsweep_iota<<<nt, SORT_THREADS, 0, s>>>(ksrc, kdst, vdst, n, shift, mask, offs, nt);
+    ksrc = kdst;
+    vsrc = vdst;
+  }
+  return hipGetLastError();
+}
+
+hipError_t group_sorted(const uint64_t* skeys, const uint32_t* svals, uint64_t n, uint32_t* rep,
+                        uint64_t* d_objects, void* ws, hipStream_t s) {
+  if (n == 0) return hipMemsetAsync(d_objects, 0, 8, s);
+  const uint32_t ng = tiles_of(n, SCAN_TILE);
+  char* p = (char*)ws;
+  uint32_t* last_head = (uint32_t*)p; p += align_up(ng * 4, 256);
+  uint32_t* heads = (uint32_t*)p; p += align_up(ng * 4, 256);
+  uint32_t* carry = (uint32_t*)p;
+  sd_group_tile_heads<<<ng, SCAN_THREADS, 0, s>>>(skeys, n, last_head, heads);
+  sd_group_carry<<<1, SCAN_THREADS, 0, s>>>(last_head, ng, carry, heads, d_objects);
+  sd_group_emit<<<ng, SCAN_THREADS, 0, s>>>(skeys, svals, n, carry, rep);
+  return hipGetLastError();
+}
+
+hipError_t group_keys(const uint64_t* keys, uint64_t n, uint32_t* rep, uint64_t* d_objects,
+                      void* ws, hipStream_t s) {
+  if (n == 0) return hipMemsetAsync(d_objects, 0, 8, s);
+  char* p = (char*)ws;
+  char* sort_ws = p; p += sort_workspace_bytes(n);
+  uint64_t* skeys = (uint64_t*)p; p += align_up(n * 8, 256);
+  uint32_t* svals = (uint32_t*)p; p += align_up(n * 4, 256);
+  hipError_t e = radix_sort_pairs(keys, nullptr, skeys, svals, n, 0, 64, sort_ws, s);
+  if (e != hipSuccess) return e;
+  return group_sorted(skeys, svals, n, rep, d_objects, p, s);
+}
+
+hipError_t group_chunked(const uint32_t* rep, uint64_t n, uint32_t chunk, uint32_t* rep_chunked,
+                         uint64_t* d_created, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (chunk == 0) return hipErrorInvalidValue;
+  sd_group_chunked<<<tiles_of(n, 256), 256, 0, s>>>(rep, n, chunk, rep_chunked,
+                                                   (unsigned long long*)d_created);
+  return hipGetLastError();
+}
+
+}  // namespace sdcas

@@ -1,0 +1,22 @@
+// sd_checksum.h — host launchers for the validator tree hash (checksum.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace sdcas {
+
+size_t checksum_workspace_bytes(uint64_t len);
+
+// BLAKE3 tree over data[0, len) whose first chunk has global index chunk0.
+// root == true: d_out8 = the 32-byte digest (this buffer is the whole input).
+// root == false: d_out8 = the subtree CV (len must then be a power-of-two multiple of
+// 1 KiB aligned at chunk0, i.e. a complete left subtree, for the result to be usable).
+hipError_t checksum_device(const uint8_t* data, uint64_t len, uint64_t chunk0, bool root,
+                           uint32_t* d_out8, void* ws, hipStream_t s);
+
+// Root digest over `cnt` subtree CVs (level-wise; ROOT on the final parent).
+hipError_t reduce_cvs_device(const uint32_t* d_cvs, uint64_t cnt, uint32_t* d_out8, void* ws,
+                             hipStream_t s);
+
+}  // namespace sdcas

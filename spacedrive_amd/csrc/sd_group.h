@@ -1,0 +1,33 @@
+// sd_group.h — host-side launchers for the sort / grouping kernels (group.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace sdcas {
+
+// Workspace bytes needed by radix_sort_pairs / group_keys for n keys.
+size_t sort_workspace_bytes(uint64_t n);
+size_t group_workspace_bytes(uint64_t n);
+
+// Stable LSD sort of (keys, vals) on bits [begin_bit, end_bit).  vals_in == nullptr means
+// vals = 0..n-1.  Results land in (keys_out, vals_out).  keys_in is not modified;
+// `ws` must hold sort_workspace_bytes(n).  n < 2^32.
+hipError_t radix_sort_pairs(const uint64_t* keys_in, const uint32_t* vals_in, uint64_t* keys_out,
+                            uint32_t* vals_out, uint64_t n, int begin_bit, int end_bit,
+                            void* ws, hipStream_t stream);
+
+// Canonical grouping: rep[i] = min{ j : keys[j] == keys[i] }; *d_objects = #distinct keys
+// (written on the device).  ws must hold group_workspace_bytes(n).
+hipError_t group_keys(const uint64_t* keys, uint64_t n, uint32_t* rep, uint64_t* d_objects,
+                      void* ws, hipStream_t stream);
+
+// Group already-sorted pairs (keys ascending, vals = original idx, stable).
+hipError_t group_sorted(const uint64_t* skeys, const uint32_t* svals, uint64_t n, uint32_t* rep,
+                        uint64_t* d_objects, void* ws, hipStream_t stream);
+
+// chunk-of-`chunk` emulation; *d_created accumulates (zero it first).
+hipError_t group_chunked(const uint32_t* rep, uint64_t n, uint32_t chunk, uint32_t* rep_chunked,
+                         uint64_t* d_created, hipStream_t stream);
+
+}  // namespace sdcas

@@ -1,0 +1,633 @@
+// sd_hip_cas.cpp — the C ABI (include/sd_hip_cas.h) over the gfx950 kernels.
+//
+// Host runtime for the batched drop-in of generate_cas_id (core/src/object/cas.rs:23-62),
+// its batch caller identifier_job_step (core/src/object/file_identifier/mod.rs:98-350)
+// and file_checksum (core/src/object/validation/hash.rs:11-25):
+//   - a context per (thread, device): compute stream + copy (side) stream, a growable
+//     device workspace and pinned staging, last-error string;
+//   - host batches are gathered into pinned staging (pread at the cas.rs:27-58 offsets
+//     for the path variant), copied with hipMemcpyAsync on the side stream, and hashed
+//     on the compute stream after an event hand-off;
+//   - no CPU hashing anywhere: every digest comes from the HIP kernels.
+#include <errno.h>
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/sd_hip_cas.h"
+#include "sd_checksum.h"
+#include "sd_group.h"
+#include "sd_kernels.h"
+#include "sd_synth.h"
+
+using namespace sdcas;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+struct sd_cas_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;  // compute
+  hipStream_t copy = nullptr;    // H2D side stream
+  hipEvent_t h2d_done = nullptr;
+  DevBuf ws;       // kernel workspace
+  DevBuf staging;  // device copy of a host batch
+  DevBuf small;    // keys / sizes / offsets of a host batch
+  void* pinned = nullptr;
+  size_t pinned_bytes = 0;
+  uint64_t* d_scalar = nullptr;  // 4 x u64 scratch for counters
+  std::string err;
+};
+
+static int fail(sd_cas_ctx* c, int code, const char* fmt, ...) {
+  if (c) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    c->err = buf;
+  }
+  return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                 \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      return fail((ctx), SD_CAS_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                  __FILE__, __LINE__);                                                     \
+  } while (0)
+
+static inline hipStream_t pick(sd_cas_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
+static inline size_t up16(size_t x) { return (x + 15) & ~(size_t)15; }
+static inline size_t up256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static int ensure(sd_cas_ctx* c, DevBuf& b, size_t bytes) {
+  if (bytes <= b.bytes) return SD_CAS_OK;
+  if (b.p) {
+    HIP_TRY(c, hipDeviceSynchronize());
+    HIP_TRY(c, hipFree(b.p));
+    b.p = nullptr;
+    b.bytes = 0;
+  }
+  size_t want = std::max(bytes, (size_t)1 << 20);
+  if (hipMalloc(&b.p, want) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(c, SD_CAS_ENOMEM, "hipMalloc(%zu) failed", want);
+  }
+  b.bytes = want;
+  return SD_CAS_OK;
+}
+
+static int ensure_pinned(sd_cas_ctx* c, size_t bytes) {
+  if (bytes <= c->pinned_bytes) return SD_CAS_OK;
+  if (c->pinned) {
+    HIP_TRY(c, hipDeviceSynchronize());
+    HIP_TRY(c, hipHostFree(c->pinned));
+    c->pinned = nullptr;
+    c->pinned_bytes = 0;
+  }
+  size_t want = std::max(bytes, (size_t)1 << 22);
+  if (hipHostMalloc(&c->pinned, want, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(c, SD_CAS_ENOMEM, "hipHostMalloc(%zu) failed", want);
+  }
+  c->pinned_bytes = want;
+  return SD_CAS_OK;
+}
+
+extern "C" {
+
+int sd_cas_abi_version(void) { return SD_CAS_ABI_VERSION; }
+
+int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
+  if (!out) return SD_CAS_EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+    (void)hipGetLastError();
+    return SD_CAS_ENODEV;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return SD_CAS_ENODEV;
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return SD_CAS_ENODEV;  // gfx950 only
+  sd_cas_ctx* c = new sd_cas_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->h2d_done, hipEventDisableTiming) != hipSuccess ||
+      hipMalloc((void**)&c->d_scalar, 64) != hipSuccess) {
+    sd_cas_ctx_destroy(c);
+    return SD_CAS_EHIP;
+  }
+  *out = c;
+  return SD_CAS_OK;
+}
+
+void sd_cas_ctx_destroy(sd_cas_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipDeviceSynchronize();
+  if (c->ws.p) (void)hipFree(c->ws.p);
+  if (c->staging.p) (void)hipFree(c->staging.p);
+  if (c->small.p) (void)hipFree(c->small.p);
+  if (c->d_scalar) (void)hipFree(c->d_scalar);
+  if (c->pinned) (void)hipHostFree(c->pinned);
+  if (c->h2d_done) (void)hipEventDestroy(c->h2d_done);
+  if (c->copy) (void)hipStreamDestroy(c->copy);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* sd_cas_last_error(const sd_cas_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+void* sd_cas_ctx_stream(sd_cas_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int sd_cas_synchronize(sd_cas_ctx* c) {
+  if (!c) return SD_CAS_EINVAL;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return SD_CAS_OK;
+}
+
+int sd_cas_alloc_pinned(sd_cas_ctx* c, size_t bytes, void** out) {
+  if (!c || !out) return SD_CAS_EINVAL;
+  if (hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(c, SD_CAS_ENOMEM, "hipHostMalloc(%zu) failed", bytes);
+  }
+  return SD_CAS_OK;
+}
+
+int sd_cas_free_pinned(sd_cas_ctx* c, void* p) {
+  if (!c) return SD_CAS_EINVAL;
+  HIP_TRY(c, hipHostFree(p));
+  return SD_CAS_OK;
+}
+
+void sd_cas_key_to_hex(uint64_t key, char out[17]) {
+  static const char* hx = "0123456789abcdef";
+  for (int i = 0; i < 16; i++) out[i] = hx[(key >> (60 - 4 * i)) & 15];
+  out[16] = 0;
+}
+
+// ---- device-resident cas ----------------------------------------------------------
+
+int sd_cas_hash_sampled_dev(sd_cas_ctx* c, const void* d_content, uint64_t stride,
+                            const uint64_t* d_sizes, size_t n, uint64_t* d_keys, void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (n == 0) return SD_CAS_OK;
+  if (!d_content || !d_sizes || !d_keys || stride < SAMPLED_CONTENT_LEN || (stride & 15) ||
+      ((uintptr_t)d_content & 15))
+    return fail(c, SD_CAS_EINVAL, "hash_sampled: bad content/stride (stride=%llu)",
+                (unsigned long long)stride);
+  HIP_TRY(c, hash_sampled((const uint8_t*)d_content, stride, d_sizes, n, d_keys, pick(c, stream)));
+  return SD_CAS_OK;
+}
+
+int sd_cas_hash_packed_dev(sd_cas_ctx* c, const void* d_arena, const uint64_t* d_offs,
+                           const uint32_t* d_lens, const uint64_t* d_sizes, size_t n,
+                           uint64_t* d_keys, void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (n == 0) return SD_CAS_OK;
+  if (!d_arena || !d_offs || !d_lens || !d_sizes || !d_keys || ((uintptr_t)d_arena & 15) ||
+      n >= (1ull << 32))
+    return fail(c, SD_CAS_EINVAL, "hash_packed: bad arguments");
+  hipStream_t s = pick(c, stream);
+  // workspace: length keys | sorted keys | order | sort workspace
+  const size_t kb = up256(n * 8), ob = up256(n * 4);
+  int rc = ensure(c, c->ws, 2 * kb + ob + sort_workspace_bytes(n));
+  if (rc) return rc;
+  char* p = (char*)c->ws.p;
+  uint64_t* lkeys = (uint64_t*)p;
+  uint64_t* skeys = (uint64_t*)(p + kb);
+  uint32_t* order = (uint32_t*)(p + 2 * kb);
+  void* sws = p + 2 * kb + ob;
+  HIP_TRY(c, length_keys(d_lens, n, lkeys, s));
+  HIP_TRY(c, radix_sort_pairs(lkeys, nullptr, skeys, order, n, 0, 16, sws, s));
+  HIP_TRY(c, hash_packed((const uint8_t*)d_arena, d_offs, d_lens, d_sizes, order, n, d_keys, s));
+  return SD_CAS_OK;
+}
+
+// ---- grouping -----------------------------------------------------------------------
+
+int sd_cas_sort_pairs_dev(sd_cas_ctx* c, const uint64_t* d_keys_in, const uint32_t* d_vals_in,
+                          size_t n, uint64_t* d_keys_out, uint32_t* d_vals_out, int begin_bit,
+                          int end_bit, void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (n == 0) return SD_CAS_OK;
+  if (!d_keys_in || !d_keys_out || !d_vals_out || n >= (1ull << 32) || begin_bit < 0 ||
+      end_bit > 64 || begin_bit >= end_bit)
+    return fail(c, SD_CAS_EINVAL, "sort_pairs: bad arguments");
+  int rc = ensure(c, c->ws, sort_workspace_bytes(n));
+  if (rc) return rc;
+  HIP_TRY(c, radix_sort_pairs(d_keys_in, d_vals_in, d_keys_out, d_vals_out, n, begin_bit, end_bit,
+                              c->ws.p, pick(c, stream)));
+  return SD_CAS_OK;
+}
+
+int sd_cas_group_dev(sd_cas_ctx* c, const uint64_t* d_keys, size_t n, uint32_t* d_rep,
+                     uint64_t* out_objects, void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (n >= (1ull << 32) || (n && (!d_keys || !d_rep)))
+    return fail(c, SD_CAS_EINVAL, "group: bad arguments");
+  hipStream_t s = pick(c, stream);
+  int rc = ensure(c, c->ws, group_workspace_bytes(n));
+  if (rc) return rc;
+  HIP_TRY(c, group_keys(d_keys, n, d_rep, c->d_scalar, c->ws.p, s));
+  if (out_objects) {
+    HIP_TRY(c, hipMemcpyAsync(out_objects, c->d_scalar, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+  }
+  return SD_CAS_OK;
+}
+
+int sd_cas_group_sorted_dev(sd_cas_ctx* c, const uint64_t* d_sorted_keys,
+                            const uint32_t* d_sorted_vals, size_t n, uint32_t* d_rep,
+                            uint64_t* out_objects, void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (n >= (1ull << 32) || (n && (!d_sorted_keys || !d_sorted_vals || !d_rep)))
+    return fail(c, SD_CAS_EINVAL, "group_sorted: bad arguments");
+  hipStream_t s = pick(c, stream);
+  int rc = ensure(c, c->ws, group_workspace_bytes(n));
+  if (rc) return rc;
+  HIP_TRY(c, group_sorted(d_sorted_keys, d_sorted_vals, n, d_rep, c->d_scalar, c->ws.p, s));
+  if (out_objects) {
+    HIP_TRY(c, hipMemcpyAsync(out_objects, c->d_scalar, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+  }
+  return SD_CAS_OK;
+}
+
+int sd_cas_group_chunked_dev(sd_cas_ctx* c, const uint32_t* d_rep, size_t n, uint32_t chunk,
+                             uint32_t* d_rep_chunked, uint64_t* out_created,
+                             uint64_t* out_linked, void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (chunk == 0 || n >= (1ull << 32) || (n && (!d_rep || !d_rep_chunked)))
+    return fail(c, SD_CAS_EINVAL, "group_chunked: bad arguments");
+  hipStream_t s = pick(c, stream);
+  uint64_t* d_created = c->d_scalar + 1;
+  HIP_TRY(c, hipMemsetAsync(d_created, 0, 8, s));
+  HIP_TRY(c, group_chunked(d_rep, n, chunk, d_rep_chunked, d_created, s));
+  uint64_t created = 0;
+  HIP_TRY(c, hipMemcpyAsync(&created, d_created, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  if (out_created) *out_created = created;
+  if (out_linked) *out_linked = n - created;
+  return SD_CAS_OK;
+}
+
+// ---- host-buffer cas (blocking) -----------------------------------------------------
+
+// Stage layout in pinned memory and on the device:
+//   [sampled contents, 57,344 B each, contiguous] [packed contents, 16-B aligned]
+//   [sizes_s u64][sizes_p u64][offs_p u64][lens_p u32]   (small metadata)
+struct Plan {
+  std::vector<size_t> sampled, packed;  // file indices
+  std::vector<uint64_t> poff;           // packed offsets (relative to packed base)
+  size_t sampled_bytes = 0, packed_bytes = 0;
+};
+
+static int plan_batch(sd_cas_ctx* c, const uint64_t* buf_lens, const uint64_t* sizes, size_t n,
+                      Plan& pl) {
+  for (size_t i = 0; i < n; i++) {
+    if (sizes[i] > MINIMUM_FILE_SIZE) {
+      if (buf_lens[i] != SAMPLED_CONTENT_LEN)
+        return fail(c, SD_CAS_EINVAL, "file %zu: size %llu > %llu needs %u sampled bytes, got %llu",
+                    i, (unsigned long long)sizes[i], (unsigned long long)MINIMUM_FILE_SIZE,
+                    SAMPLED_CONTENT_LEN, (unsigned long long)buf_lens[i]);
+      pl.sampled.push_back(i);
+    } else {
+      if (buf_lens[i] > MAX_PACKED_CONTENT_LEN)
+        return fail(c, SD_CAS_EINVAL, "file %zu: whole-file content %llu exceeds %u", i,
+                    (unsigned long long)buf_lens[i], MAX_PACKED_CONTENT_LEN);
+      pl.packed.push_back(i);
+      pl.poff.push_back(pl.packed_bytes);
+      pl.packed_bytes += up16(buf_lens[i]);
+    }
+  }
+  pl.sampled_bytes = pl.sampled.size() * (size_t)SAMPLED_CONTENT_LEN;
+  pl.packed_bytes += 16;  // tail pad
+  return SD_CAS_OK;
+}
+
+// Copies staged pinned bytes to the device, hashes both sub-batches, returns keys.
+static int run_staged(sd_cas_ctx* c, const Plan& pl, const uint64_t* sizes, size_t n,
+                      uint64_t* out_keys) {
+  const size_t ns = pl.sampled.size(), np = pl.packed.size();
+  const size_t content_bytes = pl.sampled_bytes + up256(pl.packed_bytes);
+  const size_t meta_bytes = up256((ns + np) * 8) + up256(np * 8) + up256(np * 4) + up256(n * 8);
+  int rc = ensure(c, c->staging, content_bytes + meta_bytes);
+  if (rc) return rc;
+  char* pin = (char*)c->pinned;
+  uint64_t* h_sizes = (uint64_t*)(pin + content_bytes);
+  uint64_t* h_poffs = (uint64_t*)((char*)h_sizes + up256((ns + np) * 8));
+  uint32_t* h_plens = (uint32_t*)((char*)h_poffs + up256(np * 8));
+  for (size_t k = 0; k < ns; k++) h_sizes[k] = sizes[pl.sampled[k]];
+  for (size_t k = 0; k < np; k++) h_sizes[ns + k] = sizes[pl.packed[k]];
+  for (size_t k = 0; k < np; k++) h_poffs[k] = pl.poff[k];
+  // lens were validated <= MAX_PACKED; recover them from the offsets' caller data
+  char* dev = (char*)c->staging.p;
+  uint64_t* d_sizes = (uint64_t*)(dev + content_bytes);
+  uint64_t* d_poffs = (uint64_t*)((char*)d_sizes + up256((ns + np) * 8));
+  uint32_t* d_plens = (uint32_t*)((char*)d_poffs + up256(np * 8));
+  uint64_t* d_keys = (uint64_t*)((char*)d_plens + up256(np * 4));
+  (void)h_plens;
+  HIP_TRY(c, hipMemcpyAsync(dev, pin, content_bytes + meta_bytes - up256(n * 8),
+                            hipMemcpyHostToDevice, c->copy));
+  HIP_TRY(c, hipEventRecord(c->h2d_done, c->copy));
+  HIP_TRY(c, hipStreamWaitEvent(c->stream, c->h2d_done, 0));
+  if (ns) {
+    rc = sd_cas_hash_sampled_dev(c, dev, SAMPLED_CONTENT_LEN, d_sizes, ns, d_keys, c->stream);
+    if (rc) return rc;
+  }
+  if (np) {
+    rc = sd_cas_hash_packed_dev(c, dev + pl.sampled_bytes, d_poffs, d_plens, d_sizes + ns, np,
+                                d_keys + ns, c->stream);
+    if (rc) return rc;
+  }
+  uint64_t* h_keys = (uint64_t*)pin;  // reuse staging for the result
+  HIP_TRY(c, hipMemcpyAsync(h_keys, d_keys, (ns + np) * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  for (size_t k = 0; k < ns; k++) out_keys[pl.sampled[k]] = h_keys[k];
+  for (size_t k = 0; k < np; k++) out_keys[pl.packed[k]] = h_keys[ns + k];
+  return SD_CAS_OK;
+}
+
+static size_t staged_pinned_bytes(const Plan& pl, size_t n) {
+  const size_t ns = pl.sampled.size(), np = pl.packed.size();
+  return pl.sampled_bytes + up256(pl.packed_bytes) + up256((ns + np) * 8) + up256(np * 8) +
+         up256(np * 4) + up256(n * 8);
+}
+
+int sd_cas_generate_cas_ids(sd_cas_ctx* c, const uint8_t* const* bufs, const uint64_t* buf_lens,
+                            const uint64_t* sizes, size_t n, uint64_t* out_keys) {
+  if (!c) return SD_CAS_EINVAL;
+  if (n == 0) return SD_CAS_OK;
+  if (!bufs || !buf_lens || !sizes || !out_keys || n >= (1ull << 32))
+    return fail(c, SD_CAS_EINVAL, "generate_cas_ids: null argument");
+  HIP_TRY(c, hipSetDevice(c->device));
+  Plan pl;
+  int rc = plan_batch(c, buf_lens, sizes, n, pl);
+  if (rc) return rc;
+  rc = ensure_pinned(c, staged_pinned_bytes(pl, n));
+  if (rc) return rc;
+  char* pin = (char*)c->pinned;
+  for (size_t k = 0; k < pl.sampled.size(); k++)
+    memcpy(pin + k * (size_t)SAMPLED_CONTENT_LEN, bufs[pl.sampled[k]], SAMPLED_CONTENT_LEN);
+  char* pbase = pin + pl.sampled_bytes;
+  const size_t ns = pl.sampled.size(), np = pl.packed.size();
+  const size_t content_bytes = pl.sampled_bytes + up256(pl.packed_bytes);
+  uint32_t* h_plens = (uint32_t*)(pin + content_bytes + up256((ns + np) * 8) + up256(np * 8));
+  for (size_t k = 0; k < np; k++) {
+    const size_t i = pl.packed[k];
+    if (buf_lens[i]) memcpy(pbase + pl.poff[k], bufs[i], buf_lens[i]);
+    h_plens[k] = (uint32_t)buf_lens[i];
+  }
+  return run_staged(c, pl, sizes, n, out_keys);
+}
+
+int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
+                                       const uint64_t* sizes, size_t n, uint64_t* out_keys,
+                                       int32_t* status) {
+  if (!c) return SD_CAS_EINVAL;
+  if (n == 0) return SD_CAS_OK;
+  if (!paths || !sizes || !out_keys || !status || n >= (1ull << 32))
+    return fail(c, SD_CAS_EINVAL, "generate_cas_ids_from_paths: null argument");
+  HIP_TRY(c, hipSetDevice(c->device));
+  // content length per file: sampled 57,344; whole file = actual length (cas.rs:29 reads
+  // the file, not `size` bytes) -> stat it.
+  std::vector<uint64_t> lens(n, 0);
+  for (size_t i = 0; i < n; i++) {
+    status[i] = 0;
+    out_keys[i] = 0;
+    if (sizes[i] > MINIMUM_FILE_SIZE) {
+      lens[i] = SAMPLED_CONTENT_LEN;
+    } else {
+      struct stat st;
+      if (stat(paths[i], &st) != 0) { status[i] = -errno; continue; }
+      if ((uint64_t)st.st_size > MAX_PACKED_CONTENT_LEN) { status[i] = -EFBIG; continue; }
+      lens[i] = (uint64_t)st.st_size;
+    }
+  }
+  Plan pl;
+  int rc = plan_batch(c, lens.data(), sizes, n, pl);
+  if (rc) return rc;
+  rc = ensure_pinned(c, staged_pinned_bytes(pl, n));
+  if (rc) return rc;
+  char* pin = (char*)c->pinned;
+  const size_t ns = pl.sampled.size(), np = pl.packed.size();
+  const size_t content_bytes = pl.sampled_bytes + up256(pl.packed_bytes);
+  uint32_t* h_plens = (uint32_t*)(pin + content_bytes + up256((ns + np) * 8) + up256(np * 8));
+  for (size_t k = 0; k < np; k++) h_plens[k] = (uint32_t)lens[pl.packed[k]];
+  // gather: pread straight into pinned staging, files spread over a few threads
+  struct Task { size_t i; char* dst; };
+  std::vector<Task> tasks;
+  tasks.reserve(ns + np);
+  for (size_t k = 0; k < ns; k++) tasks.push_back({pl.sampled[k], pin + k * (size_t)SAMPLED_CONTENT_LEN});
+  for (size_t k = 0; k < np; k++) tasks.push_back({pl.packed[k], pin + pl.sampled_bytes + pl.poff[k]});
+  std::atomic<size_t> next{0};
+  auto worker = [&]() {
+    for (;;) {
+      const size_t t = next.fetch_add(1);
+      if (t >= tasks.size()) return;
+      const size_t i = tasks[t].i;
+      if (status[i]) continue;
+      int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
+      if (fd < 0) { status[i] = -errno; continue; }
+      // cas.rs:35-58 offsets: header at 0, sample k at 8192 + k*jump, footer at size-8192
+      uint64_t offs[6], lns[6];
+      int parts;
+      if (sizes[i] > MINIMUM_FILE_SIZE) {
+        const uint64_t jump = (sizes[i] - 2 * HEADER_OR_FOOTER_SIZE) / SAMPLE_COUNT;
+        offs[0] = 0; lns[0] = HEADER_OR_FOOTER_SIZE;
+        for (int k = 0; k < 4; k++) { offs[1 + k] = HEADER_OR_FOOTER_SIZE + k * jump; lns[1 + k] = SAMPLE_SIZE; }
+        offs[5] = sizes[i] - HEADER_OR_FOOTER_SIZE; lns[5] = HEADER_OR_FOOTER_SIZE;
+        parts = 6;
+      } else {
+        offs[0] = 0; lns[0] = lens[i];
+        parts = 1;
+      }
+      char* dst = tasks[t].dst;
+      for (int k = 0; k < parts && !status[i]; k++) {
+        size_t got = 0;
+        while (got < lns[k]) {
+          ssize_t r = pread(fd, dst + got, lns[k] - got, (off_t)(offs[k] + got));
+          if (r < 0) { if (errno == EINTR) continue; status[i] = -errno; break; }
+          if (r == 0) { status[i] = -EIO; break; }  // UnexpectedEof
+          got += (size_t)r;
+        }
+        dst += lns[k];
+      }
+      close(fd);
+    }
+  };
+  const unsigned nth = std::max(1u, std::min(16u, (unsigned)((n + 63) / 64)));
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < nth; t++) th.emplace_back(worker);
+  worker();
+  for (auto& t : th) t.join();
+  rc = run_staged(c, pl, sizes, n, out_keys);
+  if (rc) return rc;
+  for (size_t i = 0; i < n; i++)
+    if (status[i]) out_keys[i] = 0;
+  return SD_CAS_OK;
+}
+
+// ---- file_checksum --------------------------------------------------------------------
+
+int sd_cas_checksum_dev(sd_cas_ctx* c, const void* d_data, uint64_t len, uint8_t out[32],
+                        void* stream) {
+  if (!c || !out) return SD_CAS_EINVAL;
+  if ((len && !d_data) || ((uintptr_t)d_data & 15))
+    return fail(c, SD_CAS_EINVAL, "checksum: bad data pointer");
+  hipStream_t s = pick(c, stream);
+  int rc = ensure(c, c->ws, checksum_workspace_bytes(len));
+  if (rc) return rc;
+  uint32_t* d_out = (uint32_t*)c->d_scalar;
+  HIP_TRY(c, checksum_device((const uint8_t*)d_data, len, 0, true, d_out, c->ws.p, s));
+  HIP_TRY(c, hipMemcpyAsync(out, d_out, 32, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  return SD_CAS_OK;
+}
+
+int sd_cas_file_checksum(sd_cas_ctx* c, const char* path, char out_hex[65], int* err_no) {
+  if (!c || !path || !out_hex) return SD_CAS_EINVAL;
+  if (err_no) *err_no = 0;
+  HIP_TRY(c, hipSetDevice(c->device));
+  int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) {
+    if (err_no) *err_no = errno;
+    return fail(c, SD_CAS_EIO, "open(%s): %s", path, strerror(errno));
+  }
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    if (err_no) *err_no = errno;
+    close(fd);
+    return fail(c, SD_CAS_EIO, "fstat(%s): %s", path, strerror(errno));
+  }
+  const uint64_t len = (uint64_t)st.st_size;
+  const uint64_t SEG = 64ull << 20;  // 65,536 chunks: a complete left subtree
+  const uint64_t nseg = len <= SEG ? 1 : (len + SEG - 1) / SEG;
+  const size_t seg_bytes = (size_t)std::min<uint64_t>(len ? len : 1, SEG);
+  // two pinned + two device segment buffers (double-buffered: read k+1 while hashing k)
+  int rc = ensure_pinned(c, 2 * up256(seg_bytes + 16));
+  if (rc) { close(fd); return rc; }
+  const size_t cvs_bytes = up256(nseg * 32);
+  rc = ensure(c, c->staging, 2 * up256(seg_bytes + 16) + cvs_bytes);
+  if (rc) { close(fd); return rc; }
+  // every kernel runs on c->stream, so segments and the final reduce share one workspace
+  rc = ensure(c, c->ws, std::max(checksum_workspace_bytes(std::min<uint64_t>(len, SEG)),
+                                 checksum_workspace_bytes(nseg * 1024)));
+  if (rc) { close(fd); return rc; }
+  char* pin[2] = {(char*)c->pinned, (char*)c->pinned + up256(seg_bytes + 16)};
+  char* dev[2] = {(char*)c->staging.p, (char*)c->staging.p + up256(seg_bytes + 16)};
+  uint32_t* d_cvs = (uint32_t*)((char*)c->staging.p + 2 * up256(seg_bytes + 16));
+  hipEvent_t done[2];
+  HIP_TRY(c, hipEventCreateWithFlags(&done[0], hipEventDisableTiming));
+  HIP_TRY(c, hipEventCreateWithFlags(&done[1], hipEventDisableTiming));
+  int result = SD_CAS_OK;
+  for (uint64_t sgi = 0; sgi < nseg && result == SD_CAS_OK; sgi++) {
+    const int b = (int)(sgi & 1);
+    const uint64_t off = sgi * SEG;
+    const uint64_t want = std::min<uint64_t>(SEG, len - off);
+    if (sgi >= 2) (void)hipEventSynchronize(done[b]);  // pinned[b] free again
+    uint64_t got = 0;
+    while (got < want) {  // hash.rs:16-20 reads until a short read; regular files: EOF
+      ssize_t r = pread(fd, pin[b] + got, want - got, (off_t)(off + got));
+      if (r < 0) { if (errno == EINTR) continue; if (err_no) *err_no = errno; result = fail(c, SD_CAS_EIO, "read(%s): %s", path, strerror(errno)); break; }
+      if (r == 0) break;
+      got += (uint64_t)r;
+    }
+    if (result) break;
+    if (got != want) { if (err_no) *err_no = EIO; result = fail(c, SD_CAS_EIO, "short read on %s", path); break; }
+    hipError_t e = hipMemcpyAsync(dev[b], pin[b], up16(want), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess)
+      e = checksum_device((const uint8_t*)dev[b], want, off >> 10, nseg == 1, d_cvs + 8 * sgi,
+                          c->ws.p, c->stream);
+    if (e == hipSuccess) e = hipEventRecord(done[b], c->stream);
+    if (e != hipSuccess) result = fail(c, SD_CAS_EHIP, "checksum segment: %s", hipGetErrorString(e));
+  }
+  close(fd);
+  uint8_t digest[32];
+  if (result == SD_CAS_OK) {
+    uint32_t* d_out = (uint32_t*)c->d_scalar;
+    hipError_t e = hipSuccess;
+    if (nseg == 1) e = hipMemcpyAsync(d_out, d_cvs, 32, hipMemcpyDeviceToDevice, c->stream);
+    else e = reduce_cvs_device(d_cvs, nseg, d_out, c->ws.p, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(digest, d_out, 32, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) result = fail(c, SD_CAS_EHIP, "checksum reduce: %s", hipGetErrorString(e));
+  }
+  (void)hipStreamSynchronize(c->stream);
+  (void)hipEventDestroy(done[0]);
+  (void)hipEventDestroy(done[1]);
+  if (result) return result;
+  static const char* hx = "0123456789abcdef";
+  for (int i = 0; i < 32; i++) { out_hex[2 * i] = hx[digest[i] >> 4]; out_hex[2 * i + 1] = hx[digest[i] & 15]; }
+  out_hex[64] = 0;
+  return SD_CAS_OK;
+}
+
+// ---- synthetic inputs ----------------------------------------------------------------
+
+int sd_cas_synth_sampled_dev(sd_cas_ctx* c, uint64_t seed, uint64_t file0, size_t n,
+                             uint32_t dup_permille, void* d_content, uint64_t stride,
+                             uint64_t* d_sizes, void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (n == 0) return SD_CAS_OK;
+  if (!d_content || !d_sizes || stride < SAMPLED_CONTENT_LEN || (stride & 15) || dup_permille > 1000)
+    return fail(c, SD_CAS_EINVAL, "synth_sampled: bad arguments");
+  HIP_TRY(c, synth_sampled(seed, file0, n, dup_permille, (uint8_t*)d_content, stride, d_sizes,
+                           pick(c, stream)));
+  return SD_CAS_OK;
+}
+
+int sd_cas_synth_small_dev(sd_cas_ctx* c, uint64_t seed, uint64_t file0, size_t n,
+                           uint32_t dup_permille, uint64_t* d_sizes, uint32_t* d_lens,
+                           uint64_t* d_offs, void* d_arena, uint64_t* out_arena_bytes,
+                           void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (!d_sizes || !d_lens || !d_offs || dup_permille > 1000)
+    return fail(c, SD_CAS_EINVAL, "synth_small: bad arguments");
+  hipStream_t s = pick(c, stream);
+  if (n == 0) { if (out_arena_bytes) *out_arena_bytes = 16; return SD_CAS_OK; }
+  HIP_TRY(c, synth_small_sizes(seed, file0, n, dup_permille, d_sizes, d_lens, s));
+  // offsets: 16-B aligned packing, computed on the host from the lens (small: 4 B/file)
+  std::vector<uint32_t> lens(n);
+  HIP_TRY(c, hipMemcpyAsync(lens.data(), d_lens, n * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  std::vector<uint64_t> offs(n);
+  uint64_t o = 0;
+  for (size_t i = 0; i < n; i++) { offs[i] = o; o += up16(lens[i]); }
+  o += 16;
+  if (out_arena_bytes) *out_arena_bytes = o;
+  HIP_TRY(c, hipMemcpyAsync(d_offs, offs.data(), n * 8, hipMemcpyHostToDevice, s));
+  if (d_arena) HIP_TRY(c, synth_small_content(seed, file0, n, dup_permille, d_offs, d_lens,
+                                              (uint8_t*)d_arena, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  return SD_CAS_OK;
+}
+
+int sd_cas_synth_roots_dev(sd_cas_ctx* c, uint64_t seed, uint64_t file0, size_t n,
+                           uint32_t dup_permille, uint64_t* d_roots, void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (n && !d_roots) return fail(c, SD_CAS_EINVAL, "synth_roots: null");
+  HIP_TRY(c, synth_roots(seed, file0, n, dup_permille, d_roots, pick(c, stream)));
+  return SD_CAS_OK;
+}
+
+}  // extern "C"

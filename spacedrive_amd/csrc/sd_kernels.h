@@ -1,0 +1,32 @@
+// sd_kernels.h — internal constants shared by the HIP kernels and the C-ABI layer.
+#pragma once
+#include <stdint.h>
+
+namespace sdcas {
+
+// core/src/object/cas.rs:10-15
+constexpr uint64_t SAMPLE_COUNT = 4;
+constexpr uint64_t SAMPLE_SIZE = 1024 * 10;
+constexpr uint64_t HEADER_OR_FOOTER_SIZE = 1024 * 8;
+constexpr uint64_t MINIMUM_FILE_SIZE = 1024 * 100;
+constexpr uint32_t SAMPLED_CONTENT_LEN =
+    (uint32_t)(2 * HEADER_OR_FOOTER_SIZE + SAMPLE_COUNT * SAMPLE_SIZE);  // 57,344
+// cas.rs:18 const_assert!((HEADER_OR_FOOTER_SIZE * 2 + SAMPLE_COUNT * SAMPLE_SIZE) < MINIMUM_FILE_SIZE)
+static_assert(2 * HEADER_OR_FOOTER_SIZE + SAMPLE_COUNT * SAMPLE_SIZE < MINIMUM_FILE_SIZE, "cas.rs:18");
+// cas.rs:21 const_assert!(SAMPLE_SIZE > HEADER_OR_FOOTER_SIZE)
+static_assert(SAMPLE_SIZE > HEADER_OR_FOOTER_SIZE, "cas.rs:21");
+
+// The packed (whole-file) kernel keeps a 7-deep CV stack: messages of <= 128 chunks.
+constexpr uint32_t MAX_PACKED_CONTENT_LEN = 128u * 1024u - 8u;
+
+}  // namespace sdcas
+
+#include <hip/hip_runtime.h>
+namespace sdcas {
+hipError_t hash_sampled(const uint8_t* content, uint64_t stride, const uint64_t* sizes,
+                        uint64_t n, uint64_t* keys, hipStream_t s);
+hipError_t hash_packed(const uint8_t* arena, const uint64_t* offs, const uint32_t* lens,
+                       const uint64_t* sizes, const uint32_t* order, uint64_t n, uint64_t* keys,
+                       hipStream_t s);
+hipError_t length_keys(const uint32_t* lens, uint64_t n, uint64_t* out, hipStream_t s);
+}  // namespace sdcas

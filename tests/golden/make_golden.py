@@ -1,0 +1,174 @@
+"""Generates tests/golden/golden.json — the committed golden vectors for the cas path.
+
+Run:  python tests/golden/make_golden.py      (CPU only; uses the oracle, not the product)
+
+Provenance of each section (see DESIGN.md "Parity"):
+  * "derive_key_kat"   — copied from the reference's own test: DERIVE_B3_EXPECTED,
+    crates/crypto/src/keys/hashing.rs:210-213 (test :323-328), material = KEY (0x23 x 32,
+    :132-136) || SALT (0xFF x 16, :138-141), context :121.  Externally pinned.
+  * "blake3_public"    — BLAKE3("") / BLAKE3("abc"), public values quoted in SURVEY.md §8c.
+    Externally pinned.
+  * "blake3_lengths"   — BLAKE3 of the i % 251 byte pattern at lengths straddling chunk and
+    tree boundaries, produced by the C oracle and REQUIRED to agree with its recursive and
+    level-wise formulations and with the independent pure-Python restatement.
+  * "cas"              — cas_ids of synthetic files (content = splitmix64 stream keyed by
+    (seed, file), shared with the device generator), sizes per SURVEY.md §8c, including the
+    100 KiB threshold (cas.rs:27, inclusive) and a > 4 GiB file (virtual image: only the
+    bytes at the cas.rs:35-58 offsets are generated).  Cross-checked C vs Python oracle.
+  * "grouping"         — hand-built duplicate layouts with canonical reps and the literal
+    replay of identifier_job_step (mod.rs:98-350) in 100-row chunks.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+from oracle.pyoracle import (  # noqa: E402
+    MINIMUM_FILE_SIZE,
+    Oracle,
+    np_file_key,
+    np_mix64,
+    py_blake3,
+    py_cas_id,
+    py_derive_key,
+    py_sample_plan,
+)
+
+_G = np.uint64(0x9E3779B97F4A7C15)
+
+
+def virtual_file_bytes(seed: int, file: int, off: int, length: int) -> bytes:
+    """Bytes [off, off+length) of the synthetic file image (same stream as np_content)."""
+    w0, w1 = off // 8, (off + length + 7) // 8
+    key = np_file_key(seed, file)
+    with np.errstate(over="ignore"):
+        w = np_mix64(key + (np.arange(w0 + 1, w1 + 1, dtype=np.uint64) * _G))
+    b = w.astype("<u8").tobytes()
+    return b[off - 8 * w0: off - 8 * w0 + length]
+
+
+def gather_virtual(seed: int, file: int, size: int) -> bytes:
+    if size <= MINIMUM_FILE_SIZE:
+        return virtual_file_bytes(seed, file, 0, size)
+    return b"".join(virtual_file_bytes(seed, file, o, ln) for o, ln in py_sample_plan(size))
+
+
+def replay_identifier(keys: list[int], chunk: int = 100):
+    """Literal replay of identifier_job_step over a fresh library (mod.rs:98-350):
+    Objects table in creation order; HashMap iteration := ascending idx."""
+    objects = []          # list of (object_id, set of cas)
+    cas_to_objs = {}      # cas -> [object ids] in creation order
+    obj_of = {}
+    created_total = linked_total = 0
+    for c0 in range(0, len(keys), chunk):
+        rows = list(range(c0, min(len(keys), c0 + chunk)))
+        # :181-198 existing Objects whose file_paths carry any of this chunk's cas
+        existing = {k: cas_to_objs[k] for k in {keys[i] for i in rows} if k in cas_to_objs}
+        linked = []
+        for i in rows:  # :202-238 link to the FIRST existing Object (lowest id)
+            if keys[i] in existing:
+                obj_of[i] = min(existing[keys[i]])
+                linked.append(i)
+        for i in rows:  # :246-311 one new Object per remaining file
+            if keys[i] not in existing:
+                oid = len(objects)
+                objects.append(oid)
+                obj_of[i] = oid
+                cas_to_objs.setdefault(keys[i], []).append(oid)
+                created_total += 1
+        linked_total += len(linked)
+    owner = {}
+    for i in sorted(obj_of):
+        owner.setdefault(obj_of[i], i)
+    rep_chunked = [owner[obj_of[i]] for i in range(len(keys))]
+    return rep_chunked, created_total, linked_total
+
+
+def canonical(keys: list[int]):
+    first = {}
+    rep = []
+    for i, k in enumerate(keys):
+        first.setdefault(k, i)
+        rep.append(first[k])
+    return rep, len(first)
+
+
+def main() -> None:
+    o = Oracle()
+    out: dict = {"generator": "tests/golden/make_golden.py"}
+    material = bytes([0x23] * 32 + [0xFF] * 16)
+    ctx = "spacedrive 2023-02-09 17:44:14 test key derivation"
+    expected = bytes([27, 34, 251, 101, 201, 89, 78, 90, 20, 175, 62, 206, 200, 153, 166, 103,
+                      118, 179, 194, 44, 216, 26, 48, 120, 137, 157, 60, 234, 234, 53, 46, 60])
+    assert o.derive_key(ctx, material) == expected == py_derive_key(ctx, material)
+    out["derive_key_kat"] = {"context": ctx, "material_hex": material.hex(), "expected_hex": expected.hex(),
+                             "source": "crates/crypto/src/keys/hashing.rs:210-213,323-328"}
+    pub = {"": "af1349b9f5f9a1a6a0404dea36dcc9499bcb25c9adc112b7cc9a93cae41f3262",
+           "abc": "6437b3ac38465133ffb63b75273a8db548c558465d79db03fd359c6cd5bd9d85"}
+    for s, h in pub.items():
+        assert o.blake3(s.encode()).hex() == h == py_blake3(s.encode()).hex()
+    out["blake3_public"] = pub
+
+    lens = [0, 1, 63, 64, 65, 1023, 1024, 1025, 2048, 2049, 3072, 3073, 4096, 4097, 5120, 5121,
+            6144, 6145, 7168, 7169, 8192, 8193, 16384, 31744, 57352, 65536, 102400, 102408, 140000]
+    rows = []
+    for n in lens:
+        d = bytes(i % 251 for i in range(n))
+        h = o.blake3(d)
+        assert h == o.blake3_recursive(d) == o.blake3_levelwise(d), n
+        if n <= 20000:
+            assert h == py_blake3(d), n
+        rows.append({"len": n, "hex": h.hex()})
+    out["blake3_lengths"] = {"pattern": "byte i = i % 251", "vectors": rows}
+
+    seed = 0x5DCA50001
+    sizes = [1, 63, 64, 65, 1015, 1016, 1017, 1024, 2040, 102399, 102400, 102401, 102402,
+             10 ** 6, (1 << 32) + 7]
+    cas = []
+    for f, s in enumerate(sizes):
+        content = gather_virtual(seed, f, s)
+        cid = o.cas_id(content, s)
+        assert cid == py_cas_id(content, s), s
+        cas.append({"file": f, "size": s, "content_len": len(content), "cas_id": cid,
+                    "plan": py_sample_plan(s) if s > MINIMUM_FILE_SIZE else None})
+    out["cas"] = {"seed": seed, "content": "splitmix64 words mix64(file_key(seed,file)+(w+1)*GAMMA), LE",
+                  "files": cas}
+
+    layouts = {}
+    rng = np.random.default_rng(7)
+    # (a) all distinct; (b) all identical; (c) pairs across a chunk edge; (d) dups inside
+    # the first chunk + later links; (e) random 30 % duplicates over 350 files
+    a = [int(x) for x in rng.integers(0, 2 ** 63, 250)]
+    b = [0xDEADBEEF] * 230
+    c = [int(x) for x in rng.integers(0, 2 ** 63, 220)]
+    c[150] = c[99]; c[100] = c[99]; c[201] = c[0]
+    d = [int(x) for x in rng.integers(0, 2 ** 63, 300)]
+    d[5] = d[3]; d[7] = d[3]; d[120] = d[3]; d[250] = d[5]; d[299] = d[98]
+    e = []
+    for i in range(350):
+        e.append(e[int(rng.integers(0, i))] if i and rng.random() < 0.3 else int(rng.integers(0, 2 ** 64, dtype=np.uint64)))
+    for name, keys in {"distinct": a, "identical": b, "chunk_edge": c, "first_chunk_dups": d,
+                       "dup30": e}.items():
+        rep, objs = canonical(keys)
+        rc, created, linked = replay_identifier(keys)
+        orep, oobjs = o.group_canonical(np.array(keys, dtype=np.uint64))
+        assert list(orep) == rep and oobjs == objs, name
+        crep, cc, cl = o.group_chunked(np.array(keys, dtype=np.uint64), 100)
+        assert list(crep) == rc and cc == created and cl == linked, name
+        layouts[name] = {"keys": [f"{k:016x}" for k in keys], "rep": rep, "objects": objs,
+                         "rep_chunked": rc, "created": created, "linked": linked}
+    out["grouping"] = {"chunk": 100, "layouts": layouts}
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden.json")
+    with open(path, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print("wrote", path)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,268 @@
+"""GPU parity tests (MI355X): the HIP path through the C ABI vs the oracle, bit-exact.
+
+Covers every hot-path row of SURVEY.md §8a that the build implements: K1 sampled cas,
+K2 whole-file cas (ragged lengths, the inclusive 100 KiB edge, the 8-byte tail chunk),
+the host drop-ins (buffers and paths, with per-file I/O errors), grouping (canonical and
+the chunk-of-100 replay), the radix sort, the validator checksum (device buffer and
+streamed file), and — at BASELINE sizes — size-independent properties.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle.pyoracle import MINIMUM_FILE_SIZE, SAMPLED_CONTENT_LEN, np_content, py_sample_plan
+from tests.golden.make_golden import canonical, gather_virtual, replay_identifier
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def dev64(a: np.ndarray):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint64).view(np.int64)).cuda()
+
+
+def host64(t) -> np.ndarray:
+    return t.cpu().numpy().view(np.uint64)
+
+
+def sampled_batch(rng, n, stride=SAMPLED_CONTENT_LEN):
+    content = rng.integers(0, 256, (n, stride), dtype=np.uint8)
+    sizes = rng.integers(MINIMUM_FILE_SIZE + 1, 2 ** 40, n, dtype=np.uint64)
+    return content, sizes
+
+
+def test_sampled_kernel_vs_oracle(eng, oracle):
+    rng = np.random.default_rng(1)
+    for n, stride in [(1, SAMPLED_CONTENT_LEN), (63, SAMPLED_CONTENT_LEN), (1000, SAMPLED_CONTENT_LEN),
+                      (257, SAMPLED_CONTENT_LEN + 48)]:
+        content, sizes = sampled_batch(rng, n, stride)
+        want = oracle.fast_cas_keys_strided(content.reshape(-1), stride, SAMPLED_CONTENT_LEN, sizes, 8)
+        keys = torch.zeros(n, dtype=torch.int64, device="cuda")
+        eng.hash_sampled(torch.from_numpy(content).cuda(), dev64(sizes), keys, stride=stride)
+        assert (host64(keys) == want).all(), (n, stride)
+
+
+def test_sampled_golden(eng, golden):
+    g = golden["cas"]
+    files = [f for f in g["files"] if f["size"] > MINIMUM_FILE_SIZE]
+    content = np.stack([np.frombuffer(gather_virtual(g["seed"], f["file"], f["size"]), np.uint8)
+                        for f in files])
+    sizes = np.array([f["size"] for f in files], dtype=np.uint64)
+    keys = torch.zeros(len(files), dtype=torch.int64, device="cuda")
+    eng.hash_sampled(torch.from_numpy(content).cuda(), dev64(sizes), keys)
+    got = [f"{k:016x}" for k in host64(keys)]
+    assert got == [f["cas_id"] for f in files]
+
+
+def packed_arena(contents):
+    offs, o = [], 0
+    for c in contents:
+        offs.append(o)
+        o += (len(c) + 15) // 16 * 16
+    arena = np.zeros(o + 64, dtype=np.uint8)
+    for c, off in zip(contents, offs):
+        arena[off:off + len(c)] = np.frombuffer(c, np.uint8)
+    return arena, np.array(offs, dtype=np.uint64)
+
+
+EDGE_LENS = (list(range(0, 130)) + [1015, 1016, 1017, 1023, 1024, 1025, 2040, 2041, 2047, 2048,
+             4088, 4096, 16376, 32760, 65528, 102399, 102400, 57344, 130000, 128 * 1024 - 8])
+
+
+def test_packed_kernel_edges_vs_oracle(eng, oracle):
+    rng = np.random.default_rng(2)
+    lens = EDGE_LENS + [int(x) for x in rng.integers(0, 102401, 1500)]
+    contents = [rng.integers(0, 256, L, dtype=np.uint8).tobytes() for L in lens]
+    # neighbour garbage must not leak into a message: fill the padding with 0xFF
+    arena, offs = packed_arena(contents)
+    for c, off in zip(contents, offs):
+        pad = (len(c) + 15) // 16 * 16 - len(c)
+        arena[off + len(c): off + len(c) + pad] = 0xFF
+    sizes = np.array([L if L <= MINIMUM_FILE_SIZE else L * 3 + 200_000 for L in lens], dtype=np.uint64)
+    want = oracle.cas_keys(arena, offs, np.array(lens, dtype=np.uint64), sizes)
+    keys = torch.zeros(len(lens), dtype=torch.int64, device="cuda")
+    eng.hash_packed(torch.from_numpy(arena).cuda(), dev64(offs),
+                    torch.tensor(lens, dtype=torch.int32, device="cuda"), dev64(sizes), keys)
+    got = host64(keys)
+    bad = [(lens[i], f"{got[i]:016x}", f"{want[i]:016x}") for i in range(len(lens)) if got[i] != want[i]]
+    assert not bad, bad[:10]
+
+
+def test_host_generate_cas_ids_mixed(eng, oracle, golden):
+    g = golden["cas"]
+    items = [(gather_virtual(g["seed"], f["file"], f["size"]), f["size"]) for f in g["files"]]
+    assert eng.generate_cas_ids(items) == [f["cas_id"] for f in g["files"]]
+    rng = np.random.default_rng(3)
+    items = []
+    for i in range(300):
+        if rng.random() < 0.5:
+            s = int(rng.integers(MINIMUM_FILE_SIZE + 1, 2 ** 33))
+            items.append((rng.integers(0, 256, SAMPLED_CONTENT_LEN, dtype=np.uint8).tobytes(), s))
+        else:
+            s = int(rng.integers(0, MINIMUM_FILE_SIZE + 1))
+            items.append((rng.integers(0, 256, s, dtype=np.uint8).tobytes(), s))
+    assert eng.generate_cas_ids(items) == [oracle.cas_id(b, s) for b, s in items]
+    with pytest.raises(Exception):
+        eng.generate_cas_ids([(b"x" * 100, 10 ** 7)])  # sampled size needs 57,344 bytes
+
+
+def test_generate_from_paths_and_errors(eng, oracle, tmp_path):
+    import spacedrive_amd as sd
+    rng = np.random.default_rng(4)
+    paths, sizes, imgs = [], [], []
+    for i, size in enumerate([1, 100, 1024, 102400, 102401, 250_000, 3_000_001]):
+        img = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
+        p = tmp_path / f"f{i}"
+        p.write_bytes(img)
+        paths.append(str(p)); sizes.append(size); imgs.append(img)
+    paths.append(str(tmp_path / "missing")); sizes.append(5000)
+    short = tmp_path / "short"
+    short.write_bytes(b"z" * 120_000)
+    paths.append(str(short)); sizes.append(10 ** 7)  # stale metadata: read_exact -> EOF
+    keys, errs = eng.generate_cas_keys_from_paths(paths, sizes)
+    for i in range(7):
+        assert errs[i] == 0
+        assert f"{keys[i]:016x}" == oracle.generate_cas_id(paths[i], sizes[i])
+    assert errs[7] == 2  # ENOENT
+    assert errs[8] == 5  # EIO (UnexpectedEof)
+    # the single-file drop-in raises like io::Error
+    assert sd.generate_cas_id(paths[5], sizes[5]) == oracle.generate_cas_id(paths[5], sizes[5])
+    with pytest.raises(OSError):
+        sd.generate_cas_id(paths[7], 5000)
+
+
+def test_sort_pairs_vs_numpy(eng):
+    rng = np.random.default_rng(5)
+    for n in [1, 255, 4096, 4097, 100_003]:
+        k = rng.integers(0, 2 ** 64, n, dtype=np.uint64)
+        k[: n // 3] = k[n // 2] if n > 2 else k[0]  # ties: stability matters
+        ko = torch.empty(n, dtype=torch.int64, device="cuda")
+        vo = torch.empty(n, dtype=torch.int32, device="cuda")
+        eng.sort_pairs(dev64(k), None, ko, vo)
+        order = np.argsort(k, kind="stable")
+        assert (host64(ko) == k[order]).all()
+        assert (vo.cpu().numpy() == order).all()
+        # top-byte partition pass (the multi-GPU split) is stable on the top 8 bits
+        eng.sort_pairs(dev64(k), None, ko, vo, 56, 64)
+        order = np.argsort(k >> np.uint64(56), kind="stable")
+        assert (vo.cpu().numpy() == order).all()
+
+
+def test_group_vs_oracle(eng, oracle, golden):
+    for name, lay in golden["grouping"]["layouts"].items():
+        keys = np.array([int(k, 16) for k in lay["keys"]], dtype=np.uint64)
+        rep = torch.empty(len(keys), dtype=torch.int32, device="cuda")
+        objects = eng.group(dev64(keys), rep)
+        assert rep.cpu().tolist() == lay["rep"] and objects == lay["objects"], name
+        rc = torch.empty_like(rep)
+        c, ln = eng.group_chunked(rep, rc, 100)
+        assert rc.cpu().tolist() == lay["rep_chunked"] and (c, ln) == (lay["created"], lay["linked"]), name
+    rng = np.random.default_rng(6)
+    for n, pool in [(1, 1), (5000, 5000), (300_001, 50_000), (50_000, 1), (1 << 20, 700_000)]:
+        base = rng.integers(0, 2 ** 64, pool, dtype=np.uint64)
+        keys = base[rng.integers(0, pool, n)]
+        rep = torch.empty(n, dtype=torch.int32, device="cuda")
+        objects = eng.group(dev64(keys), rep)
+        orep, oobj = oracle.group_canonical(keys)
+        assert objects == oobj
+        assert (rep.cpu().numpy().astype(np.uint32) == orep).all()
+        rc = torch.empty_like(rep)
+        c, ln = eng.group_chunked(rep, rc, 100)
+        crep, cc, cl = oracle.group_chunked(keys, 100)
+        assert (c, ln) == (cc, cl) and (rc.cpu().numpy().astype(np.uint32) == crep).all()
+
+
+CHECKSUM_LENS = [0, 1, 63, 64, 65, 1023, 1024, 1025, 2048, 4097, 255 * 1024, 256 * 1024,
+                 256 * 1024 + 1, 257 * 1024 + 3, 512 * 1024, 65536 * 1024 + 5, 3 * 256 * 1024 * 256 + 777]
+
+
+def test_checksum_device_vs_oracle(eng, oracle):
+    rng = np.random.default_rng(7)
+    for L in CHECKSUM_LENS:
+        d = rng.integers(0, 256, L, dtype=np.uint8)
+        buf = torch.zeros(L + 16, dtype=torch.uint8, device="cuda")
+        buf[:L] = torch.from_numpy(d).cuda()
+        assert eng.checksum_dev(buf, L) == oracle.blake3(d.tobytes()).hex(), L
+
+
+def test_file_checksum_streamed(eng, oracle, tmp_path):
+    import spacedrive_amd as sd
+    rng = np.random.default_rng(8)
+    for L in [0, 1, 1 << 20, (64 << 20) - 1, (64 << 20), (64 << 20) + 1, (2 * 64 << 20) + 12345]:
+        p = tmp_path / f"v{L}"
+        p.write_bytes(rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+        assert eng.file_checksum(str(p)) == oracle.file_checksum(str(p)), L
+        p.unlink()
+    with pytest.raises(OSError):
+        sd.file_checksum(str(tmp_path / "nope"))
+
+
+def test_synth_matches_oracle_generator(eng, oracle):
+    n, seed = 64, 12345
+    content = torch.empty((n, SAMPLED_CONTENT_LEN), dtype=torch.uint8, device="cuda")
+    sizes = torch.empty(n, dtype=torch.int64, device="cuda")
+    eng.synth_sampled(seed, 1000, n, content, sizes, SAMPLED_CONTENT_LEN, dup_permille=300)
+    c = content.cpu().numpy()
+    s = host64(sizes)
+    L = oracle.L
+    for i in range(n):
+        root = L.orc_synth_root(seed, 1000 + i, 300)
+        assert c[i].tobytes() == oracle.fill_content(seed, root, SAMPLED_CONTENT_LEN)
+        assert s[i] == L.orc_synth_size(seed, root, 0)
+
+
+def test_bench_scale_properties(eng, oracle):
+    """At bench scale (1.25M sampled files/GPU, 72 GB in HBM): parity on a random subset and
+    grouping == the generator's duplicate truth for every file."""
+    n, seed, dup = 1_250_000, 77, 300
+    content = torch.empty((n, SAMPLED_CONTENT_LEN), dtype=torch.uint8, device="cuda")
+    sizes = torch.empty(n, dtype=torch.int64, device="cuda")
+    eng.synth_sampled(seed, 0, n, content, sizes, SAMPLED_CONTENT_LEN, dup_permille=dup)
+    keys = torch.empty(n, dtype=torch.int64, device="cuda")
+    eng.hash_sampled(content, sizes, keys)
+    rep = torch.empty(n, dtype=torch.int32, device="cuda")
+    objects = eng.group(keys, rep)
+    roots = torch.empty(n, dtype=torch.int64, device="cuda")
+    eng.synth_roots(seed, 0, n, roots, dup_permille=dup)
+    r = roots.cpu().numpy()
+    uniq, inv = np.unique(r, return_inverse=True)
+    first = np.full(len(uniq), n, dtype=np.int64)
+    np.minimum.at(first, inv, np.arange(n))
+    assert objects == len(uniq)
+    assert (rep.cpu().numpy() == first[inv]).all()
+    idx = np.random.default_rng(9).choice(n, 3000, replace=False)
+    sub = content[torch.from_numpy(idx).cuda()].cpu().numpy()
+    want = oracle.fast_cas_keys_strided(sub.reshape(-1), SAMPLED_CONTENT_LEN, SAMPLED_CONTENT_LEN,
+                                        host64(sizes)[idx], 8)
+    assert (host64(keys)[idx] == want).all()
+    del content
+
+
+def test_identifier_job_step(eng, oracle, tmp_path):
+    import spacedrive_amd as sd
+    rng = np.random.default_rng(10)
+    blobs = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes()
+             for s in [10, 5000, 102400, 150_000, 900_000]]
+    paths = []
+    for i in range(260):
+        p = tmp_path / f"p{i:03d}"
+        if i % 37 == 5:
+            p.write_bytes(b"")  # empty: no cas_id, own Object (mod.rs:78-86)
+        else:
+            p.write_bytes(blobs[int(rng.integers(0, len(blobs)))] if rng.random() < 0.5
+                          else rng.integers(0, 256, int(rng.integers(1, 200_000)), dtype=np.uint8).tobytes())
+        paths.append(str(p))
+    res = sd.identifier_job_step(paths, eng=eng)
+    keys = []
+    for p in paths:
+        size = os.path.getsize(p)
+        keys.append(None if size == 0 else int(oracle.generate_cas_id(p, size), 16))
+    for i, p in enumerate(paths):
+        want = None if keys[i] is None else f"{keys[i]:016x}"
+        assert res.metadata[i].cas_id == want
+    # replay with unique sentinels for the cas-less rows (each gets its own Object)
+    rk = [k if k is not None else -(i + 1) for i, k in enumerate(keys)]
+    rc, created, linked = replay_identifier(rk, 100)
+    assert [res.object_of[i] for i in range(len(paths))] == rc
+    assert (res.total_created, res.total_linked) == (created, linked)

@@ -1,0 +1,154 @@
+"""CPU tests: the oracle against the golden vectors and the reference's own KAT.
+
+The oracle is a restatement of the reference path (oracle/oracle.h); before any GPU
+parity claim rests on it, it is pinned here:
+  * derive_key KAT from crates/crypto/src/keys/hashing.rs:210-213 (the reference's only
+    in-repo BLAKE3 known answer),
+  * public BLAKE3("") / BLAKE3("abc"),
+  * three independent tree formulations + a pure-Python restatement agreeing,
+  * cas.rs:35-58 offsets simulated literally,
+  * grouping against a literal replay of identifier_job_step (mod.rs:98-350).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle.pyoracle import (
+    MINIMUM_FILE_SIZE,
+    SAMPLED_CONTENT_LEN,
+    np_content,
+    py_blake3,
+    py_cas_id,
+    py_derive_key,
+    py_sample_plan,
+)
+from tests.golden.make_golden import canonical, gather_virtual, replay_identifier
+
+
+def test_derive_key_kat_from_reference(oracle, golden):
+    kat = golden["derive_key_kat"]
+    mat = bytes.fromhex(kat["material_hex"])
+    assert oracle.derive_key(kat["context"], mat).hex() == kat["expected_hex"]
+    assert py_derive_key(kat["context"], mat).hex() == kat["expected_hex"]
+
+
+def test_public_vectors(oracle, golden):
+    for s, h in golden["blake3_public"].items():
+        assert oracle.blake3(s.encode()).hex() == h
+        assert py_blake3(s.encode()).hex() == h
+
+
+def test_length_vectors_three_formulations(oracle, golden):
+    for row in golden["blake3_lengths"]["vectors"]:
+        d = bytes(i % 251 for i in range(row["len"]))
+        assert oracle.blake3(d).hex() == row["hex"]
+        assert oracle.blake3_recursive(d).hex() == row["hex"]
+        assert oracle.blake3_levelwise(d).hex() == row["hex"]
+
+
+@pytest.mark.parametrize("n", [0, 1, 64, 1024, 1025, 3000, 8193])
+def test_python_restatement_agrees(oracle, n):
+    d = np_content(11, n, n)
+    assert py_blake3(d) == oracle.blake3(d)
+
+
+def test_formulations_random_lengths(oracle):
+    rng = np.random.default_rng(3)
+    for n in rng.integers(0, 300_000, 40):
+        d = rng.integers(0, 256, int(n), dtype=np.uint8).tobytes()
+        a = oracle.blake3(d)
+        assert a == oracle.blake3_recursive(d) == oracle.blake3_levelwise(d)
+
+
+def test_sample_plan_matches_literal_loop(oracle):
+    # cas.rs:35-58: header at 0, samples at 8192 + k*jump, footer at size - 8192
+    for size in [102401, 102402, 123457, 10 ** 6, 2 ** 31 + 5, 2 ** 40 + 3]:
+        plan = py_sample_plan(size)
+        assert plan == oracle.sample_plan(size)
+        jump = (size - 2 * 8192) // 4
+        assert plan == [(0, 8192)] + [(8192 + k * jump, 10240) for k in range(4)] + [(size - 8192, 8192)]
+        assert sum(ln for _, ln in plan) == SAMPLED_CONTENT_LEN
+
+
+def test_golden_cas_ids(oracle, golden):
+    g = golden["cas"]
+    for f in g["files"]:
+        content = gather_virtual(g["seed"], f["file"], f["size"])
+        assert len(content) == f["content_len"]
+        assert oracle.cas_id(content, f["size"]) == f["cas_id"]
+        assert py_cas_id(content, f["size"]) == f["cas_id"]
+        # inclusive 100 KiB threshold (cas.rs:27)
+        assert (f["content_len"] == f["size"]) == (f["size"] <= MINIMUM_FILE_SIZE)
+
+
+def test_gather_from_files_matches_image(oracle, tmp_path):
+    rng = np.random.default_rng(5)
+    for size in [0, 1, 100, 102400, 102401, 300_000, 1_000_003]:
+        img = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
+        p = tmp_path / f"f{size}"
+        p.write_bytes(img)
+        got = oracle.gather_path(str(p), size)
+        want = img if size <= MINIMUM_FILE_SIZE else b"".join(img[o:o + ln] for o, ln in py_sample_plan(size))
+        assert got == want
+        assert oracle.generate_cas_id(str(p), size) == oracle.cas_id(want, size)
+
+
+def test_gather_short_file_is_eof_error(oracle, tmp_path):
+    p = tmp_path / "short"
+    p.write_bytes(b"x" * 150_000)
+    with pytest.raises(OSError):
+        oracle.gather_path(str(p), 10 ** 7)  # size from stale metadata: read_exact -> EOF
+
+
+def test_file_checksum(oracle, tmp_path):
+    for n in [0, 1, 1024, 1025, 1 << 20, (1 << 20) + 17]:
+        d = np_content(9, n, n)
+        p = tmp_path / f"c{n}"
+        p.write_bytes(d)
+        assert oracle.file_checksum(str(p)) == oracle.blake3(d).hex()
+
+
+def test_grouping_golden(oracle, golden):
+    g = golden["grouping"]
+    for name, lay in g["layouts"].items():
+        keys = np.array([int(k, 16) for k in lay["keys"]], dtype=np.uint64)
+        rep, objs = oracle.group_canonical(keys)
+        assert list(rep) == lay["rep"] and objs == lay["objects"], name
+        rc, c, ln = oracle.group_chunked(keys, g["chunk"])
+        assert list(rc) == lay["rep_chunked"] and (c, ln) == (lay["created"], lay["linked"]), name
+
+
+def test_grouping_random_vs_replay(oracle):
+    rng = np.random.default_rng(11)
+    for trial in range(20):
+        n = int(rng.integers(1, 700))
+        pool = rng.integers(0, 2 ** 64, max(1, n // int(rng.integers(1, 6))), dtype=np.uint64)
+        keys = pool[rng.integers(0, len(pool), n)]
+        rep, objs = canonical([int(k) for k in keys])
+        orep, oobjs = oracle.group_canonical(keys)
+        assert list(orep) == rep and oobjs == objs
+        rc, c, ln = replay_identifier([int(k) for k in keys], 100)
+        crep, cc, cl = oracle.group_chunked(keys, 100)
+        assert list(crep) == rc and (cc, cl) == (c, ln)
+
+
+def test_simd_baseline_matches_scalar(oracle):
+    rng = np.random.default_rng(2)
+    n = 48
+    arena = rng.integers(0, 256, n * SAMPLED_CONTENT_LEN, dtype=np.uint8)
+    sizes = rng.integers(102401, 2 ** 32, n, dtype=np.uint64)
+    a = oracle.cas_keys_strided(arena, SAMPLED_CONTENT_LEN, SAMPLED_CONTENT_LEN, sizes)
+    b = oracle.fast_cas_keys_strided(arena, SAMPLED_CONTENT_LEN, SAMPLED_CONTENT_LEN, sizes, threads=2)
+    assert (a == b).all()
+    for L in [0, 55, 56, 57, 1016, 1017, 4000, 102400]:
+        ar = rng.integers(0, 256, 16 * max(L, 1) + 64, dtype=np.uint8)
+        offs = np.arange(16, dtype=np.uint64) * L
+        ln = np.full(16, L, dtype=np.uint64)
+        assert (oracle.cas_keys(ar, offs, ln, ln) == oracle.fast_cas_keys(ar, offs, ln, ln)).all()
+
+
+def test_synth_generator_shared_definitions(oracle):
+    # the device generator (spacedrive_amd/csrc/synth.hip) uses these exact definitions
+    for f in [0, 1, 77, 10 ** 6]:
+        assert oracle.fill_content(3, f, 1000) == np_content(3, f, 1000)
