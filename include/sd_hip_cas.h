@@ -19,8 +19,10 @@
  *     when size <= SD_CAS_MINIMUM_FILE_SIZE (cas.rs:27-29), otherwise the 57,344
  *     gathered bytes header || 4 samples || footer (cas.rs:31-58).
  *   - *_dev functions take device pointers already resident in HBM and a hipStream_t
- *     passed as void* (NULL = the context's own stream); they enqueue and return
- *     without synchronising unless stated.  Host-buffer functions are blocking.
+ *     passed as void* (NULL = the HIP null/default stream, as in HIP; pass
+ *     sd_cas_ctx_stream(ctx) for the context's own stream); they enqueue and return
+ *     without synchronising unless stated.  Host-buffer functions are blocking and run
+ *     on the context's streams.
  *   - Contexts are not thread-safe; use one per (thread, device).
  */
 #ifndef SD_HIP_CAS_H

@@ -215,6 +215,10 @@ class Oracle:
         L.orc_group_canonical.restype = ctypes.c_uint64
         L.orc_group_chunked.argtypes = [u64p, sz, sz, u32p, u64p, u64p]
         L.orc_fill_content.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, sz]
+        L.orc_synth_root.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]
+        L.orc_synth_root.restype = ctypes.c_uint64
+        L.orc_synth_size.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]
+        L.orc_synth_size.restype = ctypes.c_uint64
         self.L = L
         _ = u8p
 
@@ -331,6 +335,12 @@ class Oracle:
         self.L.orc_group_chunked(_p64(keys), len(keys), chunk, _p32(rep), ctypes.byref(c),
                                  ctypes.byref(ln))
         return rep, int(c.value), int(ln.value)
+
+    def synth_root(self, seed: int, file: int, dup_permille: int) -> int:
+        return int(self.L.orc_synth_root(seed, file, dup_permille))
+
+    def synth_size(self, seed: int, root: int, kind: int) -> int:
+        return int(self.L.orc_synth_size(seed, root, kind))
 
     def fill_content(self, seed: int, file: int, length: int) -> bytes:
         buf = ctypes.create_string_buffer(max(length, 1))

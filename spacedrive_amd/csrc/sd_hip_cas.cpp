@@ -71,7 +71,9 @@ static int fail(sd_cas_ctx* c, int code, const char* fmt, ...) {
                   __FILE__, __LINE__);                                                     \
   } while (0)
 
-static inline hipStream_t pick(sd_cas_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
+// NULL = the HIP null (default) stream, exactly as in HIP itself: a caller on the
+// default stream (torch's default) must be ordered with our kernels.
+static inline hipStream_t pick(sd_cas_ctx* c, void* s) { (void)c; return (hipStream_t)s; }
 static inline size_t up16(size_t x) { return (x + 15) & ~(size_t)15; }
 static inline size_t up256(size_t x) { return (x + 255) & ~(size_t)255; }
 

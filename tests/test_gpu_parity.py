@@ -205,11 +205,13 @@ def test_synth_matches_oracle_generator(eng, oracle):
     eng.synth_sampled(seed, 1000, n, content, sizes, SAMPLED_CONTENT_LEN, dup_permille=300)
     c = content.cpu().numpy()
     s = host64(sizes)
-    L = oracle.L
+    roots = set()
     for i in range(n):
-        root = L.orc_synth_root(seed, 1000 + i, 300)
+        root = oracle.synth_root(seed, 1000 + i, 300)
+        roots.add(root)
         assert c[i].tobytes() == oracle.fill_content(seed, root, SAMPLED_CONTENT_LEN)
-        assert s[i] == L.orc_synth_size(seed, root, 0)
+        assert int(s[i]) == oracle.synth_size(seed, root, 0)
+    assert len(roots) < n  # the 30 % duplicate chain is exercised
 
 
 def test_bench_scale_properties(eng, oracle):
