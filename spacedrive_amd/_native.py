@@ -11,7 +11,8 @@ import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsd_hip_cas.so")
+# SD_HIP_CAS_LIB lets profiling tools A/B two builds of the same library; default in-tree.
+LIB_PATH = os.environ.get("SD_HIP_CAS_LIB") or os.path.join(HERE, "libsd_hip_cas.so")
 CSRC = os.path.join(HERE, "csrc")
 
 SD_CAS_OK = 0
