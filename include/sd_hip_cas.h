@@ -88,6 +88,15 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* ctx, const char* const* paths
                                        const uint64_t* sizes, size_t n, uint64_t* out_keys,
                                        int32_t* status);
 
+/* End-to-end sampled path from host memory (BASELINE config 3 "pre-staged in pinned host
+ * memory"): n contents of 57,344 B at h_content + i*stride (pin it with
+ * sd_cas_alloc_pinned for overlap), sizes and keys in host memory.  Batches of
+ * batch_files (0 = 32,768) ping-pong between an H2D copy on the side stream and K1 +
+ * D2H of the keys on the compute stream.  Blocking. */
+int sd_cas_hash_sampled_host(sd_cas_ctx* ctx, const void* h_content, uint64_t stride,
+                             const uint64_t* h_sizes, size_t n, uint64_t* h_keys,
+                             size_t batch_files);
+
 /* 16 lowercase hex chars + NUL: the cas_id String of cas.rs:61 */
 void sd_cas_key_to_hex(uint64_t key, char out[17]);
 

@@ -32,6 +32,7 @@ SIGNATURES = [
     ("sd_cas_free_pinned", _i, [_vp, _vp]),
     ("sd_cas_generate_cas_ids", _i, [_vp, _vp, _vp, _vp, _sz, _vp]),
     ("sd_cas_generate_cas_ids_from_paths", _i, [_vp, _vp, _vp, _sz, _vp, _vp]),
+    ("sd_cas_hash_sampled_host", _i, [_vp, _vp, _u64, _vp, _sz, _vp, _sz]),
     ("sd_cas_key_to_hex", None, [_u64, _cp]),
     ("sd_cas_hash_sampled_dev", _i, [_vp, _vp, _u64, _vp, _sz, _vp, _vp]),
     ("sd_cas_hash_packed_dev", _i, [_vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp]),
@@ -69,6 +70,8 @@ def lib() -> ctypes.CDLL:
                 "Run spacedrive_amd._native.build() (or __graft_entry__.build()).")
         L = ctypes.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
+            if os.environ.get("SD_HIP_CAS_LIB") and not hasattr(L, name):
+                continue  # an older build under A/B profiling may lack newer entry points
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

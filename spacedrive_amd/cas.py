@@ -141,6 +141,27 @@ class CasEngine:
             self._check(rc, "generate_cas_ids_from_paths")
         return keys, -status
 
+    def alloc_pinned(self, nbytes: int) -> np.ndarray:
+        """Page-locked host buffer (uint8 numpy view); free with free_pinned."""
+        p = ctypes.c_void_p()
+        self._check(self.L.sd_cas_alloc_pinned(self.h, int(nbytes), ctypes.byref(p)), "alloc_pinned")
+        buf = (ctypes.c_uint8 * int(nbytes)).from_address(p.value)
+        return np.frombuffer(buf, dtype=np.uint8)
+
+    def free_pinned(self, arr: np.ndarray) -> None:
+        self._check(self.L.sd_cas_free_pinned(self.h, int(arr.ctypes.data)), "free_pinned")
+
+    def hash_sampled_host(self, content: np.ndarray, sizes: np.ndarray, stride: int = SAMPLED_CONTENT_LEN,
+                          batch_files: int = 0) -> np.ndarray:
+        """End-to-end K1 from host memory (H2D pipelined with hashing)."""
+        n = len(sizes)
+        sz = np.ascontiguousarray(sizes, dtype=np.uint64)
+        keys = np.zeros(n, dtype=np.uint64)
+        self._check(self.L.sd_cas_hash_sampled_host(self.h, int(content.ctypes.data), int(stride),
+                                                    _np_ptr(sz), n, _np_ptr(keys), int(batch_files)),
+                    "hash_sampled_host")
+        return keys
+
     def file_checksum(self, path: str) -> str:
         out = ctypes.create_string_buffer(65)
         err = ctypes.c_int(0)

@@ -489,6 +489,60 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
   return SD_CAS_OK;
 }
 
+int sd_cas_hash_sampled_host(sd_cas_ctx* c, const void* h_content, uint64_t stride,
+                             const uint64_t* h_sizes, size_t n, uint64_t* h_keys,
+                             size_t batch_files) {
+  if (!c) return SD_CAS_EINVAL;
+  if (n == 0) return SD_CAS_OK;
+  if (!h_content || !h_sizes || !h_keys || stride < SAMPLED_CONTENT_LEN || (stride & 15))
+    return fail(c, SD_CAS_EINVAL, "hash_sampled_host: bad arguments");
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (batch_files == 0) batch_files = 32768;
+  batch_files = std::min(batch_files, n);
+  // two device slots: [content | sizes | keys], ping-ponged between the copy stream (H2D of
+  // batch k+1) and the compute stream (K1 on batch k, then D2H of its keys)
+  const size_t cbytes = up256(batch_files * stride), sbytes = up256(batch_files * 8);
+  const size_t slot = cbytes + 2 * sbytes;
+  int rc = ensure(c, c->staging, 2 * slot);
+  if (rc) return rc;
+  hipEvent_t h2d[2], done[2];
+  for (int i = 0; i < 2; i++) {
+    HIP_TRY(c, hipEventCreateWithFlags(&h2d[i], hipEventDisableTiming));
+    HIP_TRY(c, hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
+  }
+  int result = SD_CAS_OK;
+  const size_t nb = (n + batch_files - 1) / batch_files;
+  for (size_t k = 0; k < nb && result == SD_CAS_OK; k++) {
+    const int b = (int)(k & 1);
+    const size_t f0 = k * batch_files, m = std::min(batch_files, n - f0);
+    char* base = (char*)c->staging.p + b * slot;
+    uint8_t* d_content = (uint8_t*)base;
+    uint64_t* d_sizes = (uint64_t*)(base + cbytes);
+    uint64_t* d_keys = (uint64_t*)(base + cbytes + sbytes);
+    hipError_t e = hipSuccess;
+    if (k >= 2) e = hipStreamWaitEvent(c->copy, done[b], 0);  // slot b's previous batch done
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(d_content, (const char*)h_content + f0 * stride, m * stride,
+                         hipMemcpyHostToDevice, c->copy);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(d_sizes, h_sizes + f0, m * 8, hipMemcpyHostToDevice, c->copy);
+    if (e == hipSuccess) e = hipEventRecord(h2d[b], c->copy);
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, h2d[b], 0);
+    if (e == hipSuccess) e = hash_sampled(d_content, stride, d_sizes, m, d_keys, c->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(h_keys + f0, d_keys, m * 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipEventRecord(done[b], c->stream);
+    if (e != hipSuccess) result = fail(c, SD_CAS_EHIP, "hash_sampled_host: %s", hipGetErrorString(e));
+  }
+  (void)hipStreamSynchronize(c->stream);
+  (void)hipStreamSynchronize(c->copy);
+  for (int i = 0; i < 2; i++) {
+    (void)hipEventDestroy(h2d[i]);
+    (void)hipEventDestroy(done[i]);
+  }
+  return result;
+}
+
 // ---- file_checksum --------------------------------------------------------------------
 
 int sd_cas_checksum_dev(sd_cas_ctx* c, const void* d_data, uint64_t len, uint8_t out[32],

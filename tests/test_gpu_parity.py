@@ -268,3 +268,24 @@ def test_identifier_job_step(eng, oracle, tmp_path):
     rc, created, linked = replay_identifier(rk, 100)
     assert [res.object_of[i] for i in range(len(paths))] == rc
     assert (res.total_created, res.total_linked) == (created, linked)
+
+
+def test_sampled_host_pipeline(eng, oracle):
+    """End-to-end path from (pinned) host memory: H2D of batch k+1 overlaps K1 on batch k."""
+    rng = np.random.default_rng(12)
+    n = 5000
+    pinned = eng.alloc_pinned(n * SAMPLED_CONTENT_LEN)
+    try:
+        pinned[:] = rng.integers(0, 256, n * SAMPLED_CONTENT_LEN, dtype=np.uint8)
+        sizes = rng.integers(MINIMUM_FILE_SIZE + 1, 2 ** 40, n, dtype=np.uint64)
+        want = oracle.fast_cas_keys_strided(pinned, SAMPLED_CONTENT_LEN, SAMPLED_CONTENT_LEN, sizes, 8)
+        for batch in [0, 1, 999, 1024, 5000]:
+            got = eng.hash_sampled_host(pinned, sizes, batch_files=batch)
+            assert (got == want).all(), batch
+    finally:
+        eng.free_pinned(pinned)
+    # pageable memory works too (synchronous copies)
+    host = rng.integers(0, 256, 300 * SAMPLED_CONTENT_LEN, dtype=np.uint8)
+    sizes = rng.integers(MINIMUM_FILE_SIZE + 1, 2 ** 40, 300, dtype=np.uint64)
+    assert (eng.hash_sampled_host(host, sizes, batch_files=128) ==
+            oracle.cas_keys_strided(host, SAMPLED_CONTENT_LEN, SAMPLED_CONTENT_LEN, sizes)).all()

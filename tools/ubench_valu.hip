@@ -1,0 +1,116 @@
+// ubench_valu.hip — gfx950 VALU microbenchmarks for the BLAKE3 ARX instruction mix.
+// Measures, at full occupancy with 8 independent chains per lane, the throughput of each
+// integer op K1 uses (and candidate replacements), plus the dependent-chain latency, and
+// the compute-only rate of the real compression function (no memory traffic).
+// Build: hipcc --offload-arch=gfx950 -O3 -o ubench tools/ubench_valu.hip
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../spacedrive_amd/csrc/blake3_device.hpp"
+
+#define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
+
+constexpr int ITERS = 4096;
+
+#define OP8(ASM)                                                                              \
+  asm volatile(ASM : "+v"(a0) : "v"(b)); asm volatile(ASM : "+v"(a1) : "v"(b));             \
+  asm volatile(ASM : "+v"(a2) : "v"(b)); asm volatile(ASM : "+v"(a3) : "v"(b));             \
+  asm volatile(ASM : "+v"(a4) : "v"(b)); asm volatile(ASM : "+v"(a5) : "v"(b));             \
+  asm volatile(ASM : "+v"(a6) : "v"(b)); asm volatile(ASM : "+v"(a7) : "v"(b));
+
+#define KERNEL(NAME, ASM)                                                                     \
+  __global__ void __launch_bounds__(256) NAME(uint32_t* out, uint32_t seed) {               \
+    uint32_t a0 = threadIdx.x ^ seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,    \
+             a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7, b = seed * 3u + 1u;                        \
+    for (int i = 0; i < ITERS; ++i) { OP8(ASM) }                                              \
+    out[blockIdx.x * 256 + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;              \
+  }
+
+KERNEL(k_xor, "v_xor_b32 %0, %0, %1")
+KERNEL(k_add, "v_add_u32 %0, %0, %1")
+KERNEL(k_add3, "v_add3_u32 %0, %0, %1, %0")
+KERNEL(k_alignbit, "v_alignbit_b32 %0, %0, %0, 7")
+KERNEL(k_xor3, "v_bitop3_b32 %0, %0, %1, %0 bitop3:0x96")
+KERNEL(k_perm, "v_perm_b32 %0, %0, %0, %1")
+KERNEL(k_lshlor, "v_lshl_or_b32 %0, %0, 7, %1")
+KERNEL(k_xor_e64, "v_xor_b32_e64 %0, %0, %1")
+KERNEL(k_pkadd16, "v_pk_add_u16 %0, %0, %1")
+
+// dependent chain: one accumulator
+__global__ void __launch_bounds__(64) k_dep_alignbit(uint32_t* out, uint32_t seed) {
+  uint32_t a = threadIdx.x ^ seed;
+  for (int i = 0; i < ITERS * 8; ++i) asm volatile("v_alignbit_b32 %0, %0, %0, 7" : "+v"(a));
+  out[blockIdx.x * 64 + threadIdx.x] = a;
+}
+__global__ void __launch_bounds__(64) k_dep_xor(uint32_t* out, uint32_t seed) {
+  uint32_t a = threadIdx.x ^ seed, b = seed;
+  for (int i = 0; i < ITERS * 8; ++i) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a) : "v"(b));
+  out[blockIdx.x * 64 + threadIdx.x] = a;
+}
+
+// compute-only compression: the real compress() on register data, 64 compressions/lane
+__global__ void __launch_bounds__(256) k_compress(uint32_t* out, uint32_t seed) {
+  uint32_t cv[8];
+  sdcas::set_iv(cv);
+  uint32_t m[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) m[i] = threadIdx.x * 16 + i + seed;
+  for (int i = 0; i < 64; ++i) {
+    sdcas::compress(cv, m, (uint32_t)i, 0u, 64u, 0u);
+    m[i & 15] ^= cv[0];  // keep the chain live without changing the instruction mix much
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = cv[0] ^ cv[7];
+}
+
+template <typename K>
+static float timeit(K kern, dim3 grid, dim3 block, uint32_t* out) {
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  hipLaunchKernelGGL(kern, grid, block, 0, 0, out, 1u);  // warm
+  (void)hipDeviceSynchronize();
+  (void)hipEventRecord(a, 0);
+  for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(kern, grid, block, 0, 0, out, (uint32_t)r);
+  (void)hipEventRecord(b, 0);
+  (void)hipEventSynchronize(b);
+  float ms;
+  (void)hipEventElapsedTime(&ms, a, b);
+  return ms / 5;
+}
+
+int main() {
+  hipDeviceProp_t p;
+  CHECK(hipGetDeviceProperties(&p, 0));
+  printf("device %s CUs %d clock %d kHz\n", p.gcnArchName, p.multiProcessorCount, p.clockRate);
+  uint32_t* out;
+  const int blocks = p.multiProcessorCount * 8 * 4;  // 32 waves/CU worth of 256-thread blocks
+  CHECK(hipMalloc(&out, (size_t)blocks * 256 * 4));
+  const double simds = p.multiProcessorCount * 4.0;
+  struct { const char* n; void (*k)(uint32_t*, uint32_t); } ks[] = {
+      {"v_xor_b32 (VOP2)", k_xor}, {"v_add_u32 (VOP2)", k_add}, {"v_add3_u32", k_add3},
+      {"v_alignbit_b32", k_alignbit}, {"v_bitop3_b32 (xor3)", k_xor3}, {"v_perm_b32", k_perm},
+      {"v_lshl_or_b32", k_lshlor}, {"v_xor_b32_e64 (VOP3 enc)", k_xor_e64},
+      {"v_pk_add_u16", k_pkadd16}};
+  for (auto& k : ks) {
+    float ms = timeit(k.k, dim3(blocks), dim3(256), out);
+    const double winstr = (double)blocks * 4 * ITERS * 8;  // wave-instructions
+    const double rate = winstr / (ms * 1e-3);
+    printf("%-28s %8.3f ms  %.3e wave-instr/s  = %.3f wave-instr/SIMD/ns  (2.4GHz full rate = 1.2)\n",
+           k.n, ms, rate, rate / simds / 1e9);
+  }
+  {
+    float ms = timeit(k_dep_alignbit, dim3(p.multiProcessorCount * 4), dim3(64), out);
+    printf("dep chain alignbit, 1 wave/SIMD: %.2f ns/instr\n", ms * 1e6 / (ITERS * 8));
+    ms = timeit(k_dep_xor, dim3(p.multiProcessorCount * 4), dim3(64), out);
+    printf("dep chain xor, 1 wave/SIMD: %.2f ns/instr\n", ms * 1e6 / (ITERS * 8));
+  }
+  for (int wps : {1, 2, 3, 4, 8}) {  // waves per SIMD
+    const int nb = p.multiProcessorCount * wps;  // 256-thread blocks = 4 waves = 1 per SIMD
+    float ms = timeit(k_compress, dim3(nb), dim3(256), out);
+    const double comps = (double)nb * 256 * 64;
+    printf("compress-only, %d waves/SIMD: %.3f ms  %.3e compressions/s  -> %.1f M sampled files/s (953 each)\n",
+           wps, ms, comps / (ms * 1e-3), comps / (ms * 1e-3) / 953 / 1e6);
+  }
+  return 0;
+}
