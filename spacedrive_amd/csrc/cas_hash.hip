@@ -167,11 +167,34 @@ __device__ __forceinline__ void compress_pair(uint32_t (&cv)[8], const uint4 (&A
   c1 = A[7].w;
 }
 
-__device__ __forceinline__ uint64_t cas_lane_sampled(const uint4* __restrict__ q, uint64_t size) {
+// The 5-deep chaining-value stack lives in LDS, word-major [depth][word][thread] so every
+// push/pop is a conflict-free dword access.  It is touched once per 1 KiB chunk (16
+// compressions), and moving its 40 words per lane out of VGPRs takes the kernel from 3
+// to 4 waves per SIMD (VGPR budget <= 128); 40 KiB per 256-lane block = 4 blocks/CU.
+constexpr int SAMPLED_DEPTH = 5;  // popcount(55) pending subtrees at most
+constexpr int SAMPLED_BLOCK = 256;
+
+struct LdsStack {
+  uint32_t (*s)[8][SAMPLED_BLOCK];
+  uint32_t t;
+  uint32_t sp = 0;  // wave-uniform on the sampled path
+  __device__ __forceinline__ void push(const uint32_t (&cv)[8]) {
+#pragma unroll
+    for (int w = 0; w < 8; ++w) s[sp][w][t] = cv[w];
+    ++sp;
+  }
+  __device__ __forceinline__ void pop(uint32_t (&out)[8]) {
+    --sp;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) out[w] = s[sp][w][t];
+  }
+};
+
+__device__ __forceinline__ uint64_t cas_lane_sampled(const uint4* __restrict__ q, uint64_t size,
+                                                     LdsStack& stk) {
   uint32_t c0 = (uint32_t)size, c1 = (uint32_t)(size >> 32);
   uint4 A[8], B[8];
   load_pair(q, 0, A);
-  CvStack<5> stk;  // 56 chunks: at most popcount(55) = 5 pending subtrees
   uint32_t cv[8];
   for (uint32_t c = 0; c < SAMPLED_CHUNKS; ++c) {
     set_iv(cv);
@@ -199,7 +222,7 @@ __device__ __forceinline__ uint64_t cas_lane_sampled(const uint4* __restrict__ q
     set_iv(cv);
     compress(cv, m, SAMPLED_CHUNKS, 0u, 8u, CHUNK_START | CHUNK_END);
   }
-  // 56 = 0b111000: stack holds the 32-, 16- and 8-chunk subtrees
+  // 56 = 0b111000: the stack holds the 32-, 16- and 8-chunk subtrees
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
     uint32_t left[8];
@@ -210,14 +233,16 @@ __device__ __forceinline__ uint64_t cas_lane_sampled(const uint4* __restrict__ q
 }
 
 // K1: sampled path, uniform 57,344-B contents at a fixed stride (>= 57,344, 16-B aligned).
-extern "C" __global__ void __launch_bounds__(256)
+extern "C" __global__ void __launch_bounds__(SAMPLED_BLOCK)
 sd_cas_sampled_kernel(const uint8_t* __restrict__ content, uint64_t stride,
                       const uint64_t* __restrict__ sizes, uint64_t n,
                       uint64_t* __restrict__ keys) {
-  const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= n) return;
+  __shared__ uint32_t stack_lds[SAMPLED_DEPTH][8][SAMPLED_BLOCK];
+  const uint64_t f = (uint64_t)blockIdx.x * SAMPLED_BLOCK + threadIdx.x;
+  if (f >= n) return;  // no barrier below: each lane only touches its own stack column
+  LdsStack stk{stack_lds, threadIdx.x};
   const uint4* q = reinterpret_cast<const uint4*>(content + f * stride);
-  keys[f] = cas_lane_sampled(q, sizes[f]);
+  keys[f] = cas_lane_sampled(q, sizes[f], stk);
 }
 
 // K2: general path, any content length <= 2^32 - 9 (whole-file <= 102,400 or sampled),

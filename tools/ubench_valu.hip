@@ -36,6 +36,14 @@ KERNEL(k_perm, "v_perm_b32 %0, %0, %0, %1")
 KERNEL(k_lshlor, "v_lshl_or_b32 %0, %0, 7, %1")
 KERNEL(k_xor_e64, "v_xor_b32_e64 %0, %0, %1")
 KERNEL(k_pkadd16, "v_pk_add_u16 %0, %0, %1")
+KERNEL(k_sdwa_hi, "v_xor_b32_sdwa %0, %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0")
+KERNEL(k_sdwa_lo, "v_xor_b32_sdwa %0, %0, %1 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_1")
+KERNEL(k_sdwa_byte, "v_mov_b32_sdwa %0, %1 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0")
+KERNEL(k_lshr, "v_lshrrev_b32 %0, 7, %0")
+KERNEL(k_bfi, "v_bfi_b32 %0, %0, %1, %0")
+KERNEL(k_or, "v_or_b32 %0, %0, %1")
+KERNEL(k_add_e64, "v_add_u32_e64 %0, %0, %1")
+KERNEL(k_lshladd, "v_lshl_add_u32 %0, %0, 7, %1")
 
 // dependent chain: one accumulator
 __global__ void __launch_bounds__(64) k_dep_alignbit(uint32_t* out, uint32_t seed) {
@@ -91,7 +99,11 @@ int main() {
       {"v_xor_b32 (VOP2)", k_xor}, {"v_add_u32 (VOP2)", k_add}, {"v_add3_u32", k_add3},
       {"v_alignbit_b32", k_alignbit}, {"v_bitop3_b32 (xor3)", k_xor3}, {"v_perm_b32", k_perm},
       {"v_lshl_or_b32", k_lshlor}, {"v_xor_b32_e64 (VOP3 enc)", k_xor_e64},
-      {"v_pk_add_u16", k_pkadd16}};
+      {"v_pk_add_u16", k_pkadd16},
+      {"v_xor_b32_sdwa WORD_1<-WORD_0", k_sdwa_hi}, {"v_xor_b32_sdwa WORD_0<-WORD_1", k_sdwa_lo},
+      {"v_mov_b32_sdwa BYTE_3<-BYTE_0", k_sdwa_byte}, {"v_lshrrev_b32", k_lshr},
+      {"v_bfi_b32", k_bfi}, {"v_or_b32", k_or},
+      {"v_add_u32_e64", k_add_e64}, {"v_lshl_add_u32", k_lshladd}};
   for (auto& k : ks) {
     float ms = timeit(k.k, dim3(blocks), dim3(256), out);
     const double winstr = (double)blocks * 4 * ITERS * 8;  // wave-instructions
