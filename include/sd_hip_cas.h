@@ -45,8 +45,8 @@ extern "C" {
 #define SD_CAS_SAMPLED_CONTENT_LEN (2u * SD_CAS_HEADER_OR_FOOTER_SIZE + SD_CAS_SAMPLE_COUNT * SD_CAS_SAMPLE_SIZE)
 /* file_identifier/mod.rs:34 */
 #define SD_CAS_CHUNK_SIZE 100u
-/* largest content the packed kernel takes (128 BLAKE3 chunks incl. the size prefix) */
-#define SD_CAS_MAX_PACKED_CONTENT_LEN (128u * 1024u - 8u)
+/* largest content the packed kernel takes (104 BLAKE3 chunks incl. the size prefix) */
+#define SD_CAS_MAX_PACKED_CONTENT_LEN (104u * 1024u - 8u)
 
 #define SD_CAS_OK 0
 #define SD_CAS_EINVAL (-1)  /* bad argument (null pointer, misaligned, too large) */

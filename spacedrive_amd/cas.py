@@ -36,7 +36,7 @@ HEADER_OR_FOOTER_SIZE = 1024 * 8
 MINIMUM_FILE_SIZE = 1024 * 100
 SAMPLED_CONTENT_LEN = 2 * HEADER_OR_FOOTER_SIZE + SAMPLE_COUNT * SAMPLE_SIZE  # 57,344
 CHUNK_SIZE = 100
-MAX_PACKED_CONTENT_LEN = 128 * 1024 - 8
+MAX_PACKED_CONTENT_LEN = 104 * 1024 - 8
 
 
 def key_to_cas_id(key: int) -> str:

@@ -5,17 +5,21 @@
 //   cas.rs:27-29) or header 8 KiB || 4 x 10 KiB samples || footer 8 KiB (cas.rs:31-58,
 //   gathered on the host); cas_id = hex(BLAKE3(M)[0..8]) (cas.rs:61).
 //
-// Mapping: ONE FILE PER LANE.  Every lane walks its own message block by block and keeps
-// the BLAKE3 chaining-value stack in registers.  For the sampled path every file has the
-// same 57 chunks, so all control flow (block loop, stack merges) is wave-uniform and
-// every lane does useful work in every cycle: 953 compressions per lane, no cross-lane
-// traffic, no LDS.  For the whole-file path files are pre-sorted by message length
-// (tiny key sort on device) so the lanes of a wave finish together.
+// Mapping: ONE FILE PER LANE.  Every lane walks its own message and keeps the BLAKE3
+// chaining-value stack in an LDS column of its own.  For the sampled path every file has
+// the same 57 chunks, so all control flow (block loop, stack merges) is wave-uniform and
+// every lane does useful work in every instruction: 953 compressions per lane, no
+// cross-lane traffic.  For the whole-file path files are pre-sorted by message length
+// (on-device key sort) so the lanes of a wave finish together.
 //
-// Memory: each lane streams its message with 4 x global_load_dwordx4 per 64-B block,
-// prefetched one block ahead so the loads overlap the ~680-instruction compression.
-// The le64(size) prefix shifts the content by exactly two 32-bit words, which becomes
-// register renaming (a 2-word carry), not byte shuffling.
+// Memory: each lane streams its message one 128-B line (a block pair, 8 x
+// global_load_dwordx4) at a time, prefetched one pair ahead.  The le64(size) prefix
+// shifts the content by exactly two 32-bit words, which becomes register renaming (a
+// 2-word carry), not byte shuffling.
+//
+// Bound: VALU issue.  On gfx950 v_alignbit_b32 / v_add3_u32 (like every 3-input or SDWA
+// VALU op except v_bitop3) issue at half rate (tools/ubench_valu.hip,
+// profiles/r01_ubench_valu.log), so a compression costs ~1014 full-rate issue slots.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -23,113 +27,6 @@
 #include "sd_kernels.h"
 
 namespace sdcas {
-
-// Shift-register CV stack: every index is a compile-time constant so it stays in VGPRs.
-template <int D>
-struct CvStack {
-  uint32_t s[D][8];
-  __device__ __forceinline__ void push(const uint32_t (&cv)[8]) {
-#pragma unroll
-    for (int d = D - 1; d > 0; --d)
-#pragma unroll
-      for (int w = 0; w < 8; ++w) s[d][w] = s[d - 1][w];
-#pragma unroll
-    for (int w = 0; w < 8; ++w) s[0][w] = cv[w];
-  }
-  __device__ __forceinline__ void pop(uint32_t (&out)[8]) {
-#pragma unroll
-    for (int w = 0; w < 8; ++w) out[w] = s[0][w];
-#pragma unroll
-    for (int d = 0; d < D - 1; ++d)
-#pragma unroll
-      for (int w = 0; w < 8; ++w) s[d][w] = s[d + 1][w];
-  }
-};
-
-// Hash M = le64(size) || content[0, clen) in this lane.  `q` = content as 16-B quads,
-// 16-B aligned.  FIXED_CLEN > 0 compiles the sampled path (every lane same length);
-// FIXED_CLEN == 0 is the general path (quad loads predicated on the content length).
-template <uint32_t FIXED_CLEN, int DEPTH>
-__device__ __forceinline__ uint64_t cas_lane(const uint4* __restrict__ q, uint32_t clen_rt,
-                                             uint64_t size) {
-  const uint32_t clen = FIXED_CLEN ? FIXED_CLEN : clen_rt;
-  const uint32_t mlen = clen + 8u;
-  const uint32_t nblocks = (mlen + 63u) >> 6;            // >= 1
-  const uint32_t nchunks = (mlen + 1023u) >> 10;         // >= 1
-
-  uint32_t carry0 = (uint32_t)size, carry1 = (uint32_t)(size >> 32);
-  uint4 a0, a1, a2, a3;
-  auto load_block = [&](uint32_t j) {
-    const uint32_t b0 = j << 6;  // content byte of quad 4j
-    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-    if (FIXED_CLEN) {
-      // sampled: block j < 896 is fully inside the content; block 896 has no content
-      if (b0 < clen) { a0 = q[4 * j]; a1 = q[4 * j + 1]; a2 = q[4 * j + 2]; a3 = q[4 * j + 3]; }
-      else { a0 = z; a1 = z; a2 = z; a3 = z; }
-    } else {
-      a0 = (b0 < clen) ? q[4 * j] : z;
-      a1 = (b0 + 16u < clen) ? q[4 * j + 1] : z;
-      a2 = (b0 + 32u < clen) ? q[4 * j + 2] : z;
-      a3 = (b0 + 48u < clen) ? q[4 * j + 3] : z;
-    }
-  };
-  load_block(0);
-
-  CvStack<DEPTH> stk;
-  uint32_t depth = 0;
-  uint32_t cv[8];
-  uint32_t j = 0;  // global block index
-  for (uint32_t c = 0; c < nchunks; ++c) {
-    const bool last = (c + 1 == nchunks);
-    const uint32_t cblocks = last ? (nblocks - 16u * c) : 16u;
-    set_iv(cv);
-    for (uint32_t b = 0; b < cblocks; ++b, ++j) {
-      uint32_t m[16];
-      m[0] = carry0; m[1] = carry1;
-      m[2] = a0.x; m[3] = a0.y; m[4] = a0.z; m[5] = a0.w;
-      m[6] = a1.x; m[7] = a1.y; m[8] = a1.z; m[9] = a1.w;
-      m[10] = a2.x; m[11] = a2.y; m[12] = a2.z; m[13] = a2.w;
-      m[14] = a3.x; m[15] = a3.y;
-      carry0 = a3.z; carry1 = a3.w;
-      const uint32_t rem = mlen - (j << 6);
-      const uint32_t blen = rem < 64u ? rem : 64u;
-      if (!FIXED_CLEN && blen < 64u) {
-        // zero message bytes past the end (the quads may hold neighbour bytes)
-#pragma unroll
-        for (int w = 0; w < 16; ++w) {
-          const int vb = (int)blen - 4 * w;
-          const uint32_t keep = vb >= 4 ? 0xFFFFFFFFu : (vb <= 0 ? 0u : ((1u << (8 * vb)) - 1u));
-          m[w] &= keep;
-        }
-      }
-      if (j + 1 < nblocks) load_block(j + 1);
-      uint32_t flags = (b == 0 ? (uint32_t)CHUNK_START : 0u) |
-                       (b + 1 == cblocks ? (uint32_t)CHUNK_END : 0u);
-      if (last && c == 0 && b + 1 == cblocks) flags |= ROOT;  // single-chunk message
-      compress(cv, m, c, 0u, blen, flags);
-    }
-    if (!last) {
-      // left-balanced tree: merge while the completed-chunk count has trailing zeros
-      uint32_t total = c + 1;
-      while ((total & 1u) == 0u) {
-        uint32_t left[8];
-        stk.pop(left);
-        --depth;
-        parent(cv, left, cv, 0u);
-        total >>= 1;
-      }
-      stk.push(cv);
-      ++depth;
-    }
-  }
-  while (depth > 0) {
-    uint32_t left[8];
-    stk.pop(left);
-    --depth;
-    parent(cv, left, cv, depth == 0 ? (uint32_t)ROOT : 0u);
-  }
-  return key_of(cv);
-}
 
 // ---- K1: the sampled path, specialised --------------------------------------------
 // Every message is le64(size) || 57,344 B: 56 full chunks (448 block PAIRS) + one 8-byte
@@ -245,18 +142,113 @@ sd_cas_sampled_kernel(const uint8_t* __restrict__ content, uint64_t stride,
   keys[f] = cas_lane_sampled(q, sizes[f], stk);
 }
 
-// K2: general path, any content length <= 2^32 - 9 (whole-file <= 102,400 or sampled),
-// files visited in `order` (sorted by length so a wave's lanes finish together).
-extern "C" __global__ void __launch_bounds__(256)
+// ---- K2: the whole-file (packed) path ------------------------------------------------
+// Ragged messages of up to PACKED_MAX_CHUNKS chunks, one file per lane, lanes visited
+// longest-first (on-device length sort) so a wave's lanes run the same trip counts.
+// Same line-batched loads as K1 (a 128-B block pair per batch, prefetched one pair
+// ahead; quads past the content are not loaded, bytes past the message are masked) and
+// an LDS CV stack (per-lane depth, word-major).
+constexpr int PACKED_DEPTH = 6;    // popcount(c) for c <= 103 completed chunks
+constexpr int PACKED_BLOCK = 256;
+
+__device__ __forceinline__ void load_pair_pred(const uint4* __restrict__ q, uint32_t P,
+                                               uint32_t clen, uint4 (&buf)[8]) {
+  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+  const uint32_t b0 = P << 7;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) buf[i] = (b0 + 16u * i < clen) ? q[8u * P + i] : z;
+}
+
+__device__ __forceinline__ void mask_tail(uint32_t (&m)[16], uint32_t blen) {
+#pragma unroll
+  for (int w = 0; w < 16; ++w) {
+    const int vb = (int)blen - 4 * w;
+    m[w] &= vb >= 4 ? 0xFFFFFFFFu : (vb <= 0 ? 0u : ((1u << (8 * vb)) - 1u));
+  }
+}
+
+__device__ __forceinline__ uint64_t cas_lane_packed(const uint4* __restrict__ q, uint32_t clen,
+                                                    uint64_t size,
+                                                    uint32_t (*stk)[8][PACKED_BLOCK], uint32_t t) {
+  const uint32_t mlen = clen + 8u;
+  const uint32_t nblocks = (mlen + 63u) >> 6;   // >= 1
+  const uint32_t nchunks = (mlen + 1023u) >> 10;
+  const uint32_t npairs = (nblocks + 1u) >> 1;
+  uint32_t c0 = (uint32_t)size, c1 = (uint32_t)(size >> 32);
+  uint4 A[8], B[8];
+  load_pair_pred(q, 0, clen, A);
+  uint32_t sp = 0;
+  uint32_t cv[8];
+  for (uint32_t c = 0; c < nchunks; ++c) {
+    const bool last = (c + 1 == nchunks);
+    const uint32_t cblocks = last ? (nblocks - 16u * c) : 16u;
+    set_iv(cv);
+    for (uint32_t b = 0; b < cblocks; b += 2) {
+      const uint32_t P = 8u * c + (b >> 1);
+      if (P + 1 < npairs) load_pair_pred(q, P + 1, clen, B);
+      const uint32_t j = 16u * c + b;  // global block index of the pair's first block
+      const bool root1 = last && c == 0;
+      {
+        uint32_t m[16] = {c0, c1, A[0].x, A[0].y, A[0].z, A[0].w, A[1].x, A[1].y,
+                          A[1].z, A[1].w, A[2].x, A[2].y, A[2].z, A[2].w, A[3].x, A[3].y};
+        const uint32_t rem = mlen - (j << 6), blen = rem < 64u ? rem : 64u;
+        if (blen < 64u) mask_tail(m, blen);
+        const bool end = (b + 1 == cblocks);
+        const uint32_t f = (b == 0 ? (uint32_t)CHUNK_START : 0u) | (end ? (uint32_t)CHUNK_END : 0u) |
+                           (end && root1 ? (uint32_t)ROOT : 0u);
+        compress(cv, m, c, 0u, blen, f);
+      }
+      if (b + 1 < cblocks) {
+        uint32_t m[16] = {A[3].z, A[3].w, A[4].x, A[4].y, A[4].z, A[4].w, A[5].x, A[5].y,
+                          A[5].z, A[5].w, A[6].x, A[6].y, A[6].z, A[6].w, A[7].x, A[7].y};
+        const uint32_t rem = mlen - ((j + 1) << 6), blen = rem < 64u ? rem : 64u;
+        if (blen < 64u) mask_tail(m, blen);
+        const bool end = (b + 2 == cblocks);
+        const uint32_t f = (end ? (uint32_t)CHUNK_END : 0u) | (end && root1 ? (uint32_t)ROOT : 0u);
+        compress(cv, m, c, 0u, blen, f);
+      }
+      c0 = A[7].z;
+      c1 = A[7].w;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) A[i] = B[i];
+    }
+    if (!last) {
+      uint32_t total = c + 1;
+      while ((total & 1u) == 0u) {
+        uint32_t left[8];
+        --sp;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) left[w] = stk[sp][w][t];
+        parent(cv, left, cv, 0u);
+        total >>= 1;
+      }
+#pragma unroll
+      for (int w = 0; w < 8; ++w) stk[sp][w][t] = cv[w];
+      ++sp;
+    }
+  }
+  while (sp > 0) {
+    uint32_t left[8];
+    --sp;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) left[w] = stk[sp][w][t];
+    parent(cv, left, cv, sp == 0 ? (uint32_t)ROOT : 0u);
+  }
+  return key_of(cv);
+}
+
+// K2: whole-file path, content length <= MAX_PACKED_CONTENT_LEN, files visited in `order`.
+extern "C" __global__ void __launch_bounds__(PACKED_BLOCK)
 sd_cas_packed_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                      const uint32_t* __restrict__ lens, const uint64_t* __restrict__ sizes,
                      const uint32_t* __restrict__ order, uint64_t n,
                      uint64_t* __restrict__ keys) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ uint32_t stack_lds[PACKED_DEPTH][8][PACKED_BLOCK];
+  const uint64_t t = (uint64_t)blockIdx.x * PACKED_BLOCK + threadIdx.x;
   if (t >= n) return;
   const uint32_t f = order ? order[t] : (uint32_t)t;
   const uint4* q = reinterpret_cast<const uint4*>(arena + offs[f]);
-  keys[f] = cas_lane<0, 7>(q, lens[f], sizes[f]);
+  keys[f] = cas_lane_packed(q, lens[f], sizes[f], stack_lds, threadIdx.x);
 }
 
 }  // namespace sdcas

@@ -16,8 +16,9 @@ static_assert(2 * HEADER_OR_FOOTER_SIZE + SAMPLE_COUNT * SAMPLE_SIZE < MINIMUM_F
 // cas.rs:21 const_assert!(SAMPLE_SIZE > HEADER_OR_FOOTER_SIZE)
 static_assert(SAMPLE_SIZE > HEADER_OR_FOOTER_SIZE, "cas.rs:21");
 
-// The packed (whole-file) kernel keeps a 7-deep CV stack: messages of <= 128 chunks.
-constexpr uint32_t MAX_PACKED_CONTENT_LEN = 128u * 1024u - 8u;
+// The packed (whole-file) kernel keeps a 6-deep CV stack: messages of <= 104 chunks
+// (a whole file is <= 102,400 + 8 bytes = 101 chunks).
+constexpr uint32_t MAX_PACKED_CONTENT_LEN = 104u * 1024u - 8u;
 
 }  // namespace sdcas
 

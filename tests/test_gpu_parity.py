@@ -67,7 +67,7 @@ def packed_arena(contents):
 
 
 EDGE_LENS = (list(range(0, 130)) + [1015, 1016, 1017, 1023, 1024, 1025, 2040, 2041, 2047, 2048,
-             4088, 4096, 16376, 32760, 65528, 102399, 102400, 57344, 130000, 128 * 1024 - 8])
+             4088, 4096, 16376, 32760, 65528, 102399, 102400, 57344, 104000, 104 * 1024 - 8])
 
 
 def test_packed_kernel_edges_vs_oracle(eng, oracle):

@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Measures the BASELINE.json configs other than bench.py's headline (one JSON line each).
+
+  --config 1  10k files (log-uniform 1 KiB..10 MiB) on tmpfs: GPU drop-in
+              (pread gather at the cas.rs offsets -> pinned -> K1/K2) vs the CPU oracle
+              (gather + hash), 1 thread and all cores.
+  --config 2  1M whole-file messages (size uniform 1..102,400) resident in HBM: K2
+              (length sort + hash), plus the CPU oracle on a sample.
+  --config 3e end-to-end sampled path from pinned host memory (PCIe-inclusive), K1 with
+              H2D of batch k+1 overlapping hashing of batch k.
+  --config 5  validator: full BLAKE3 of a resident buffer (default 64 GiB) with K3, and a
+              streamed file_checksum of a file on tmpfs (read + H2D + K3).
+Every GPU result is checked against the oracle on (a sample of) the same input.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import shutil
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+THREADS = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+
+
+def emit(d):
+    print(json.dumps(d), flush=True)
+
+
+def config1(eng, orc, n_files: int, root: str):
+    rng = np.random.default_rng(1)
+    sizes = np.exp(rng.uniform(math.log(1024), math.log(10 * 1024 * 1024), n_files)).astype(np.int64)
+    os.makedirs(root, exist_ok=True)
+    paths = []
+    for i, s in enumerate(sizes):
+        p = os.path.join(root, f"f{i:05d}")
+        with open(p, "wb") as fh:
+            fh.write(rng.integers(0, 256, int(s), dtype=np.uint8).tobytes())
+        paths.append(p)
+    total = int(sizes.sum())
+    try:
+        eng.generate_cas_keys_from_paths(paths[:64], sizes[:64])  # warm
+        t = time.perf_counter()
+        keys, errs = eng.generate_cas_keys_from_paths(paths, sizes)
+        gpu = time.perf_counter() - t
+        assert not errs.any()
+        t = time.perf_counter()
+        want = [orc.generate_cas_id(p, int(s)) for p, s in zip(paths, sizes)]
+        cpu1 = time.perf_counter() - t
+        ok = all(f"{k:016x}" == w for k, w in zip(keys, want))
+        emit({"config": 1, "files": n_files, "bytes_on_disk": total,
+              "small_fraction": float((sizes <= 102400).mean()),
+              "gpu_dropin_files_per_s": n_files / gpu, "gpu_s": gpu,
+              "cpu_oracle_1thread_files_per_s": n_files / cpu1, "parity": ok,
+              "note": "tmpfs page cache; GPU path = pread gather (16 threads) + pinned H2D + K1/K2"})
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+
+
+def config2(eng, orc, n: int, reps: int):
+    import torch
+    sizes = torch.empty(n, dtype=torch.int64, device="cuda")
+    lens = torch.empty(n, dtype=torch.int32, device="cuda")
+    offs = torch.empty(n, dtype=torch.int64, device="cuda")
+    nbytes = eng.synth_small(11, 0, n, sizes, lens, offs, None)
+    arena = torch.empty(nbytes + 64, dtype=torch.uint8, device="cuda")
+    eng.synth_small(11, 0, n, sizes, lens, offs, arena)
+    keys = torch.empty(n, dtype=torch.int64, device="cuda")
+    eng.hash_packed(arena, offs, lens, sizes, keys)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        eng.hash_packed(arena, offs, lens, sizes, keys)
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) / 1e3)
+    t = float(np.median(ts))
+    msg_bytes = int(lens.sum().item()) + 8 * n
+    blocks = ((lens.to(torch.int64) + 8 + 63) // 64)
+    chunks = ((lens.to(torch.int64) + 8 + 1023) // 1024)
+    comps = int((blocks + chunks - 1).sum().item())
+    # oracle on a sample
+    idx = np.random.default_rng(2).choice(n, 2000, replace=False)
+    h_off = offs.cpu().numpy()
+    h_len = lens.cpu().numpy()
+    h_sz = sizes.cpu().numpy().view(np.uint64)
+    k = keys.cpu().numpy().view(np.uint64)
+    sub = [(arena[h_off[i]:h_off[i] + h_len[i]].cpu().numpy().tobytes(), int(h_sz[i])) for i in idx]
+    ok = all(orc.cas_key(b, s) == k[i] for (b, s), i in zip(sub, idx))
+    t0 = time.perf_counter()
+    for b, s in sub:
+        orc.cas_key(b, s)
+    cpu1 = (time.perf_counter() - t0) / len(sub)
+    emit({"config": 2, "files": n, "message_bytes": msg_bytes, "compressions": comps,
+          "k2_ms": t * 1e3, "files_per_s": n / t, "hashed_gb_per_s": msg_bytes / t / 1e9,
+          "valu_slot_frac": comps * 1014 / 64 / t / (1024 * 2.4e9 / 2),
+          "hbm_frac": msg_bytes / t / 8e12, "parity_sample": ok,
+          "cpu_scalar_1thread_files_per_s": 1 / cpu1,
+          "cpu_scalar_all_cores_files_per_s_est": THREADS / cpu1, "cores": THREADS})
+
+
+def config3e(eng, orc, n: int, batch: int):
+    pinned = eng.alloc_pinned(n * 57344)
+    try:
+        rng = np.random.default_rng(3)
+        chunk = 1 << 26
+        for o in range(0, n * 57344, chunk):
+            m = min(chunk, n * 57344 - o)
+            pinned[o:o + m] = rng.integers(0, 256, m, dtype=np.uint8)
+        sizes = rng.integers(102401, 2 ** 40, n, dtype=np.uint64)
+        eng.hash_sampled_host(pinned[: 1024 * 57344], sizes[:1024], batch_files=batch)
+        t = time.perf_counter()
+        keys = eng.hash_sampled_host(pinned, sizes, batch_files=batch)
+        dt = time.perf_counter() - t
+        m = 4096
+        ok = bool((orc.fast_cas_keys_strided(pinned[: m * 57344], 57344, 57344, sizes[:m], THREADS)
+                   == keys[:m]).all())
+        emit({"config": "3-e2e", "files": n, "batch_files": batch, "seconds": dt,
+              "files_per_s": n / dt, "h2d_gb_per_s": n * 57344 / dt / 1e9,
+              "hashed_gb_per_s": n * 57352 / dt / 1e9, "parity_first_4096": ok,
+              "note": "PCIe-inclusive: pinned host -> HBM on a side stream, overlapped with K1"})
+    finally:
+        eng.free_pinned(pinned)
+
+
+def config5(eng, orc, gib: float, file_mb: int):
+    import torch
+    n = int(gib * (1 << 30))
+    buf = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
+    # fill on device with the synthetic generator: n // 57,344 whole 57,344-B records
+    # (never past the buffer); the < 57,344-B tail is zeroed
+    files = n // 57344
+    sz = torch.empty(max(files, 1), dtype=torch.int64, device="cuda")
+    eng.synth_sampled(5, 0, files, buf, sz, 57344)
+    buf[files * 57344:].zero_()
+    torch.cuda.synchronize()
+    eng.checksum_dev(buf, min(n, 1 << 30))
+    t = time.perf_counter()
+    digest = eng.checksum_dev(buf, n)
+    dt = time.perf_counter() - t
+    # parity on a 1 GiB prefix (full 64 GiB on one CPU thread would take minutes)
+    pre = 1 << 30
+    d1 = eng.checksum_dev(buf, pre)
+    ok = d1 == orc.blake3(buf[:pre].cpu().numpy().tobytes()).hex()
+    comps = n // 64 + n // 1024
+    emit({"config": 5, "bytes": n, "seconds": dt, "gb_per_s": n / dt / 1e9, "digest": digest,
+          "valu_slot_frac": comps * 1014 / 64 / dt / (1024 * 2.4e9 / 2), "hbm_frac": n / dt / 8e12,
+          "parity_1gib_prefix": ok})
+    del buf
+    torch.cuda.empty_cache()
+    # streamed file_checksum through pinned staging (tmpfs file)
+    path = "/dev/shm/sdcas_validator.bin"
+    try:
+        rng = np.random.default_rng(5)
+        with open(path, "wb") as fh:
+            for _ in range(file_mb // 64):
+                fh.write(rng.integers(0, 256, 64 << 20, dtype=np.uint8).tobytes())
+        eng.file_checksum(path)
+        t = time.perf_counter()
+        h = eng.file_checksum(path)
+        dt = time.perf_counter() - t
+        t = time.perf_counter()
+        w = orc.file_checksum(path)
+        cpu = time.perf_counter() - t
+        emit({"config": "5-file", "bytes": os.path.getsize(path), "gpu_seconds": dt,
+              "gpu_gb_per_s": os.path.getsize(path) / dt / 1e9, "cpu_oracle_1thread_gb_per_s":
+              os.path.getsize(path) / cpu / 1e9, "parity": h == w})
+    finally:
+        if os.path.exists(path):
+            os.unlink(path)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", action="append", required=True)
+    ap.add_argument("--c1-files", type=int, default=10_000)
+    ap.add_argument("--c2-files", type=int, default=1_000_000)
+    ap.add_argument("--c3-files", type=int, default=200_000)
+    ap.add_argument("--c3-batch", type=int, default=32768)
+    ap.add_argument("--c5-gib", type=float, default=64.0)
+    ap.add_argument("--c5-file-mb", type=int, default=4096)
+    a = ap.parse_args()
+    import torch  # noqa: F401
+
+    from oracle.pyoracle import Oracle
+    from spacedrive_amd import CasEngine
+    eng = CasEngine(0)
+    orc = Oracle()
+    for c in a.config:
+        if c == "1":
+            config1(eng, orc, a.c1_files, "/dev/shm/sdcas_c1")
+        elif c == "2":
+            config2(eng, orc, a.c2_files, 5)
+        elif c == "3e":
+            config3e(eng, orc, a.c3_files, a.c3_batch)
+        elif c == "5":
+            config5(eng, orc, a.c5_gib, a.c5_file_mb)
+
+
+if __name__ == "__main__":
+    main()

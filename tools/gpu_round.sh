@@ -1,0 +1,15 @@
+#!/bin/bash
+# Full GPU pass: parity suite, smoke, headline bench, rocprofv3 kernel stats of the bench,
+# the other BASELINE configs.  Each GPU step has its own time limit; stop at first failure.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/round
+mkdir -p $OUT
+cd $R
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; exit 1; }
+timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo SMOKE_FAIL; exit 1; }
+timeout -k 10 400 python3 -u bench.py > $OUT/bench.log 2>&1 || { echo BENCH_FAIL; exit 1; }
+timeout -k 10 900 python3 -u tools/bench_configs.py ${CONFIGS:---config 2 --config 3e --config 5 --config 1} > $OUT/configs.log 2>&1 || { echo CONFIGS_FAIL; exit 1; }
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench --output-format csv -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu-baseline > $OUT/bench_prof.log 2>&1 || { echo PROF_FAIL; exit 1; }
+echo ROUND_OK
