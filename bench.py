@@ -32,8 +32,13 @@ MSG_BYTES = 57352            # le64(size) || 57,344 sampled bytes
 COMPRESSIONS = 953           # 897 chunk blocks + 56 parents per sampled message
 SPEC_OPS = 792               # int32 ops per compression (7 rounds x 8 G x 14 + 8)
 HW_OPS = 680                 # VALU instructions per compression as compiled (add3/alignbit)
+# Issue slots per wave-compression: 230 v_xor + 112 v_add (full rate, 1 slot) and
+# 224 v_alignbit + 112 v_add3 (half rate on gfx950, 2 slots; profiles/r01_ubench_valu.log)
+SLOTS = 230 + 112 + 2 * (224 + 112)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # 256 CUs x 4 SIMD32 x 32 lanes x 2.4 GHz = 78.6
+# full-rate wave64 VALU issue: 1024 SIMDs x 2.4 GHz / 2 cycles = 1228.8 G slots/s
+SLOT_PEAK_G = 1024 * 2.4e9 / 2 / 1e9
 
 
 def main() -> None:
@@ -121,14 +126,17 @@ def main() -> None:
     achieved = F * MSG_BYTES / (kern_ms / 1e3) / 1e9  # per-GPU kernel GB/s
     valu = F * COMPRESSIONS * SPEC_OPS / (kern_ms / 1e3) / 1e12
     valu_hw = F * COMPRESSIONS * HW_OPS / (kern_ms / 1e3) / 1e12
+    slots = F * COMPRESSIONS * SLOTS / 64 / (kern_ms / 1e3) / 1e9  # G wave-issue-slots/s
 
+    # HBM bytes per launch from PMC (TCC_MISS_sum x 128-B lines, committed summary of the
+    # separate rocprofv3 --pmc pass on the same kernel), scaled to this launch's files
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_sampled_kernel.json")
     if os.path.exists(pmc):
         with open(pmc) as fh:
-            traffic = json.load(fh).get("hbm_bytes_per_launch_per_file")
-            if traffic is not None:
-                traffic = traffic * F
+            per_file = json.load(fh).get("hbm_bytes_per_file")
+            if per_file is not None:
+                traffic = per_file * F
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -158,18 +166,25 @@ def main() -> None:
                 "objects": objects,
             },
             "roofline": {
+                # K1 is bound by VALU issue, not HBM: BLAKE3's rotates (v_alignbit_b32) and
+                # 3-input adds (v_add3_u32) issue at half rate on gfx950 (measured), so the
+                # roof is full-rate wave64 issue slots; the HBM view is in "hbm".
                 "kernel": "sd_cas_sampled_kernel",
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
+                "bound": "valu",
+                "achieved": slots,
+                "peak": SLOT_PEAK_G,
+                "unit": "G wave-issue-slots/s",
+                "frac": slots / SLOT_PEAK_G,
                 "traffic": traffic,
                 "kernel_ms": kern_ms,
-                "algorithmic_bytes_per_launch": F * MSG_BYTES,
-                "valu": {"achieved_spec_tops": valu, "achieved_hw_tops": valu_hw,
-                         "peak_tops": VALU_PEAK_TOPS, "frac_spec": valu / VALU_PEAK_TOPS,
-                         "frac_hw": valu_hw / VALU_PEAK_TOPS},
+                "work_per_file": {"message_bytes": MSG_BYTES, "compressions": COMPRESSIONS,
+                                  "issue_slots_per_wave_compression": SLOTS},
+                "hbm": {"achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS,
+                        "algorithmic_bytes_per_launch": F * MSG_BYTES,
+                        "traffic_over_algorithmic": (traffic / (F * MSG_BYTES)) if traffic else None},
+                "int_ops": {"achieved_spec_tops": valu, "achieved_hw_instr_tops": valu_hw,
+                            "peak_full_rate_tops": VALU_PEAK_TOPS},
             },
             "cpu_baseline": cpu,
         }
