@@ -17,6 +17,7 @@ from .cas import (  # noqa: F401
     file_checksum,
     generate_cas_id,
     generate_cas_ids,
+    get_shard_hex,
     identifier_job_step,
     key_to_cas_id,
 )

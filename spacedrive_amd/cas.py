@@ -345,3 +345,9 @@ def identifier_job_step(paths: Sequence[str], chunk: int = CHUNK_SIZE,
             res.object_of[i] = i
             res.total_created += 1
     return res
+
+
+def get_shard_hex(cas_id: str) -> str:
+    """Thumbnail shard directory of a cas_id: its first three hex chars
+    (core/src/object/media/thumbnail/shard.rs:10-13), 4096 shards 000..fff."""
+    return cas_id[0:3]

@@ -289,3 +289,30 @@ def test_sampled_host_pipeline(eng, oracle):
     sizes = rng.integers(MINIMUM_FILE_SIZE + 1, 2 ** 40, 300, dtype=np.uint64)
     assert (eng.hash_sampled_host(host, sizes, batch_files=128) ==
             oracle.cas_keys_strided(host, SAMPLED_CONTENT_LEN, SAMPLED_CONTENT_LEN, sizes)).all()
+
+
+def test_sharded_group_rccl_world1(eng, oracle):
+    """The multi-GPU grouping path (spacedrive_amd/shard.py) on the GPU with the nccl (= RCCL)
+    backend: world size 1 here (one GPU per box); the world-2/4 exchange logic is covered
+    with gloo in tests/test_shard_cpu.py."""
+    import socket
+
+    import torch.distributed as dist
+
+    from spacedrive_amd.shard import HipShardOps, sharded_group
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        rng = np.random.default_rng(13)
+        pool = rng.integers(0, 2 ** 64, 40_000, dtype=np.uint64)
+        keys = pool[rng.integers(0, len(pool), 100_000)]
+        res = sharded_group(dev64(keys), 5_000_000, HipShardOps(eng))
+        orep, oobj = oracle.group_canonical(keys)
+        assert res.objects == oobj
+        assert (res.rep.cpu().numpy() == orep.astype(np.int64) + 5_000_000).all()
+    finally:
+        dist.destroy_process_group()

@@ -8,6 +8,8 @@
               (length sort + hash), plus the CPU oracle on a sample.
   --config 3e end-to-end sampled path from pinned host memory (PCIe-inclusive), K1 with
               H2D of batch k+1 overlapping hashing of batch k.
+  --config 4  one rank's share of the 100M-file library (12.5M files, 30 % duplicates):
+              K1 over resident batches, then Object grouping of all 12.5M keys.
   --config 5  validator: full BLAKE3 of a resident buffer (default 64 GiB) with K3, and a
               streamed file_checksum of a file on tmpfs (read + H2D + K3).
 Every GPU result is checked against the oracle on (a sample of) the same input.
@@ -132,6 +134,53 @@ def config3e(eng, orc, n: int, batch: int):
         eng.free_pinned(pinned)
 
 
+def config4(eng, orc, n_total: int, batch: int, dup: int):
+    """One rank's share of the 100M-file / 8-GPU library (12.5M files): hash in resident
+    batches of `batch` files (content regenerated per batch on the device, untimed), keep
+    all keys, then group all of them (radix sort + runs).  Grouping is checked against the
+    generator's duplicate truth for every file."""
+    import torch
+    content = torch.empty((batch, 57344), dtype=torch.uint8, device="cuda")
+    sizes = torch.empty(batch, dtype=torch.int64, device="cuda")
+    keys = torch.empty(n_total, dtype=torch.int64, device="cuda")
+    hash_s = 0.0
+    for f0 in range(0, n_total, batch):
+        m = min(batch, n_total - f0)
+        eng.synth_sampled(44, f0, m, content, sizes, 57344, dup_permille=dup)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        eng.hash_sampled(content, sizes, keys[f0:f0 + m], n=m)
+        b.record()
+        torch.cuda.synchronize()
+        hash_s += a.elapsed_time(b) / 1e3
+    del content
+    rep = torch.empty(n_total, dtype=torch.int32, device="cuda")
+    eng.group(keys, rep)  # warm (workspace)
+    ts = []
+    for _ in range(3):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        eng.group(keys, rep, want_objects=False)
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) / 1e3)
+    gs = float(np.median(ts))
+    objects = eng.group(keys, rep)
+    roots = torch.empty(n_total, dtype=torch.int64, device="cuda")
+    eng.synth_roots(44, 0, n_total, roots, dup_permille=dup)
+    r = roots.cpu().numpy()
+    uniq, inv = np.unique(r, return_inverse=True)
+    first = np.full(len(uniq), n_total, dtype=np.int64)
+    np.minimum.at(first, inv, np.arange(n_total))
+    ok = objects == len(uniq) and bool((rep.cpu().numpy() == first[inv]).all())
+    sort_bytes = 8 * (8 + 12 + 12) * n_total  # per pass: upsweep key read + (key,idx) read + write
+    emit({"config": "4-rank-share", "files": n_total, "dup_permille": dup,
+          "hash_kernel_s": hash_s, "hash_files_per_s": n_total / hash_s,
+          "group_s": gs, "group_keys_per_s": n_total / gs,
+          "sort_hbm_gb_per_s_algorithmic": sort_bytes / gs / 1e9, "objects": objects,
+          "grouping_equals_duplicate_truth": ok})
+
+
 def config5(eng, orc, gib: float, file_mb: int):
     import torch
     n = int(gib * (1 << 30))
@@ -186,6 +235,8 @@ def main():
     ap.add_argument("--c2-files", type=int, default=1_000_000)
     ap.add_argument("--c3-files", type=int, default=200_000)
     ap.add_argument("--c3-batch", type=int, default=32768)
+    ap.add_argument("--c4-files", type=int, default=12_500_000)
+    ap.add_argument("--c4-batch", type=int, default=1_250_000)
     ap.add_argument("--c5-gib", type=float, default=64.0)
     ap.add_argument("--c5-file-mb", type=int, default=4096)
     a = ap.parse_args()
@@ -202,6 +253,8 @@ def main():
             config2(eng, orc, a.c2_files, 5)
         elif c == "3e":
             config3e(eng, orc, a.c3_files, a.c3_batch)
+        elif c == "4":
+            config4(eng, orc, a.c4_files, a.c4_batch, 300)
         elif c == "5":
             config5(eng, orc, a.c5_gib, a.c5_file_mb)
 
