@@ -108,7 +108,8 @@ int sd_cas_hash_sampled_dev(sd_cas_ctx* ctx, const void* d_content, uint64_t str
 
 /* K2 packed path: content i at d_arena + d_offs[i] (16-B aligned), d_lens[i] bytes
  * (<= SD_CAS_MAX_PACKED_CONTENT_LEN); the arena must be readable up to the 16-B round-up
- * of every content end.  Files are visited longest-first via an on-device length sort
+ * of every content end and for at least 16 bytes from every content start (an empty
+ * content included).  Files are visited longest-first via an on-device length sort
  * (workspace in ctx). */
 int sd_cas_hash_packed_dev(sd_cas_ctx* ctx, const void* d_arena, const uint64_t* d_offs,
                            const uint32_t* d_lens, const uint64_t* d_sizes, size_t n,

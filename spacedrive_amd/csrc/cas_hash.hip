@@ -151,12 +151,15 @@ sd_cas_sampled_kernel(const uint8_t* __restrict__ content, uint64_t stride,
 constexpr int PACKED_DEPTH = 6;    // popcount(c) for c <= 103 completed chunks
 constexpr int PACKED_BLOCK = 256;
 
+// Always 8 x 16-B loads: a quad past the content is re-pointed at quad 0 (in bounds; an
+// empty content still has 16 readable bytes, see the ABI) instead of being predicated off
+// — a `cond ? q[i] : 0` load is lowered to four dword loads per quad.  Its garbage can
+// only reach the message's final block, which mask_tail() zeroes past the end.
 __device__ __forceinline__ void load_pair_pred(const uint4* __restrict__ q, uint32_t P,
                                                uint32_t clen, uint4 (&buf)[8]) {
-  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
   const uint32_t b0 = P << 7;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) buf[i] = (b0 + 16u * i < clen) ? q[8u * P + i] : z;
+  for (int i = 0; i < 8; ++i) buf[i] = q[(b0 + 16u * i < clen) ? 8u * P + i : 0u];
 }
 
 __device__ __forceinline__ void mask_tail(uint32_t (&m)[16], uint32_t blen) {
@@ -256,12 +259,27 @@ sd_cas_packed_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restri
 // ---- host launchers ----------------------------------------------------------------
 namespace sdcas {
 
-// descending block-count key so the longest messages start first and a wave's lanes
-// have (nearly) equal trip counts
+// Sort key for the K2 visiting order: (window of LEN_WINDOW consecutive files, descending
+// block count).  Inside a window the lanes of a wave get (nearly) equal trip counts; the
+// window keeps a wave's 64 lanes inside ~LEN_WINDOW files of the arena instead of spread
+// over all of it (a global length sort scattered every wave over the whole arena and
+// thrashed address translation: 4x slower on 1M files / 51 GB).
+constexpr uint32_t LEN_WINDOW_LOG2 = 10;
+constexpr uint32_t LEN_BITS = 11;  // block count <= 1664 < 2048
+
 extern "C" __global__ void __launch_bounds__(256)
 sd_cas_length_keys(const uint32_t* __restrict__ lens, uint64_t n, uint64_t* __restrict__ out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = 0xFFFFull - (((uint64_t)lens[i] + 8u + 63u) >> 6);
+  if (i < n) {
+    const uint64_t nb = ((uint64_t)lens[i] + 8u + 63u) >> 6;
+    out[i] = ((i >> LEN_WINDOW_LOG2) << LEN_BITS) | (((1ull << LEN_BITS) - 1) - nb);
+  }
+}
+
+int length_key_bits(uint64_t n) {
+  int w = 0;
+  while ((1ull << w) <= (n >> LEN_WINDOW_LOG2)) ++w;
+  return (int)LEN_BITS + w;
 }
 
 hipError_t hash_sampled(const uint8_t* content, uint64_t stride, const uint64_t* sizes,

@@ -219,7 +219,7 @@ int sd_cas_hash_packed_dev(sd_cas_ctx* c, const void* d_arena, const uint64_t* d
   uint32_t* order = (uint32_t*)(p + 2 * kb);
   void* sws = p + 2 * kb + ob;
   HIP_TRY(c, length_keys(d_lens, n, lkeys, s));
-  HIP_TRY(c, radix_sort_pairs(lkeys, nullptr, skeys, order, n, 0, 16, sws, s));
+  HIP_TRY(c, radix_sort_pairs(lkeys, nullptr, skeys, order, n, 0, length_key_bits(n), sws, s));
   HIP_TRY(c, hash_packed((const uint8_t*)d_arena, d_offs, d_lens, d_sizes, order, n, d_keys, s));
   return SD_CAS_OK;
 }

@@ -30,4 +30,5 @@ hipError_t hash_packed(const uint8_t* arena, const uint64_t* offs, const uint32_
                        const uint64_t* sizes, const uint32_t* order, uint64_t n, uint64_t* keys,
                        hipStream_t s);
 hipError_t length_keys(const uint32_t* lens, uint64_t n, uint64_t* out, hipStream_t s);
+int length_key_bits(uint64_t n);  // significant bits of the length_keys sort key
 }  // namespace sdcas
