@@ -7,7 +7,10 @@ duplicate content) with K1 and groups the cas keys into Objects — locally on o
 by key-range all-to-all over RCCL on several.  Inputs are synthesized on the device
 before the timed region (data: synthetic) and are resident in HBM when it starts.
 Weak scaling: FILES_PER_GPU (default 1.25M = 71.7 GB/GPU) per rank per step, so one step
-at 8 GPUs is the 10M-file headline job.
+at 8 GPUs is the 10M-file headline job.  Steps are pipelined the way a production job
+would run them: step i's grouping (incl. its RCCL exchange) runs on a side stream while
+step i+1 is hashed; every step's hash AND grouping complete inside the timed region
+(--no-overlap serialises them).
 
 Output: ONE JSON line on rank 0 (driver contract), with
   roofline      — K1 (sd_cas_sampled_kernel), timed by HIP events on its own stream:
@@ -51,6 +54,8 @@ def main() -> None:
     ap.add_argument("--seed", type=int, default=0x5DCA50004)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-overlap", dest="overlap", action="store_false",
+                    help="group step i before hashing step i+1 (default: overlap them)")
     args = ap.parse_args()
 
     import numpy as np
@@ -73,38 +78,65 @@ def main() -> None:
     dev = torch.device("cuda", local)
     content = torch.empty((F, 57344), dtype=torch.uint8, device=dev)
     sizes = torch.empty(F, dtype=torch.int64, device=dev)
-    keys = torch.empty(F, dtype=torch.int64, device=dev)
+    # keys double-buffered: step i's grouping (side stream) overlaps step i+1's hashing
+    keys = [torch.empty(F, dtype=torch.int64, device=dev) for _ in range(2)]
     rep = torch.empty(F, dtype=torch.int32, device=dev)
     eng.synth_sampled(args.seed, file0, F, content, sizes, 57344, dup_permille=args.dup_permille)
     torch.cuda.synchronize()
     ops = HipShardOps(eng)
+    main = torch.cuda.current_stream()
+    side = torch.cuda.Stream()
+    hashed = [torch.cuda.Event() for _ in range(2)]
+    grouped = [torch.cuda.Event() for _ in range(2)]
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
+    results = []
 
-    def step(i: int, timed: bool):
-        if timed:
-            ev[i][0].record()
-        eng.hash_sampled(content, sizes, keys)            # K1 on torch's current stream
-        if timed:
-            ev[i][1].record()
-        if world == 1:
-            return eng.group(keys, rep, want_objects=False)  # K4 + K5, stays async
-        return sharded_group(keys, file0, ops)
+    def group(i: int):
+        """Object grouping of step i's keys on the side stream (RCCL exchange at N > 1)."""
+        with torch.cuda.stream(side):
+            side.wait_event(hashed[i % 2])
+            if world == 1:
+                eng.group(keys[i % 2], rep, want_objects=False)  # K4 + K5, async
+            else:
+                results.append(sharded_group(keys[i % 2], file0, ops))
+            grouped[i % 2].record(side)
 
-    for i in range(args.warmup):
-        step(i, False)
+    def run(n: int, timed: bool):
+        if n == 0:
+            return
+        for i in range(n):
+            if i >= 2:
+                main.wait_event(grouped[i % 2])  # keys[i % 2] free again
+            if timed:
+                ev[i][0].record(main)
+            eng.hash_sampled(content, sizes, keys[i % 2])      # K1 on the main stream
+            if timed:
+                ev[i][1].record(main)
+            hashed[i % 2].record(main)
+            if args.overlap:
+                if i >= 1:
+                    group(i - 1)
+            else:
+                group(i)
+        if args.overlap:
+            group(n - 1)
+
+    run(args.warmup, False)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    results.clear()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        res = step(i, True)
+    run(args.steps, True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    keys = keys[(args.steps - 1) % 2]
+    res = results[-1] if results else None
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     km = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
@@ -163,6 +195,8 @@ def main() -> None:
                 "files_per_gpu": F,
                 "dup_permille": args.dup_permille,
                 "parallelism": f"shard-by-file x{world}" + (" + RCCL key-range all-to-all" if world > 1 else ""),
+                "pipeline": ("grouping of step i on a side stream overlaps hashing of step i+1"
+                             if args.overlap else "hash then group, serial"),
                 "objects": objects,
             },
             "roofline": {

@@ -19,19 +19,62 @@ namespace sdcas {
 
 constexpr int GROUP = 256;  // chunks (or CVs) reduced per workgroup
 
-// CV (or ROOT digest) of one chunk of `clen` <= 1024 bytes at global chunk index `ctr`.
+// CV of one FULL 1 KiB chunk (never a root: a one-chunk input takes chunk_cv below).
+// 8 pair loads (128-B lines) issued one pair ahead, ping-ponged in registers like K1.
+__device__ __forceinline__ void full_chunk_cv(const uint4* __restrict__ q, uint64_t ctr,
+                                              uint32_t (&cv)[8]) {
+  set_iv(cv);
+  uint4 A[8], B[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) A[i] = q[i];
+#pragma unroll 1
+  for (uint32_t p = 0; p < 8; p += 2) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) B[i] = q[8u * (p + 1) + i];
+    {
+      const uint32_t m[16] = {A[0].x, A[0].y, A[0].z, A[0].w, A[1].x, A[1].y, A[1].z, A[1].w,
+                              A[2].x, A[2].y, A[2].z, A[2].w, A[3].x, A[3].y, A[3].z, A[3].w};
+      compress(cv, m, (uint32_t)ctr, (uint32_t)(ctr >> 32), BLOCK_LEN, p == 0 ? (uint32_t)CHUNK_START : 0u);
+    }
+    {
+      const uint32_t m[16] = {A[4].x, A[4].y, A[4].z, A[4].w, A[5].x, A[5].y, A[5].z, A[5].w,
+                              A[6].x, A[6].y, A[6].z, A[6].w, A[7].x, A[7].y, A[7].z, A[7].w};
+      compress(cv, m, (uint32_t)ctr, (uint32_t)(ctr >> 32), BLOCK_LEN, 0u);
+    }
+    if (p + 2 < 8) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) A[i] = q[8u * (p + 2) + i];
+    }
+    {
+      const uint32_t m[16] = {B[0].x, B[0].y, B[0].z, B[0].w, B[1].x, B[1].y, B[1].z, B[1].w,
+                              B[2].x, B[2].y, B[2].z, B[2].w, B[3].x, B[3].y, B[3].z, B[3].w};
+      compress(cv, m, (uint32_t)ctr, (uint32_t)(ctr >> 32), BLOCK_LEN, 0u);
+    }
+    {
+      const uint32_t m[16] = {B[4].x, B[4].y, B[4].z, B[4].w, B[5].x, B[5].y, B[5].z, B[5].w,
+                              B[6].x, B[6].y, B[6].z, B[6].w, B[7].x, B[7].y, B[7].z, B[7].w};
+      compress(cv, m, (uint32_t)ctr, (uint32_t)(ctr >> 32), BLOCK_LEN,
+               p == 6 ? (uint32_t)CHUNK_END : 0u);
+    }
+  }
+}
+
+// CV (or ROOT digest) of one chunk of `clen` <= 1024 bytes at global chunk index `ctr`
+// (the input's last chunk; partial or empty).  Quads past the end are re-pointed at quad 0
+// (in bounds) and the final block is masked, as in K2.
 __device__ __forceinline__ void chunk_cv(const uint4* __restrict__ q, uint32_t clen, uint64_t ctr,
                                          bool root, uint32_t (&cv)[8]) {
   const uint32_t nblk = clen == 0 ? 1u : (clen + 63u) >> 6;
   set_iv(cv);
   const uint4 z = make_uint4(0u, 0u, 0u, 0u);
   uint4 a0, a1, a2, a3;
+  (void)z;
   auto load = [&](uint32_t b) {
     const uint32_t o = b << 6;
-    a0 = (o < clen) ? q[4 * b] : z;
-    a1 = (o + 16u < clen) ? q[4 * b + 1] : z;
-    a2 = (o + 32u < clen) ? q[4 * b + 2] : z;
-    a3 = (o + 48u < clen) ? q[4 * b + 3] : z;
+    a0 = q[(o < clen) ? 4 * b : 0u];
+    a1 = q[(o + 16u < clen) ? 4 * b + 1 : 0u];
+    a2 = q[(o + 32u < clen) ? 4 * b + 2 : 0u];
+    a3 = q[(o + 48u < clen) ? 4 * b + 3 : 0u];
   };
   load(0);
   for (uint32_t b = 0; b < nblk; ++b) {
@@ -102,8 +145,11 @@ sd_b3_chunk_groups(const uint8_t* __restrict__ data, uint64_t len, uint64_t chun
     const uint64_t off = c << 10;
     const uint32_t clen = (uint32_t)min((uint64_t)1024, len - off);
     uint32_t cv[8];
-    chunk_cv(reinterpret_cast<const uint4*>(data + off), clen, chunk0 + c,
-             whole_tree && nchunks == 1, cv);
+    if (clen == 1024 && nchunks > 1)
+      full_chunk_cv(reinterpret_cast<const uint4*>(data + off), chunk0 + c, cv);
+    else
+      chunk_cv(reinterpret_cast<const uint4*>(data + off), clen, chunk0 + c,
+               whole_tree && nchunks == 1, cv);
 #pragma unroll
     for (int w = 0; w < 8; ++w) cvs[t][w] = cv[w];
   }
