@@ -112,10 +112,19 @@ impl HipCas {
         Ok(unsafe { CStr::from_ptr(out.as_ptr()) }.to_string_lossy().into_owned())
     }
 
-    #[doc(hidden)]
-    pub fn raw(&mut self) -> *mut sd_cas_ctx {
-        let _ = sd_cas_group_dev as unsafe extern "C" fn(_, _, _, _, _, _) -> _;
-        self.ctx
+    /// Canonical Object grouping of device-resident keys (see `sd_cas_group_dev`); returns
+    /// the number of Objects.  `d_keys`/`d_rep` are device pointers owned by the caller.
+    ///
+    /// # Safety
+    /// `d_keys` must point to `n` u64 and `d_rep` to `n` u32 in device memory of this
+    /// context's GPU.
+    pub unsafe fn group_dev(&mut self, d_keys: *const u64, n: usize, d_rep: *mut u32) -> io::Result<u64> {
+        let mut objects = 0u64;
+        let rc = sd_cas_group_dev(self.ctx, d_keys, n, d_rep, &mut objects, ptr::null_mut());
+        if rc != 0 {
+            return Err(self.err(rc));
+        }
+        Ok(objects)
     }
 }
 

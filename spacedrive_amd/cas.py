@@ -318,7 +318,7 @@ def identifier_job_step(paths: Sequence[str], chunk: int = CHUNK_SIZE,
     for i in range(len(paths)):
         if i in res.errors:
             continue
-        res.metadata[i] = FileMetadata(None if sizes[i] == 0 else None, sizes[i])
+        res.metadata[i] = FileMetadata(None, sizes[i])  # cas_id filled below for hashed files
     ok = [j for j, i in enumerate(live) if not errs[j]]
     for j in ok:
         res.metadata[live[j]].cas_id = key_to_cas_id(keys[j])
