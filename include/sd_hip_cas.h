@@ -148,6 +148,31 @@ int sd_cas_checksum_dev(sd_cas_ctx* ctx, const void* d_data, uint64_t len, uint8
  * Returns SD_CAS_EIO with *err_no set on an I/O error. */
 int sd_cas_file_checksum(sd_cas_ctx* ctx, const char* path, char out_hex[65], int* err_no);
 
+/* ---- multi-device, single process -------------------------------------
+ * One context per shard; shard i lives on devices[i] (a device may host several shards).
+ * Grouping pulls each shard's key range from every other shard with peer copies over
+ * xGMI (hipMemcpyPeerAsync, event-ordered across devices), then groups locally; the
+ * multi-process form of the same exchange uses RCCL all-to-all (spacedrive_amd/shard.py). */
+typedef struct sd_cas_multi sd_cas_multi;
+int sd_cas_multi_create(const int* devices, int ndev, sd_cas_multi** out);
+void sd_cas_multi_destroy(sd_cas_multi* m);
+int sd_cas_multi_count(const sd_cas_multi* m);
+sd_cas_ctx* sd_cas_multi_ctx(sd_cas_multi* m, int i);
+const char* sd_cas_multi_last_error(const sd_cas_multi* m);
+/* Canonical grouping across shards: shard i holds n[i] keys (device pointer on its
+ * device) for files file0[i] .. file0[i]+n[i]-1 (file0 ascending, ranges disjoint);
+ * d_rep[i][k] (u64, device) = global idx of the file owning key k's Object;
+ * *out_objects = total Objects.  Blocking. */
+int sd_cas_multi_group(sd_cas_multi* m, const uint64_t* const* d_keys, const size_t* n,
+                       const uint64_t* file0, uint64_t* const* d_rep, uint64_t* out_objects);
+/* End to end from host memory: n sampled contents (57,344 B at h_content + i*stride) are
+ * split into contiguous shards, streamed to their devices (H2D overlapped with K1, all
+ * devices in flight), hashed and grouped.  h_keys[i] = cas key, h_rep[i] (optional) =
+ * global idx of the file owning file i's Object.  Blocking. */
+int sd_cas_multi_hash_group_sampled_host(sd_cas_multi* m, const void* h_content, uint64_t stride,
+                                         const uint64_t* h_sizes, size_t n, uint64_t* h_keys,
+                                         uint64_t* h_rep, uint64_t* out_objects);
+
 /* ---- synthetic inputs (benchmarks / tests; same generator as oracle/cas_ref.c) ------- */
 int sd_cas_synth_sampled_dev(sd_cas_ctx* ctx, uint64_t seed, uint64_t file0, size_t n,
                              uint32_t dup_permille, void* d_content, uint64_t stride,

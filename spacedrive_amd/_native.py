@@ -42,6 +42,13 @@ SIGNATURES = [
     ("sd_cas_sort_pairs_dev", _i, [_vp, _vp, _vp, _sz, _vp, _vp, _i, _i, _vp]),
     ("sd_cas_checksum_dev", _i, [_vp, _vp, _u64, _vp, _vp]),
     ("sd_cas_file_checksum", _i, [_vp, _cp, _cp, ctypes.POINTER(_i)]),
+    ("sd_cas_multi_create", _i, [_vp, _i, ctypes.POINTER(_vp)]),
+    ("sd_cas_multi_destroy", None, [_vp]),
+    ("sd_cas_multi_count", _i, [_vp]),
+    ("sd_cas_multi_ctx", _vp, [_vp, _i]),
+    ("sd_cas_multi_last_error", _cp, [_vp]),
+    ("sd_cas_multi_group", _i, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    ("sd_cas_multi_hash_group_sampled_host", _i, [_vp, _vp, _u64, _vp, _sz, _vp, _vp, _vp]),
     ("sd_cas_synth_sampled_dev", _i, [_vp, _u64, _u64, _sz, _u32, _vp, _u64, _vp, _vp]),
     ("sd_cas_synth_small_dev", _i, [_vp, _u64, _u64, _sz, _u32, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("sd_cas_synth_roots_dev", _i, [_vp, _u64, _u64, _sz, _u32, _vp, _vp]),

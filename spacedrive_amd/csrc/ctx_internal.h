@@ -1,0 +1,92 @@
+// ctx_internal.h — the sd_cas_ctx object and the host helpers shared by the C-ABI
+// translation units (sd_hip_cas.cpp, sd_multi.cpp).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+
+#include <algorithm>
+#include <string>
+
+#include "../../include/sd_hip_cas.h"
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+struct sd_cas_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;  // compute
+  hipStream_t copy = nullptr;    // H2D side stream
+  hipEvent_t h2d_done = nullptr;
+  DevBuf ws;       // kernel workspace
+  DevBuf staging;  // device copy of a host batch
+  DevBuf small;    // multi-device exchange buffers (sd_cas_multi_*)
+  void* pinned = nullptr;
+  size_t pinned_bytes = 0;
+  uint64_t* d_scalar = nullptr;  // 8 x u64 scratch for counters
+  std::string err;
+};
+
+inline int sd_fail(sd_cas_ctx* c, int code, const char* fmt, ...) {
+  if (c) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    c->err = buf;
+  }
+  return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                   \
+  do {                                                                                       \
+    hipError_t e_ = (expr);                                                                  \
+    if (e_ != hipSuccess)                                                                    \
+      return sd_fail((ctx), SD_CAS_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                     __FILE__, __LINE__);                                                    \
+  } while (0)
+
+// NULL = the HIP null (default) stream, exactly as in HIP itself: a caller on the
+// default stream (torch's default) must be ordered with our kernels.
+inline hipStream_t sd_pick(sd_cas_ctx*, void* s) { return (hipStream_t)s; }
+inline size_t up16(size_t x) { return (x + 15) & ~(size_t)15; }
+inline size_t up256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Grow a device buffer (on the CURRENT device).  Growing synchronises the device: call
+// outside hot loops / graph capture.
+inline int sd_ensure(sd_cas_ctx* c, DevBuf& b, size_t bytes) {
+  if (bytes <= b.bytes) return SD_CAS_OK;
+  if (b.p) {
+    HIP_TRY(c, hipDeviceSynchronize());
+    HIP_TRY(c, hipFree(b.p));
+    b.p = nullptr;
+    b.bytes = 0;
+  }
+  size_t want = std::max(bytes, (size_t)1 << 20);
+  if (hipMalloc(&b.p, want) != hipSuccess) {
+    (void)hipGetLastError();
+    return sd_fail(c, SD_CAS_ENOMEM, "hipMalloc(%zu) failed", want);
+  }
+  b.bytes = want;
+  return SD_CAS_OK;
+}
+
+inline int sd_ensure_pinned(sd_cas_ctx* c, size_t bytes) {
+  if (bytes <= c->pinned_bytes) return SD_CAS_OK;
+  if (c->pinned) {
+    HIP_TRY(c, hipDeviceSynchronize());
+    HIP_TRY(c, hipHostFree(c->pinned));
+    c->pinned = nullptr;
+    c->pinned_bytes = 0;
+  }
+  size_t want = std::max(bytes, (size_t)1 << 22);
+  if (hipHostMalloc(&c->pinned, want, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return sd_fail(c, SD_CAS_ENOMEM, "hipHostMalloc(%zu) failed", want);
+  }
+  c->pinned_bytes = want;
+  return SD_CAS_OK;
+}

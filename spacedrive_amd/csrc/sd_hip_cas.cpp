@@ -24,7 +24,6 @@
 #include <thread>
 #include <vector>
 
-#include "../../include/sd_hip_cas.h"
 #include "sd_checksum.h"
 #include "sd_group.h"
 #include "sd_kernels.h"
@@ -32,84 +31,13 @@
 
 using namespace sdcas;
 
-struct DevBuf {
-  void* p = nullptr;
-  size_t bytes = 0;
-};
+#include "ctx_internal.h"
 
-struct sd_cas_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;  // compute
-  hipStream_t copy = nullptr;    // H2D side stream
-  hipEvent_t h2d_done = nullptr;
-  DevBuf ws;       // kernel workspace
-  DevBuf staging;  // device copy of a host batch
-  DevBuf small;    // keys / sizes / offsets of a host batch
-  void* pinned = nullptr;
-  size_t pinned_bytes = 0;
-  uint64_t* d_scalar = nullptr;  // 4 x u64 scratch for counters
-  std::string err;
-};
-
-static int fail(sd_cas_ctx* c, int code, const char* fmt, ...) {
-  if (c) {
-    char buf[512];
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(buf, sizeof buf, fmt, ap);
-    va_end(ap);
-    c->err = buf;
-  }
-  return code;
-}
-
-#define HIP_TRY(ctx, expr)                                                                 \
-  do {                                                                                     \
-    hipError_t e_ = (expr);                                                                \
-    if (e_ != hipSuccess)                                                                  \
-      return fail((ctx), SD_CAS_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
-                  __FILE__, __LINE__);                                                     \
-  } while (0)
-
-// NULL = the HIP null (default) stream, exactly as in HIP itself: a caller on the
-// default stream (torch's default) must be ordered with our kernels.
-static inline hipStream_t pick(sd_cas_ctx* c, void* s) { (void)c; return (hipStream_t)s; }
-static inline size_t up16(size_t x) { return (x + 15) & ~(size_t)15; }
-static inline size_t up256(size_t x) { return (x + 255) & ~(size_t)255; }
-
-static int ensure(sd_cas_ctx* c, DevBuf& b, size_t bytes) {
-  if (bytes <= b.bytes) return SD_CAS_OK;
-  if (b.p) {
-    HIP_TRY(c, hipDeviceSynchronize());
-    HIP_TRY(c, hipFree(b.p));
-    b.p = nullptr;
-    b.bytes = 0;
-  }
-  size_t want = std::max(bytes, (size_t)1 << 20);
-  if (hipMalloc(&b.p, want) != hipSuccess) {
-    (void)hipGetLastError();
-    return fail(c, SD_CAS_ENOMEM, "hipMalloc(%zu) failed", want);
-  }
-  b.bytes = want;
-  return SD_CAS_OK;
-}
-
-static int ensure_pinned(sd_cas_ctx* c, size_t bytes) {
-  if (bytes <= c->pinned_bytes) return SD_CAS_OK;
-  if (c->pinned) {
-    HIP_TRY(c, hipDeviceSynchronize());
-    HIP_TRY(c, hipHostFree(c->pinned));
-    c->pinned = nullptr;
-    c->pinned_bytes = 0;
-  }
-  size_t want = std::max(bytes, (size_t)1 << 22);
-  if (hipHostMalloc(&c->pinned, want, hipHostMallocDefault) != hipSuccess) {
-    (void)hipGetLastError();
-    return fail(c, SD_CAS_ENOMEM, "hipHostMalloc(%zu) failed", want);
-  }
-  c->pinned_bytes = want;
-  return SD_CAS_OK;
-}
+// short local names for the shared helpers
+#define fail sd_fail
+#define pick sd_pick
+#define ensure sd_ensure
+#define ensure_pinned sd_ensure_pinned
 
 extern "C" {
 

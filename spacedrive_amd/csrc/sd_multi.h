@@ -1,0 +1,17 @@
+// sd_multi.h — launchers for multi.hip (single-process multi-device grouping).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sdcas {
+
+hipError_t multi_splits(const uint64_t* skeys, uint64_t n, uint32_t G, uint64_t* splits,
+                        hipStream_t s);
+hipError_t multi_gidx(const uint32_t* sidx, uint64_t n, uint64_t file0, uint64_t* gidx,
+                      hipStream_t s);
+hipError_t multi_gather(const uint32_t* rep_pos, const uint64_t* ridx, uint64_t m, uint64_t* out,
+                        hipStream_t s);
+hipError_t multi_scatter(const uint32_t* sidx, const uint64_t* back, uint64_t n, uint64_t* rep,
+                         hipStream_t s);
+
+}  // namespace sdcas

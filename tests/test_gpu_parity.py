@@ -316,3 +316,45 @@ def test_sharded_group_rccl_world1(eng, oracle):
         assert (res.rep.cpu().numpy() == orep.astype(np.int64) + 5_000_000).all()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("shards", [1, 2, 3, 4])
+def test_multi_device_group(eng, oracle, shards):
+    """Single-process multi-device grouping (sd_cas_multi_group): `shards` shards on
+    device 0, so the whole peer-copy exchange, split points and mirror run on one GPU."""
+    from spacedrive_amd.multi import MultiEngine
+    rng = np.random.default_rng(20 + shards)
+    pool = rng.integers(0, 2 ** 64, 30_000, dtype=np.uint64)
+    # keys exactly at / next to every range boundary ceil(r * 2^64 / G)
+    for r in range(1, shards):
+        b = -((-(r << 64)) // shards)
+        pool[r * 3: r * 3 + 3] = [b - 1, b, min(b + 1, 2 ** 64 - 1)]
+    keys = pool[rng.integers(0, len(pool), 90_001)]
+    me = MultiEngine([0] * shards)
+    cuts = [len(keys) * i // shards for i in range(shards + 1)]
+    parts = [dev64(keys[cuts[i]:cuts[i + 1]]) for i in range(shards)]
+    reps, objects = me.group(parts, cuts[:-1])
+    orep, oobj = oracle.group_canonical(keys)
+    assert objects == oobj
+    got = np.concatenate([r.cpu().numpy() for r in reps])
+    assert (got == orep.astype(np.int64)).all()
+    me.close()
+
+
+def test_multi_device_hash_group_host(eng, oracle):
+    from spacedrive_amd.multi import MultiEngine
+    rng = np.random.default_rng(30)
+    n = 3001
+    content = rng.integers(0, 256, (n, SAMPLED_CONTENT_LEN), dtype=np.uint8)
+    sizes = rng.integers(MINIMUM_FILE_SIZE + 1, 2 ** 40, n, dtype=np.uint64)
+    dup = rng.integers(0, n, 700)
+    src = rng.integers(0, n, 700)
+    content[dup] = content[src]
+    sizes[dup] = sizes[src]
+    want = oracle.fast_cas_keys_strided(content.reshape(-1), SAMPLED_CONTENT_LEN, SAMPLED_CONTENT_LEN, sizes, 8)
+    orep, oobj = oracle.group_canonical(want)
+    me = MultiEngine([0, 0, 0])
+    keys, rep, objects = me.hash_group_sampled_host(content.reshape(-1), sizes)
+    assert (keys == want).all()
+    assert objects == oobj and (rep == orep.astype(np.uint64)).all()
+    me.close()
