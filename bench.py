@@ -6,16 +6,18 @@ Workload (one "step"): every rank hashes its resident batch of sampled-path file
 duplicate content) with K1 and groups the cas keys into Objects — locally on one GPU,
 by key-range all-to-all over RCCL on several.  Inputs are synthesized on the device
 before the timed region (data: synthetic) and are resident in HBM when it starts.
-Weak scaling: FILES_PER_GPU (default 1.25M = 71.7 GB/GPU) per rank per step, so one step
-at 8 GPUs is the 10M-file headline job.  Steps are pipelined the way a production job
+Weak scaling: FILES_PER_GPU (default 1,310,720 = 20 x 65,536, the MI355X file-per-lane
+quantum; 75.2 GB/GPU) per rank per step, so one step at 8 GPUs is the 10M-file headline
+job (10.49 M files).  Steps are pipelined the way a production job
 would run them: step i's grouping (incl. its RCCL exchange) runs on a side stream while
 step i+1 is hashed; every step's hash AND grouping complete inside the timed region
 (--no-overlap serialises them).
 
 Output: ONE JSON line on rank 0 (driver contract), with
   roofline      — K1 (sd_cas_sampled_kernel), timed by HIP events on its own stream:
-                  algorithmic message bytes / kernel time vs the 8 TB/s HBM peak, plus the
-                  int32 VALU view (spec ops per compression) in "valu";
+                  VALU issue slots / kernel time vs the full-rate issue peak (the binding
+                  roof: BLAKE3's rotates and 3-input adds are half rate on gfx950), with the
+                  HBM byte view (vs 8 TB/s) and PMC traffic alongside;
   cpu_baseline  — the oracle's AVX-512 16-lane CPU path (oracle/cas_fast.c) on a bounded
                   sample of the SAME files on the host cores (rank 0, N=1 only); the sample's
                   keys are also checked against the GPU's.
@@ -49,7 +51,8 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--files-per-gpu", type=int, default=1_250_000)
+    ap.add_argument("--files-per-gpu", type=int, default=1_310_720,
+                    help="20 x 65,536 (the MI355X file-per-lane quantum): 10.49 M files per step at 8 GPUs")
     ap.add_argument("--dup-permille", type=int, default=300)
     ap.add_argument("--seed", type=int, default=0x5DCA50004)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)

@@ -87,6 +87,13 @@ const char* sd_cas_last_error(const sd_cas_ctx* c) { return c ? c->err.c_str() :
 
 void* sd_cas_ctx_stream(sd_cas_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
+size_t sd_cas_batch_quantum(const sd_cas_ctx* c) {
+  if (!c) return 0;
+  hipDeviceProp_t p;
+  if (hipGetDeviceProperties(&p, c->device) != hipSuccess) return 65536;
+  return (size_t)p.multiProcessorCount * 4 * 64;
+}
+
 int sd_cas_synchronize(sd_cas_ctx* c) {
   if (!c) return SD_CAS_EINVAL;
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -425,7 +432,7 @@ int sd_cas_hash_sampled_host(sd_cas_ctx* c, const void* h_content, uint64_t stri
   if (!h_content || !h_sizes || !h_keys || stride < SAMPLED_CONTENT_LEN || (stride & 15))
     return fail(c, SD_CAS_EINVAL, "hash_sampled_host: bad arguments");
   HIP_TRY(c, hipSetDevice(c->device));
-  if (batch_files == 0) batch_files = 32768;
+  if (batch_files == 0) batch_files = sd_cas_batch_quantum(c);
   batch_files = std::min(batch_files, n);
   // two device slots: [content | sizes | keys], ping-ponged between the copy stream (H2D of
   // batch k+1) and the compute stream (K1 on batch k, then D2H of its keys)

@@ -271,7 +271,7 @@ int sd_cas_multi_hash_group_sampled_host(sd_cas_multi* m, const void* h_content,
   }
   // hash every shard from host memory: batches ping-pong between H2D on the side stream
   // and K1 on the compute stream, all devices in flight together
-  const size_t batch = 32768;
+  const size_t batch = sd_cas_batch_quantum(m->ctx[0]);
   const size_t cbytes = up256(batch * stride), sbytes = up256(batch * 8);
   for (int i = 0; i < G; i++) {
     sd_cas_ctx* c = m->ctx[i];
