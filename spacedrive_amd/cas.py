@@ -37,6 +37,7 @@ MINIMUM_FILE_SIZE = 1024 * 100
 SAMPLED_CONTENT_LEN = 2 * HEADER_OR_FOOTER_SIZE + SAMPLE_COUNT * SAMPLE_SIZE  # 57,344
 CHUNK_SIZE = 100
 MAX_PACKED_CONTENT_LEN = 104 * 1024 - 8
+THRESHOLD_DEFAULT = (1 << 64) - 1  # SD_CAS_THRESHOLD_DEFAULT
 
 
 def key_to_cas_id(key: int) -> str:
@@ -106,6 +107,17 @@ class CasEngine:
 
     def synchronize(self) -> None:
         self._check(self.L.sd_cas_synchronize(self.h), "synchronize")
+
+    @property
+    def batch_quantum(self) -> int:
+        return int(self.L.sd_cas_batch_quantum(self.h))
+
+    def set_latency_threshold(self, sampled: Optional[int] = None, packed: Optional[int] = None) -> None:
+        """Batches below these sizes hash chunk-parallel (K1L); 0 = always one file per lane,
+        None = the measured default crossover."""
+        d = THRESHOLD_DEFAULT
+        self.L.sd_cas_set_latency_threshold(self.h, d if sampled is None else int(sampled),
+                                            d if packed is None else int(packed))
 
     # ---- host batches (blocking) -------------------------------------------------------
     def generate_cas_keys(self, items: Sequence[tuple[bytes, int]]) -> np.ndarray:

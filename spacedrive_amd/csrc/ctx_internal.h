@@ -26,6 +26,8 @@ struct sd_cas_ctx {
   void* pinned = nullptr;
   size_t pinned_bytes = 0;
   uint64_t* d_scalar = nullptr;  // 8 x u64 scratch for counters
+  // batches below these sizes use the chunk-parallel K1L kernel (sd_cas_set_latency_threshold)
+  size_t latency_sampled = 0, latency_packed = 0;
   std::string err;
 };
 

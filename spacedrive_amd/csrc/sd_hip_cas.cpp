@@ -64,8 +64,19 @@ int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
     sd_cas_ctx_destroy(c);
     return SD_CAS_EHIP;
   }
+  sd_cas_set_latency_threshold(c, SD_CAS_THRESHOLD_DEFAULT, SD_CAS_THRESHOLD_DEFAULT);
   *out = c;
   return SD_CAS_OK;
+}
+
+// Defaults = the measured crossovers on MI355X (profiles/r01_k1l_sweep.log): K1L wins below
+// ~0.6 of a batch quantum for sampled messages and ~0.9 for ragged whole files, where the
+// lane-per-file path also pays the length sort and the 101-chunk latency of its longest file.
+void sd_cas_set_latency_threshold(sd_cas_ctx* c, size_t sampled_files, size_t packed_files) {
+  if (!c) return;
+  const size_t q = sd_cas_batch_quantum(c);
+  c->latency_sampled = sampled_files == SD_CAS_THRESHOLD_DEFAULT ? q * 5 / 8 : sampled_files;
+  c->latency_packed = packed_files == SD_CAS_THRESHOLD_DEFAULT ? q * 7 / 8 : packed_files;
 }
 
 void sd_cas_ctx_destroy(sd_cas_ctx* c) {
@@ -131,7 +142,11 @@ int sd_cas_hash_sampled_dev(sd_cas_ctx* c, const void* d_content, uint64_t strid
       ((uintptr_t)d_content & 15))
     return fail(c, SD_CAS_EINVAL, "hash_sampled: bad content/stride (stride=%llu)",
                 (unsigned long long)stride);
-  HIP_TRY(c, hash_sampled((const uint8_t*)d_content, stride, d_sizes, n, d_keys, pick(c, stream)));
+  if (n < c->latency_sampled)  // small batch: one wave per file (K1L)
+    HIP_TRY(c, hash_chunkpar((const uint8_t*)d_content, nullptr, stride, nullptr,
+                             SAMPLED_CONTENT_LEN, d_sizes, n, d_keys, pick(c, stream)));
+  else
+    HIP_TRY(c, hash_sampled((const uint8_t*)d_content, stride, d_sizes, n, d_keys, pick(c, stream)));
   return SD_CAS_OK;
 }
 
@@ -144,6 +159,10 @@ int sd_cas_hash_packed_dev(sd_cas_ctx* c, const void* d_arena, const uint64_t* d
       n >= (1ull << 32))
     return fail(c, SD_CAS_EINVAL, "hash_packed: bad arguments");
   hipStream_t s = pick(c, stream);
+  if (n < c->latency_packed) {  // small batch: one wave per file (K1L), no length sort
+    HIP_TRY(c, hash_chunkpar((const uint8_t*)d_arena, d_offs, 0, d_lens, 0, d_sizes, n, d_keys, s));
+    return SD_CAS_OK;
+  }
   // workspace: length keys | sorted keys | order | sort workspace
   const size_t kb = up256(n * 8), ob = up256(n * 4);
   int rc = ensure(c, c->ws, 2 * kb + ob + sort_workspace_bytes(n));
@@ -463,7 +482,11 @@ int sd_cas_hash_sampled_host(sd_cas_ctx* c, const void* h_content, uint64_t stri
       e = hipMemcpyAsync(d_sizes, h_sizes + f0, m * 8, hipMemcpyHostToDevice, c->copy);
     if (e == hipSuccess) e = hipEventRecord(h2d[b], c->copy);
     if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, h2d[b], 0);
-    if (e == hipSuccess) e = hash_sampled(d_content, stride, d_sizes, m, d_keys, c->stream);
+    if (e == hipSuccess)
+      e = m < c->latency_sampled
+              ? hash_chunkpar(d_content, nullptr, stride, nullptr, SAMPLED_CONTENT_LEN, d_sizes, m,
+                              d_keys, c->stream)
+              : hash_sampled(d_content, stride, d_sizes, m, d_keys, c->stream);
     if (e == hipSuccess)
       e = hipMemcpyAsync(h_keys + f0, d_keys, m * 8, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipEventRecord(done[b], c->stream);

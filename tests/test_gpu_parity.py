@@ -32,7 +32,20 @@ def sampled_batch(rng, n, stride=SAMPLED_CONTENT_LEN):
     return content, sizes
 
 
-def test_sampled_kernel_vs_oracle(eng, oracle):
+# Each device-hash test runs both kernel families: threshold 0 forces the lane-per-file
+# kernels (K1/K2) at every n, a huge threshold forces the chunk-parallel K1L.
+PATHS = {"lane": 0, "chunkpar": 1 << 40}
+
+
+@pytest.fixture(params=list(PATHS))
+def path_eng(eng, request):
+    eng.set_latency_threshold(PATHS[request.param], PATHS[request.param])
+    yield eng
+    eng.set_latency_threshold()
+
+
+def test_sampled_kernel_vs_oracle(path_eng, oracle):
+    eng = path_eng
     rng = np.random.default_rng(1)
     for n, stride in [(1, SAMPLED_CONTENT_LEN), (63, SAMPLED_CONTENT_LEN), (1000, SAMPLED_CONTENT_LEN),
                       (257, SAMPLED_CONTENT_LEN + 48)]:
@@ -43,7 +56,8 @@ def test_sampled_kernel_vs_oracle(eng, oracle):
         assert (host64(keys) == want).all(), (n, stride)
 
 
-def test_sampled_golden(eng, golden):
+def test_sampled_golden(path_eng, golden):
+    eng = path_eng
     g = golden["cas"]
     files = [f for f in g["files"] if f["size"] > MINIMUM_FILE_SIZE]
     content = np.stack([np.frombuffer(gather_virtual(g["seed"], f["file"], f["size"]), np.uint8)
@@ -70,7 +84,8 @@ EDGE_LENS = (list(range(0, 130)) + [1015, 1016, 1017, 1023, 1024, 1025, 2040, 20
              4088, 4096, 16376, 32760, 65528, 102399, 102400, 57344, 104000, 104 * 1024 - 8])
 
 
-def test_packed_kernel_edges_vs_oracle(eng, oracle):
+def test_packed_kernel_edges_vs_oracle(path_eng, oracle):
+    eng = path_eng
     rng = np.random.default_rng(2)
     lens = EDGE_LENS + [int(x) for x in rng.integers(0, 102401, 1500)]
     contents = [rng.integers(0, 256, L, dtype=np.uint8).tobytes() for L in lens]
@@ -89,7 +104,8 @@ def test_packed_kernel_edges_vs_oracle(eng, oracle):
     assert not bad, bad[:10]
 
 
-def test_host_generate_cas_ids_mixed(eng, oracle, golden):
+def test_host_generate_cas_ids_mixed(path_eng, oracle, golden):
+    eng = path_eng
     g = golden["cas"]
     items = [(gather_virtual(g["seed"], f["file"], f["size"]), f["size"]) for f in g["files"]]
     assert eng.generate_cas_ids(items) == [f["cas_id"] for f in g["files"]]

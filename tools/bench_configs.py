@@ -57,9 +57,22 @@ def config1(eng, orc, n_files: int, root: str):
         want = [orc.generate_cas_id(p, int(s)) for p, s in zip(paths, sizes)]
         cpu1 = time.perf_counter() - t
         ok = all(f"{k:016x}" == w for k, w in zip(keys, want))
+        # the reference's own batch shape: identifier_job_step over CHUNK_SIZE = 100 paths
+        # (file_identifier/mod.rs:34), one blocking call per chunk; K1L (default threshold)
+        # vs forcing the lane-per-file kernels
+        step = {}
+        for name, thr in (("k1l", None), ("lane", 0)):
+            eng.set_latency_threshold(thr, thr)
+            t = time.perf_counter()
+            for i in range(0, n_files, 100):
+                k, e = eng.generate_cas_keys_from_paths(paths[i:i + 100], sizes[i:i + 100])
+                ok = ok and bool((k == keys[i:i + 100]).all())
+            step[name] = (time.perf_counter() - t) / ((n_files + 99) // 100) * 1e3
+        eng.set_latency_threshold()
         emit({"config": 1, "files": n_files, "bytes_on_disk": total,
               "small_fraction": float((sizes <= 102400).mean()),
               "gpu_dropin_files_per_s": n_files / gpu, "gpu_s": gpu,
+              "job_step_100_ms": {k: round(v, 3) for k, v in step.items()},
               "cpu_oracle_1thread_files_per_s": n_files / cpu1, "parity": ok,
               "note": "tmpfs page cache; GPU path = pread gather (16 threads) + pinned H2D + K1/K2"})
     finally:
