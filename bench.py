@@ -252,8 +252,16 @@ def cpu_baseline(content, sizes, keys, seconds: float):
         orc.fast_cas_keys_strided(host.reshape(-1), 57344, 57344, hs, threads)
     dt = time.perf_counter() - t0
     files = reps * m
+    # reference-faithful mode: one hashing thread, as one job's join_all
+    m1 = min(m, 4096)
+    t0 = time.perf_counter()
+    r1 = 0
+    while time.perf_counter() - t0 < 2.0:
+        orc.fast_cas_keys_strided(host[:m1].reshape(-1), 57344, 57344, hs[:m1], 1)
+        r1 += 1
+    one_thread = r1 * m1 / (time.perf_counter() - t0)
     return {"value": files / dt, "unit": "cas_ids/s", "hashed_gb_per_s": files * MSG_BYTES / dt / 1e9,
-            "cores": threads, "kind": "port",
+            "cores": threads, "kind": "port", "value_1thread": one_thread,
             "simd": "avx512 16-lane" if orc.has_simd() else "scalar",
             "sample": f"{reps} passes over the first {m} files of the bench batch (hashing only, "
                       f"messages pre-gathered in DRAM), {dt:.1f}s",

@@ -6,13 +6,72 @@
 #include <stdio.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "../../include/sd_hip_cas.h"
 
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
+};
+
+// Persistent host workers for the I/O gather (a 100-file job step cannot afford to spawn
+// threads per call).  run(k, fn) executes fn on the caller plus k-1 pool threads and
+// returns when all are done; fn pulls work items itself (atomic cursor).
+class HostPool {
+ public:
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  void run(unsigned k, const std::function<void()>& fn) {
+    if (k <= 1) { fn(); return; }
+    std::unique_lock<std::mutex> lk(mu_);
+    while (th_.size() + 1 < k) th_.emplace_back([this] { loop(); });
+    fn_ = &fn;
+    want_ = k - 1;
+    pending_ = k - 1;
+    ++gen_;
+    lk.unlock();
+    cv_.notify_all();
+    fn();
+    lk.lock();
+    done_.wait(lk, [this] { return pending_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void loop() {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || (gen_ != seen && want_ > 0); });
+      if (stop_) return;
+      seen = gen_;
+      --want_;
+      const std::function<void()>* f = fn_;
+      lk.unlock();
+      (*f)();
+      lk.lock();
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  std::vector<std::thread> th_;
+  const std::function<void()>* fn_ = nullptr;
+  unsigned want_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
 };
 
 struct sd_cas_ctx {
@@ -28,6 +87,7 @@ struct sd_cas_ctx {
   uint64_t* d_scalar = nullptr;  // 8 x u64 scratch for counters
   // batches below these sizes use the chunk-parallel K1L kernel (sd_cas_set_latency_threshold)
   size_t latency_sampled = 0, latency_packed = 0;
+  HostPool pool;  // I/O gather workers
   std::string err;
 };
 

@@ -367,17 +367,23 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
   // content length per file: sampled 57,344; whole file = actual length (cas.rs:29 reads
   // the file, not `size` bytes) -> stat it.
   std::vector<uint64_t> lens(n, 0);
-  for (size_t i = 0; i < n; i++) {
-    status[i] = 0;
-    out_keys[i] = 0;
-    if (sizes[i] > MINIMUM_FILE_SIZE) {
-      lens[i] = SAMPLED_CONTENT_LEN;
-    } else {
-      struct stat st;
-      if (stat(paths[i], &st) != 0) { status[i] = -errno; continue; }
-      if ((uint64_t)st.st_size > MAX_PACKED_CONTENT_LEN) { status[i] = -EFBIG; continue; }
-      lens[i] = (uint64_t)st.st_size;
-    }
+  const unsigned nth = std::max(1u, std::min(16u, (unsigned)((n + 7) / 8)));  // ~8 files/worker
+  {
+    std::atomic<size_t> next{0};
+    c->pool.run(nth, [&]() {
+      for (size_t i; (i = next.fetch_add(1)) < n;) {
+        status[i] = 0;
+        out_keys[i] = 0;
+        if (sizes[i] > MINIMUM_FILE_SIZE) {
+          lens[i] = SAMPLED_CONTENT_LEN;
+        } else {
+          struct stat st;
+          if (stat(paths[i], &st) != 0) { status[i] = -errno; continue; }
+          if ((uint64_t)st.st_size > MAX_PACKED_CONTENT_LEN) { status[i] = -EFBIG; continue; }
+          lens[i] = (uint64_t)st.st_size;
+        }
+      }
+    });
   }
   Plan pl;
   int rc = plan_batch(c, lens.data(), sizes, n, pl);
@@ -431,11 +437,7 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
       close(fd);
     }
   };
-  const unsigned nth = std::max(1u, std::min(16u, (unsigned)((n + 63) / 64)));
-  std::vector<std::thread> th;
-  for (unsigned t = 1; t < nth; t++) th.emplace_back(worker);
-  worker();
-  for (auto& t : th) t.join();
+  c->pool.run(nth, worker);  // at most 16 workers: the GPU box's CPU share
   rc = run_staged(c, pl, sizes, n, out_keys);
   if (rc) return rc;
   for (size_t i = 0; i < n; i++)

@@ -51,8 +51,12 @@ def config1(eng, orc, n_files: int, root: str):
         eng.generate_cas_keys_from_paths(paths[:64], sizes[:64])  # warm
         t = time.perf_counter()
         keys, errs = eng.generate_cas_keys_from_paths(paths, sizes)
-        gpu = time.perf_counter() - t
+        gpu_cold = time.perf_counter() - t  # includes growing the pinned staging once
         assert not errs.any()
+        t = time.perf_counter()
+        keys2, _ = eng.generate_cas_keys_from_paths(paths, sizes)
+        gpu = time.perf_counter() - t
+        assert (keys2 == keys).all()
         t = time.perf_counter()
         want = [orc.generate_cas_id(p, int(s)) for p, s in zip(paths, sizes)]
         cpu1 = time.perf_counter() - t
@@ -71,7 +75,7 @@ def config1(eng, orc, n_files: int, root: str):
         eng.set_latency_threshold()
         emit({"config": 1, "files": n_files, "bytes_on_disk": total,
               "small_fraction": float((sizes <= 102400).mean()),
-              "gpu_dropin_files_per_s": n_files / gpu, "gpu_s": gpu,
+              "gpu_dropin_files_per_s": n_files / gpu, "gpu_s": gpu, "gpu_s_first_call": gpu_cold,
               "job_step_100_ms": {k: round(v, 3) for k, v in step.items()},
               "cpu_oracle_1thread_files_per_s": n_files / cpu1, "parity": ok,
               "note": "tmpfs page cache; GPU path = pread gather (16 threads) + pinned H2D + K1/K2"})

@@ -44,6 +44,49 @@ KERNEL(k_bfi, "v_bfi_b32 %0, %0, %1, %0")
 KERNEL(k_or, "v_or_b32 %0, %0, %1")
 KERNEL(k_add_e64, "v_add_u32_e64 %0, %0, %1")
 KERNEL(k_lshladd, "v_lshl_add_u32 %0, %0, 7, %1")
+KERNEL(k_alignbyte, "v_alignbyte_b32 %0, %0, %0, 2")
+KERNEL(k_or3, "v_or3_b32 %0, %0, %1, %0")
+KERNEL(k_andor, "v_and_or_b32 %0, %0, %1, %0")
+KERNEL(k_mad24, "v_mad_u32_u24 %0, %0, %1, %0")
+KERNEL(k_bitop3_16, "v_bitop3_b16 %0, %0, %1, %0 bitop3:0x96")
+
+// operand-pattern variants of the half-rate ops (same reg twice vs distinct regs)
+#define KERNEL3(NAME, ASM)                                                                    \
+  __global__ void __launch_bounds__(256) NAME(uint32_t* out, uint32_t seed) {               \
+    uint32_t a0 = threadIdx.x ^ seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,    \
+             a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7, b = seed * 3u + 1u, c = seed ^ 0x55u;     \
+    for (int i = 0; i < ITERS; ++i) {                                                         \
+      asm volatile(ASM : "+v"(a0) : "v"(b), "v"(c)); asm volatile(ASM : "+v"(a1) : "v"(b), "v"(c)); \
+      asm volatile(ASM : "+v"(a2) : "v"(b), "v"(c)); asm volatile(ASM : "+v"(a3) : "v"(b), "v"(c)); \
+      asm volatile(ASM : "+v"(a4) : "v"(b), "v"(c)); asm volatile(ASM : "+v"(a5) : "v"(b), "v"(c)); \
+      asm volatile(ASM : "+v"(a6) : "v"(b), "v"(c)); asm volatile(ASM : "+v"(a7) : "v"(b), "v"(c)); \
+    }                                                                                         \
+    out[blockIdx.x * 256 + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;              \
+  }
+KERNEL3(k_alignbit_2r, "v_alignbit_b32 %0, %0, %1, 7")
+KERNEL3(k_alignbit_sh, "v_alignbit_b32 %0, %0, %0, %1")
+KERNEL3(k_add3_3r, "v_add3_u32 %0, %0, %1, %2")
+KERNEL3(k_bitop3_3r, "v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96")
+KERNEL3(k_lshlor_3r, "v_lshl_or_b32 %0, %0, %1, %2")
+
+// 64-bit register-pair ops (rotation as a 64-bit shift of a duplicated word)
+#define KERNEL64(NAME, ASM)                                                                   \
+  __global__ void __launch_bounds__(256) NAME(uint32_t* out, uint32_t seed) {               \
+    uint64_t a[8];                                                                            \
+    for (int j = 0; j < 8; ++j) a[j] = ((uint64_t)(threadIdx.x ^ seed) << 32) | (j + seed);  \
+    uint64_t b = seed * 3u + 1u;                                                              \
+    for (int i = 0; i < ITERS; ++i) {                                                         \
+      asm volatile(ASM : "+v"(a[0]) : "v"(b)); asm volatile(ASM : "+v"(a[1]) : "v"(b));     \
+      asm volatile(ASM : "+v"(a[2]) : "v"(b)); asm volatile(ASM : "+v"(a[3]) : "v"(b));     \
+      asm volatile(ASM : "+v"(a[4]) : "v"(b)); asm volatile(ASM : "+v"(a[5]) : "v"(b));     \
+      asm volatile(ASM : "+v"(a[6]) : "v"(b)); asm volatile(ASM : "+v"(a[7]) : "v"(b));     \
+    }                                                                                         \
+    uint64_t r = a[0] ^ a[1] ^ a[2] ^ a[3] ^ a[4] ^ a[5] ^ a[6] ^ a[7];                       \
+    out[blockIdx.x * 256 + threadIdx.x] = (uint32_t)r ^ (uint32_t)(r >> 32);                  \
+  }
+KERNEL64(k_lshr64, "v_lshrrev_b64 %0, 7, %0")
+KERNEL64(k_pkmov, "v_pk_mov_b32 %0, %0, %1 op_sel:[1,0]")
+KERNEL64(k_lshladd64, "v_lshl_add_u64 %0, %0, 0, %1")
 
 // dependent chain: one accumulator
 __global__ void __launch_bounds__(64) k_dep_alignbit(uint32_t* out, uint32_t seed) {
@@ -67,6 +110,44 @@ __global__ void __launch_bounds__(256) k_compress(uint32_t* out, uint32_t seed) 
   for (int i = 0; i < 64; ++i) {
     sdcas::compress(cv, m, (uint32_t)i, 0u, 64u, 0u);
     m[i & 15] ^= cv[0];  // keep the chain live without changing the instruction mix much
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = cv[0] ^ cv[7];
+}
+
+// variant: a + b + x as two full-rate adds, the message add first (off the a->b chain)
+__device__ __forceinline__ uint32_t add2(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm volatile("v_add_u32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+#define G2(a, b, c, d, x, y)                                        \
+  a = add2(add2(a, x), b); d = sdcas::rotr(d ^ a, 16); c = c + d;   \
+  b = sdcas::rotr(b ^ c, 12); a = add2(add2(a, y), b);              \
+  d = sdcas::rotr(d ^ a, 8); c = c + d; b = sdcas::rotr(b ^ c, 7);
+__device__ __forceinline__ void compress2(uint32_t (&cv)[8], const uint32_t (&m)[16], uint32_t ctr) {
+  uint32_t v0 = cv[0], v1 = cv[1], v2 = cv[2], v3 = cv[3], v4 = cv[4], v5 = cv[5], v6 = cv[6],
+           v7 = cv[7], v8 = sdcas::IV0, v9 = sdcas::IV1, v10 = sdcas::IV2, v11 = sdcas::IV3,
+           v12 = ctr, v13 = 0, v14 = 64, v15 = 0;
+#pragma unroll
+  for (int r = 0; r < 7; ++r) {
+    const uint8_t* s = sdcas::SCHED.s[r];
+    G2(v0, v4, v8, v12, m[s[0]], m[s[1]]); G2(v1, v5, v9, v13, m[s[2]], m[s[3]]);
+    G2(v2, v6, v10, v14, m[s[4]], m[s[5]]); G2(v3, v7, v11, v15, m[s[6]], m[s[7]]);
+    G2(v0, v5, v10, v15, m[s[8]], m[s[9]]); G2(v1, v6, v11, v12, m[s[10]], m[s[11]]);
+    G2(v2, v7, v8, v13, m[s[12]], m[s[13]]); G2(v3, v4, v9, v14, m[s[14]], m[s[15]]);
+  }
+  cv[0] = v0 ^ v8; cv[1] = v1 ^ v9; cv[2] = v2 ^ v10; cv[3] = v3 ^ v11;
+  cv[4] = v4 ^ v12; cv[5] = v5 ^ v13; cv[6] = v6 ^ v14; cv[7] = v7 ^ v15;
+}
+__global__ void __launch_bounds__(256) k_compress2(uint32_t* out, uint32_t seed) {
+  uint32_t cv[8];
+  sdcas::set_iv(cv);
+  uint32_t m[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) m[i] = threadIdx.x * 16 + i + seed;
+  for (int i = 0; i < 64; ++i) {
+    compress2(cv, m, (uint32_t)i);
+    m[i & 15] ^= cv[0];
   }
   out[blockIdx.x * 256 + threadIdx.x] = cv[0] ^ cv[7];
 }
@@ -103,7 +184,13 @@ int main() {
       {"v_xor_b32_sdwa WORD_1<-WORD_0", k_sdwa_hi}, {"v_xor_b32_sdwa WORD_0<-WORD_1", k_sdwa_lo},
       {"v_mov_b32_sdwa BYTE_3<-BYTE_0", k_sdwa_byte}, {"v_lshrrev_b32", k_lshr},
       {"v_bfi_b32", k_bfi}, {"v_or_b32", k_or},
-      {"v_add_u32_e64", k_add_e64}, {"v_lshl_add_u32", k_lshladd}};
+      {"v_add_u32_e64", k_add_e64}, {"v_lshl_add_u32", k_lshladd},
+      {"v_alignbyte_b32", k_alignbyte}, {"v_or3_b32", k_or3}, {"v_and_or_b32", k_andor},
+      {"v_mad_u32_u24", k_mad24}, {"v_bitop3_b16", k_bitop3_16},
+      {"v_alignbit_b32 a,a,b,7", k_alignbit_2r}, {"v_alignbit_b32 a,a,a,vS", k_alignbit_sh},
+      {"v_add3_u32 a,a,b,c", k_add3_3r}, {"v_bitop3_b32 a,a,b,c", k_bitop3_3r},
+      {"v_lshl_or_b32 a,a,b,c", k_lshlor_3r},
+      {"v_lshrrev_b64", k_lshr64}, {"v_pk_mov_b32", k_pkmov}, {"v_lshl_add_u64", k_lshladd64}};
   for (auto& k : ks) {
     float ms = timeit(k.k, dim3(blocks), dim3(256), out);
     const double winstr = (double)blocks * 4 * ITERS * 8;  // wave-instructions
@@ -123,6 +210,13 @@ int main() {
     const double comps = (double)nb * 256 * 64;
     printf("compress-only, %d waves/SIMD: %.3f ms  %.3e compressions/s  -> %.1f M sampled files/s (953 each)\n",
            wps, ms, comps / (ms * 1e-3), comps / (ms * 1e-3) / 953 / 1e6);
+  }
+  for (int wps : {1, 4, 8}) {
+    const int nb = p.multiProcessorCount * wps;
+    float ms = timeit(k_compress2, dim3(nb), dim3(256), out);
+    const double comps = (double)nb * 256 * 64;
+    printf("compress-only (add3 split), %d waves/SIMD: %.3f ms  -> %.1f M sampled files/s\n",
+           wps, ms, comps / (ms * 1e-3) / 953 / 1e6);
   }
   return 0;
 }
