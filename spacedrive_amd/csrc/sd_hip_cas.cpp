@@ -280,46 +280,58 @@ static int plan_batch(sd_cas_ctx* c, const uint64_t* buf_lens, const uint64_t* s
   return SD_CAS_OK;
 }
 
-// Copies staged pinned bytes to the device, hashes both sub-batches, returns keys.
-static int run_staged(sd_cas_ctx* c, const Plan& pl, const uint64_t* sizes, size_t n,
-                      uint64_t* out_keys) {
+// Enqueues, for a batch staged in pinned memory at `pin`: H2D to `dev` on the copy stream,
+// both hash sub-batches on the compute stream, and D2H of the keys back to `pin` (the
+// content area is reused).  `done` (optional) is recorded on the compute stream after it.
+static int enqueue_staged(sd_cas_ctx* c, const Plan& pl, const uint64_t* sizes, size_t n,
+                          char* pin, char* dev, hipEvent_t done) {
   const size_t ns = pl.sampled.size(), np = pl.packed.size();
   const size_t content_bytes = pl.sampled_bytes + up256(pl.packed_bytes);
   const size_t meta_bytes = up256((ns + np) * 8) + up256(np * 8) + up256(np * 4) + up256(n * 8);
-  int rc = ensure(c, c->staging, content_bytes + meta_bytes);
-  if (rc) return rc;
-  char* pin = (char*)c->pinned;
   uint64_t* h_sizes = (uint64_t*)(pin + content_bytes);
   uint64_t* h_poffs = (uint64_t*)((char*)h_sizes + up256((ns + np) * 8));
-  uint32_t* h_plens = (uint32_t*)((char*)h_poffs + up256(np * 8));
   for (size_t k = 0; k < ns; k++) h_sizes[k] = sizes[pl.sampled[k]];
   for (size_t k = 0; k < np; k++) h_sizes[ns + k] = sizes[pl.packed[k]];
   for (size_t k = 0; k < np; k++) h_poffs[k] = pl.poff[k];
-  // lens were validated <= MAX_PACKED; recover them from the offsets' caller data
-  char* dev = (char*)c->staging.p;
+  // (packed lens were written into the staging by the caller)
   uint64_t* d_sizes = (uint64_t*)(dev + content_bytes);
   uint64_t* d_poffs = (uint64_t*)((char*)d_sizes + up256((ns + np) * 8));
   uint32_t* d_plens = (uint32_t*)((char*)d_poffs + up256(np * 8));
   uint64_t* d_keys = (uint64_t*)((char*)d_plens + up256(np * 4));
-  (void)h_plens;
   HIP_TRY(c, hipMemcpyAsync(dev, pin, content_bytes + meta_bytes - up256(n * 8),
                             hipMemcpyHostToDevice, c->copy));
   HIP_TRY(c, hipEventRecord(c->h2d_done, c->copy));
   HIP_TRY(c, hipStreamWaitEvent(c->stream, c->h2d_done, 0));
-  if (ns) {
-    rc = sd_cas_hash_sampled_dev(c, dev, SAMPLED_CONTENT_LEN, d_sizes, ns, d_keys, c->stream);
-    if (rc) return rc;
-  }
-  if (np) {
-    rc = sd_cas_hash_packed_dev(c, dev + pl.sampled_bytes, d_poffs, d_plens, d_sizes + ns, np,
-                                d_keys + ns, c->stream);
-    if (rc) return rc;
-  }
-  uint64_t* h_keys = (uint64_t*)pin;  // reuse staging for the result
-  HIP_TRY(c, hipMemcpyAsync(h_keys, d_keys, (ns + np) * 8, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  int rc;
+  if (ns && (rc = sd_cas_hash_sampled_dev(c, dev, SAMPLED_CONTENT_LEN, d_sizes, ns, d_keys,
+                                          c->stream)))
+    return rc;
+  if (np && (rc = sd_cas_hash_packed_dev(c, dev + pl.sampled_bytes, d_poffs, d_plens,
+                                         d_sizes + ns, np, d_keys + ns, c->stream)))
+    return rc;
+  HIP_TRY(c, hipMemcpyAsync(pin, d_keys, (ns + np) * 8, hipMemcpyDeviceToHost, c->stream));
+  if (done) HIP_TRY(c, hipEventRecord(done, c->stream));
+  return SD_CAS_OK;
+}
+
+static void scatter_keys(const Plan& pl, const char* pin, uint64_t* out_keys) {
+  const uint64_t* h_keys = (const uint64_t*)pin;
+  const size_t ns = pl.sampled.size(), np = pl.packed.size();
   for (size_t k = 0; k < ns; k++) out_keys[pl.sampled[k]] = h_keys[k];
   for (size_t k = 0; k < np; k++) out_keys[pl.packed[k]] = h_keys[ns + k];
+}
+
+static size_t staged_pinned_bytes(const Plan& pl, size_t n);
+
+// One staged batch, blocking: staging at c->pinned, device copy in c->staging.
+static int run_staged(sd_cas_ctx* c, const Plan& pl, const uint64_t* sizes, size_t n,
+                      uint64_t* out_keys) {
+  int rc = ensure(c, c->staging, staged_pinned_bytes(pl, n));
+  if (rc) return rc;
+  if ((rc = enqueue_staged(c, pl, sizes, n, (char*)c->pinned, (char*)c->staging.p, nullptr)))
+    return rc;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  scatter_keys(pl, (const char*)c->pinned, out_keys);
   return SD_CAS_OK;
 }
 
@@ -385,60 +397,87 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
       }
     });
   }
-  Plan pl;
-  int rc = plan_batch(c, lens.data(), sizes, n, pl);
+  // Windows of GATHER_WINDOW files, double-buffered: the pool gathers window w into one
+  // pinned slot while the GPU copies and hashes window w-1 from the other.
+  constexpr size_t GATHER_WINDOW = 2048;
+  const size_t nw = (n + GATHER_WINDOW - 1) / GATHER_WINDOW;
+  std::vector<Plan> plans(nw);
+  size_t slot = 0;
+  for (size_t w = 0; w < nw; w++) {
+    const size_t f0 = w * GATHER_WINDOW, m = std::min(GATHER_WINDOW, n - f0);
+    int rc = plan_batch(c, lens.data() + f0, sizes + f0, m, plans[w]);
+    if (rc) return rc;
+    slot = std::max(slot, up256(staged_pinned_bytes(plans[w], m)));
+  }
+  const int nslots = nw > 1 ? 2 : 1;
+  int rc = ensure_pinned(c, nslots * slot);
   if (rc) return rc;
-  rc = ensure_pinned(c, staged_pinned_bytes(pl, n));
-  if (rc) return rc;
-  char* pin = (char*)c->pinned;
-  const size_t ns = pl.sampled.size(), np = pl.packed.size();
-  const size_t content_bytes = pl.sampled_bytes + up256(pl.packed_bytes);
-  uint32_t* h_plens = (uint32_t*)(pin + content_bytes + up256((ns + np) * 8) + up256(np * 8));
-  for (size_t k = 0; k < np; k++) h_plens[k] = (uint32_t)lens[pl.packed[k]];
-  // gather: pread straight into pinned staging, files spread over a few threads
-  struct Task { size_t i; char* dst; };
-  std::vector<Task> tasks;
-  tasks.reserve(ns + np);
-  for (size_t k = 0; k < ns; k++) tasks.push_back({pl.sampled[k], pin + k * (size_t)SAMPLED_CONTENT_LEN});
-  for (size_t k = 0; k < np; k++) tasks.push_back({pl.packed[k], pin + pl.sampled_bytes + pl.poff[k]});
-  std::atomic<size_t> next{0};
-  auto worker = [&]() {
-    for (;;) {
-      const size_t t = next.fetch_add(1);
-      if (t >= tasks.size()) return;
-      const size_t i = tasks[t].i;
-      if (status[i]) continue;
-      int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
-      if (fd < 0) { status[i] = -errno; continue; }
-      // cas.rs:35-58 offsets: header at 0, sample k at 8192 + k*jump, footer at size-8192
-      uint64_t offs[6], lns[6];
-      int parts;
-      if (sizes[i] > MINIMUM_FILE_SIZE) {
-        const uint64_t jump = (sizes[i] - 2 * HEADER_OR_FOOTER_SIZE) / SAMPLE_COUNT;
-        offs[0] = 0; lns[0] = HEADER_OR_FOOTER_SIZE;
-        for (int k = 0; k < 4; k++) { offs[1 + k] = HEADER_OR_FOOTER_SIZE + k * jump; lns[1 + k] = SAMPLE_SIZE; }
-        offs[5] = sizes[i] - HEADER_OR_FOOTER_SIZE; lns[5] = HEADER_OR_FOOTER_SIZE;
-        parts = 6;
-      } else {
-        offs[0] = 0; lns[0] = lens[i];
-        parts = 1;
-      }
-      char* dst = tasks[t].dst;
-      for (int k = 0; k < parts && !status[i]; k++) {
-        size_t got = 0;
-        while (got < lns[k]) {
-          ssize_t r = pread(fd, dst + got, lns[k] - got, (off_t)(offs[k] + got));
-          if (r < 0) { if (errno == EINTR) continue; status[i] = -errno; break; }
-          if (r == 0) { status[i] = -EIO; break; }  // UnexpectedEof
-          got += (size_t)r;
+  if ((rc = ensure(c, c->staging, nslots * slot))) return rc;
+  hipEvent_t done[2] = {nullptr, nullptr};
+  for (int b = 0; b < nslots; b++)
+    HIP_TRY(c, hipEventCreateWithFlags(&done[b], hipEventDisableTiming));
+  auto gather = [&](size_t w, char* pin) {
+    const Plan& pl = plans[w];
+    const size_t f0 = w * GATHER_WINDOW, m = std::min(GATHER_WINDOW, n - f0);
+    const size_t ns = pl.sampled.size(), np = pl.packed.size();
+    const size_t content_bytes = pl.sampled_bytes + up256(pl.packed_bytes);
+    uint32_t* h_plens = (uint32_t*)(pin + content_bytes + up256((ns + np) * 8) + up256(np * 8));
+    for (size_t k = 0; k < np; k++) h_plens[k] = (uint32_t)lens[f0 + pl.packed[k]];
+    std::atomic<size_t> next{0};
+    c->pool.run(std::max(1u, std::min(16u, (unsigned)((m + 7) / 8))), [&]() {
+      for (size_t t; (t = next.fetch_add(1)) < ns + np;) {
+        const size_t li = t < ns ? pl.sampled[t] : pl.packed[t - ns];
+        const size_t i = f0 + li;
+        if (status[i]) continue;
+        char* dst = t < ns ? pin + t * (size_t)SAMPLED_CONTENT_LEN
+                           : pin + pl.sampled_bytes + pl.poff[t - ns];
+        int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
+        if (fd < 0) { status[i] = -errno; continue; }
+        // cas.rs:35-58 offsets: header at 0, sample k at 8192 + k*jump, footer at size-8192
+        uint64_t offs[6], lns[6];
+        int parts;
+        if (sizes[i] > MINIMUM_FILE_SIZE) {
+          const uint64_t jump = (sizes[i] - 2 * HEADER_OR_FOOTER_SIZE) / SAMPLE_COUNT;
+          offs[0] = 0; lns[0] = HEADER_OR_FOOTER_SIZE;
+          for (int k = 0; k < 4; k++) { offs[1 + k] = HEADER_OR_FOOTER_SIZE + k * jump; lns[1 + k] = SAMPLE_SIZE; }
+          offs[5] = sizes[i] - HEADER_OR_FOOTER_SIZE; lns[5] = HEADER_OR_FOOTER_SIZE;
+          parts = 6;
+        } else {
+          offs[0] = 0; lns[0] = lens[i];
+          parts = 1;
         }
-        dst += lns[k];
+        for (int k = 0; k < parts && !status[i]; k++) {
+          size_t got = 0;
+          while (got < lns[k]) {
+            ssize_t r = pread(fd, dst + got, lns[k] - got, (off_t)(offs[k] + got));
+            if (r < 0) { if (errno == EINTR) continue; status[i] = -errno; break; }
+            if (r == 0) { status[i] = -EIO; break; }  // UnexpectedEof
+            got += (size_t)r;
+          }
+          dst += lns[k];
+        }
+        close(fd);
       }
-      close(fd);
-    }
+    });
   };
-  c->pool.run(nth, worker);  // at most 16 workers: the GPU box's CPU share
-  rc = run_staged(c, pl, sizes, n, out_keys);
+  char* pin0 = (char*)c->pinned;
+  char* dev0 = (char*)c->staging.p;
+  auto finish = [&](size_t w) -> int {
+    const int b = (int)(w & 1);
+    HIP_TRY(c, hipEventSynchronize(done[b]));
+    scatter_keys(plans[w], pin0 + b * slot, out_keys + w * GATHER_WINDOW);
+    return SD_CAS_OK;
+  };
+  for (size_t w = 0; w < nw && rc == 0; w++) {
+    const int b = (int)(w & 1);
+    if (w >= 2 && (rc = finish(w - 2))) break;  // slot b free again
+    gather(w, pin0 + b * slot);
+    const size_t f0 = w * GATHER_WINDOW, m = std::min(GATHER_WINDOW, n - f0);
+    rc = enqueue_staged(c, plans[w], sizes + f0, m, pin0 + b * slot, dev0 + b * slot, done[b]);
+  }
+  for (size_t w = nw >= 2 ? nw - 2 : 0; w < nw && rc == 0; w++) rc = finish(w);
+  if (rc) (void)hipStreamSynchronize(c->stream);
+  for (int b = 0; b < nslots; b++) (void)hipEventDestroy(done[b]);
   if (rc) return rc;
   for (size_t i = 0; i < n; i++)
     if (status[i]) out_keys[i] = 0;

@@ -148,6 +148,28 @@ def test_generate_from_paths_and_errors(eng, oracle, tmp_path):
         sd.generate_cas_id(paths[7], 5000)
 
 
+def test_from_paths_windowed_pipeline(eng, oracle, tmp_path):
+    """> 2 gather windows (2,048 files each): slots reused, errors in several windows."""
+    rng = np.random.default_rng(14)
+    n = 5000
+    sizes = [int(s) for s in np.exp(rng.uniform(0, np.log(400_000), n)).astype(np.int64)]
+    paths = []
+    for i, s in enumerate(sizes):
+        p = tmp_path / f"g{i}"
+        if i % 997 != 13:  # a missing file in each window
+            p.write_bytes(rng.integers(0, 256, s, dtype=np.uint8).tobytes())
+        paths.append(str(p))
+    keys, errs = eng.generate_cas_keys_from_paths(paths, sizes)
+    for i in range(n):
+        if i % 997 == 13:
+            assert errs[i] == 2 and keys[i] == 0, i
+        else:
+            assert errs[i] == 0, i
+    check = [i for i in range(n) if i % 997 != 13][::7]
+    bad = [i for i in check if f"{keys[i]:016x}" != oracle.generate_cas_id(paths[i], sizes[i])]
+    assert not bad, bad[:5]
+
+
 def test_sort_pairs_vs_numpy(eng):
     rng = np.random.default_rng(5)
     for n in [1, 255, 4096, 4097, 100_003]:
