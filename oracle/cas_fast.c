@@ -225,3 +225,57 @@ void orc_fast_cas_keys(const uint8_t* arena, const uint64_t* offs, const uint64_
     for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
   free(th); free(jobs);
 }
+
+/* Config-1 all-cores baseline with the SIMD hasher: each worker gathers its files
+ * (orc_gather_path: the cas.rs offsets) and hashes sampled files 16 at a time with
+ * cas16; whole (ragged) files use the scalar restatement.  keys[i] = 0 and
+ * status[i] = -errno for a failed file. */
+typedef struct {
+  const char* const* paths; const uint64_t* sizes; size_t n; int t, threads, simd;
+  uint64_t* keys; int32_t* status;
+} fpjob_t;
+
+static void* fast_paths_worker(void* p) {
+  fpjob_t* j = (fpjob_t*)p;
+  const size_t S = ORC_SAMPLED_CONTENT_LEN, SMALL = ORC_MINIMUM_FILE_SIZE + 1;
+  uint8_t* grp = malloc(16 * S);
+  uint8_t* one = malloc(SMALL > S ? SMALL : S);
+  size_t gi[16];
+  uint64_t gs[16], gk[16];
+  int ng = 0;
+  for (size_t i = (size_t)j->t; i < j->n; i += (size_t)j->threads) {
+    const int sampled = j->sizes[i] > ORC_MINIMUM_FILE_SIZE;
+    uint8_t* dst = (sampled && j->simd) ? grp + (size_t)ng * S : one;
+    int64_t got = orc_gather_path(j->paths[i], j->sizes[i], dst, sampled ? S : SMALL);
+    if (got < 0) { j->keys[i] = 0; j->status[i] = (int32_t)got; continue; }
+    j->status[i] = 0;
+    if (!(sampled && j->simd)) { j->keys[i] = orc_cas_key(dst, (size_t)got, j->sizes[i]); continue; }
+    gi[ng] = i; gs[ng] = j->sizes[i]; ng++;
+    if (ng == 16) {
+      const uint8_t* ptr[16];
+      for (int l = 0; l < 16; l++) ptr[l] = grp + (size_t)l * S;
+      cas16(ptr, gs, S, gk);
+      for (int l = 0; l < 16; l++) j->keys[gi[l]] = gk[l];
+      ng = 0;
+    }
+  }
+  for (int l = 0; l < ng; l++) j->keys[gi[l]] = orc_cas_key(grp + (size_t)l * S, S, gs[l]);
+  free(grp); free(one);
+  return NULL;
+}
+
+void orc_fast_generate_cas_keys_paths(const char* const* paths, const uint64_t* sizes, size_t n,
+                                      int threads, uint64_t* keys, int32_t* status) {
+  const int simd = orc_fast_has_simd();
+  if (threads < 1) threads = 1;
+  pthread_t* th = calloc((size_t)threads, sizeof *th);
+  fpjob_t* jobs = calloc((size_t)threads, sizeof *jobs);
+  for (int t = 0; t < threads; t++) {
+    jobs[t] = (fpjob_t){paths, sizes, n, t, threads, simd, keys, status};
+    if (threads == 1) fast_paths_worker(&jobs[t]);
+    else pthread_create(&th[t], NULL, fast_paths_worker, &jobs[t]);
+  }
+  if (threads > 1)
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+  free(th); free(jobs);
+}

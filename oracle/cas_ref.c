@@ -179,6 +179,46 @@ int orc_generate_cas_id(const char* path, uint64_t size, char out[17]) {
   return 0;
 }
 
+/* Config-1 CPU baseline, all cores: orc_generate_cas_id over many paths, files statically
+ * interleaved over `threads` workers (each file is an independent job, as in the
+ * reference's join_all over a chunk, mod.rs:105-116). keys[i] = 0 and status[i] = -errno
+ * for a failed file. */
+typedef struct {
+  const char* const* paths; const uint64_t* sizes; size_t n; int t, threads;
+  uint64_t* keys; int32_t* status;
+} pjob_t;
+
+static void* paths_worker(void* p) {
+  pjob_t* j = (pjob_t*)p;
+  uint8_t* buf = malloc(ORC_MINIMUM_FILE_SIZE + 1 > ORC_SAMPLED_CONTENT_LEN ? ORC_MINIMUM_FILE_SIZE + 1
+                                                                          : ORC_SAMPLED_CONTENT_LEN);
+  for (size_t i = (size_t)j->t; i < j->n; i += (size_t)j->threads) {
+    int64_t got = orc_gather_path(j->paths[i], j->sizes[i], buf,
+                                  ORC_MINIMUM_FILE_SIZE + 1 > ORC_SAMPLED_CONTENT_LEN
+                                      ? ORC_MINIMUM_FILE_SIZE + 1 : ORC_SAMPLED_CONTENT_LEN);
+    if (got < 0) { j->keys[i] = 0; j->status[i] = (int32_t)got; continue; }
+    j->keys[i] = orc_cas_key(buf, (size_t)got, j->sizes[i]);
+    j->status[i] = 0;
+  }
+  free(buf);
+  return NULL;
+}
+
+void orc_generate_cas_keys_paths(const char* const* paths, const uint64_t* sizes, size_t n,
+                                 int threads, uint64_t* keys, int32_t* status) {
+  if (threads < 1) threads = 1;
+  pthread_t* th = calloc((size_t)threads, sizeof *th);
+  pjob_t* jobs = calloc((size_t)threads, sizeof *jobs);
+  for (int t = 0; t < threads; t++) {
+    jobs[t] = (pjob_t){paths, sizes, n, t, threads, keys, status};
+    if (threads == 1) paths_worker(&jobs[t]);
+    else pthread_create(&th[t], NULL, paths_worker, &jobs[t]);
+  }
+  if (threads > 1)
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+  free(th); free(jobs);
+}
+
 /* hash.rs:11-25: read 1 MiB at a time into one Hasher, stop at the first short read,
  * full 64-hex digest.  (The reference stops at the first read shorter than 1 MiB; on
  * regular files that is EOF, so this equals the full-file hash.) */

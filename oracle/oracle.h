@@ -71,6 +71,10 @@ void orc_cas_keys_strided(const uint8_t* arena, uint64_t stride, uint64_t conten
 void orc_key_hex(uint64_t key, char out[17]);
 /* generate_cas_id(path, size) -> 0 and out[17], or -errno */
 int orc_generate_cas_id(const char* path, uint64_t size, char out[17]);
+void orc_generate_cas_keys_paths(const char* const* paths, const uint64_t* sizes, size_t n,
+                                 int threads, uint64_t* keys, int32_t* status);
+void orc_fast_generate_cas_keys_paths(const char* const* paths, const uint64_t* sizes, size_t n,
+                                      int threads, uint64_t* keys, int32_t* status);
 /* file_checksum(path) -> 0 and 64-hex, or -errno (hash.rs:11-25) */
 int orc_file_checksum(const char* path, char out[65]);
 

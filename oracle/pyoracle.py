@@ -207,6 +207,11 @@ class Oracle:
         L.orc_fast_has_simd.restype = ctypes.c_int
         L.orc_generate_cas_id.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
         L.orc_generate_cas_id.restype = ctypes.c_int
+        L.orc_generate_cas_keys_paths.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                                  ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_generate_cas_keys_paths.restype = None
+        L.orc_fast_generate_cas_keys_paths.argtypes = L.orc_generate_cas_keys_paths.argtypes
+        L.orc_fast_generate_cas_keys_paths.restype = None
         L.orc_file_checksum.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
         L.orc_file_checksum.restype = ctypes.c_int
         L.orc_gather_path.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p, sz]
@@ -304,6 +309,20 @@ class Oracle:
         if rc != 0:
             raise OSError(-rc, os.strerror(-rc), path)
         return out.value.decode()
+
+    def generate_cas_keys_paths(self, paths, sizes, threads: int = 1, simd: bool = False):
+        """(keys u64, status -errno) for many paths, files interleaved over `threads`;
+        simd=True hashes sampled files 16 at a time with the AVX-512 baseline."""
+        n = len(paths)
+        enc = [os.fsencode(p) for p in paths]
+        parr = (ctypes.c_char_p * n)(*enc)
+        sz = np.ascontiguousarray(sizes, dtype=np.uint64)
+        keys = np.zeros(n, dtype=np.uint64)
+        status = np.zeros(n, dtype=np.int32)
+        fn = self.L.orc_fast_generate_cas_keys_paths if simd else self.L.orc_generate_cas_keys_paths
+        fn(ctypes.cast(parr, ctypes.c_void_p), sz.ctypes.data, n, int(threads), keys.ctypes.data,
+           status.ctypes.data)
+        return keys, status
 
     def file_checksum(self, path: str) -> str:
         out = ctypes.create_string_buffer(65)

@@ -600,15 +600,29 @@ int sd_cas_file_checksum(sd_cas_ctx* c, const char* path, char out_hex[65], int*
     const uint64_t off = sgi * SEG;
     const uint64_t want = std::min<uint64_t>(SEG, len - off);
     if (sgi >= 2) (void)hipEventSynchronize(done[b]);  // pinned[b] free again
-    uint64_t got = 0;
-    while (got < want) {  // hash.rs:16-20 reads until a short read; regular files: EOF
-      ssize_t r = pread(fd, pin[b] + got, want - got, (off_t)(off + got));
-      if (r < 0) { if (errno == EINTR) continue; if (err_no) *err_no = errno; result = fail(c, SD_CAS_EIO, "read(%s): %s", path, strerror(errno)); break; }
-      if (r == 0) break;
-      got += (uint64_t)r;
+    // the segment is read as 4 MiB pieces by the pool (one reader tops out near 5-10 GB/s);
+    // hash.rs:16-20 reads until a short read — a file shorter than its stat is an error here
+    constexpr uint64_t PIECE = 4ull << 20;
+    const uint64_t npieces = (want + PIECE - 1) / PIECE;
+    std::atomic<uint64_t> next{0};
+    std::atomic<int> rd_err{0};
+    c->pool.run((unsigned)std::min<uint64_t>(8, npieces), [&]() {
+      for (uint64_t p; (p = next.fetch_add(1)) < npieces && !rd_err.load();) {
+        const uint64_t p0 = p * PIECE, pn = std::min(PIECE, want - p0);
+        uint64_t got = 0;
+        while (got < pn) {
+          ssize_t r = pread(fd, pin[b] + p0 + got, pn - got, (off_t)(off + p0 + got));
+          if (r < 0 && errno == EINTR) continue;
+          if (r <= 0) { rd_err.store(r < 0 ? errno : EIO); break; }
+          got += (uint64_t)r;
+        }
+      }
+    });
+    if (int e = rd_err.load()) {
+      if (err_no) *err_no = e;
+      result = fail(c, SD_CAS_EIO, "read(%s): %s", path, e == EIO ? "short read" : strerror(e));
+      break;
     }
-    if (result) break;
-    if (got != want) { if (err_no) *err_no = EIO; result = fail(c, SD_CAS_EIO, "short read on %s", path); break; }
     hipError_t e = hipMemcpyAsync(dev[b], pin[b], up16(want), hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess)
       e = checksum_device((const uint8_t*)dev[b], want, off >> 10, nseg == 1, d_cvs + 8 * sgi,

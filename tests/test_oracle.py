@@ -94,6 +94,22 @@ def test_gather_from_files_matches_image(oracle, tmp_path):
         assert oracle.generate_cas_id(str(p), size) == oracle.cas_id(want, size)
 
 
+def test_paths_baseline_matches_single_file(oracle, tmp_path):
+    """The all-cores config-1 CPU baseline equals generate_cas_id file by file."""
+    rng = np.random.default_rng(6)
+    paths, sizes = [], []
+    for i, size in enumerate([0, 7, 4096, 102400, 102401, 500_000] * 3 + [300_000] * 40):
+        p = tmp_path / f"p{i}"
+        p.write_bytes(rng.integers(0, 256, size, dtype=np.uint8).tobytes())
+        paths.append(str(p)); sizes.append(size)
+    paths.append(str(tmp_path / "missing")); sizes.append(10)
+    for threads, simd in ((1, False), (4, False), (1, True), (3, True)):
+        keys, status = oracle.generate_cas_keys_paths(paths, sizes, threads, simd)
+        assert status[-1] == -2 and keys[-1] == 0
+        assert [f"{k:016x}" for k in keys[:-1]] == [oracle.generate_cas_id(p, s)
+                                                     for p, s in zip(paths[:-1], sizes[:-1])]
+
+
 def test_gather_short_file_is_eof_error(oracle, tmp_path):
     p = tmp_path / "short"
     p.write_bytes(b"x" * 150_000)
