@@ -133,6 +133,18 @@ int sd_cas_hash_packed_dev(sd_cas_ctx* ctx, const void* d_arena, const uint64_t*
  * out_objects != NULL.  n < 2^32. */
 int sd_cas_group_dev(sd_cas_ctx* ctx, const uint64_t* d_keys, size_t n, uint32_t* d_rep,
                      uint64_t* out_objects, void* stream);
+/* Generalised grouping (the receive side of the multi-GPU exchange):
+ * d_out[i] = min{ vals[j] : key[j] == key[i] } (vals NULL = identity, i.e. sd_cas_group_dev);
+ * *out_objects = distinct keys (blocks when non-NULL).  n <= ~41M per call. */
+int sd_cas_group_min_dev(sd_cas_ctx* ctx, const uint64_t* d_keys, const uint32_t* d_vals, size_t n,
+                         uint32_t* d_out, uint64_t* out_objects, void* stream);
+/* Key-range partition for the exchange: part(k) = floor(k * parts / 2^64) (BLAKE3 keys are
+ * uniform).  d_keys_out / d_pos_out = keys and their input positions, part-contiguous in
+ * part order (order inside a part unspecified); d_counts[p] (u64, device) = part sizes.
+ * parts <= 16384. */
+int sd_cas_partition_dev(sd_cas_ctx* ctx, const uint64_t* d_keys, size_t n, uint32_t parts,
+                         uint64_t* d_keys_out, uint32_t* d_pos_out, uint64_t* d_counts,
+                         void* stream);
 /* Same on already-sorted pairs (keys ascending, vals = file idx, stable). */
 int sd_cas_group_sorted_dev(sd_cas_ctx* ctx, const uint64_t* d_sorted_keys,
                             const uint32_t* d_sorted_vals, size_t n, uint32_t* d_rep,

@@ -206,6 +206,23 @@ class CasEngine:
                     "group")
         return int(obj.value) if want_objects else None
 
+    def group_min(self, keys, vals, out, stream: Optional[int] = None,
+                  want_objects: bool = True) -> Optional[int]:
+        """out[i] = min{ vals[j] : keys[j] == keys[i] } (vals None = identity)."""
+        n = int(keys.numel())
+        obj = ctypes.c_uint64(0)
+        self._check(self.L.sd_cas_group_min_dev(
+            self.h, _ptr(keys), _ptr(vals) if vals is not None else None, n, _ptr(out),
+            ctypes.byref(obj) if want_objects else None, _stream(stream)), "group_min")
+        return int(obj.value) if want_objects else None
+
+    def partition(self, keys, parts: int, keys_out, pos_out, counts, stream: Optional[int] = None) -> None:
+        """Key-range partition part(k) = floor(k * parts / 2^64), part-contiguous output."""
+        n = int(keys.numel())
+        self._check(self.L.sd_cas_partition_dev(self.h, _ptr(keys), n, int(parts), _ptr(keys_out),
+                                                _ptr(pos_out), _ptr(counts), _stream(stream)),
+                    "partition")
+
     def group_sorted(self, skeys, svals, rep, stream: Optional[int] = None) -> int:
         n = int(skeys.numel())
         obj = ctypes.c_uint64(0)

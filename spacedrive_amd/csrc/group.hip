@@ -306,8 +306,8 @@ size_t group_workspace_bytes(uint64_t n) {
          3 * align_up(ng * 4, 256) + 256;
 }
 
-static hipError_t exclusive_scan_u32(const uint32_t* in, uint32_t* out, uint64_t m,
-                                     uint32_t* partial, hipStream_t s) {
+hipError_t exclusive_scan_u32(const uint32_t* in, uint32_t* out, uint64_t m, uint32_t* partial,
+                              hipStream_t s) {
   const uint32_t nt = tiles_of(m, SCAN_TILE);
   if (nt <= 1) {
     sd_scan_tiles<<<1, SCAN_THREADS, 0, s>>>(in, m, out, nullptr);

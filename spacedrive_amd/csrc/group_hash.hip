@@ -1,0 +1,416 @@
+// group_hash.hip — Object grouping on gfx950 without a full sort (K4h + K5h).
+//
+// Replaces the grouping logic of core/src/object/file_identifier/mod.rs:98-350 (the
+// unique_cas_ids HashSet :149-154, the `cas_id IN (...)` Object lookup :181-198 and the
+// linear `find` over existing Objects :214-224) with the canonical contract of SURVEY.md
+// §8c: rep(f) = min{ g : key(g) == key(f) }, objects = #distinct keys.
+//
+// The grouping never needs the keys in order — only equal keys side by side — so instead
+// of an 8-pass LSD sort (256 B/key of HBM traffic, ~40 launches) it is:
+//   K4h-a  sd_part_hist     per-block bucket histogram, [bucket][block] table   8 B/key read
+//          exclusive scan of the table (sd_group.h exclusive_scan_u32)
+//   K4h-b  sd_part_scatter  keys -> bucket-contiguous (mixed key, position)   8 B read, 12 B write
+//   K5h    sd_bucket_min    one workgroup per bucket: LDS hash table of the bucket's distinct
+//                           keys with an atomic min of the value, then every position looks
+//                           its key up and writes the min                     12 B read, 4 B write
+// ≈ 44 B/key and 6 launches.  The bucket is the top bits of a bijective mix of the key, so
+// any set of DISTINCT keys spreads evenly (BLAKE3 keys are uniform anyway; test keys such
+// as 0..n-1 are not), while duplicates — however many — share one table slot.  A bucket
+// whose distinct keys overflow the LDS table (never for uniform keys: mean <= 1,536
+// distinct per bucket vs 3,584 allowed) is redone by the same workgroup in a global-memory
+// table; results do not depend on the order the scatter wrote the bucket in.
+//
+// The same two kernels give the key-RANGE partition of the multi-GPU exchange (SURVEY §8e:
+// dest = floor(key * G / 2^64)), with the bucket function applied to the raw key.
+// Integer/byte work bound by HBM and LDS atomics; nothing here is reshaped into a GEMM.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sd_group.h"
+
+namespace sdcas {
+
+// Every loop below moves ITEMS keys per thread per trip with all loads issued before the
+// first use: one trip = one memory latency for PART_THREADS x ITEMS keys (a load-per-trip
+// loop at 8 waves/CU was latency-bound at 0.45 TB/s).
+constexpr int PART_THREADS = 512;
+constexpr int ITEMS = 8;
+constexpr uint32_t PART_TILE = PART_THREADS * ITEMS;  // 4096 keys per block trip
+constexpr int MIN_THREADS = 512;
+constexpr uint32_t TABLE = 8192;          // LDS slots per bucket (96 KiB)
+constexpr uint32_t TABLE_FILL = 7168;     // 7/8: above this the bucket goes to global memory
+constexpr uint32_t MAX_BUCKETS = 16384;   // LDS cursor table of the partition kernels (64 KiB)
+constexpr uint64_t TARGET_PER_BUCKET = 3072;
+constexpr uint64_t MAX_TABLE_ENTRIES = 2ull << 20;  // [bucket][block] table (8 MiB)
+
+// splitmix64 finalizer: a bijection on u64, so distinct keys stay distinct
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// mode 0 (grouping): bucket = top bits of mix64(key), the stored key is mix64(key)
+// mode 1 (range partition): bucket = floor(key * nb / 2^64), the stored key is the key
+template <int MODE>
+__device__ __forceinline__ uint64_t stored_key(uint64_t k) {
+  return MODE == 0 ? mix64(k) : k;
+}
+__device__ __forceinline__ uint32_t bucket_of(uint64_t stored, uint32_t nb) {
+  return (uint32_t)__umul64hi(stored, (uint64_t)nb);
+}
+
+template <int MODE>
+__device__ void part_hist_body(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb,
+                               uint64_t per_block, uint32_t* __restrict__ hist, uint32_t nblk) {
+  extern __shared__ uint32_t cnt[];
+  for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS) cnt[b] = 0;
+  __syncthreads();
+  const uint64_t lo = (uint64_t)blockIdx.x * per_block;
+  const uint64_t hi = lo + per_block < n ? lo + per_block : n;
+  for (uint64_t base = lo; base < hi; base += PART_TILE) {
+    uint64_t k[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
+      k[j] = i < hi ? keys[i] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
+      if (i < hi) atomicAdd(&cnt[bucket_of(stored_key<MODE>(k[j]), nb)], 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS)
+    hist[(uint64_t)b * nblk + blockIdx.x] = cnt[b];
+}
+
+template <int MODE>
+__device__ void part_scatter_body(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb,
+                                  uint64_t per_block, const uint32_t* __restrict__ offs,
+                                  uint32_t nblk, uint64_t* __restrict__ out_keys,
+                                  uint32_t* __restrict__ out_pos) {
+  extern __shared__ uint32_t cur[];
+  for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS)
+    cur[b] = offs[(uint64_t)b * nblk + blockIdx.x];
+  __syncthreads();
+  const uint64_t lo = (uint64_t)blockIdx.x * per_block;
+  const uint64_t hi = lo + per_block < n ? lo + per_block : n;
+  for (uint64_t base = lo; base < hi; base += PART_TILE) {
+    uint64_t k[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
+      k[j] = i < hi ? stored_key<MODE>(keys[i]) : 0;
+    }
+    uint32_t p[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
+      p[j] = i < hi ? atomicAdd(&cur[bucket_of(k[j], nb)], 1u) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
+      if (i < hi) {
+        out_keys[p[j]] = k[j];
+        out_pos[p[j]] = (uint32_t)i;
+      }
+    }
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(PART_THREADS)
+sd_part_hist_mix(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb, uint64_t per_block,
+                 uint32_t* __restrict__ hist, uint32_t nblk) {
+  part_hist_body<0>(keys, n, nb, per_block, hist, nblk);
+}
+extern "C" __global__ void __launch_bounds__(PART_THREADS)
+sd_part_hist_range(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb, uint64_t per_block,
+                   uint32_t* __restrict__ hist, uint32_t nblk) {
+  part_hist_body<1>(keys, n, nb, per_block, hist, nblk);
+}
+extern "C" __global__ void __launch_bounds__(PART_THREADS)
+sd_part_scatter_mix(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb, uint64_t per_block,
+                    const uint32_t* __restrict__ offs, uint32_t nblk, uint64_t* __restrict__ out_keys,
+                    uint32_t* __restrict__ out_pos) {
+  part_scatter_body<0>(keys, n, nb, per_block, offs, nblk, out_keys, out_pos);
+}
+extern "C" __global__ void __launch_bounds__(PART_THREADS)
+sd_part_scatter_range(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb, uint64_t per_block,
+                      const uint32_t* __restrict__ offs, uint32_t nblk, uint64_t* __restrict__ out_keys,
+                      uint32_t* __restrict__ out_pos) {
+  part_scatter_body<1>(keys, n, nb, per_block, offs, nblk, out_keys, out_pos);
+}
+
+// counts[b] = size of part b (from the scanned [bucket][block] table)
+extern "C" __global__ void __launch_bounds__(256)
+sd_part_counts(const uint32_t* __restrict__ offs, uint32_t nb, uint32_t nblk, uint64_t n,
+               uint64_t* __restrict__ counts) {
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  if (b < nb) {
+    const uint64_t s = offs[(uint64_t)b * nblk];
+    const uint64_t e = b + 1 < nb ? offs[(uint64_t)(b + 1) * nblk] : n;
+    counts[b] = e - s;
+  }
+}
+
+// Linear-probing tables: LDS (the normal case) and global memory (overflow).  `fresh`
+// counts keys this thread inserted first.  Returns false if the table has no room.
+__device__ __forceinline__ bool lds_insert(uint64_t* tk, uint32_t* tv, uint32_t slot, uint64_t k,
+                                           uint32_t v, uint64_t empty, uint32_t& fresh) {
+  for (uint32_t probe = 0; probe < TABLE; ++probe) {
+    uint64_t cur = tk[slot];
+    if (cur == empty) {
+      const uint64_t old = atomicCAS((unsigned long long*)&tk[slot], (unsigned long long)empty,
+                                     (unsigned long long)k);
+      if (old == empty) { ++fresh; cur = k; } else { cur = old; }
+    }
+    if (cur == k) {
+      atomicMin(&tv[slot], v);
+      return true;
+    }
+    slot = (slot + 1) & (TABLE - 1);
+  }
+  return false;
+}
+
+__device__ __forceinline__ uint32_t lds_find(const uint64_t* tk, uint32_t slot, uint64_t k) {
+  while (tk[slot] != k) slot = (slot + 1) & (TABLE - 1);  // present by construction
+  return slot;
+}
+
+// global tables are read with device-scope atomic loads: other waves of this workgroup
+// CAS the slots at L2, and a plain load could be served a stale line from this CU's L1
+__device__ __forceinline__ uint64_t gload(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void g_insert(uint64_t* tk, uint32_t* tv, uint64_t cap, uint64_t slot,
+                                         uint64_t k, uint32_t v, uint64_t empty, uint32_t& fresh) {
+  for (;;) {  // cap = 2 x the bucket's keys: a free slot always exists
+    uint64_t cur = gload(&tk[slot]);
+    if (cur == empty) {
+      const uint64_t old = atomicCAS((unsigned long long*)&tk[slot], (unsigned long long)empty,
+                                     (unsigned long long)k);
+      if (old == empty) { ++fresh; cur = k; } else { cur = old; }
+    }
+    if (cur == k) {
+      atomicMin(&tv[slot], v);
+      return;
+    }
+    slot = slot + 1 == cap ? 0 : slot + 1;
+  }
+}
+
+__device__ __forceinline__ uint64_t g_find(const uint64_t* tk, uint64_t cap, uint64_t slot, uint64_t k) {
+  while (gload(&tk[slot]) != k) slot = slot + 1 == cap ? 0 : slot + 1;
+  return slot;
+}
+
+// One workgroup per bucket of the mixed-key partition (nb = 2^bits, bits >= 1).
+// out[pos] = min{ val(j) : key(j) == key(pos) }, val(j) = vals ? vals[j] : j;
+// *objects += distinct keys.  gkeys/gvals: 2n-slot overflow tables (touched only on overflow).
+// A bucket of <= PART_TILE keys (all but pathological ones) is loaded once and kept in
+// registers for the lookup; larger buckets stream in PART_TILE trips.
+extern "C" __global__ void __launch_bounds__(MIN_THREADS)
+sd_bucket_min(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ ppos,
+              const uint32_t* __restrict__ vals, const uint32_t* __restrict__ offs, uint32_t nb,
+              uint32_t bits, uint32_t nblk, uint64_t n, uint32_t* __restrict__ out,
+              unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
+              uint32_t* __restrict__ gvals) {
+  __shared__ uint64_t tk[TABLE];
+  __shared__ uint32_t tv[TABLE];
+  __shared__ uint32_t distinct;
+  __shared__ int overflow;
+  const uint32_t b = blockIdx.x;
+  const uint64_t s = offs[(uint64_t)b * nblk];
+  const uint64_t e = b + 1 < nb ? offs[(uint64_t)(b + 1) * nblk] : n;
+  if (s == e) return;  // uniform for the whole workgroup
+  // every stored key of this bucket has top bits == b, so a key from bucket b^1 is never stored
+  const uint64_t empty = (uint64_t)(b ^ 1u) << (64 - bits);
+  for (uint32_t i = threadIdx.x; i < TABLE; i += MIN_THREADS) { tk[i] = empty; tv[i] = 0xFFFFFFFFu; }
+  if (threadIdx.x == 0) { distinct = 0; overflow = 0; }
+  uint64_t k[ITEMS];
+  uint32_t p[ITEMS];
+  for (uint64_t base = s; base < e; base += PART_TILE) {
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint64_t i = base + (uint64_t)j * MIN_THREADS + threadIdx.x;
+      k[j] = i < e ? pkeys[i] : empty;
+      p[j] = i < e ? ppos[i] : 0u;
+    }
+    uint32_t v[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) v[j] = (vals && k[j] != empty) ? vals[p[j]] : p[j];
+    __syncthreads();  // table initialised (first trip) / overflow flag visible
+    if (overflow) break;
+    uint32_t fresh = 0;
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j)
+      if (k[j] != empty) ok &= lds_insert(tk, tv, (uint32_t)k[j] & (TABLE - 1), k[j], v[j], empty, fresh);
+    if (fresh && atomicAdd(&distinct, fresh) + fresh > TABLE_FILL) overflow = 1;
+    if (!ok) overflow = 1;
+  }
+  __syncthreads();
+  if (!overflow) {
+    if (e - s <= PART_TILE) {  // the one trip's keys are still in registers
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j)
+        if (k[j] != empty) out[p[j]] = tv[lds_find(tk, (uint32_t)k[j] & (TABLE - 1), k[j])];
+    } else {
+      for (uint64_t base = s; base < e; base += PART_TILE) {
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+          const uint64_t i = base + (uint64_t)j * MIN_THREADS + threadIdx.x;
+          k[j] = i < e ? pkeys[i] : empty;
+          p[j] = i < e ? ppos[i] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j)
+          if (k[j] != empty) out[p[j]] = tv[lds_find(tk, (uint32_t)k[j] & (TABLE - 1), k[j])];
+      }
+    }
+    if (threadIdx.x == 0) atomicAdd(objects, (unsigned long long)distinct);
+    return;
+  }
+  // Overflow: redo the bucket in its own 2m-slot global table (load <= 1/2).
+  const uint64_t m = e - s, cap = 2 * m;
+  uint64_t* gk = gkeys + 2 * s;
+  uint32_t* gv = gvals + 2 * s;
+  for (uint64_t i = threadIdx.x; i < cap; i += MIN_THREADS) { gk[i] = empty; gv[i] = 0xFFFFFFFFu; }
+  if (threadIdx.x == 0) distinct = 0;
+  __threadfence();
+  __syncthreads();
+  uint32_t fresh = 0;
+  for (uint64_t i = s + threadIdx.x; i < e; i += MIN_THREADS) {
+    const uint64_t kk = pkeys[i];
+    const uint32_t pp = ppos[i];
+    g_insert(gk, gv, cap, (kk & 0xFFFFFFFFull) % cap, kk, vals ? vals[pp] : pp, empty, fresh);
+  }
+  if (fresh) atomicAdd(&distinct, fresh);
+  __threadfence();
+  __syncthreads();
+  for (uint64_t i = s + threadIdx.x; i < e; i += MIN_THREADS) {
+    const uint64_t kk = pkeys[i];
+    const uint64_t slot = g_find(gk, cap, (kk & 0xFFFFFFFFull) % cap, kk);
+    out[ppos[i]] = __hip_atomic_load(&gv[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (threadIdx.x == 0) atomicAdd(objects, (unsigned long long)distinct);
+}
+
+}  // namespace sdcas
+
+// ---- host launchers ----------------------------------------------------------------
+namespace sdcas {
+
+static inline size_t al256(size_t x) { return (x + 255) / 256 * 256; }
+
+struct PartPlan {
+  uint32_t nb, bits, nblk;
+  uint64_t per_block;
+};
+
+// blocks: whole PART_TILE trips, about 2 per CU-slot, and a [bucket][block] table of at
+// most MAX_TABLE_ENTRIES (the table is written, scanned and read once per grouping)
+static PartPlan part_plan(uint64_t n, uint32_t nb, uint32_t bits) {
+  PartPlan p{nb, bits, 1, PART_TILE};
+  const uint64_t trips = n ? (n + PART_TILE - 1) / PART_TILE : 1;
+  uint64_t maxblk = MAX_TABLE_ENTRIES / nb;
+  if (maxblk < 1) maxblk = 1;
+  const uint64_t nblk = trips < maxblk ? trips : maxblk;
+  const uint64_t per = (trips + nblk - 1) / nblk;  // trips per block
+  p.per_block = per * PART_TILE;
+  p.nblk = (uint32_t)((n + p.per_block - 1) / p.per_block);
+  if (p.nblk == 0) p.nblk = 1;
+  return p;
+}
+
+static PartPlan mix_plan(uint64_t n) {
+  uint32_t bits = 1;
+  while (bits < 14 && ((uint64_t)1 << bits) * TARGET_PER_BUCKET < n) ++bits;
+  return part_plan(n, 1u << bits, bits);
+}
+
+bool hash_group_supported(uint64_t n) {
+  // nb <= 16384 buckets at <= ~5,000 distinct keys each on average (table fill 7,168)
+  return n < (1ull << 32) && n <= (uint64_t)MAX_BUCKETS * 5000;
+}
+
+static size_t part_ws(const PartPlan& p, uint64_t n) {
+  const uint64_t m = (uint64_t)p.nb * p.nblk;
+  return al256(n * 8) + al256(n * 4) + 2 * al256(m * 4) + al256(((m + 4095) / 4096) * 4 + 4);
+}
+
+size_t hash_group_workspace_bytes(uint64_t n) {
+  const PartPlan p = mix_plan(n);
+  return part_ws(p, n) + al256(2 * n * 8) + al256(2 * n * 4);
+}
+
+size_t partition_workspace_bytes(uint64_t n, uint32_t parts) {
+  const PartPlan p = part_plan(n, parts, 0);
+  const uint64_t m = (uint64_t)p.nb * p.nblk;
+  return 2 * al256(m * 4) + al256(((m + 4095) / 4096) * 4 + 4);
+}
+
+static hipError_t run_partition(const uint64_t* keys, uint64_t n, const PartPlan& p, int mode,
+                                uint64_t* out_keys, uint32_t* out_pos, uint32_t* hist,
+                                uint32_t* offs, uint32_t* partial, hipStream_t s) {
+  const uint64_t m = (uint64_t)p.nb * p.nblk;
+  const size_t lds = (size_t)p.nb * 4;
+  if (mode == 0)
+    sd_part_hist_mix<<<p.nblk, PART_THREADS, lds, s>>>(keys, n, p.nb, p.per_block, hist, p.nblk);
+  else
+    sd_part_hist_range<<<p.nblk, PART_THREADS, lds, s>>>(keys, n, p.nb, p.per_block, hist, p.nblk);
+  hipError_t e = exclusive_scan_u32(hist, offs, m, partial, s);
+  if (e != hipSuccess) return e;
+  if (mode == 0)
+    sd_part_scatter_mix<<<p.nblk, PART_THREADS, lds, s>>>(keys, n, p.nb, p.per_block, offs, p.nblk,
+                                                          out_keys, out_pos);
+  else
+    sd_part_scatter_range<<<p.nblk, PART_THREADS, lds, s>>>(keys, n, p.nb, p.per_block, offs,
+                                                            p.nblk, out_keys, out_pos);
+  return hipGetLastError();
+}
+
+hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n, uint32_t* out,
+                          uint64_t* d_objects, void* ws, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(d_objects, 0, 8, s);
+  if (e != hipSuccess || n == 0) return e;
+  if (!hash_group_supported(n)) return hipErrorInvalidValue;
+  const PartPlan p = mix_plan(n);
+  const uint64_t m = (uint64_t)p.nb * p.nblk;
+  char* q = (char*)ws;
+  uint64_t* pkeys = (uint64_t*)q; q += al256(n * 8);
+  uint32_t* ppos = (uint32_t*)q; q += al256(n * 4);
+  uint32_t* hist = (uint32_t*)q; q += al256(m * 4);
+  uint32_t* offs = (uint32_t*)q; q += al256(m * 4);
+  uint32_t* partial = (uint32_t*)q; q += al256(((m + 4095) / 4096) * 4 + 4);
+  uint64_t* gkeys = (uint64_t*)q; q += al256(2 * n * 8);
+  uint32_t* gvals = (uint32_t*)q;
+  e = run_partition(keys, n, p, 0, pkeys, ppos, hist, offs, partial, s);
+  if (e != hipSuccess) return e;
+  sd_bucket_min<<<p.nb, MIN_THREADS, 0, s>>>(pkeys, ppos, vals, offs, p.nb, p.bits, p.nblk, n, out,
+                                             (unsigned long long*)d_objects, gkeys, gvals);
+  return hipGetLastError();
+}
+
+hipError_t partition_range(const uint64_t* keys, uint64_t n, uint32_t parts, uint64_t* out_keys,
+                           uint32_t* out_pos, uint64_t* d_counts, void* ws, hipStream_t s) {
+  if (parts == 0 || parts > MAX_BUCKETS || n >= (1ull << 32)) return hipErrorInvalidValue;
+  if (n == 0) return hipMemsetAsync(d_counts, 0, (size_t)parts * 8, s);
+  const PartPlan p = part_plan(n, parts, 0);
+  const uint64_t m = (uint64_t)p.nb * p.nblk;
+  char* q = (char*)ws;
+  uint32_t* hist = (uint32_t*)q; q += al256(m * 4);
+  uint32_t* offs = (uint32_t*)q; q += al256(m * 4);
+  uint32_t* partial = (uint32_t*)q;
+  hipError_t e = run_partition(keys, n, p, 1, out_keys, out_pos, hist, offs, partial, s);
+  if (e != hipSuccess) return e;
+  sd_part_counts<<<(parts + 255) / 256, 256, 0, s>>>(offs, p.nb, p.nblk, n, d_counts);
+  return hipGetLastError();
+}
+
+}  // namespace sdcas

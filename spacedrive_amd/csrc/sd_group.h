@@ -26,6 +26,24 @@ hipError_t group_keys(const uint64_t* keys, uint64_t n, uint32_t* rep, uint64_t*
 hipError_t group_sorted(const uint64_t* skeys, const uint32_t* svals, uint64_t n, uint32_t* rep,
                         uint64_t* d_objects, void* ws, hipStream_t stream);
 
+// Device-wide exclusive scan of m <= 4096^2 u32 (partial: >= m/4096 + 1 u32 of scratch).
+hipError_t exclusive_scan_u32(const uint32_t* in, uint32_t* out, uint64_t m, uint32_t* partial,
+                              hipStream_t stream);
+
+// ---- group_hash.hip: grouping without a full sort -------------------------------------
+bool hash_group_supported(uint64_t n);
+size_t hash_group_workspace_bytes(uint64_t n);
+size_t partition_workspace_bytes(uint64_t n, uint32_t parts);
+// out[i] = min{ val(j) : keys[j] == keys[i] } with val(j) = vals ? vals[j] : j;
+// *d_objects = #distinct keys (written on the device).  n < 2^32.
+hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n, uint32_t* out,
+                          uint64_t* d_objects, void* ws, hipStream_t stream);
+// Key-range partition: part(k) = floor(k * parts / 2^64); out_keys/out_pos hold the keys and
+// their input positions part-contiguous (order inside a part unspecified), d_counts[p] the
+// part sizes.  ws: partition_workspace_bytes(n, parts).
+hipError_t partition_range(const uint64_t* keys, uint64_t n, uint32_t parts, uint64_t* out_keys,
+                           uint32_t* out_pos, uint64_t* d_counts, void* ws, hipStream_t stream);
+
 // chunk-of-`chunk` emulation; *d_created accumulates (zero it first).
 hipError_t group_chunked(const uint32_t* rep, uint64_t n, uint32_t chunk, uint32_t* rep_chunked,
                          uint64_t* d_created, hipStream_t stream);

@@ -201,13 +201,50 @@ int sd_cas_group_dev(sd_cas_ctx* c, const uint64_t* d_keys, size_t n, uint32_t* 
   if (n >= (1ull << 32) || (n && (!d_keys || !d_rep)))
     return fail(c, SD_CAS_EINVAL, "group: bad arguments");
   hipStream_t s = pick(c, stream);
-  int rc = ensure(c, c->ws, group_workspace_bytes(n));
-  if (rc) return rc;
-  HIP_TRY(c, group_keys(d_keys, n, d_rep, c->d_scalar, c->ws.p, s));
+  if (hash_group_supported(n)) {  // K4h/K5h: bucket partition + LDS hash min (no full sort)
+    int rc = ensure(c, c->ws, hash_group_workspace_bytes(n));
+    if (rc) return rc;
+    HIP_TRY(c, hash_group_min(d_keys, nullptr, n, d_rep, c->d_scalar, c->ws.p, s));
+  } else {  // beyond ~41M keys per call: LSD radix sort + run heads (K4 + K5)
+    int rc = ensure(c, c->ws, group_workspace_bytes(n));
+    if (rc) return rc;
+    HIP_TRY(c, group_keys(d_keys, n, d_rep, c->d_scalar, c->ws.p, s));
+  }
   if (out_objects) {
     HIP_TRY(c, hipMemcpyAsync(out_objects, c->d_scalar, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
   }
+  return SD_CAS_OK;
+}
+
+int sd_cas_group_min_dev(sd_cas_ctx* c, const uint64_t* d_keys, const uint32_t* d_vals, size_t n,
+                         uint32_t* d_out, uint64_t* out_objects, void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (n >= (1ull << 32) || (n && (!d_keys || !d_out)))
+    return fail(c, SD_CAS_EINVAL, "group_min: bad arguments");
+  if (!hash_group_supported(n)) return fail(c, SD_CAS_EINVAL, "group_min: batch too large");
+  hipStream_t s = pick(c, stream);
+  int rc = ensure(c, c->ws, hash_group_workspace_bytes(n));
+  if (rc) return rc;
+  HIP_TRY(c, hash_group_min(d_keys, d_vals, n, d_out, c->d_scalar, c->ws.p, s));
+  if (out_objects) {
+    HIP_TRY(c, hipMemcpyAsync(out_objects, c->d_scalar, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+  }
+  return SD_CAS_OK;
+}
+
+int sd_cas_partition_dev(sd_cas_ctx* c, const uint64_t* d_keys, size_t n, uint32_t parts,
+                         uint64_t* d_keys_out, uint32_t* d_pos_out, uint64_t* d_counts,
+                         void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (parts == 0 || parts > 16384 || n >= (1ull << 32) || !d_counts ||
+      (n && (!d_keys || !d_keys_out || !d_pos_out)))
+    return fail(c, SD_CAS_EINVAL, "partition: bad arguments");
+  hipStream_t s = pick(c, stream);
+  int rc = ensure(c, c->ws, partition_workspace_bytes(n, parts));
+  if (rc) return rc;
+  HIP_TRY(c, partition_range(d_keys, n, parts, d_keys_out, d_pos_out, d_counts, c->ws.p, s));
   return SD_CAS_OK;
 }
 

@@ -6,35 +6,36 @@ Reference: the grouping of core/src/object/file_identifier/mod.rs:98-350 (SURVEY
 The reference runs on one host thread; here G ranks (one process per GPU) each hash
 their contiguous slice of files (no communication), then:
 
-  1. local stable sort of (key, local idx)                  [HIP radix sort]
-  2. split points of the key ranges dest(k) = floor(k * G / 2^64) on the sorted keys
-  3. all_to_all_single of keys and global idx (counts first)   [RCCL]
-  4. local stable sort of the received (key, recv position) -> runs -> rep = head's
-     global idx (received runs arrive in rank order and each run is idx-ascending, so
-     the head of an equal-key run holds the global minimum idx)   [HIP]
-  5. mirror all_to_all_single of the reps; scatter into local idx order  [RCCL]
+  1. key-range partition of the local keys, dest(k) = floor(k * G / 2^64)
+     (BLAKE3 keys are uniform)                                   [HIP: sd_cas_partition_dev]
+  2. all_to_all_single of the part sizes, then of keys and global file idx  [RCCL]
+  3. grouping of the received pairs: rep = min global idx over equal keys
+                                                                 [HIP: sd_cas_group_min_dev]
+  4. mirror all_to_all_single of the reps; scatter to local file order  [RCCL]
 
-``ops`` supplies the three device primitives; in production it is the HIP engine
+Every key lives on exactly one rank after step 2, so step 3's minimum is the global one:
+rep(f) = min{ g : key(g) == key(f) } over all ranks, the single-GPU contract.
+
+``ops`` supplies the device primitives; in production it is the HIP engine
 (:class:`HipShardOps`).  Tests on CPU pass a host implementation to check the exchange
 logic with the gloo backend — that is a test double for the kernels, not a fallback.
 """
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Optional, Protocol
+from typing import Protocol
 
 import torch
 import torch.distributed as dist
 
-SIGN = -(1 << 63)  # int64 bit pattern of 0x8000_0000_0000_0000
-
 
 class ShardOps(Protocol):
-    def sort_pairs(self, keys: torch.Tensor, vals: Optional[torch.Tensor]) -> tuple[torch.Tensor, torch.Tensor]:
-        """stable sort of u64 keys (int64 storage) -> (sorted keys, int32 vals)"""
+    def partition(self, keys: torch.Tensor, parts: int) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """key-range partition -> (part-contiguous keys, their int32 input positions,
+        int64 part sizes)"""
 
-    def group_sorted(self, skeys: torch.Tensor, svals: torch.Tensor) -> tuple[torch.Tensor, int]:
-        """rep[svals[i]] = svals[head(i)] (int32), objects"""
+    def group_min(self, keys: torch.Tensor, vals: torch.Tensor) -> tuple[torch.Tensor, int]:
+        """out[i] = min{ vals[j] : keys[j] == keys[i] } (int32), distinct keys"""
 
 
 class HipShardOps:
@@ -43,36 +44,19 @@ class HipShardOps:
     def __init__(self, eng):
         self.eng = eng
 
-    def sort_pairs(self, keys, vals):
+    def partition(self, keys, parts):
         n = keys.numel()
         ko = torch.empty_like(keys)
-        vo = torch.empty(n, dtype=torch.int32, device=keys.device)
-        self.eng.sort_pairs(keys, vals, ko, vo, 0, 64, stream=torch.cuda.current_stream().cuda_stream)
-        return ko, vo
+        po = torch.empty(n, dtype=torch.int32, device=keys.device)
+        counts = torch.empty(parts, dtype=torch.int64, device=keys.device)
+        self.eng.partition(keys, parts, ko, po, counts,
+                           stream=torch.cuda.current_stream().cuda_stream)
+        return ko, po, counts
 
-    def group_sorted(self, skeys, svals):
-        rep = torch.empty(skeys.numel(), dtype=torch.int32, device=skeys.device)
-        objects = self.eng.group_sorted(skeys, svals, rep,
-                                        stream=torch.cuda.current_stream().cuda_stream)
-        return rep, objects
-
-
-def key_range_splits(sorted_keys: torch.Tensor, world: int) -> torch.Tensor:
-    """counts[r] = #keys with floor(k * world / 2^64) == r, keys sorted as unsigned u64.
-
-    Flipping the sign bit maps unsigned order onto signed int64 order, so the boundaries
-    ceil(r * 2^64 / world) can be located with torch.searchsorted."""
-    flipped = sorted_keys ^ SIGN
-    bounds = []
-    for r in range(1, world):
-        b = -((-(r << 64)) // world)  # ceil(r * 2^64 / world), unsigned
-        fb = b ^ (1 << 63)            # sign-flipped ...
-        bounds.append(fb - (1 << 64) if fb >= (1 << 63) else fb)  # ... as int64
-    bt = torch.tensor(bounds, dtype=torch.int64, device=sorted_keys.device)
-    pos = torch.searchsorted(flipped, bt)  # number of keys < boundary
-    edges = torch.cat([torch.zeros(1, dtype=torch.int64, device=pos.device), pos,
-                       torch.tensor([sorted_keys.numel()], dtype=torch.int64, device=pos.device)])
-    return edges[1:] - edges[:-1]
+    def group_min(self, keys, vals):
+        out = torch.empty(keys.numel(), dtype=torch.int32, device=keys.device)
+        objects = self.eng.group_min(keys, vals, out, stream=torch.cuda.current_stream().cuda_stream)
+        return out, objects
 
 
 @dataclass
@@ -89,29 +73,29 @@ def sharded_group(local_keys: torch.Tensor, file0: int, ops: ShardOps,
     rank = dist.get_rank(group)
     dev = local_keys.device
     n = local_keys.numel()
-    skeys, sidx = ops.sort_pairs(local_keys, None)               # 1
-    send_counts = key_range_splits(skeys, world)                  # 2
+    pkeys, ppos, send_counts = ops.partition(local_keys, world)     # 1
     recv_counts = torch.empty_like(send_counts)
-    dist.all_to_all_single(recv_counts, send_counts, group=group)  # counts exchange
+    dist.all_to_all_single(recv_counts, send_counts, group=group)  # 2: sizes
     sc = send_counts.cpu().tolist()
     rc = recv_counts.cpu().tolist()
-    gidx = sidx.to(torch.int64) + file0
+    gidx = ppos.to(torch.int64) + file0
     rkeys = torch.empty(sum(rc), dtype=torch.int64, device=dev)
     ridx = torch.empty(sum(rc), dtype=torch.int64, device=dev)
-    dist.all_to_all_single(rkeys, skeys, rc, sc, group=group)     # 3
+    dist.all_to_all_single(rkeys, pkeys, rc, sc, group=group)     # 2: keys, global idx
     dist.all_to_all_single(ridx, gidx, rc, sc, group=group)
     m = rkeys.numel()
     if m:
-        k2, pos = ops.sort_pairs(rkeys, None)                     # 4
-        rep_pos, objects = ops.group_sorted(k2, pos)
-        rep_global = ridx[rep_pos.to(torch.int64)]
+        if int(ridx.max().item()) >= (1 << 32):
+            raise ValueError("sharded_group: global file idx must fit in u32")
+        rep_min, objects = ops.group_min(rkeys, ridx.to(torch.int32))  # 3
+        rep_global = rep_min.to(torch.int64) & 0xFFFFFFFF
     else:
         rep_global = torch.empty(0, dtype=torch.int64, device=dev)
         objects = 0
     back = torch.empty(n, dtype=torch.int64, device=dev)
-    dist.all_to_all_single(back, rep_global, sc, rc, group=group)  # 5
+    dist.all_to_all_single(back, rep_global, sc, rc, group=group)  # 4
     rep = torch.empty(n, dtype=torch.int64, device=dev)
-    rep[sidx.to(torch.int64)] = back
+    rep[ppos.to(torch.int64)] = back
     tot = torch.tensor([objects], dtype=torch.int64, device=dev)
     dist.all_reduce(tot, group=group)
     return ShardResult(rep=rep, objects=int(tot.item()), sent=n - int(sc[rank]))

@@ -211,6 +211,82 @@ def test_group_vs_oracle(eng, oracle, golden):
         assert (c, ln) == (cc, cl) and (rc.cpu().numpy().astype(np.uint32) == crep).all()
 
 
+MASK64 = (1 << 64) - 1
+
+
+def unmix64(m: int) -> int:
+    """Inverse of the splitmix64 finalizer the hash grouping buckets by (group_hash.hip)."""
+    def unxorshift(z, s):
+        x = z
+        for _ in range(64 // s + 1):
+            x = z ^ (x >> s)
+        return x & MASK64
+    m = unxorshift(m, 31)
+    m = (m * pow(0x94D049BB133111EB, -1, 1 << 64)) & MASK64
+    m = unxorshift(m, 27)
+    m = (m * pow(0xBF58476D1CE4E5B9, -1, 1 << 64)) & MASK64
+    return unxorshift(m, 30)
+
+
+def test_group_hash_adversarial_keys(eng, oracle):
+    """K4h/K5h on key sets that are not uniform: small integers, one key repeated, and
+    8,000 distinct keys crafted (inverse mix) into ONE bucket so its LDS table overflows
+    and the global-memory table takes over — every case vs the oracle's canonical grouping."""
+    rng = np.random.default_rng(40)
+    crafted = np.array([unmix64(int(x) >> 3) for x in rng.integers(0, 2 ** 63, 8000, dtype=np.uint64)],
+                       dtype=np.uint64)  # mix64(key) has top 3 bits 0: all in bucket 0 of 8
+    cases = {
+        "small ints": rng.integers(0, 3000, 9000, dtype=np.uint64),
+        "iota": np.arange(70_000, dtype=np.uint64),
+        "one key": np.full(100_000, 0xDEADBEEF, dtype=np.uint64),
+        "zero and max": rng.choice(np.array([0, 2 ** 64 - 1], dtype=np.uint64), 5000),
+        "crafted overflow": crafted[rng.integers(0, len(crafted), 12_000)],
+        "crafted distinct": crafted,
+    }
+    for name, keys in cases.items():
+        rep = torch.empty(len(keys), dtype=torch.int32, device="cuda")
+        objects = eng.group(dev64(keys), rep)
+        orep, oobj = oracle.group_canonical(keys)
+        assert objects == oobj, name
+        assert (rep.cpu().numpy().astype(np.uint32) == orep).all(), name
+
+
+def test_group_min_vs_numpy(eng):
+    rng = np.random.default_rng(41)
+    for n, pool in [(1, 1), (777, 100), (250_000, 90_000), (2_000_000, 1_500_000)]:
+        base = rng.integers(0, 2 ** 64, pool, dtype=np.uint64)
+        keys = base[rng.integers(0, pool, n)]
+        vals = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+        out = torch.empty(n, dtype=torch.int32, device="cuda")
+        objects = eng.group_min(dev64(keys), torch.from_numpy(vals.view(np.int32)).cuda(), out)
+        uniq, inv = np.unique(keys, return_inverse=True)
+        mins = np.full(len(uniq), 0xFFFFFFFF, dtype=np.uint32)
+        np.minimum.at(mins, inv, vals)
+        assert objects == len(uniq)
+        assert (out.cpu().numpy().view(np.uint32) == mins[inv]).all()
+
+
+def test_partition_range_vs_numpy(eng):
+    from tests.test_shard_cpu import range_part
+    rng = np.random.default_rng(42)
+    for n, parts in [(0, 3), (1, 1), (1000, 2), (123_457, 3), (1 << 20, 8), (50_000, 7)]:
+        keys = rng.integers(0, 2 ** 64, n, dtype=np.uint64)
+        if n >= 8:
+            keys[:8] = [0, 1, 2 ** 63 - 1, 2 ** 63, 2 ** 64 - 1, -((-(1 << 64)) // 3), (1 << 64) // 3, 5]
+        ko = torch.empty(max(n, 1), dtype=torch.int64, device="cuda")
+        po = torch.empty(max(n, 1), dtype=torch.int32, device="cuda")
+        counts = torch.empty(parts, dtype=torch.int64, device="cuda")
+        eng.partition(dev64(keys) if n else torch.empty(0, dtype=torch.int64, device="cuda"),
+                      parts, ko, po, counts)
+        want = np.bincount(range_part(keys, parts), minlength=parts)
+        assert counts.cpu().tolist() == want.tolist()
+        if n == 0:
+            continue
+        k, p = host64(ko)[:n], po.cpu().numpy()[:n]
+        assert (np.sort(p) == np.arange(n)).all() and (keys[p] == k).all()
+        assert (np.diff(range_part(k, parts)) >= 0).all()  # part-contiguous in part order
+
+
 CHECKSUM_LENS = [0, 1, 63, 64, 65, 1023, 1024, 1025, 2048, 4097, 255 * 1024, 256 * 1024,
                  256 * 1024 + 1, 257 * 1024 + 3, 512 * 1024, 65536 * 1024 + 5, 3 * 256 * 1024 * 256 + 777]
 

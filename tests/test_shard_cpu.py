@@ -14,28 +14,35 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 
+def range_part(k: np.ndarray, parts: int) -> np.ndarray:
+    """floor(k * parts / 2^64) for u64 k, exactly (the contract of sd_cas_partition_dev)."""
+    hi, lo = k >> np.uint64(32), k & np.uint64(0xFFFFFFFF)
+    t = hi * np.uint64(parts) + ((lo * np.uint64(parts)) >> np.uint64(32))
+    return (t >> np.uint64(32)).astype(np.int64)
+
+
 class HostOps:
-    """Test double of HipShardOps: numpy stable sort + run heads, same contracts."""
+    """Test double of HipShardOps (numpy), same contracts: the partition's order inside a
+    part is unspecified, so the double scrambles it to keep the exchange honest."""
 
-    def sort_pairs(self, keys, vals):
+    def __init__(self, seed: int = 0):
+        self.rng = np.random.default_rng(seed)
+
+    def partition(self, keys, parts):
         k = keys.numpy().view(np.uint64)
-        order = np.argsort(k, kind="stable")
-        v = order if vals is None else vals.numpy()[order]
+        d = range_part(k, parts)
+        order = np.lexsort((self.rng.random(len(k)), d))  # part-contiguous, scrambled inside
+        counts = np.bincount(d, minlength=parts).astype(np.int64)
         return (torch.from_numpy(k[order].view(np.int64).copy()),
-                torch.from_numpy(v.astype(np.int32)))
+                torch.from_numpy(order.astype(np.int32)), torch.from_numpy(counts))
 
-    def group_sorted(self, skeys, svals):
-        k = skeys.numpy()
-        v = svals.numpy()
-        rep = np.empty(len(k), dtype=np.int32)
-        head = 0
-        objects = 0
-        for i in range(len(k)):
-            if i == 0 or k[i] != k[i - 1]:
-                head = i
-                objects += 1
-            rep[v[i]] = v[head]
-        return torch.from_numpy(rep), objects
+    def group_min(self, keys, vals):
+        k = keys.numpy()
+        v = vals.numpy().view(np.uint32)
+        uniq, inv = np.unique(k, return_inverse=True)
+        mins = np.full(len(uniq), 0xFFFFFFFF, dtype=np.uint32)
+        np.minimum.at(mins, inv, v)
+        return torch.from_numpy(mins[inv].view(np.int32).copy()), len(uniq)
 
 
 def _free_port():
@@ -89,11 +96,12 @@ def test_sharded_group_matches_canonical(world, oracle):
     assert (rep == orep.astype(np.int64)).all()
 
 
-def test_key_range_splits_boundaries():
-    from spacedrive_amd.shard import key_range_splits
+def test_range_part_boundaries():
     k = np.array([0, 1, 2 ** 62, 2 ** 63 - 1, 2 ** 63, 3 * 2 ** 62, 2 ** 64 - 1], dtype=np.uint64)
-    t = torch.from_numpy(np.sort(k).view(np.int64).copy())
-    assert key_range_splits(t, 2).tolist() == [4, 3]
-    assert key_range_splits(t, 4).tolist() == [2, 2, 1, 2]
-    assert key_range_splits(t, 3).tolist() == [3, 2, 2]
-    assert key_range_splits(t, 1).tolist() == [7]
+    assert range_part(k, 2).tolist() == [0, 0, 0, 0, 1, 1, 1]
+    assert range_part(k, 4).tolist() == [0, 0, 1, 1, 2, 3, 3]
+    assert range_part(k, 3).tolist() == [0, 0, 0, 1, 1, 2, 2]
+    assert range_part(k, 1).tolist() == [0] * 7
+    for parts in (3, 5, 7, 8):
+        for x in k.tolist():
+            assert range_part(np.array([x], dtype=np.uint64), parts)[0] == (x * parts) >> 64
