@@ -41,6 +41,9 @@ HW_OPS = 680                 # VALU instructions per compression as compiled (ad
 # 224 v_alignbit + 112 v_add3 (half rate on gfx950, 2 slots; profiles/r01_ubench_valu.log)
 SLOTS = 230 + 112 + 2 * (224 + 112)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+# grouping (group_hash.hip): hist read 8 + scatter read 8 / write 12 + refine read 12 /
+# write 12 + bucket read 12 + rep write 4 = 68 B/key when the refine level runs
+GROUP_BYTES_PER_KEY = 68
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # 256 CUs x 4 SIMD32 x 32 lanes x 2.4 GHz = 78.6
 # full-rate wave64 VALU issue: 1024 SIMDs x 2.4 GHz / 2 cycles = 1228.8 G slots/s
 SLOT_PEAK_G = 1024 * 2.4e9 / 2 / 1e9
@@ -100,7 +103,7 @@ def main() -> None:
         with torch.cuda.stream(side):
             side.wait_event(hashed[i % 2])
             if world == 1:
-                eng.group(keys[i % 2], rep, want_objects=False)  # K4 + K5, async
+                eng.group(keys[i % 2], rep, want_objects=False)  # K4h + K5h, async
             else:
                 results.append(sharded_group(keys[i % 2], file0, ops))
             grouped[i % 2].record(side)
@@ -154,6 +157,19 @@ def main() -> None:
         objects = eng.group(keys, rep)
     else:
         objects = res.objects
+    # the grouping alone (after the timed region: inside the steps it overlaps the next K1
+    # on a side stream and shares the CUs with it, so its own speed is measured serially)
+    group_ms = None
+    if world == 1:
+        gts = []
+        for _ in range(5):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(main)
+            eng.group(keys, rep, want_objects=False)
+            b.record(main)
+            b.synchronize()
+            gts.append(a.elapsed_time(b))
+        group_ms = float(np.median(gts))
 
     files_total = world * F * args.steps
     value = files_total / dt
@@ -222,6 +238,14 @@ def main() -> None:
                         "traffic_over_algorithmic": (traffic / (F * MSG_BYTES)) if traffic else None},
                 "int_ops": {"achieved_spec_tops": valu, "achieved_hw_instr_tops": valu_hw,
                             "peak_full_rate_tops": VALU_PEAK_TOPS},
+            },
+            "group": None if group_ms is None else {
+                # Object grouping of one step's keys alone (K4h partition + K5h LDS hash
+                # min), HIP events around it on the stream it runs on, after the timed region
+                "ms": group_ms, "keys": F,
+                "algorithmic_bytes_per_key": GROUP_BYTES_PER_KEY,
+                "achieved_gb_s": F * GROUP_BYTES_PER_KEY / (group_ms / 1e3) / 1e9,
+                "hbm_frac": F * GROUP_BYTES_PER_KEY / (group_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
             },
             "cpu_baseline": cpu,
         }

@@ -7,18 +7,23 @@
 //
 // The grouping never needs the keys in order — only equal keys side by side — so instead
 // of an 8-pass LSD sort (256 B/key of HBM traffic, ~40 launches) it is:
-//   K4h-a  sd_part_hist     per-block bucket histogram, [bucket][block] table   8 B/key read
+//   K4h-a  sd_part_hist     per-block coarse-bucket histogram, [bucket][block] table  8 B/key read
 //          exclusive scan of the table (sd_group.h exclusive_scan_u32)
-//   K4h-b  sd_part_scatter  keys -> bucket-contiguous (mixed key, position)   8 B read, 12 B write
-//   K5h    sd_bucket_min    one workgroup per bucket: LDS hash table of the bucket's distinct
-//                           keys with an atomic min of the value, then every position looks
-//                           its key up and writes the min                     12 B read, 4 B write
-// ≈ 44 B/key and 6 launches.  The bucket is the top bits of a bijective mix of the key, so
-// any set of DISTINCT keys spreads evenly (BLAKE3 keys are uniform anyway; test keys such
-// as 0..n-1 are not), while duplicates — however many — share one table slot.  A bucket
-// whose distinct keys overflow the LDS table (never for uniform keys: mean <= 1,536
-// distinct per bucket vs 3,584 allowed) is redone by the same workgroup in a global-memory
-// table; results do not depend on the order the scatter wrote the bucket in.
+//   K4h-b  sd_part_scatter  keys -> coarse-bucket-contiguous (mixed key, position),
+//                           LDS-staged so stores are coalesced runs          8 B read, 12 B write
+//   K4h-c  sd_part_refine   one workgroup per coarse bucket splits it by the next bits
+//                           (only when > 2^8 buckets are needed)             12 B read, 12 B write
+//   K5h    sd_bucket_min    one workgroup per fine bucket: LDS hash table of the bucket's
+//                           distinct keys with an atomic min of the value, then every
+//                           position looks its key up and writes the min     12 B read, 4 B write
+// = 68 B/key (44 without the refine level) in 7-8 launches.  Measured at 12.5M keys: 0.46 ms
+// vs 2.9 ms for the LSD path (profiles/r01_group_hash_v*.log).  The bucket is the top bits
+// of a bijective mix of the key, so any set of DISTINCT keys spreads evenly (BLAKE3 keys are
+// uniform anyway; test keys such as 0..n-1 are not), while duplicates — however many —
+// share one table slot.  A bucket whose distinct keys overflow the LDS table (never for
+// uniform keys: mean <= 1,536 distinct per bucket vs 3,584 allowed) is redone by the same
+// workgroup in a global-memory table; results do not depend on the order the scatter wrote
+// the bucket in.
 //
 // The same two kernels give the key-RANGE partition of the multi-GPU exchange (SURVEY §8e:
 // dest = floor(key * G / 2^64)), with the bucket function applied to the raw key.
@@ -37,10 +42,10 @@ constexpr int PART_THREADS = 512;
 constexpr int ITEMS = 8;
 constexpr uint32_t PART_TILE = PART_THREADS * ITEMS;  // 4096 keys per block trip
 constexpr int MIN_THREADS = 512;
-constexpr uint32_t TABLE = 8192;          // LDS slots per bucket (96 KiB)
-constexpr uint32_t TABLE_FILL = 7168;     // 7/8: above this the bucket goes to global memory
+constexpr uint32_t TABLE = 4096;          // LDS slots per bucket (48 KiB: 3 workgroups/CU)
+constexpr uint32_t TABLE_FILL = 3584;     // 7/8: above this the bucket goes to global memory
 constexpr uint32_t MAX_BUCKETS = 16384;   // LDS cursor table of the partition kernels (64 KiB)
-constexpr uint64_t TARGET_PER_BUCKET = 3072;
+constexpr uint64_t TARGET_PER_BUCKET = 1536;
 constexpr uint64_t MAX_TABLE_ENTRIES = 2ull << 20;  // [bucket][block] table (8 MiB)
 
 // splitmix64 finalizer: a bijection on u64, so distinct keys stay distinct
@@ -86,6 +91,84 @@ __device__ void part_hist_body(const uint64_t* __restrict__ keys, uint64_t n, ui
     hist[(uint64_t)b * nblk + blockIdx.x] = cnt[b];
 }
 
+// Exclusive scan of cnt[0..nb) into out (both LDS) by the whole PART_THREADS block.
+__device__ void lds_exclusive_scan(const uint32_t* cnt, uint32_t* out, uint32_t nb) {
+  __shared__ uint32_t wsum[PART_THREADS / 64];
+  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+  const uint32_t per = (nb + PART_THREADS - 1) / PART_THREADS;
+  const uint32_t lo = t * per < nb ? t * per : nb, hi = lo + per < nb ? lo + per : nb;
+  uint32_t sum = 0;
+  for (uint32_t i = lo; i < hi; ++i) sum += cnt[i];
+  uint32_t inc = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= (uint32_t)o) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t run = inc - sum;
+  for (uint32_t i = 0; i < w; ++i) run += wsum[i];
+  for (uint32_t i = lo; i < hi; ++i) { out[i] = run; run += cnt[i]; }
+  __syncthreads();
+}
+
+// LDS-staged scatter of one trip (<= PART_TILE keys at trip indices [0, trip_n)): the
+// keys are first counting-sorted by bucket in LDS, then written so that consecutive
+// lanes store consecutive slots of one bucket's run — coalesced, instead of 64 buckets
+// (= 64 cache lines) per store instruction.  gcur[b] = next global slot of bucket b for
+// this block.  tcnt must be zero on entry and is left zero.
+constexpr uint32_t STAGED_MAX_NB = 1024;
+template <typename BucketFn>
+__device__ __forceinline__ void staged_trip(const uint64_t (&k)[ITEMS], const uint32_t (&pos)[ITEMS],
+                                            uint32_t trip_n, uint32_t nb, BucketFn bfn,
+                                            uint32_t* gcur, uint32_t* tcnt, uint32_t* tstart,
+                                            uint64_t* skey, uint32_t* spos,
+                                            uint64_t* __restrict__ out_keys,
+                                            uint32_t* __restrict__ out_pos) {
+  uint32_t bk[ITEMS], r[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t t = (uint32_t)j * PART_THREADS + threadIdx.x;
+    bk[j] = t < trip_n ? bfn(k[j]) : 0u;
+    r[j] = t < trip_n ? atomicAdd(&tcnt[bk[j]], 1u) : 0u;
+  }
+  __syncthreads();
+  lds_exclusive_scan(tcnt, tstart, nb);
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t t = (uint32_t)j * PART_THREADS + threadIdx.x;
+    if (t < trip_n) {
+      const uint32_t slot = tstart[bk[j]] + r[j];
+      skey[slot] = k[j];
+      spos[slot] = pos[j];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t t = (uint32_t)j * PART_THREADS + threadIdx.x;
+    if (t < trip_n) {
+      const uint64_t kk = skey[t];
+      const uint32_t b = bfn(kk);
+      const uint32_t dest = gcur[b] + (t - tstart[b]);
+      out_keys[dest] = kk;
+      out_pos[dest] = spos[t];
+    }
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS) {
+    gcur[b] += tcnt[b];
+    tcnt[b] = 0;
+  }
+  __syncthreads();
+}
+
+// dynamic LDS of the scatter kernels: staged = gcur | tcnt | tstart | skey | spos
+__host__ __device__ constexpr size_t scatter_lds_bytes(uint32_t nb) {
+  return nb <= STAGED_MAX_NB ? (size_t)(3 * nb + 1) * 4 + (size_t)PART_TILE * 12 : (size_t)nb * 4;
+}
+
 template <int MODE>
 __device__ void part_scatter_body(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb,
                                   uint64_t per_block, const uint32_t* __restrict__ offs,
@@ -94,9 +177,32 @@ __device__ void part_scatter_body(const uint64_t* __restrict__ keys, uint64_t n,
   extern __shared__ uint32_t cur[];
   for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS)
     cur[b] = offs[(uint64_t)b * nblk + blockIdx.x];
-  __syncthreads();
   const uint64_t lo = (uint64_t)blockIdx.x * per_block;
   const uint64_t hi = lo + per_block < n ? lo + per_block : n;
+  if (nb <= STAGED_MAX_NB) {
+    uint32_t* tcnt = cur + nb;
+    uint32_t* tstart = cur + 2 * nb;
+    uint64_t* skey = reinterpret_cast<uint64_t*>(cur + 3 * nb + (nb & 1u));  // 8-B aligned
+    uint32_t* spos = reinterpret_cast<uint32_t*>(skey + PART_TILE);
+    for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS) tcnt[b] = 0;
+    __syncthreads();
+    auto bfn = [nb](uint64_t x) { return bucket_of(x, nb); };
+    for (uint64_t base = lo; base < hi; base += PART_TILE) {
+      uint64_t k[ITEMS];
+      uint32_t q[ITEMS];
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) {
+        const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
+        k[j] = i < hi ? stored_key<MODE>(keys[i]) : 0;
+        q[j] = (uint32_t)i;
+      }
+      const uint64_t left = hi - base;
+      staged_trip(k, q, left < PART_TILE ? (uint32_t)left : PART_TILE, nb, bfn, cur, tcnt, tstart,
+                  skey, spos, out_keys, out_pos);
+    }
+    return;
+  }
+  __syncthreads();
   for (uint64_t base = lo; base < hi; base += PART_TILE) {
     uint64_t k[ITEMS];
 #pragma unroll
@@ -153,6 +259,75 @@ sd_part_counts(const uint32_t* __restrict__ offs, uint32_t nb, uint32_t nblk, ui
     const uint64_t s = offs[(uint64_t)b * nblk];
     const uint64_t e = b + 1 < nb ? offs[(uint64_t)(b + 1) * nblk] : n;
     counts[b] = e - s;
+  }
+}
+
+// starts[b] = first position of bucket b (single-level partition)
+extern "C" __global__ void __launch_bounds__(256)
+sd_part_starts(const uint32_t* __restrict__ offs, uint32_t nb, uint32_t nblk,
+               uint32_t* __restrict__ starts) {
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  if (b < nb) starts[b] = offs[(uint64_t)b * nblk];
+}
+
+// Second partition level: one workgroup per coarse bucket (top b1 bits of the stored key)
+// splits it by the next b2 bits, in place order -> out (bucket-contiguous within the
+// segment, runs of ~PART_TILE / 2^b2 keys per trip: coalesced).  starts[c * 2^b2 + j] =
+// first position of fine bucket (c, j).  A single-level partition with 2^(b1+b2) buckets
+// writes runs of ~1-3 keys per bucket per block, which costs 5-10x in scattered stores
+// (tools/ubench_scatter.hip); two coalesced levels move more bytes in less time.
+constexpr uint32_t MAX_FINE = 64;
+extern "C" __global__ void __launch_bounds__(PART_THREADS)
+sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict__ in_pos,
+               const uint32_t* __restrict__ offs1, uint32_t nb1, uint32_t nblk1, uint64_t n,
+               uint32_t b1, uint32_t b2, uint64_t* __restrict__ out_keys,
+               uint32_t* __restrict__ out_pos, uint32_t* __restrict__ starts) {
+  __shared__ uint32_t cnt[MAX_FINE], gcur[MAX_FINE], tcnt[MAX_FINE], tstart[MAX_FINE];
+  __shared__ uint64_t skey[PART_TILE];
+  __shared__ uint32_t spos[PART_TILE];
+  const uint32_t c = blockIdx.x, nb2 = 1u << b2;
+  const uint64_t s = offs1[(uint64_t)c * nblk1];
+  const uint64_t e = c + 1 < nb1 ? offs1[(uint64_t)(c + 1) * nblk1] : n;
+  if (threadIdx.x < nb2) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint64_t base = s; base < e; base += PART_TILE) {
+    uint64_t k[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
+      k[j] = i < e ? in_keys[i] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
+      if (i < e) atomicAdd(&cnt[(uint32_t)((k[j] << b1) >> (64 - b2))], 1u);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = (uint32_t)s;
+    for (uint32_t j = 0; j < nb2; ++j) {
+      const uint32_t x = cnt[j];
+      gcur[j] = run;
+      starts[(uint64_t)c * nb2 + j] = run;
+      run += x;
+    }
+  }
+  if (threadIdx.x < nb2) tcnt[threadIdx.x] = 0;
+  __syncthreads();
+  auto bfn = [b1, b2](uint64_t x) { return (uint32_t)((x << b1) >> (64 - b2)); };
+  for (uint64_t base = s; base < e; base += PART_TILE) {
+    uint64_t k[ITEMS];
+    uint32_t q[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
+      k[j] = i < e ? in_keys[i] : 0;
+      q[j] = i < e ? in_pos[i] : 0;
+    }
+    const uint64_t left = e - base;
+    staged_trip(k, q, left < PART_TILE ? (uint32_t)left : PART_TILE, nb2, bfn, gcur, tcnt, tstart,
+                skey, spos, out_keys, out_pos);
   }
 }
 
@@ -216,8 +391,8 @@ __device__ __forceinline__ uint64_t g_find(const uint64_t* tk, uint64_t cap, uin
 // registers for the lookup; larger buckets stream in PART_TILE trips.
 extern "C" __global__ void __launch_bounds__(MIN_THREADS)
 sd_bucket_min(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ ppos,
-              const uint32_t* __restrict__ vals, const uint32_t* __restrict__ offs, uint32_t nb,
-              uint32_t bits, uint32_t nblk, uint64_t n, uint32_t* __restrict__ out,
+              const uint32_t* __restrict__ vals, const uint32_t* __restrict__ starts, uint32_t nb,
+              uint32_t bits, uint64_t n, uint32_t* __restrict__ out,
               unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
               uint32_t* __restrict__ gvals) {
   __shared__ uint64_t tk[TABLE];
@@ -225,8 +400,8 @@ sd_bucket_min(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ p
   __shared__ uint32_t distinct;
   __shared__ int overflow;
   const uint32_t b = blockIdx.x;
-  const uint64_t s = offs[(uint64_t)b * nblk];
-  const uint64_t e = b + 1 < nb ? offs[(uint64_t)(b + 1) * nblk] : n;
+  const uint64_t s = starts[b];
+  const uint64_t e = b + 1 < nb ? starts[b + 1] : n;
   if (s == e) return;  // uniform for the whole workgroup
   // every stored key of this bucket has top bits == b, so a key from bucket b^1 is never stored
   const uint64_t empty = (uint64_t)(b ^ 1u) << (64 - bits);
@@ -313,12 +488,13 @@ struct PartPlan {
   uint64_t per_block;
 };
 
-// blocks: whole PART_TILE trips, about 2 per CU-slot, and a [bucket][block] table of at
-// most MAX_TABLE_ENTRIES (the table is written, scanned and read once per grouping)
+// blocks: whole PART_TILE trips, at most ~1024 blocks (4 per CU) and a [bucket][block]
+// table of at most MAX_TABLE_ENTRIES (written, scanned and read once per partition)
 static PartPlan part_plan(uint64_t n, uint32_t nb, uint32_t bits) {
   PartPlan p{nb, bits, 1, PART_TILE};
   const uint64_t trips = n ? (n + PART_TILE - 1) / PART_TILE : 1;
   uint64_t maxblk = MAX_TABLE_ENTRIES / nb;
+  if (maxblk > 1024) maxblk = 1024;
   if (maxblk < 1) maxblk = 1;
   const uint64_t nblk = trips < maxblk ? trips : maxblk;
   const uint64_t per = (trips + nblk - 1) / nblk;  // trips per block
@@ -328,38 +504,49 @@ static PartPlan part_plan(uint64_t n, uint32_t nb, uint32_t bits) {
   return p;
 }
 
-static PartPlan mix_plan(uint64_t n) {
+// Grouping plan: 2^B final buckets of ~TARGET_PER_BUCKET keys, B = b1 + b2 with a coarse
+// first level of at most 2^8 buckets (long coalesced runs per block) and a refine level.
+struct GroupPlan {
+  PartPlan l1;
+  uint32_t b1, b2;
+  uint32_t nb() const { return 1u << (b1 + b2); }
+};
+
+static GroupPlan group_plan(uint64_t n) {
   uint32_t bits = 1;
   while (bits < 14 && ((uint64_t)1 << bits) * TARGET_PER_BUCKET < n) ++bits;
-  return part_plan(n, 1u << bits, bits);
+  GroupPlan g;
+  g.b1 = bits < 8 ? bits : 8;
+  g.b2 = bits - g.b1;
+  g.l1 = part_plan(n, 1u << g.b1, g.b1);
+  return g;
 }
 
 bool hash_group_supported(uint64_t n) {
-  // nb <= 16384 buckets at <= ~5,000 distinct keys each on average (table fill 7,168)
-  return n < (1ull << 32) && n <= (uint64_t)MAX_BUCKETS * 5000;
+  // nb <= 16384 buckets at <= ~2,500 distinct keys each on average (table fill 3,584)
+  return n < (1ull << 32) && n <= (uint64_t)MAX_BUCKETS * 2500;
 }
 
-static size_t part_ws(const PartPlan& p, uint64_t n) {
+static size_t table_ws(const PartPlan& p) {
   const uint64_t m = (uint64_t)p.nb * p.nblk;
-  return al256(n * 8) + al256(n * 4) + 2 * al256(m * 4) + al256(((m + 4095) / 4096) * 4 + 4);
+  return 2 * al256(m * 4) + al256(((m + 4095) / 4096) * 4 + 4);
 }
 
 size_t hash_group_workspace_bytes(uint64_t n) {
-  const PartPlan p = mix_plan(n);
-  return part_ws(p, n) + al256(2 * n * 8) + al256(2 * n * 4);
+  const GroupPlan g = group_plan(n);
+  return 2 * (al256(n * 8) + al256(n * 4)) + table_ws(g.l1) + al256((size_t)g.nb() * 4) +
+         al256(2 * n * 8) + al256(2 * n * 4);
 }
 
 size_t partition_workspace_bytes(uint64_t n, uint32_t parts) {
-  const PartPlan p = part_plan(n, parts, 0);
-  const uint64_t m = (uint64_t)p.nb * p.nblk;
-  return 2 * al256(m * 4) + al256(((m + 4095) / 4096) * 4 + 4);
+  return table_ws(part_plan(n, parts, 0));
 }
 
 static hipError_t run_partition(const uint64_t* keys, uint64_t n, const PartPlan& p, int mode,
                                 uint64_t* out_keys, uint32_t* out_pos, uint32_t* hist,
                                 uint32_t* offs, uint32_t* partial, hipStream_t s) {
   const uint64_t m = (uint64_t)p.nb * p.nblk;
-  const size_t lds = (size_t)p.nb * 4;
+  const size_t lds = (size_t)p.nb * 4, slds = scatter_lds_bytes(p.nb);
   if (mode == 0)
     sd_part_hist_mix<<<p.nblk, PART_THREADS, lds, s>>>(keys, n, p.nb, p.per_block, hist, p.nblk);
   else
@@ -367,11 +554,11 @@ static hipError_t run_partition(const uint64_t* keys, uint64_t n, const PartPlan
   hipError_t e = exclusive_scan_u32(hist, offs, m, partial, s);
   if (e != hipSuccess) return e;
   if (mode == 0)
-    sd_part_scatter_mix<<<p.nblk, PART_THREADS, lds, s>>>(keys, n, p.nb, p.per_block, offs, p.nblk,
-                                                          out_keys, out_pos);
+    sd_part_scatter_mix<<<p.nblk, PART_THREADS, slds, s>>>(keys, n, p.nb, p.per_block, offs, p.nblk,
+                                                           out_keys, out_pos);
   else
-    sd_part_scatter_range<<<p.nblk, PART_THREADS, lds, s>>>(keys, n, p.nb, p.per_block, offs,
-                                                            p.nblk, out_keys, out_pos);
+    sd_part_scatter_range<<<p.nblk, PART_THREADS, slds, s>>>(keys, n, p.nb, p.per_block, offs,
+                                                             p.nblk, out_keys, out_pos);
   return hipGetLastError();
 }
 
@@ -380,20 +567,33 @@ hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n
   hipError_t e = hipMemsetAsync(d_objects, 0, 8, s);
   if (e != hipSuccess || n == 0) return e;
   if (!hash_group_supported(n)) return hipErrorInvalidValue;
-  const PartPlan p = mix_plan(n);
-  const uint64_t m = (uint64_t)p.nb * p.nblk;
+  const GroupPlan g = group_plan(n);
+  const uint64_t m = (uint64_t)g.l1.nb * g.l1.nblk;
   char* q = (char*)ws;
-  uint64_t* pkeys = (uint64_t*)q; q += al256(n * 8);
-  uint32_t* ppos = (uint32_t*)q; q += al256(n * 4);
+  uint64_t* k1 = (uint64_t*)q; q += al256(n * 8);
+  uint32_t* p1 = (uint32_t*)q; q += al256(n * 4);
+  uint64_t* k2 = (uint64_t*)q; q += al256(n * 8);
+  uint32_t* p2 = (uint32_t*)q; q += al256(n * 4);
   uint32_t* hist = (uint32_t*)q; q += al256(m * 4);
   uint32_t* offs = (uint32_t*)q; q += al256(m * 4);
   uint32_t* partial = (uint32_t*)q; q += al256(((m + 4095) / 4096) * 4 + 4);
+  uint32_t* starts = (uint32_t*)q; q += al256((size_t)g.nb() * 4);
   uint64_t* gkeys = (uint64_t*)q; q += al256(2 * n * 8);
   uint32_t* gvals = (uint32_t*)q;
-  e = run_partition(keys, n, p, 0, pkeys, ppos, hist, offs, partial, s);
+  e = run_partition(keys, n, g.l1, 0, k1, p1, hist, offs, partial, s);
   if (e != hipSuccess) return e;
-  sd_bucket_min<<<p.nb, MIN_THREADS, 0, s>>>(pkeys, ppos, vals, offs, p.nb, p.bits, p.nblk, n, out,
-                                             (unsigned long long*)d_objects, gkeys, gvals);
+  const uint64_t* fk = k1;
+  const uint32_t* fp = p1;
+  if (g.b2 == 0) {
+    sd_part_starts<<<(g.l1.nb + 255) / 256, 256, 0, s>>>(offs, g.l1.nb, g.l1.nblk, starts);
+  } else {
+    sd_part_refine<<<g.l1.nb, PART_THREADS, 0, s>>>(k1, p1, offs, g.l1.nb, g.l1.nblk, n, g.b1, g.b2,
+                                                    k2, p2, starts);
+    fk = k2;
+    fp = p2;
+  }
+  sd_bucket_min<<<g.nb(), MIN_THREADS, 0, s>>>(fk, fp, vals, starts, g.nb(), g.b1 + g.b2, n, out,
+                                               (unsigned long long*)d_objects, gkeys, gvals);
   return hipGetLastError();
 }
 

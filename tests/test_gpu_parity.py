@@ -243,6 +243,12 @@ def test_group_hash_adversarial_keys(eng, oracle):
         "crafted overflow": crafted[rng.integers(0, len(crafted), 12_000)],
         "crafted distinct": crafted,
     }
+    # two-level partition (> 786K keys) with one fine bucket overflowing: 10K distinct keys
+    # whose mixed top 14 bits are 0, among 1M uniform keys
+    deep = np.array([unmix64(int(x) >> 14) for x in rng.integers(0, 2 ** 63, 10_000, dtype=np.uint64)],
+                    dtype=np.uint64)
+    big = np.concatenate([rng.integers(0, 2 ** 64, 990_000, dtype=np.uint64), deep])
+    cases["two-level overflow"] = big[rng.permutation(len(big))]
     for name, keys in cases.items():
         rep = torch.empty(len(keys), dtype=torch.int32, device="cuda")
         objects = eng.group(dev64(keys), rep)
