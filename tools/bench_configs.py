@@ -197,9 +197,9 @@ def config4(eng, orc, n_total: int, batch: int, dup: int):
     first = np.full(len(uniq), n_total, dtype=np.int64)
     np.minimum.at(first, inv, np.arange(n_total))
     ok = objects == len(uniq) and bool((rep.cpu().numpy() == first[inv]).all())
-    # K4h/K5h algorithmic bytes: hist read 8 + scatter read 8 / write 12 + bucket read 12 +
-    # rep write 4 = 44 B/key
-    group_bytes = 44 * n_total
+    # K4h/K5h algorithmic bytes: hist read 8 + scatter read 8 / write 12 + refine read 12 /
+    # write 12 + bucket read 12 + rep write 4 = 68 B/key
+    group_bytes = 68 * n_total
     emit({"config": "4-rank-share", "files": n_total, "dup_permille": dup,
           "hash_kernel_s": hash_s, "hash_files_per_s": n_total / hash_s,
           "group_s": gs, "group_keys_per_s": n_total / gs,
