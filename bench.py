@@ -71,9 +71,17 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    rehearsal = bool(os.environ.get("SD_BENCH_ONE_DEVICE"))
+    if rehearsal:
+        # rehearsal of the N > 1 code path with every rank on one GPU (RCCL refuses two
+        # ranks on one device, so the exchange goes through gloo): not a measurement
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from spacedrive_amd import CasEngine
     from spacedrive_amd.shard import HipShardOps, sharded_group
