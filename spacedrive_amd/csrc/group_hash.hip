@@ -7,7 +7,8 @@
 //
 // The grouping never needs the keys in order — only equal keys side by side — so instead
 // of an 8-pass LSD sort (256 B/key of HBM traffic, ~40 launches) it is:
-//   K4h-a  sd_part_hist     per-block coarse-bucket histogram, [bucket][block] table  8 B/key read
+//   K4h-a  sd_part_hist     per-block coarse-bucket histogram, [bucket][block] table,
+//                           and the prefill out[i] = val(i)                  8 B read, 4 B write
 //          exclusive scan of the table (sd_group.h exclusive_scan_u32)
 //   K4h-b  sd_part_scatter  keys -> coarse-bucket-contiguous (mixed key, position),
 //                           LDS-staged so stores are coalesced runs          8 B read, 12 B write
@@ -15,7 +16,8 @@
 //                           (only when > 2^8 buckets are needed)             12 B read, 12 B write
 //   K5h    sd_bucket_min    one workgroup per fine bucket: LDS hash table of the bucket's
 //                           distinct keys with an atomic min of the value, then every
-//                           position looks its key up and writes the min     12 B read, 4 B write
+//                           position looks its key up; it stores the min only where it
+//                           differs from the prefill (duplicates)            12 B read, <= 4 B write
 // = 68 B/key (44 without the refine level) in 7-8 launches.  Measured at 12.5M keys: 0.46 ms
 // vs 2.9 ms for the LSD path (profiles/r01_group_hash_v*.log).  The bucket is the top bits
 // of a bijective mix of the key, so any set of DISTINCT keys spreads evenly (BLAKE3 keys are
@@ -65,9 +67,15 @@ __device__ __forceinline__ uint32_t bucket_of(uint64_t stored, uint32_t nb) {
   return (uint32_t)__umul64hi(stored, (uint64_t)nb);
 }
 
+// prefill (grouping only): out[i] = val(i) for every position, streamed with the key
+// read, so that sd_bucket_min only stores where a key's minimum differs from the
+// position's own value — a scattered 4-B store costs a 32-B HBM write (PMC:
+// profiles/r01_pmc_group.json), and most positions are their key's first occurrence.
 template <int MODE>
 __device__ void part_hist_body(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb,
-                               uint64_t per_block, uint32_t* __restrict__ hist, uint32_t nblk) {
+                               uint64_t per_block, uint32_t* __restrict__ hist, uint32_t nblk,
+                               const uint32_t* __restrict__ vals = nullptr,
+                               uint32_t* __restrict__ prefill = nullptr) {
   extern __shared__ uint32_t cnt[];
   for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS) cnt[b] = 0;
   __syncthreads();
@@ -79,6 +87,13 @@ __device__ void part_hist_body(const uint64_t* __restrict__ keys, uint64_t n, ui
     for (int j = 0; j < ITEMS; ++j) {
       const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
       k[j] = i < hi ? keys[i] : 0;
+    }
+    if (prefill) {
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) {
+        const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
+        if (i < hi) prefill[i] = vals ? vals[i] : (uint32_t)i;
+      }
     }
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
@@ -229,8 +244,9 @@ __device__ void part_scatter_body(const uint64_t* __restrict__ keys, uint64_t n,
 
 extern "C" __global__ void __launch_bounds__(PART_THREADS)
 sd_part_hist_mix(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb, uint64_t per_block,
-                 uint32_t* __restrict__ hist, uint32_t nblk) {
-  part_hist_body<0>(keys, n, nb, per_block, hist, nblk);
+                 uint32_t* __restrict__ hist, uint32_t nblk, const uint32_t* __restrict__ vals,
+                 uint32_t* __restrict__ prefill) {
+  part_hist_body<0>(keys, n, nb, per_block, hist, nblk, vals, prefill);
 }
 extern "C" __global__ void __launch_bounds__(PART_THREADS)
 sd_part_hist_range(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb, uint64_t per_block,
@@ -385,7 +401,8 @@ __device__ __forceinline__ uint64_t g_find(const uint64_t* tk, uint64_t cap, uin
 }
 
 // One workgroup per bucket of the mixed-key partition (nb = 2^bits, bits >= 1).
-// out[pos] = min{ val(j) : key(j) == key(pos) }, val(j) = vals ? vals[j] : j;
+// out[pos] = min{ val(j) : key(j) == key(pos) }, val(j) = vals ? vals[j] : j, stored only
+// where it differs from val(pos): sd_part_hist_mix prefilled out[pos] = val(pos);
 // *objects += distinct keys.  gkeys/gvals: 2n-slot overflow tables (touched only on overflow).
 // A bucket of <= PART_TILE keys (all but pathological ones) is loaded once and kept in
 // registers for the lookup; larger buckets stream in PART_TILE trips.
@@ -408,7 +425,7 @@ sd_bucket_min(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ p
   for (uint32_t i = threadIdx.x; i < TABLE; i += MIN_THREADS) { tk[i] = empty; tv[i] = 0xFFFFFFFFu; }
   if (threadIdx.x == 0) { distinct = 0; overflow = 0; }
   uint64_t k[ITEMS];
-  uint32_t p[ITEMS];
+  uint32_t p[ITEMS], v[ITEMS];
   for (uint64_t base = s; base < e; base += PART_TILE) {
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
@@ -416,7 +433,6 @@ sd_bucket_min(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ p
       k[j] = i < e ? pkeys[i] : empty;
       p[j] = i < e ? ppos[i] : 0u;
     }
-    uint32_t v[ITEMS];
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) v[j] = (vals && k[j] != empty) ? vals[p[j]] : p[j];
     __syncthreads();  // table initialised (first trip) / overflow flag visible
@@ -434,7 +450,10 @@ sd_bucket_min(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ p
     if (e - s <= PART_TILE) {  // the one trip's keys are still in registers
 #pragma unroll
       for (int j = 0; j < ITEMS; ++j)
-        if (k[j] != empty) out[p[j]] = tv[lds_find(tk, (uint32_t)k[j] & (TABLE - 1), k[j])];
+        if (k[j] != empty) {
+          const uint32_t mv = tv[lds_find(tk, (uint32_t)k[j] & (TABLE - 1), k[j])];
+          if (mv != v[j]) out[p[j]] = mv;  // out[] was prefilled with the own value
+        }
     } else {
       for (uint64_t base = s; base < e; base += PART_TILE) {
 #pragma unroll
@@ -445,7 +464,10 @@ sd_bucket_min(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ p
         }
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j)
-          if (k[j] != empty) out[p[j]] = tv[lds_find(tk, (uint32_t)k[j] & (TABLE - 1), k[j])];
+          if (k[j] != empty) {
+            const uint32_t mv = tv[lds_find(tk, (uint32_t)k[j] & (TABLE - 1), k[j])];
+            if (mv != (vals ? vals[p[j]] : p[j])) out[p[j]] = mv;
+          }
       }
     }
     if (threadIdx.x == 0) atomicAdd(objects, (unsigned long long)distinct);
@@ -470,8 +492,10 @@ sd_bucket_min(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ p
   __syncthreads();
   for (uint64_t i = s + threadIdx.x; i < e; i += MIN_THREADS) {
     const uint64_t kk = pkeys[i];
+    const uint32_t pp = ppos[i];
     const uint64_t slot = g_find(gk, cap, (kk & 0xFFFFFFFFull) % cap, kk);
-    out[ppos[i]] = __hip_atomic_load(&gv[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t mv = __hip_atomic_load(&gv[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (mv != (vals ? vals[pp] : pp)) out[pp] = mv;
   }
   if (threadIdx.x == 0) atomicAdd(objects, (unsigned long long)distinct);
 }
@@ -544,11 +568,13 @@ size_t partition_workspace_bytes(uint64_t n, uint32_t parts) {
 
 static hipError_t run_partition(const uint64_t* keys, uint64_t n, const PartPlan& p, int mode,
                                 uint64_t* out_keys, uint32_t* out_pos, uint32_t* hist,
-                                uint32_t* offs, uint32_t* partial, hipStream_t s) {
+                                uint32_t* offs, uint32_t* partial, hipStream_t s,
+                                const uint32_t* vals = nullptr, uint32_t* prefill = nullptr) {
   const uint64_t m = (uint64_t)p.nb * p.nblk;
   const size_t lds = (size_t)p.nb * 4, slds = scatter_lds_bytes(p.nb);
   if (mode == 0)
-    sd_part_hist_mix<<<p.nblk, PART_THREADS, lds, s>>>(keys, n, p.nb, p.per_block, hist, p.nblk);
+    sd_part_hist_mix<<<p.nblk, PART_THREADS, lds, s>>>(keys, n, p.nb, p.per_block, hist, p.nblk,
+                                                       vals, prefill);
   else
     sd_part_hist_range<<<p.nblk, PART_THREADS, lds, s>>>(keys, n, p.nb, p.per_block, hist, p.nblk);
   hipError_t e = exclusive_scan_u32(hist, offs, m, partial, s);
@@ -580,7 +606,7 @@ hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n
   uint32_t* starts = (uint32_t*)q; q += al256((size_t)g.nb() * 4);
   uint64_t* gkeys = (uint64_t*)q; q += al256(2 * n * 8);
   uint32_t* gvals = (uint32_t*)q;
-  e = run_partition(keys, n, g.l1, 0, k1, p1, hist, offs, partial, s);
+  e = run_partition(keys, n, g.l1, 0, k1, p1, hist, offs, partial, s, vals, out);
   if (e != hipSuccess) return e;
   const uint64_t* fk = k1;
   const uint32_t* fp = p1;
