@@ -12,7 +12,8 @@
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
 
 // mode 0: real (file f), 1: window of 32 files (L2), 2: broadcast (file 0 for every lane),
-// 4: real with non-temporal loads
+// 4: real with non-temporal loads, 5: LINE-tiled layout (64-file tiles, 128-B lines
+// interleaved), 6: QUAD-tiled layout (16-B quads interleaved: every load coalesced)
 template <int MODE>
 __global__ void __launch_bounds__(256) k1_variant(const uint8_t* __restrict__ content, uint64_t stride,
                                                   const uint64_t* __restrict__ sizes, uint64_t n,
@@ -23,8 +24,15 @@ __global__ void __launch_bounds__(256) k1_variant(const uint8_t* __restrict__ co
   if (f < n) {
     const uint64_t g = (MODE == 0 || MODE == 4) ? f : (MODE == 1 ? (f & 31) : 0);
     sdcas::LdsStack stk{stack_lds, threadIdx.x};
-    const uint4* q = reinterpret_cast<const uint4*>(content + g * stride);
-    keys[f] = sdcas::cas_lane_sampled<MODE == 4>(q, sizes[f], stk);
+    if (MODE == 5 || MODE == 6) {
+      const uint4* q = reinterpret_cast<const uint4*>(content + (f >> 6) * 64 * stride) +
+                       (MODE == 5 ? (f & 63) * 8 : (f & 63));
+      keys[f] = MODE == 5 ? sdcas::cas_lane_sampled<false, sdcas::LAYOUT_LINE>(q, sizes[f], stk)
+                          : sdcas::cas_lane_sampled<false, sdcas::LAYOUT_QUAD>(q, sizes[f], stk);
+    } else {
+      const uint4* q = reinterpret_cast<const uint4*>(content + g * stride);
+      keys[f] = sdcas::cas_lane_sampled<MODE == 4>(q, sizes[f], stk);
+    }
   }
   uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
   if (threadIdx.x == 0) {
@@ -78,14 +86,14 @@ int main() {
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
   const char* names[] = {"K1 real (HBM)", "K1 window 32 files (L2)", "K1 broadcast", "compress-only x953",
-                         "K1 real, nt loads"};
+                         "K1 real, nt loads", "K1 LINE-tiled layout", "K1 QUAD-tiled layout"};
   for (int data = 0; data < 2; ++data) {
   if (data == 1) {
     fill_random<<<4096, 256>>>((uint32_t*)content, n * stride / 4, 7u);
     CHECK(hipDeviceSynchronize());
   }
   printf("--- content: %s ---\n", data ? "random" : "constant 0x5a");
-  for (int mode = 0; mode < 5; ++mode) {
+  for (int mode = 0; mode < 7; ++mode) {
     float best = 1e9;
     double ghz = 0;
     for (int rep = 0; rep < 4; ++rep) {
@@ -97,6 +105,8 @@ int main() {
       if (mode == 2) k1_variant<2><<<blocks, 256>>>(content, stride, sizes, n, keys, clk);
       if (mode == 3) k_compress<<<blocks, 256>>>(out, 1u, clk);
       if (mode == 4) k1_variant<4><<<blocks, 256>>>(content, stride, sizes, n, keys, clk);
+      if (mode == 5) k1_variant<5><<<blocks, 256>>>(content, stride, sizes, n, keys, clk);
+      if (mode == 6) k1_variant<6><<<blocks, 256>>>(content, stride, sizes, n, keys, clk);
       (void)hipEventRecord(b, 0);
       CHECK(hipEventSynchronize(b));
       float ms;
