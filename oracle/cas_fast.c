@@ -6,8 +6,9 @@
  * (`hash_many`) compresses 16 independent chunks per zmm lane group.  This baseline
  * gives the CPU the same SIMD width: 16 files per lane group, one file per 32-bit
  * lane, BLAKE3 chaining-value stack per lane (same tree as blake3_ref.c), so the GPU
- * is compared against a SIMD host, not a scalar strawman.  Files of unequal length
- * in a group fall back to the scalar restatement.  Hosts without AVX-512F use the
+ * is compared against a SIMD host, not a scalar strawman.  A group of files of unequal
+ * length is hashed file by file, chunk-parallel (16 chunks of one file per lane group,
+ * as the crate's `hash_many` does for one input).  Hosts without AVX-512F use the
  * scalar path everywhere.  Results are checked against blake3_ref.c by tests.
  */
 #define _GNU_SOURCE
@@ -167,6 +168,113 @@ AVX512 static void cas16(const uint8_t* const content[16], const uint64_t size[1
     out[l] = ((uint64_t)__builtin_bswap32(w0[l]) << 32) | __builtin_bswap32(w1[l]);
 }
 
+/* compress16 with per-lane block length and flags; lanes outside `active` keep cv. */
+AVX512 static inline void compress16v(__m512i cv[8], const __m512i m[16], __m512i ctr_lo,
+                                      __m512i blen, __m512i flags, __mmask16 active) {
+  __m512i s0 = cv[0], s1 = cv[1], s2 = cv[2], s3 = cv[3], s4 = cv[4], s5 = cv[5], s6 = cv[6], s7 = cv[7];
+  __m512i s8 = _mm512_set1_epi32((int)IV32[0]), s9 = _mm512_set1_epi32((int)IV32[1]);
+  __m512i s10 = _mm512_set1_epi32((int)IV32[2]), s11 = _mm512_set1_epi32((int)IV32[3]);
+  __m512i s12 = ctr_lo, s13 = _mm512_setzero_si512(), s14 = blen, s15 = flags;
+  for (int r = 0; r < 7; r++) {
+    const uint8_t* z = SCHED[r];
+    G(s0, s4, s8, s12, m[z[0]], m[z[1]]);
+    G(s1, s5, s9, s13, m[z[2]], m[z[3]]);
+    G(s2, s6, s10, s14, m[z[4]], m[z[5]]);
+    G(s3, s7, s11, s15, m[z[6]], m[z[7]]);
+    G(s0, s5, s10, s15, m[z[8]], m[z[9]]);
+    G(s1, s6, s11, s12, m[z[10]], m[z[11]]);
+    G(s2, s7, s8, s13, m[z[12]], m[z[13]]);
+    G(s3, s4, s9, s14, m[z[14]], m[z[15]]);
+  }
+  cv[0] = _mm512_mask_xor_epi32(cv[0], active, s0, s8); cv[1] = _mm512_mask_xor_epi32(cv[1], active, s1, s9);
+  cv[2] = _mm512_mask_xor_epi32(cv[2], active, s2, s10); cv[3] = _mm512_mask_xor_epi32(cv[3], active, s3, s11);
+  cv[4] = _mm512_mask_xor_epi32(cv[4], active, s4, s12); cv[5] = _mm512_mask_xor_epi32(cv[5], active, s5, s13);
+  cv[6] = _mm512_mask_xor_epi32(cv[6], active, s6, s14); cv[7] = _mm512_mask_xor_epi32(cv[7], active, s7, s15);
+}
+
+/* One cas message hashed chunk-parallel, the way the blake3 crate's `hash_many` hashes one
+ * input: 16 chunks per lane group (the partial last chunk rides in the last group as a
+ * masked lane), then the parent levels 16 pairs at a time (level-wise pair-and-promote ==
+ * the left-balanced tree).  Messages of one chunk and of more than 128 chunks use the
+ * scalar restatement. */
+#define CP_MAX 128
+AVX512 static uint64_t cas_chunkpar16(const uint8_t* content, size_t clen, uint64_t size) {
+  const uint64_t mlen = (uint64_t)clen + 8;
+  const uint64_t nchunks = (mlen + 1023) / 1024;
+  if (nchunks <= 1 || nchunks > CP_MAX) return orc_cas_key(content, clen, size);
+  uint8_t head[1024] __attribute__((aligned(64)));
+  uint8_t tail[1024] __attribute__((aligned(64)));
+  memcpy(head, &size, 8); /* le64(size): x86 is little-endian */
+  memcpy(head + 8, content, 1016);
+  const uint64_t tlen = mlen - (nchunks - 1) * 1024; /* 1..1024 bytes in the last chunk */
+  memset(tail, 0, sizeof tail);
+  memcpy(tail, content + (nchunks - 1) * 1024 - 8, tlen);
+  const uint32_t tblk = (uint32_t)((tlen + 63) / 64);
+  uint32_t cvs[2][CP_MAX][8] __attribute__((aligned(64)));
+  const __m512i lane = _mm512_setr_epi32(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+  for (uint64_t c0 = 0; c0 < nchunks; c0 += 16) {
+    const uint8_t* ptr[16];
+    uint32_t nblk[16];
+    for (int l = 0; l < 16; l++) {
+      const uint64_t c = c0 + (uint64_t)l < nchunks ? c0 + (uint64_t)l : c0;
+      ptr[l] = c == 0 ? head : (c + 1 == nchunks ? tail : content + c * 1024 - 8);
+      nblk[l] = c0 + (uint64_t)l >= nchunks ? 0 : (c + 1 == nchunks ? tblk : 16);
+    }
+    const __m512i vnblk = _mm512_loadu_si512((const void*)nblk);
+    const __m512i ctr = _mm512_add_epi32(_mm512_set1_epi32((int)c0), lane);
+    __m512i cv[8];
+    for (int i = 0; i < 8; i++) cv[i] = _mm512_set1_epi32((int)IV32[i]);
+    for (uint32_t b = 0; b < 16; b++) {
+      const __m512i vb = _mm512_set1_epi32((int)b);
+      const __mmask16 act = _mm512_cmplt_epu32_mask(vb, vnblk);
+      if (!act) break;
+      const __mmask16 end = _mm512_cmpeq_epi32_mask(_mm512_add_epi32(vb, _mm512_set1_epi32(1)), vnblk);
+      const __m512i last_len = _mm512_mask_blend_epi32((__mmask16)(1u << (nchunks - 1 - c0 < 16 ? nchunks - 1 - c0 : 16)),
+                                                       _mm512_set1_epi32(64),
+                                                       _mm512_set1_epi32((int)(tlen - 64 * (tblk - 1))));
+      const __m512i blen = _mm512_mask_blend_epi32(end, _mm512_set1_epi32(64), last_len);
+      __m512i flags = _mm512_mask_blend_epi32(end, _mm512_setzero_si512(), _mm512_set1_epi32(2));
+      if (b == 0) flags = _mm512_or_si512(flags, _mm512_set1_epi32(1));
+      __m512i r[16];
+      for (int l = 0; l < 16; l++)
+        r[l] = _mm512_loadu_si512((const void*)(ptr[l] + 64 * (b < nblk[l] ? b : 0)));
+      transpose16(r);
+      compress16v(cv, r, ctr, blen, flags, act);
+    }
+    uint32_t w[8][16] __attribute__((aligned(64)));
+    for (int i = 0; i < 8; i++) _mm512_store_si512((void*)w[i], cv[i]);
+    for (int l = 0; l < 16 && c0 + (uint64_t)l < nchunks; l++)
+      for (int i = 0; i < 8; i++) cvs[0][c0 + (uint64_t)l][i] = w[i][l];
+  }
+  /* parent levels, 16 pairs per compression group */
+  uint32_t count = (uint32_t)nchunks;
+  int cur = 0;
+  while (count > 1) {
+    const uint32_t pairs = count / 2;
+    const uint32_t flags = 4u | (count == 2 ? 8u : 0u);
+    for (uint32_t p0 = 0; p0 < pairs; p0 += 16) {
+      const __m512i pidx = _mm512_min_epu32(_mm512_add_epi32(_mm512_set1_epi32((int)p0), lane),
+                                            _mm512_set1_epi32((int)(pairs - 1)));
+      const __m512i base = _mm512_mullo_epi32(pidx, _mm512_set1_epi32(16)); /* 2 cvs x 8 words */
+      __m512i m[16], cv[8];
+      for (int i = 0; i < 16; i++)
+        m[i] = _mm512_i32gather_epi32(_mm512_add_epi32(base, _mm512_set1_epi32(i)),
+                                      (const void*)cvs[cur], 4);
+      for (int i = 0; i < 8; i++) cv[i] = _mm512_set1_epi32((int)IV32[i]);
+      compress16v(cv, m, _mm512_setzero_si512(), _mm512_set1_epi32(64), _mm512_set1_epi32((int)flags),
+                  (__mmask16)0xFFFF);
+      uint32_t w[8][16] __attribute__((aligned(64)));
+      for (int i = 0; i < 8; i++) _mm512_store_si512((void*)w[i], cv[i]);
+      for (uint32_t l = 0; l < 16 && p0 + l < pairs; l++)
+        for (int i = 0; i < 8; i++) cvs[cur ^ 1][p0 + l][i] = w[i][l];
+    }
+    if (count & 1) memcpy(cvs[cur ^ 1][pairs], cvs[cur][count - 1], 32);
+    count = pairs + (count & 1);
+    cur ^= 1;
+  }
+  return ((uint64_t)__builtin_bswap32(cvs[cur][0][0]) << 32) | __builtin_bswap32(cvs[cur][0][1]);
+}
+
 typedef struct {
   const uint8_t* arena; const uint64_t* offs; const uint64_t* lens; const uint64_t* sizes;
   uint64_t stride, clen; size_t lo, hi; uint64_t* out; int simd;
@@ -187,7 +295,7 @@ static void* fast_worker(void* p) {
       if (uniform) cas16(ptr, j->sizes + i, (size_t)cl, j->out + i);
       else
         for (int l = 0; l < 16; l++)
-          j->out[i + l] = orc_cas_key(ptr[l], (size_t)j->lens[i + l], j->sizes[i + l]);
+          j->out[i + l] = cas_chunkpar16(ptr[l], (size_t)j->lens[i + l], j->sizes[i + l]);
     }
   }
   for (; i < j->hi; i++) {
@@ -228,7 +336,7 @@ void orc_fast_cas_keys(const uint8_t* arena, const uint64_t* offs, const uint64_
 
 /* Config-1 all-cores baseline with the SIMD hasher: each worker gathers its files
  * (orc_gather_path: the cas.rs offsets) and hashes sampled files 16 at a time with
- * cas16; whole (ragged) files use the scalar restatement.  keys[i] = 0 and
+ * cas16; whole (ragged) files are hashed chunk-parallel (cas_chunkpar16).  keys[i] = 0 and
  * status[i] = -errno for a failed file. */
 typedef struct {
   const char* const* paths; const uint64_t* sizes; size_t n; int t, threads, simd;
@@ -249,7 +357,10 @@ static void* fast_paths_worker(void* p) {
     int64_t got = orc_gather_path(j->paths[i], j->sizes[i], dst, sampled ? S : SMALL);
     if (got < 0) { j->keys[i] = 0; j->status[i] = (int32_t)got; continue; }
     j->status[i] = 0;
-    if (!(sampled && j->simd)) { j->keys[i] = orc_cas_key(dst, (size_t)got, j->sizes[i]); continue; }
+    if (!(sampled && j->simd)) {
+      j->keys[i] = j->simd ? cas_chunkpar16(dst, (size_t)got, j->sizes[i]) : orc_cas_key(dst, (size_t)got, j->sizes[i]);
+      continue;
+    }
     gi[ng] = i; gs[ng] = j->sizes[i]; ng++;
     if (ng == 16) {
       const uint8_t* ptr[16];

@@ -162,6 +162,15 @@ def test_simd_baseline_matches_scalar(oracle):
         offs = np.arange(16, dtype=np.uint64) * L
         ln = np.full(16, L, dtype=np.uint64)
         assert (oracle.cas_keys(ar, offs, ln, ln) == oracle.fast_cas_keys(ar, offs, ln, ln)).all()
+    # unequal lengths in a group: chunk-parallel path (16 chunks of one file per lane
+    # group, the tail chunk a masked lane, SIMD parent levels) — lengths straddle the
+    # chunk, 16-chunk-group and 128-chunk (scalar) boundaries
+    lens = np.array([1016, 1017, 2040, 2041, 16376, 16377, 17400, 32773, 102399, 102400,
+                     63, 5000, 131064, 131065, 50000, 16 * 1024 * 3 - 8], dtype=np.uint64)
+    offs = np.concatenate([[0], np.cumsum((lens + 15) // 16 * 16)[:-1]]).astype(np.uint64)
+    ar = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
+    sz = lens + rng.integers(0, 3, 16, dtype=np.uint64)  # size prefix need not equal the length
+    assert (oracle.cas_keys(ar, offs, lens, sz) == oracle.fast_cas_keys(ar, offs, lens, sz, threads=2)).all()
 
 
 def test_synth_generator_shared_definitions(oracle):
