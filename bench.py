@@ -29,6 +29,7 @@ import json
 import os
 import sys
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -62,6 +63,11 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", dest="overlap", action="store_false",
                     help="group step i before hashing step i+1 (default: overlap them)")
+    ap.add_argument("--exchange", action="store_true",
+                    help="use the key-range all-to-all grouping even at N=1 (RCCL world 1): "
+                         "measures the exchange path's cost on one GPU")
+    ap.add_argument("--inline-group", action="store_true",
+                    help="issue the grouping from the main thread (A/B of the worker thread)")
     args = ap.parse_args()
 
     import numpy as np
@@ -77,7 +83,13 @@ def main() -> None:
         # ranks on one device, so the exchange goes through gloo): not a measurement
         local = 0
     torch.cuda.set_device(local)
-    if world > 1:
+    sharded = world > 1 or args.exchange
+    if world == 1 and args.exchange:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if sharded:
         if rehearsal:
             dist.init_process_group("gloo")
         else:
@@ -92,49 +104,66 @@ def main() -> None:
     dev = torch.device("cuda", local)
     content = torch.empty((F, 57344), dtype=torch.uint8, device=dev)
     sizes = torch.empty(F, dtype=torch.int64, device=dev)
-    # keys double-buffered: step i's grouping (side stream) overlaps step i+1's hashing
-    keys = [torch.empty(F, dtype=torch.int64, device=dev) for _ in range(2)]
+    # keys triple-buffered: step i's grouping (side stream) overlaps steps i+1 and i+2's
+    # hashing, so a grouping that waits for CU slots behind K1 never stalls the next K1
+    NBUF = 3
+    keys = [torch.empty(F, dtype=torch.int64, device=dev) for _ in range(NBUF)]
     rep = torch.empty(F, dtype=torch.int32, device=dev)
     eng.synth_sampled(args.seed, file0, F, content, sizes, 57344, dup_permille=args.dup_permille)
     torch.cuda.synchronize()
     ops = HipShardOps(eng)
     main = torch.cuda.current_stream()
     side = torch.cuda.Stream()
-    hashed = [torch.cuda.Event() for _ in range(2)]
-    grouped = [torch.cuda.Event() for _ in range(2)]
+    hashed = [torch.cuda.Event() for _ in range(NBUF)]
+    grouped = [torch.cuda.Event() for _ in range(NBUF)]
+    pending = [None] * NBUF
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
     results = []
+    # The exchange path reads part sizes back to the host (all_to_all_single needs host
+    # split lists), so it blocks its caller: it runs on a worker thread, and the main
+    # thread only ever waits on it when it reuses that step's key buffer.
+    worker = None
+    if not args.inline_group:
+        worker = ThreadPoolExecutor(1, initializer=torch.cuda.set_device, initargs=(local,))
 
     def group(i: int):
-        """Object grouping of step i's keys on the side stream (RCCL exchange at N > 1)."""
+        """Object grouping of step i's keys on the side stream (RCCL exchange when sharded)."""
+        b = i % NBUF
         with torch.cuda.stream(side):
-            side.wait_event(hashed[i % 2])
-            if world == 1:
-                eng.group(keys[i % 2], rep, want_objects=False)  # K4h + K5h, async
+            side.wait_event(hashed[b])
+            if not sharded:
+                eng.group(keys[b], rep, want_objects=False)  # K4h + K5h, async
             else:
-                results.append(sharded_group(keys[i % 2], file0, ops))
-            grouped[i % 2].record(side)
+                results.append(sharded_group(keys[b], file0, ops))
+            grouped[b].record(side)
+
+    def launch_group(i: int):
+        b = i % NBUF
+        pending[b] = worker.submit(group, i) if worker is not None else group(i)
+
+    def wait_group(b: int):
+        if pending[b] is not None:
+            if worker is not None:
+                pending[b].result()
+            main.wait_event(grouped[b])
+            pending[b] = None
 
     def run(n: int, timed: bool):
-        if n == 0:
-            return
         for i in range(n):
-            if i >= 2:
-                main.wait_event(grouped[i % 2])  # keys[i % 2] free again
+            b = i % NBUF
+            wait_group(b)                       # keys[b] free again
             if timed:
                 ev[i][0].record(main)
-            eng.hash_sampled(content, sizes, keys[i % 2])      # K1 on the main stream
+            eng.hash_sampled(content, sizes, keys[b])      # K1 on the main stream
             if timed:
                 ev[i][1].record(main)
-            hashed[i % 2].record(main)
-            if args.overlap:
-                if i >= 1:
-                    group(i - 1)
-            else:
-                group(i)
-        if args.overlap:
-            group(n - 1)
+            hashed[b].record(main)
+            launch_group(i)
+            if not args.overlap:
+                wait_group(b)
+        for b in range(NBUF):
+            wait_group(b)
 
     run(args.warmup, False)
     torch.cuda.synchronize()
@@ -149,26 +178,26 @@ def main() -> None:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    keys = keys[(args.steps - 1) % 2]
+    keys = keys[(args.steps - 1) % NBUF]
     res = results[-1] if results else None
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     km = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
-    if world > 1:
+    if sharded:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(km, op=dist.ReduceOp.MAX)
     dt = float(t.item())
     kern_ms = float(km.item())
 
     # objects (for the record) — outside the timed region
-    if world == 1:
+    if not sharded:
         objects = eng.group(keys, rep)
     else:
         objects = res.objects
     # the grouping alone (after the timed region: inside the steps it overlaps the next K1
     # on a side stream and shares the CUs with it, so its own speed is measured serially)
     group_ms = None
-    if world == 1:
+    if not sharded:
         gts = []
         for _ in range(5):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -221,9 +250,10 @@ def main() -> None:
                             f"{F} files/GPU/step ({world * F} per step at n_gpus={world})",
                 "files_per_gpu": F,
                 "dup_permille": args.dup_permille,
-                "parallelism": f"shard-by-file x{world}" + (" + RCCL key-range all-to-all" if world > 1 else ""),
-                "pipeline": ("grouping of step i on a side stream overlaps hashing of step i+1"
-                             if args.overlap else "hash then group, serial"),
+                "parallelism": f"shard-by-file x{world}" + (" + RCCL key-range all-to-all" if sharded else ""),
+                "pipeline": ("grouping of step i on a side stream (issued from a worker thread) "
+                             "overlaps hashing of steps i+1 and i+2" if args.overlap
+                             else "hash then group, serial"),
                 "objects": objects,
             },
             "roofline": {
@@ -258,7 +288,9 @@ def main() -> None:
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if worker is not None:
+        worker.shutdown()
+    if sharded:
         dist.destroy_process_group()
 
 
