@@ -3,8 +3,12 @@
 // Replaces file_checksum (core/src/object/validation/hash.rs:11-25), which feeds the whole
 // file through ONE blake3::Hasher on one thread, 1 MiB at a time, and returns the full
 // 64-hex digest.  Here the file is hashed tree-parallel:
-//   sd_b3_chunk_groups: one lane per 1 KiB chunk, 256 chunks per workgroup; chunk CVs
-//     go to LDS and the workgroup pair-and-promotes them to ONE subtree CV (8 levels).
+//   sd_b3_chunk_groups: 256 lanes x LC chunks per workgroup (iteration j: lane t hashes
+//     chunk j*256+t, so each wave load still covers 64 consecutive KiB); chunk CVs go to
+//     LDS and the workgroup pair-and-promotes them to ONE subtree CV (8 + log2 LC levels).
+//     LC > 1 amortises the reduction's idle lanes: with LC = 1 the upper levels run one
+//     mostly idle wave each for 16 wave-compressions of chunk work per wave (~7 % of
+//     issue slots); with LC = 4 every lane is busy through the first two levels.
 //   sd_b3_reduce_cvs: the same pair-and-promote over 256 CVs at a time, repeated until
 //     one CV remains; only the very last parent carries ROOT.
 // Level-wise pair-and-promote over aligned groups of 2^k equals BLAKE3's left-balanced
@@ -17,7 +21,12 @@
 
 namespace sdcas {
 
-constexpr int GROUP = 256;  // chunks (or CVs) reduced per workgroup
+constexpr int GROUP = 256;  // threads per workgroup = CVs per reduce workgroup
+#ifndef K3_LANE_CHUNKS
+#define K3_LANE_CHUNKS 4   // chunks per lane in sd_b3_chunk_groups (profiles/r01_k3_lc.log)
+#endif
+constexpr uint64_t GROUP_CHUNKS = (uint64_t)GROUP * K3_LANE_CHUNKS;  // chunks per subtree
+static_assert((K3_LANE_CHUNKS & (K3_LANE_CHUNKS - 1)) == 0, "subtrees must be 2^k chunks");
 
 // CV of one FULL 1 KiB chunk (never a root: a one-chunk input takes chunk_cv below).
 // 8 pair loads (128-B lines) issued one pair ahead, ping-ponged in registers like K1.
@@ -96,66 +105,83 @@ __device__ __forceinline__ void chunk_cv(const uint4* __restrict__ q, uint32_t c
   }
 }
 
-// Pair-and-promote `count` (<= 256) CVs held in LDS cv[GROUP][8] down to one (in cv[0]).
+// Pair-and-promote `count` (<= PER * 256) CVs held in LDS cvs[][8] down to one (in cvs[0]).
 // `root_last`: the final parent carries ROOT (only when this is the whole tree's top).
+// Thread t computes the parents t, t+256, ... of a level; all reads of a level finish
+// before its writes (parent p overwrites slot p, which another thread's pair may read).
+template <int PER>
 __device__ __forceinline__ void lds_reduce(uint32_t (*cvs)[8], uint32_t count, bool root_last) {
   const uint32_t t = threadIdx.x;
   while (count > 1) {
     const uint32_t pairs = count >> 1;
-    uint32_t out[8];
-    if (t < pairs) {
-      uint32_t l[8], r[8];
-#pragma unroll
-      for (int w = 0; w < 8; ++w) { l[w] = cvs[2 * t][w]; r[w] = cvs[2 * t + 1][w]; }
-      parent(out, l, r, (root_last && count == 2) ? (uint32_t)ROOT : 0u);
-    }
-    uint32_t promoted[8];
     const bool odd = count & 1u;
-    if (odd && t == pairs) {
+    uint32_t out[PER][8];
 #pragma unroll
-      for (int w = 0; w < 8; ++w) promoted[w] = cvs[count - 1][w];
+    for (int k = 0; k < PER; ++k) {
+      const uint32_t p = t + (uint32_t)k * GROUP;
+      if (p < pairs) {
+        uint32_t l[8], r[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) { l[w] = cvs[2 * p][w]; r[w] = cvs[2 * p + 1][w]; }
+        parent(out[k], l, r, (root_last && count == 2) ? (uint32_t)ROOT : 0u);
+      } else if (odd && p == pairs) {
+#pragma unroll
+        for (int w = 0; w < 8; ++w) out[k][w] = cvs[count - 1][w];
+      }
     }
     __syncthreads();
-    if (t < pairs) {
 #pragma unroll
-      for (int w = 0; w < 8; ++w) cvs[t][w] = out[w];
-    }
-    if (odd && t == pairs) {
+    for (int k = 0; k < PER; ++k) {
+      const uint32_t p = t + (uint32_t)k * GROUP;
+      if (p < pairs || (odd && p == pairs)) {
 #pragma unroll
-      for (int w = 0; w < 8; ++w) cvs[t][w] = promoted[w];
+        for (int w = 0; w < 8; ++w) cvs[p][w] = out[k][w];
+      }
     }
     __syncthreads();
     count = pairs + (odd ? 1u : 0u);
   }
 }
 
-// One workgroup = chunks [g*256, g*256+256) of the buffer (global chunk index chunk0 + ...).
+// One workgroup = chunks [g*GC, g*GC+GC) of the buffer (global chunk index chunk0 + ...).
 // out[g] = subtree CV; when nchunks_total == 1 the single chunk is the root (digest).
+template <int LC>
+__device__ __forceinline__ void chunk_groups(const uint8_t* __restrict__ data, uint64_t len,
+                                             uint64_t chunk0, uint32_t* __restrict__ out,
+                                             int root_if_single_group, uint32_t (*cvs)[8]) {
+  constexpr uint32_t GC = GROUP * LC;
+  const uint64_t nchunks = len == 0 ? 1 : (len + 1023) >> 10;
+  const uint64_t first = (uint64_t)blockIdx.x * GC;
+  const uint32_t count = (uint32_t)min((uint64_t)GC, nchunks - first);
+  const uint32_t t = threadIdx.x;
+  const bool whole_tree = root_if_single_group && nchunks <= (uint64_t)GC;
+#pragma unroll 1
+  for (uint32_t j = 0; j < LC; ++j) {
+    const uint32_t i = j * GROUP + t;
+    if (i < count) {
+      const uint64_t c = first + i;
+      const uint64_t off = c << 10;
+      const uint32_t clen = (uint32_t)min((uint64_t)1024, len - off);
+      uint32_t cv[8];
+      if (clen == 1024 && nchunks > 1)
+        full_chunk_cv(reinterpret_cast<const uint4*>(data + off), chunk0 + c, cv);
+      else
+        chunk_cv(reinterpret_cast<const uint4*>(data + off), clen, chunk0 + c,
+                 whole_tree && nchunks == 1, cv);
+#pragma unroll
+      for (int w = 0; w < 8; ++w) cvs[i][w] = cv[w];
+    }
+  }
+  __syncthreads();
+  lds_reduce<(LC + 1) / 2>(cvs, count, whole_tree);
+  if (t < 8) out[(uint64_t)blockIdx.x * 8 + t] = cvs[0][t];
+}
+
 extern "C" __global__ void __launch_bounds__(GROUP)
 sd_b3_chunk_groups(const uint8_t* __restrict__ data, uint64_t len, uint64_t chunk0,
                    uint32_t* __restrict__ out, int root_if_single_group) {
-  __shared__ uint32_t cvs[GROUP][8];
-  const uint64_t nchunks = len == 0 ? 1 : (len + 1023) >> 10;
-  const uint64_t first = (uint64_t)blockIdx.x * GROUP;
-  const uint32_t count = (uint32_t)min((uint64_t)GROUP, nchunks - first);
-  const uint32_t t = threadIdx.x;
-  const bool whole_tree = root_if_single_group && nchunks <= (uint64_t)GROUP;
-  if (t < count) {
-    const uint64_t c = first + t;
-    const uint64_t off = c << 10;
-    const uint32_t clen = (uint32_t)min((uint64_t)1024, len - off);
-    uint32_t cv[8];
-    if (clen == 1024 && nchunks > 1)
-      full_chunk_cv(reinterpret_cast<const uint4*>(data + off), chunk0 + c, cv);
-    else
-      chunk_cv(reinterpret_cast<const uint4*>(data + off), clen, chunk0 + c,
-               whole_tree && nchunks == 1, cv);
-#pragma unroll
-    for (int w = 0; w < 8; ++w) cvs[t][w] = cv[w];
-  }
-  __syncthreads();
-  lds_reduce(cvs, count, whole_tree);
-  if (t < 8) out[(uint64_t)blockIdx.x * 8 + t] = cvs[0][t];
+  __shared__ uint32_t cvs[GROUP * K3_LANE_CHUNKS][8];
+  chunk_groups<K3_LANE_CHUNKS>(data, len, chunk0, out, root_if_single_group, cvs);
 }
 
 // Reduce groups of 256 CVs: in[cnt][8] -> out[ceil(cnt/256)][8].
@@ -171,13 +197,13 @@ sd_b3_reduce_cvs(const uint32_t* __restrict__ in, uint64_t cnt, uint32_t* __rest
     for (int w = 0; w < 8; ++w) cvs[t][w] = in[(first + t) * 8 + w];
   }
   __syncthreads();
-  lds_reduce(cvs, count, root_if_single_group && cnt <= (uint64_t)GROUP);
+  lds_reduce<1>(cvs, count, root_if_single_group && cnt <= (uint64_t)GROUP);
   if (t < 8) out[(uint64_t)blockIdx.x * 8 + t] = cvs[0][t];
 }
 
 size_t checksum_workspace_bytes(uint64_t len) {
   const uint64_t nchunks = len == 0 ? 1 : (len + 1023) >> 10;
-  const uint64_t g = (nchunks + GROUP - 1) / GROUP;
+  const uint64_t g = (nchunks + GROUP_CHUNKS - 1) / GROUP_CHUNKS;
   return 2 * ((g * 32 + 255) / 256 * 256) + 512;
 }
 
@@ -197,7 +223,7 @@ static hipError_t reduce_to_one(uint32_t* a, uint32_t* b, uint64_t cnt, bool roo
 hipError_t checksum_device(const uint8_t* data, uint64_t len, uint64_t chunk0, bool root,
                            uint32_t* d_out8, void* ws, hipStream_t s) {
   const uint64_t nchunks = len == 0 ? 1 : (len + 1023) >> 10;
-  const uint64_t g = (nchunks + GROUP - 1) / GROUP;
+  const uint64_t g = (nchunks + GROUP_CHUNKS - 1) / GROUP_CHUNKS;
   if (g >= (1ull << 31)) return hipErrorInvalidValue;
   uint32_t* a = (uint32_t*)ws;
   uint32_t* b = (uint32_t*)((char*)ws + (g * 32 + 255) / 256 * 256);
