@@ -71,13 +71,21 @@ int sd_cas_synchronize(sd_cas_ctx* ctx);
  * wave round (measured: 1,250,000 files 51.2 M files/s vs 1,310,720 files 55.7 M/s). */
 size_t sd_cas_batch_quantum(const sd_cas_ctx* ctx);
 /* Batches of fewer than `sampled_files` sampled files (sd_cas_hash_sampled_dev/_host) or
- * `packed_files` whole files (sd_cas_hash_packed_dev) are hashed chunk-parallel — one wave
- * per file, a lane per 1 KiB chunk, LDS tree merge — for latency (~16 + log2(chunks)
- * compression times per file instead of 953); larger batches use one file per lane for
+ * `packed_files` whole files (sd_cas_hash_packed_dev) are hashed chunk-parallel — a lane
+ * per 1 KiB chunk (or per 4+ chunks, sd_cas_set_chunkpar_split), cross-lane tree merge —
+ * for latency (~16 + log2(chunks) compression times per file instead of 953); larger
+ * batches use one file per lane for
  * throughput.  Both paths give identical keys.  0 = always one file per lane;
- * SD_CAS_THRESHOLD_DEFAULT = the measured crossover (5/8 and 7/8 of the batch quantum). */
+ * SD_CAS_THRESHOLD_DEFAULT = the measured crossover (3/4 and 7/8 of the batch quantum). */
 #define SD_CAS_THRESHOLD_DEFAULT ((size_t)-1)
 void sd_cas_set_latency_threshold(sd_cas_ctx* ctx, size_t sampled_files, size_t packed_files);
+/* Shape of the chunk-parallel path: batches of at least `sampled_files` / `packed_files`
+ * files pack four files per wave (16 lanes per file, 4+ consecutive chunks per lane, lane
+ * subtrees merged across lanes with DPP row shifts), smaller ones take one wave per file
+ * (a lane per chunk, lowest latency).  Identical keys either way.  0 = always four per
+ * wave; SD_CAS_THRESHOLD_DEFAULT = the measured crossover (sampled: 3/64 of the batch
+ * quantum; whole files: never, four ragged lengths per wave run at the longest one's). */
+void sd_cas_set_chunkpar_split(sd_cas_ctx* ctx, size_t sampled_files, size_t packed_files);
 /* page-locked host staging for the gather (replaces the per-file Box<[u8]> of cas.rs:32) */
 int sd_cas_alloc_pinned(sd_cas_ctx* ctx, size_t bytes, void** out);
 int sd_cas_free_pinned(sd_cas_ctx* ctx, void* p);

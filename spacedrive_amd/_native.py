@@ -30,6 +30,7 @@ SIGNATURES = [
     ("sd_cas_synchronize", _i, [_vp]),
     ("sd_cas_batch_quantum", _sz, [_vp]),
     ("sd_cas_set_latency_threshold", None, [_vp, _sz, _sz]),
+    ("sd_cas_set_chunkpar_split", None, [_vp, _sz, _sz]),
     ("sd_cas_alloc_pinned", _i, [_vp, _sz, ctypes.POINTER(_vp)]),
     ("sd_cas_free_pinned", _i, [_vp, _vp]),
     ("sd_cas_generate_cas_ids", _i, [_vp, _vp, _vp, _vp, _sz, _vp]),

@@ -119,6 +119,13 @@ class CasEngine:
         self.L.sd_cas_set_latency_threshold(self.h, d if sampled is None else int(sampled),
                                             d if packed is None else int(packed))
 
+    def set_chunkpar_split(self, sampled: Optional[int] = None, packed: Optional[int] = None) -> None:
+        """K1L batches of at least this many files pack 4 files per wave (16-lane segments);
+        smaller ones use a wave per file.  0 = always 4 per wave, None = measured default."""
+        d = THRESHOLD_DEFAULT
+        self.L.sd_cas_set_chunkpar_split(self.h, d if sampled is None else int(sampled),
+                                         d if packed is None else int(packed))
+
     # ---- host batches (blocking) -------------------------------------------------------
     def generate_cas_keys(self, items: Sequence[tuple[bytes, int]]) -> np.ndarray:
         """Batched ``generate_cas_id`` over already-gathered content: items = (buf, size)."""

@@ -265,11 +265,13 @@ __device__ __forceinline__ uint64_t cas_lane_packed(const uint4* __restrict__ q,
 }
 
 // ---- K1L: chunk-parallel latency path (small batches) ---------------------------------
-// One wave per file, one lane per 1 KiB chunk, then a level-wise pair-and-promote merge of
-// the chunk CVs in LDS.  A file's latency is ~16 + log2(chunks) compression times instead
-// of the lane-per-file kernels' 953, at ~68 % lane efficiency — the right trade when a
-// batch is too small to fill the chip (the reference's job step is 100 files,
-// file_identifier/mod.rs:34).  Chosen by the host below sd_cas_set_latency_threshold.
+// A file per wave (a lane per 1 KiB chunk) or per 16-lane segment (4+ chunks per lane),
+// then a level-wise pair-and-promote merge of the lanes' subtree CVs across lanes (DPP row
+// shifts inside a 16-lane row).  A file's latency is ~16 + log2(chunks) compression times
+// instead of the lane-per-file kernels' 953, at ~68 % (wave per file) / ~84 % (4 files per
+// wave) lane efficiency — the right trade when a batch is too small to fill the chip (the
+// reference's job step is 100 files, file_identifier/mod.rs:34).  Chosen by the host below
+// sd_cas_set_latency_threshold; the shape by sd_cas_set_chunkpar_split.
 constexpr int CP_MAX_CHUNKS = 104;
 
 // CV of chunk c of M = le64(size) || content[0, clen); ROOT when M is a single chunk.
@@ -321,60 +323,117 @@ __device__ __forceinline__ void cas_chunk_cv(const uint4* __restrict__ q, uint32
   }
 }
 
-// One 64-lane workgroup per file.  offs == nullptr: content i at arena + i*stride with
-// length fixed_len (the sampled layout); else arena + offs[i], lens[i] bytes.
-extern "C" __global__ void __launch_bounds__(64)
+// Value of `x` held by lane (lane + S) of the same file segment (S < SEG, a power of two;
+// lanes past the wave's end read 0 and are never used).  S < 16 stays inside a DPP row:
+// DPP row_shl:S (lane i reads lane i + S of its 16-lane row) — no LDS, no extra issue.
+// S = 16, 32 (only in 64-lane segments) cross rows: ds_bpermute (__shfl_down).
+template <uint32_t S>
+__device__ __forceinline__ uint32_t from_lane_above(uint32_t x) {
+  if constexpr (S < 16)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x100 | (int)S, 0xF, 0xF, true);
+  else
+    return __shfl_down(x, S, 64);
+}
+
+// Level-wise pair-and-promote across the lanes of a segment: item i (a subtree CV) sits in
+// segment lane i*s at the level with stride s; the left lane of a pair pulls its partner's
+// 8 CV words with one cross-lane move each and compresses the parent.  `count` items at
+// entry; ROOT on the last pair.  Every lane runs the moves (DPP needs full exec).
+template <int SEG, uint32_t S>
+__device__ __forceinline__ void segment_merge(uint32_t (&cv)[8], uint32_t sl, uint32_t& count) {
+  if constexpr (S < (uint32_t)SEG) {
+    uint32_t r[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) r[w] = from_lane_above<S>(cv[w]);
+    const bool left = (sl & (2u * S - 1u)) == 0u;
+    if (count > 1u && left && sl / S + 1u < count) parent(cv, cv, r, count == 2u ? (uint32_t)ROOT : 0u);
+    count = (count + 1u) >> 1;
+    segment_merge<SEG, 2u * S>(cv, sl, count);
+  }
+}
+
+// K1L: a file per SEG-lane segment (64/SEG files per wave).  Segment lane l hashes the
+// CPL consecutive chunks [l*CPL, (l+1)*CPL) (CPL = the smallest power of two with
+// CPL*SEG >= chunks), merges them into one subtree CV through an LDS stack column of its
+// own, and the segment then merges the lanes' subtree CVs across lanes.  Aligned
+// power-of-two groups make this exactly BLAKE3's left-balanced tree (level-wise
+// pair-and-promote, oracle formulation 3).
+//   SEG = 64: one file per wave, CPL = 1 for sampled messages (57 chunks): latency ~16 + 6
+//             compression times — the smallest batches;
+//   SEG = 16: four files per wave, CPL = 4: 64 + 3 block/parent compressions per lane and
+//             4 cross-lane levels — ~25 % fewer wave-compressions per file, 3x the latency,
+//             for mid-size batches (crossovers in profiles/r01_k1l_seg_sweep.log).
+constexpr int CP_DEPTH = 3;  // CPL <= 8 -> at most 3 pending subtrees per lane
+
+template <int SEG>
+__device__ __forceinline__ void chunkpar_wave(const uint8_t* __restrict__ arena,
+                                              const uint64_t* __restrict__ offs, uint64_t stride,
+                                              const uint32_t* __restrict__ lens, uint32_t fixed_len,
+                                              const uint64_t* __restrict__ sizes, uint64_t n,
+                                              uint64_t* __restrict__ keys) {
+  __shared__ uint32_t stk[CP_DEPTH][8][64];  // word-major per-lane columns: conflict-free
+  const uint32_t lane = threadIdx.x;
+  const uint32_t sl = lane % SEG;
+  const uint64_t f = (uint64_t)blockIdx.x * (64 / SEG) + lane / SEG;
+  uint32_t clen = 0, nchunks = 0;
+  uint64_t size = 0;
+  const uint4* q = nullptr;
+  if (f < n) {
+    q = reinterpret_cast<const uint4*>(arena + (offs ? offs[f] : f * stride));
+    clen = offs ? lens[f] : fixed_len;
+    size = sizes[f];
+    nchunks = (clen + 8u + 1023u) >> 10;
+  }
+  const bool ok = nchunks != 0 && nchunks <= CP_MAX_CHUNKS;  // caller contract: <= 104 chunks
+  uint32_t cpl = 1;
+  while (cpl * SEG < nchunks) cpl <<= 1;
+  const bool whole = nchunks <= cpl;  // the file fits in segment lane 0: it holds the root
+  const uint32_t c0 = ok ? sl * cpl : 0u;
+  const uint32_t c1 = ok ? min(nchunks, c0 + cpl) : 0u;
+  uint32_t cv[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+  uint32_t sp = 0;
+  for (uint32_t c = c0; c < c1; ++c) {
+    cas_chunk_cv(q, clen, size, c, cv);  // ROOT already set for a one-chunk message
+    uint32_t total = c - c0 + 1u;
+    while ((total & 1u) == 0u) {
+      uint32_t l[8];
+      --sp;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) l[w] = stk[sp][w][lane];
+      parent(cv, l, cv, (whole && c + 1u == nchunks && sp == 0u) ? (uint32_t)ROOT : 0u);
+      total >>= 1;
+    }
+#pragma unroll
+    for (int w = 0; w < 8; ++w) stk[sp][w][lane] = cv[w];
+    ++sp;
+  }
+  // a partial (last) group: merge its pending subtrees right to left
+  if (sp > 0u) {
+    --sp;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) cv[w] = stk[sp][w][lane];
+    while (sp > 0u) {
+      uint32_t l[8];
+      --sp;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) l[w] = stk[sp][w][lane];
+      parent(cv, l, cv, (whole && sp == 0u) ? (uint32_t)ROOT : 0u);
+    }
+  }
+  uint32_t count = whole ? 1u : (nchunks + cpl - 1u) / cpl;  // lane subtrees of this file
+  segment_merge<SEG, 1u>(cv, sl, count);
+  if (f < n && sl == 0u) keys[f] = ok ? key_of(cv) : 0ull;
+}
+
+// offs == nullptr: content i at arena + i*stride with length fixed_len (the sampled
+// layout); else arena + offs[i], lens[i] bytes.  One 64-lane workgroup = 64/SEG files.
+template <int SEG>
+__global__ void __launch_bounds__(64)
 sd_cas_chunkpar_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                        uint64_t stride, const uint32_t* __restrict__ lens, uint32_t fixed_len,
                        const uint64_t* __restrict__ sizes, uint64_t n,
                        uint64_t* __restrict__ keys) {
-  __shared__ uint32_t cvs[CP_MAX_CHUNKS][8];
-  const uint64_t f = blockIdx.x;
-  if (f >= n) return;  // grid == n: never taken, kept as a guard
-  const uint32_t lane = threadIdx.x;
-  const uint4* q = reinterpret_cast<const uint4*>(arena + (offs ? offs[f] : f * stride));
-  const uint32_t clen = offs ? lens[f] : fixed_len;
-  const uint64_t size = sizes[f];
-  const uint32_t nchunks = (clen + 8u + 1023u) >> 10;
-  if (nchunks > CP_MAX_CHUNKS) {  // caller contract (<= MAX_PACKED_CONTENT_LEN): never write LDS OOB
-    if (lane == 0) keys[f] = 0;
-    return;
-  }
-  for (uint32_t c = lane; c < nchunks; c += 64) {
-    uint32_t cv[8];
-    cas_chunk_cv(q, clen, size, c, cv);
-#pragma unroll
-    for (int w = 0; w < 8; ++w) cvs[c][w] = cv[w];
-  }
-  __syncthreads();
-  uint32_t count = nchunks;
-  while (count > 1) {  // left-balanced tree == level-wise pair-and-promote
-    const uint32_t pairs = count >> 1;  // <= 52 < 64: one pair per lane
-    const bool odd = count & 1u;
-    uint32_t out[8];
-    if (lane < pairs) {
-      uint32_t l[8], r[8];
-#pragma unroll
-      for (int w = 0; w < 8; ++w) { l[w] = cvs[2 * lane][w]; r[w] = cvs[2 * lane + 1][w]; }
-      parent(out, l, r, count == 2 ? (uint32_t)ROOT : 0u);
-    } else if (odd && lane == pairs) {
-#pragma unroll
-      for (int w = 0; w < 8; ++w) out[w] = cvs[count - 1][w];  // promoted unchanged
-    }
-    __syncthreads();
-    if (lane < pairs + (odd ? 1u : 0u)) {
-#pragma unroll
-      for (int w = 0; w < 8; ++w) cvs[lane][w] = out[w];
-    }
-    __syncthreads();
-    count = pairs + (odd ? 1u : 0u);
-  }
-  if (lane == 0) {
-    uint32_t cv[8];
-#pragma unroll
-    for (int w = 0; w < 8; ++w) cv[w] = cvs[0][w];
-    keys[f] = key_of(cv);
-  }
+  chunkpar_wave<SEG>(arena, offs, stride, lens, fixed_len, sizes, n, keys);
 }
 
 // K2: whole-file path, content length <= MAX_PACKED_CONTENT_LEN, files visited in `order`.
@@ -439,11 +498,15 @@ hipError_t hash_packed(const uint8_t* arena, const uint64_t* offs, const uint32_
 
 hipError_t hash_chunkpar(const uint8_t* arena, const uint64_t* offs, uint64_t stride,
                          const uint32_t* lens, uint32_t fixed_len, const uint64_t* sizes,
-                         uint64_t n, uint64_t* keys, hipStream_t s) {
+                         uint64_t n, uint64_t* keys, int seg, hipStream_t s) {
   if (n == 0) return hipSuccess;
   if (n >= (1ull << 31)) return hipErrorInvalidValue;
-  sd_cas_chunkpar_kernel<<<(uint32_t)n, 64, 0, s>>>(arena, offs, stride, lens, fixed_len, sizes, n,
-                                                    keys);
+  if (seg == 16)
+    sd_cas_chunkpar_kernel<16><<<(uint32_t)((n + 3) / 4), 64, 0, s>>>(arena, offs, stride, lens,
+                                                                      fixed_len, sizes, n, keys);
+  else
+    sd_cas_chunkpar_kernel<64><<<(uint32_t)n, 64, 0, s>>>(arena, offs, stride, lens, fixed_len,
+                                                         sizes, n, keys);
   return hipGetLastError();
 }
 

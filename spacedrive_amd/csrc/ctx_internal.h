@@ -87,6 +87,12 @@ struct sd_cas_ctx {
   uint64_t* d_scalar = nullptr;  // 8 x u64 scratch for counters
   // batches below these sizes use the chunk-parallel K1L kernel (sd_cas_set_latency_threshold)
   size_t latency_sampled = 0, latency_packed = 0;
+  // K1L batches of at least this many files pack 4 files per wave (16-lane segments),
+  // smaller ones take a wave per file (sd_cas_set_chunkpar_split)
+  size_t seg16_sampled = 0, seg16_packed = 0;
+  int chunkpar_seg(size_t n, bool sampled) const {
+    return n >= (sampled ? seg16_sampled : seg16_packed) ? 16 : 64;
+  }
   HostPool pool;  // I/O gather workers
   std::string err;
 };

@@ -65,18 +65,34 @@ int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
     return SD_CAS_EHIP;
   }
   sd_cas_set_latency_threshold(c, SD_CAS_THRESHOLD_DEFAULT, SD_CAS_THRESHOLD_DEFAULT);
+  sd_cas_set_chunkpar_split(c, SD_CAS_THRESHOLD_DEFAULT, SD_CAS_THRESHOLD_DEFAULT);
   *out = c;
   return SD_CAS_OK;
 }
 
-// Defaults = the measured crossovers on MI355X (profiles/r01_k1l_sweep.log): K1L wins below
-// ~0.6 of a batch quantum for sampled messages and ~0.9 for ragged whole files, where the
-// lane-per-file path also pays the length sort and the 101-chunk latency of its longest file.
+// Defaults = the measured crossovers on MI355X (profiles/r01_k1l_seg_sweep.log): K1L (four
+// files per wave) wins below ~0.75 of a batch quantum for sampled messages (49,152 files:
+// 1.12 vs 1.16 ms; 65,536: 1.48 vs 1.28) and K1L (a wave per file) below ~0.9 for ragged
+// whole files, where the lane-per-file path also pays the length sort and the 101-chunk
+// latency of its longest file.
 void sd_cas_set_latency_threshold(sd_cas_ctx* c, size_t sampled_files, size_t packed_files) {
   if (!c) return;
   const size_t q = sd_cas_batch_quantum(c);
-  c->latency_sampled = sampled_files == SD_CAS_THRESHOLD_DEFAULT ? q * 5 / 8 : sampled_files;
+  c->latency_sampled = sampled_files == SD_CAS_THRESHOLD_DEFAULT ? q * 3 / 4 : sampled_files;
   c->latency_packed = packed_files == SD_CAS_THRESHOLD_DEFAULT ? q * 7 / 8 : packed_files;
+}
+
+// Defaults = the measured crossovers between the two K1L shapes (profiles/
+// r01_k1l_seg_sweep.log): a wave per file while the batch cannot fill the chip's SIMDs,
+// four files per wave once the lower wave-compression count per file wins.
+void sd_cas_set_chunkpar_split(sd_cas_ctx* c, size_t sampled_files, size_t packed_files) {
+  if (!c) return;
+  // sampled: crossover between 2,048 (0.078 vs 0.116 ms) and 4,096 files (0.139 vs 0.120);
+  // ragged whole files: 16-lane segments lose everywhere (four random lengths per wave run
+  // at the longest one's chunks-per-lane), so packed batches keep a wave per file
+  const size_t q = sd_cas_batch_quantum(c);
+  c->seg16_sampled = sampled_files == SD_CAS_THRESHOLD_DEFAULT ? q * 3 / 64 : sampled_files;
+  c->seg16_packed = packed_files == SD_CAS_THRESHOLD_DEFAULT ? (size_t)-1 : packed_files;
 }
 
 void sd_cas_ctx_destroy(sd_cas_ctx* c) {
@@ -144,7 +160,8 @@ int sd_cas_hash_sampled_dev(sd_cas_ctx* c, const void* d_content, uint64_t strid
                 (unsigned long long)stride);
   if (n < c->latency_sampled)  // small batch: one wave per file (K1L)
     HIP_TRY(c, hash_chunkpar((const uint8_t*)d_content, nullptr, stride, nullptr,
-                             SAMPLED_CONTENT_LEN, d_sizes, n, d_keys, pick(c, stream)));
+                             SAMPLED_CONTENT_LEN, d_sizes, n, d_keys, c->chunkpar_seg(n, true),
+                             pick(c, stream)));
   else
     HIP_TRY(c, hash_sampled((const uint8_t*)d_content, stride, d_sizes, n, d_keys, pick(c, stream)));
   return SD_CAS_OK;
@@ -160,7 +177,8 @@ int sd_cas_hash_packed_dev(sd_cas_ctx* c, const void* d_arena, const uint64_t* d
     return fail(c, SD_CAS_EINVAL, "hash_packed: bad arguments");
   hipStream_t s = pick(c, stream);
   if (n < c->latency_packed) {  // small batch: one wave per file (K1L), no length sort
-    HIP_TRY(c, hash_chunkpar((const uint8_t*)d_arena, d_offs, 0, d_lens, 0, d_sizes, n, d_keys, s));
+    HIP_TRY(c, hash_chunkpar((const uint8_t*)d_arena, d_offs, 0, d_lens, 0, d_sizes, n, d_keys,
+                             c->chunkpar_seg(n, false), s));
     return SD_CAS_OK;
   }
   // workspace: length keys | sorted keys | order | sort workspace
@@ -563,7 +581,7 @@ int sd_cas_hash_sampled_host(sd_cas_ctx* c, const void* h_content, uint64_t stri
     if (e == hipSuccess)
       e = m < c->latency_sampled
               ? hash_chunkpar(d_content, nullptr, stride, nullptr, SAMPLED_CONTENT_LEN, d_sizes, m,
-                              d_keys, c->stream)
+                              d_keys, c->chunkpar_seg(m, true), c->stream)
               : hash_sampled(d_content, stride, d_sizes, m, d_keys, c->stream);
     if (e == hipSuccess)
       e = hipMemcpyAsync(h_keys + f0, d_keys, m * 8, hipMemcpyDeviceToHost, c->stream);

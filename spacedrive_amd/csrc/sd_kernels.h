@@ -30,9 +30,10 @@ hipError_t hash_packed(const uint8_t* arena, const uint64_t* offs, const uint32_
                        const uint64_t* sizes, const uint32_t* order, uint64_t n, uint64_t* keys,
                        hipStream_t s);
 hipError_t length_keys(const uint32_t* lens, uint64_t n, uint64_t* out, hipStream_t s);
-// K1L: one wave per file, lane per chunk (offs == nullptr: strided, fixed_len bytes each)
+// K1L: a file per `seg`-lane segment (64: one wave per file, lane per chunk; 16: four files
+// per wave, 4+ chunks per lane) (offs == nullptr: strided, fixed_len bytes each)
 hipError_t hash_chunkpar(const uint8_t* arena, const uint64_t* offs, uint64_t stride,
                          const uint32_t* lens, uint32_t fixed_len, const uint64_t* sizes,
-                         uint64_t n, uint64_t* keys, hipStream_t s);
+                         uint64_t n, uint64_t* keys, int seg, hipStream_t s);
 int length_key_bits(uint64_t n);  // significant bits of the length_keys sort key
 }  // namespace sdcas

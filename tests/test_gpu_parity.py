@@ -32,16 +32,20 @@ def sampled_batch(rng, n, stride=SAMPLED_CONTENT_LEN):
     return content, sizes
 
 
-# Each device-hash test runs both kernel families: threshold 0 forces the lane-per-file
-# kernels (K1/K2) at every n, a huge threshold forces the chunk-parallel K1L.
-PATHS = {"lane": 0, "chunkpar": 1 << 40}
+# Each device-hash test runs every kernel shape: threshold 0 forces the lane-per-file
+# kernels (K1/K2) at every n, a huge threshold forces the chunk-parallel K1L — with a wave
+# per file (split huge) or four files per wave with DPP cross-lane merges (split 0).
+PATHS = {"lane": (0, None), "chunkpar": (1 << 40, 1 << 40), "chunkpar16": (1 << 40, 0)}
 
 
 @pytest.fixture(params=list(PATHS))
 def path_eng(eng, request):
-    eng.set_latency_threshold(PATHS[request.param], PATHS[request.param])
+    thr, split = PATHS[request.param]
+    eng.set_latency_threshold(thr, thr)
+    eng.set_chunkpar_split(split, split)
     yield eng
     eng.set_latency_threshold()
+    eng.set_chunkpar_split()
 
 
 def test_sampled_kernel_vs_oracle(path_eng, oracle):

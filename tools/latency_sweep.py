@@ -1,4 +1,5 @@
-"""Crossover sweep: lane-per-file kernels (K1/K2) vs chunk-parallel K1L by batch size.
+"""Crossover sweep: lane-per-file kernels (K1/K2) vs chunk-parallel K1L (a wave per file,
+and four files per wave) by batch size.
 
 Times sd_cas_hash_sampled_dev / sd_cas_hash_packed_dev with the latency threshold forced
 to each path, on torch's current stream (the engine launches there), median of R reps.
@@ -33,7 +34,7 @@ def timed(fn, reps=20):
 def main():
     eng = CasEngine(0)
     q = eng.batch_quantum
-    ns = [1, 100, 1000, 4096, 16384, 32768, 49152, q, 2 * q, 4 * q]
+    ns = [1, 100, 512, 1024, 2048, 4096, 8192, 16384, 32768, 49152, q, 98304, 2 * q, 4 * q]
     nmax = max(ns)
     content = torch.empty(nmax * SAMPLED, dtype=torch.uint8, device="cuda")
     sizes = torch.empty(nmax, dtype=torch.int64, device="cuda")
@@ -50,8 +51,10 @@ def main():
     rows = []
     for n in ns:
         row = {"n": n}
-        for name, thr in (("lane", 0), ("chunkpar", 1 << 40)):
+        for name, thr, split in (("lane", 0, 0), ("chunkpar", 1 << 40, 1 << 40),
+                                 ("chunkpar16", 1 << 40, 0)):
             eng.set_latency_threshold(thr, thr)
+            eng.set_chunkpar_split(split, split)
             t = timed(lambda: eng.hash_sampled(content, sizes[:n], keys, stride=SAMPLED, n=n))
             row[f"sampled_{name}_ms"] = round(t, 4)
             t = timed(lambda: eng.hash_packed(arena, soffs[:n], slens[:n], ssizes[:n], keys[:n]))
@@ -59,6 +62,7 @@ def main():
         rows.append(row)
         print(json.dumps(row), flush=True)
     eng.set_latency_threshold()
+    eng.set_chunkpar_split()
 
 
 if __name__ == "__main__":
