@@ -150,6 +150,27 @@ void sd_cas_key_to_hex(uint64_t key, char out[17]) {
 
 // ---- device-resident cas ----------------------------------------------------------
 
+// Sampled batch dispatch.  Below the latency threshold: K1L.  Otherwise K1 over whole batch
+// quanta (one file per lane fills every SIMD's wave slots exactly) and the remainder r:
+// with K1 as well when r >= the threshold, else K1L after it — a partial K1 wave round
+// costs a whole K1 latency however few files it holds (profiles/r01_k1l_seg_sweep.log:
+// 98,304 files 2.34 ms on K1 alone vs 1.26 + 0.76 ms split).
+static hipError_t dispatch_sampled(sd_cas_ctx* c, const uint8_t* content, uint64_t stride,
+                                   const uint64_t* sizes, size_t n, uint64_t* keys,
+                                   hipStream_t s) {
+  if (n < c->latency_sampled)
+    return hash_chunkpar(content, nullptr, stride, nullptr, SAMPLED_CONTENT_LEN, sizes, n, keys,
+                         c->chunkpar_seg(n, true), s);
+  const size_t q = sd_cas_batch_quantum(c);
+  const size_t r = n % q;
+  if (n < q || r == 0 || r >= c->latency_sampled) return hash_sampled(content, stride, sizes, n, keys, s);
+  const size_t full = n - r;
+  hipError_t e = hash_sampled(content, stride, sizes, full, keys, s);
+  if (e != hipSuccess) return e;
+  return hash_chunkpar(content + full * stride, nullptr, stride, nullptr, SAMPLED_CONTENT_LEN,
+                       sizes + full, r, keys + full, c->chunkpar_seg(r, true), s);
+}
+
 int sd_cas_hash_sampled_dev(sd_cas_ctx* c, const void* d_content, uint64_t stride,
                             const uint64_t* d_sizes, size_t n, uint64_t* d_keys, void* stream) {
   if (!c) return SD_CAS_EINVAL;
@@ -158,12 +179,8 @@ int sd_cas_hash_sampled_dev(sd_cas_ctx* c, const void* d_content, uint64_t strid
       ((uintptr_t)d_content & 15))
     return fail(c, SD_CAS_EINVAL, "hash_sampled: bad content/stride (stride=%llu)",
                 (unsigned long long)stride);
-  if (n < c->latency_sampled)  // small batch: one wave per file (K1L)
-    HIP_TRY(c, hash_chunkpar((const uint8_t*)d_content, nullptr, stride, nullptr,
-                             SAMPLED_CONTENT_LEN, d_sizes, n, d_keys, c->chunkpar_seg(n, true),
-                             pick(c, stream)));
-  else
-    HIP_TRY(c, hash_sampled((const uint8_t*)d_content, stride, d_sizes, n, d_keys, pick(c, stream)));
+  HIP_TRY(c, dispatch_sampled(c, (const uint8_t*)d_content, stride, d_sizes, n, d_keys,
+                              pick(c, stream)));
   return SD_CAS_OK;
 }
 
@@ -579,10 +596,7 @@ int sd_cas_hash_sampled_host(sd_cas_ctx* c, const void* h_content, uint64_t stri
     if (e == hipSuccess) e = hipEventRecord(h2d[b], c->copy);
     if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, h2d[b], 0);
     if (e == hipSuccess)
-      e = m < c->latency_sampled
-              ? hash_chunkpar(d_content, nullptr, stride, nullptr, SAMPLED_CONTENT_LEN, d_sizes, m,
-                              d_keys, c->chunkpar_seg(m, true), c->stream)
-              : hash_sampled(d_content, stride, d_sizes, m, d_keys, c->stream);
+      e = dispatch_sampled(c, d_content, stride, d_sizes, m, d_keys, c->stream);
     if (e == hipSuccess)
       e = hipMemcpyAsync(h_keys + f0, d_keys, m * 8, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipEventRecord(done[b], c->stream);

@@ -365,6 +365,31 @@ def test_bench_scale_properties(eng, oracle):
     del content
 
 
+def test_sampled_quantum_plus_remainder(eng, oracle):
+    """Default dispatch of a batch that is not a whole number of quanta: K1 over the whole
+    quanta, then K1L (either shape) on the remainder — identical keys to K1 on everything,
+    and to the oracle across the boundary."""
+    q = eng.batch_quantum
+    for r in (1000, 5000):  # remainder on the wave-per-file / four-per-wave K1L shape
+        n = q + r
+        content = torch.empty((n, SAMPLED_CONTENT_LEN), dtype=torch.uint8, device="cuda")
+        sizes = torch.empty(n, dtype=torch.int64, device="cuda")
+        eng.synth_sampled(31 + r, 0, n, content, sizes, SAMPLED_CONTENT_LEN)
+        auto = torch.empty(n, dtype=torch.int64, device="cuda")
+        eng.hash_sampled(content, sizes, auto)
+        eng.set_latency_threshold(0, 0)
+        lane = torch.empty(n, dtype=torch.int64, device="cuda")
+        eng.hash_sampled(content, sizes, lane)
+        eng.set_latency_threshold()
+        assert torch.equal(auto, lane), r
+        idx = np.arange(q - 300, q + 300)
+        sub = content[q - 300:q + 300].cpu().numpy()
+        want = oracle.fast_cas_keys_strided(sub.reshape(-1), SAMPLED_CONTENT_LEN, SAMPLED_CONTENT_LEN,
+                                            host64(sizes)[idx], 8)
+        assert (host64(auto)[idx] == want).all(), r
+        del content
+
+
 def test_identifier_job_step(eng, oracle, tmp_path):
     import spacedrive_amd as sd
     rng = np.random.default_rng(10)

@@ -34,7 +34,8 @@ def timed(fn, reps=20):
 def main():
     eng = CasEngine(0)
     q = eng.batch_quantum
-    ns = [1, 100, 512, 1024, 2048, 4096, 8192, 16384, 32768, 49152, q, 98304, 2 * q, 4 * q]
+    ns = [1, 100, 512, 1024, 2048, 4096, 8192, 16384, 32768, 49152, q, q + 4096, q + q // 2,
+          2 * q, 2 * q + 20000, 4 * q]
     nmax = max(ns)
     content = torch.empty(nmax * SAMPLED, dtype=torch.uint8, device="cuda")
     sizes = torch.empty(nmax, dtype=torch.int64, device="cuda")
@@ -59,6 +60,9 @@ def main():
             row[f"sampled_{name}_ms"] = round(t, 4)
             t = timed(lambda: eng.hash_packed(arena, soffs[:n], slens[:n], ssizes[:n], keys[:n]))
             row[f"packed_{name}_ms"] = round(t, 4)
+        eng.set_latency_threshold()
+        eng.set_chunkpar_split()
+        row["sampled_auto_ms"] = round(timed(lambda: eng.hash_sampled(content, sizes[:n], keys, stride=SAMPLED, n=n)), 4)
         rows.append(row)
         print(json.dumps(row), flush=True)
     eng.set_latency_threshold()
