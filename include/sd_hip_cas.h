@@ -74,8 +74,8 @@ size_t sd_cas_batch_quantum(const sd_cas_ctx* ctx);
  * `packed_files` whole files (sd_cas_hash_packed_dev) are hashed chunk-parallel — a lane
  * per 1 KiB chunk (or per 4+ chunks, sd_cas_set_chunkpar_split), cross-lane tree merge —
  * for latency (~16 + log2(chunks) compression times per file instead of 953); larger
- * batches use one file per lane for
- * throughput.  Both paths give identical keys.  0 = always one file per lane;
+ * batches use one file per lane for throughput.  Both paths give identical keys.
+ * 0 = always one file per lane;
  * SD_CAS_THRESHOLD_DEFAULT = the measured crossover (3/4 and 7/8 of the batch quantum). */
 #define SD_CAS_THRESHOLD_DEFAULT ((size_t)-1)
 void sd_cas_set_latency_threshold(sd_cas_ctx* ctx, size_t sampled_files, size_t packed_files);
@@ -102,8 +102,10 @@ int sd_cas_generate_cas_ids(sd_cas_ctx* ctx, const uint8_t* const* bufs, const u
 /* Same, gathering each file from its path with pread at the cas.rs:27-58 offsets.
  * status[i] = 0, or -errno for a file that failed to open/read (a short read of a sampled
  * file is -EIO == tokio's UnexpectedEof); such files get out_keys[i] = 0 and are to be
- * dropped from the step like mod.rs:125-141 does.  Returns SD_CAS_OK unless the batch
- * itself failed. */
+ * dropped from the step like mod.rs:125-141 does.  A whole file (size <= 100 KiB) is
+ * hashed as it is on disk even when its length no longer matches `size` (cas.rs:29 reads
+ * the file, not `size` bytes; one longer than the whole-file limit goes through the
+ * validator tree).  Returns SD_CAS_OK unless the batch itself failed. */
 int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* ctx, const char* const* paths,
                                        const uint64_t* sizes, size_t n, uint64_t* out_keys,
                                        int32_t* status);

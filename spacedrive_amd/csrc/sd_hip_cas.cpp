@@ -448,26 +448,17 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
   if (!paths || !sizes || !out_keys || !status || n >= (1ull << 32))
     return fail(c, SD_CAS_EINVAL, "generate_cas_ids_from_paths: null argument");
   HIP_TRY(c, hipSetDevice(c->device));
-  // content length per file: sampled 57,344; whole file = actual length (cas.rs:29 reads
-  // the file, not `size` bytes) -> stat it.
+  // Content length per file: sampled 57,344; whole file = its actual length (cas.rs:29
+  // reads the file, not `size` bytes).  The plan assumes the actual length is `size` (the
+  // metadata the caller just read, mod.rs:63,78-79); the gather checks it with fstat on
+  // the open descriptor — no separate stat pass and path walk — and a whole file whose
+  // length changed is re-read and hashed after the windows (`redo`).
   std::vector<uint64_t> lens(n, 0);
-  const unsigned nth = std::max(1u, std::min(16u, (unsigned)((n + 7) / 8)));  // ~8 files/worker
-  {
-    std::atomic<size_t> next{0};
-    c->pool.run(nth, [&]() {
-      for (size_t i; (i = next.fetch_add(1)) < n;) {
-        status[i] = 0;
-        out_keys[i] = 0;
-        if (sizes[i] > MINIMUM_FILE_SIZE) {
-          lens[i] = SAMPLED_CONTENT_LEN;
-        } else {
-          struct stat st;
-          if (stat(paths[i], &st) != 0) { status[i] = -errno; continue; }
-          if ((uint64_t)st.st_size > MAX_PACKED_CONTENT_LEN) { status[i] = -EFBIG; continue; }
-          lens[i] = (uint64_t)st.st_size;
-        }
-      }
-    });
+  std::vector<uint8_t> redo(n, 0);
+  for (size_t i = 0; i < n; i++) {
+    status[i] = 0;
+    out_keys[i] = 0;
+    lens[i] = sizes[i] > MINIMUM_FILE_SIZE ? SAMPLED_CONTENT_LEN : sizes[i];
   }
   // Windows of GATHER_WINDOW files, double-buffered: the pool gathers window w into one
   // pinned slot while the GPU copies and hashes window w-1 from the other.
@@ -505,6 +496,11 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
                            : pin + pl.sampled_bytes + pl.poff[t - ns];
         int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
         if (fd < 0) { status[i] = -errno; continue; }
+        if (sizes[i] <= MINIMUM_FILE_SIZE) {
+          struct stat st;
+          if (fstat(fd, &st) != 0) { status[i] = -errno; close(fd); continue; }
+          if ((uint64_t)st.st_size != lens[i]) { redo[i] = 1; close(fd); continue; }
+        }
         // cas.rs:35-58 offsets: header at 0, sample k at 8192 + k*jump, footer at size-8192
         uint64_t offs[6], lns[6];
         int parts;
@@ -518,12 +514,15 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
           offs[0] = 0; lns[0] = lens[i];
           parts = 1;
         }
-        for (int k = 0; k < parts && !status[i]; k++) {
+        for (int k = 0; k < parts && !status[i] && !redo[i]; k++) {
           size_t got = 0;
           while (got < lns[k]) {
             ssize_t r = pread(fd, dst + got, lns[k] - got, (off_t)(offs[k] + got));
             if (r < 0) { if (errno == EINTR) continue; status[i] = -errno; break; }
-            if (r == 0) { status[i] = -EIO; break; }  // UnexpectedEof
+            if (r == 0) {  // sampled: UnexpectedEof; whole file: it shrank after fstat
+              if (sizes[i] > MINIMUM_FILE_SIZE) status[i] = -EIO; else redo[i] = 1;
+              break;
+            }
             got += (size_t)r;
           }
           dst += lns[k];
@@ -551,6 +550,64 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
   if (rc) (void)hipStreamSynchronize(c->stream);
   for (int b = 0; b < nslots; b++) (void)hipEventDestroy(done[b]);
   if (rc) return rc;
+  // whole files whose length is not their metadata size: read them as they are now
+  // (fs::read, cas.rs:29) and hash the few of them as one host batch
+  std::vector<size_t> ri;
+  for (size_t i = 0; i < n; i++)
+    if (redo[i] && !status[i]) ri.push_back(i);
+  if (!ri.empty()) {
+    std::vector<std::vector<uint8_t>> bufs(ri.size());
+    std::vector<const uint8_t*> bp;
+    std::vector<uint64_t> bl, bs;
+    std::vector<size_t> bi;
+    for (size_t k = 0; k < ri.size(); k++) {
+      const size_t i = ri[k];
+      int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
+      if (fd < 0) { status[i] = -errno; continue; }
+      std::vector<uint8_t>& b = bufs[k];
+      struct stat st;
+      b.resize(8 + std::max<size_t>(fstat(fd, &st) == 0 ? (size_t)st.st_size : 0, 1 << 16));
+      size_t got = 0;
+      for (;;) {  // to EOF, whatever fstat said
+        if (8 + got == b.size()) b.resize(b.size() * 2);
+        ssize_t r = read(fd, b.data() + 8 + got, b.size() - 8 - got);
+        if (r < 0) { if (errno == EINTR) continue; status[i] = -errno; break; }
+        if (r == 0) break;
+        got += (size_t)r;
+      }
+      close(fd);
+      if (status[i]) continue;
+      if (got > MAX_PACKED_CONTENT_LEN) {
+        // longer than any whole-file message the cas kernels take (the metadata said
+        // <= 100 KiB): hash M = le64(size) || content with the validator tree (K3)
+        for (int j = 0; j < 8; j++) b[j] = (uint8_t)(sizes[i] >> (8 * j));
+        void* d = nullptr;
+        uint8_t dg[32];
+        int rc2 = hipMalloc(&d, up256(8 + got)) == hipSuccess &&
+                          hipMemcpy(d, b.data(), 8 + got, hipMemcpyHostToDevice) == hipSuccess
+                      ? sd_cas_checksum_dev(c, d, 8 + got, dg, nullptr)
+                      : fail(c, SD_CAS_EHIP, "from_paths: long whole file");
+        if (d) (void)hipFree(d);
+        if (rc2) return rc2;
+        uint64_t key = 0;
+        for (int j = 0; j < 8; j++) key = (key << 8) | dg[j];
+        out_keys[i] = key;
+        continue;
+      }
+      b.erase(b.begin(), b.begin() + 8);
+      b.resize(got);
+      bp.push_back(b.data());
+      bl.push_back(got);
+      bs.push_back(sizes[i]);
+      bi.push_back(i);
+    }
+    if (!bi.empty()) {
+      std::vector<uint64_t> k(bi.size());
+      rc = sd_cas_generate_cas_ids(c, bp.data(), bl.data(), bs.data(), bi.size(), k.data());
+      if (rc) return rc;
+      for (size_t j = 0; j < bi.size(); j++) out_keys[bi[j]] = k[j];
+    }
+  }
   for (size_t i = 0; i < n; i++)
     if (status[i]) out_keys[i] = 0;
   return SD_CAS_OK;

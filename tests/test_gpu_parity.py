@@ -140,10 +140,16 @@ def test_generate_from_paths_and_errors(eng, oracle, tmp_path):
     short = tmp_path / "short"
     short.write_bytes(b"z" * 120_000)
     paths.append(str(short)); sizes.append(10 ** 7)  # stale metadata: read_exact -> EOF
+    # stale metadata on the whole-file path: cas.rs:29 hashes le64(size) || the file as it
+    # is now (shrunk; grown within, and far beyond, the whole-file message limit)
+    for j, (actual, size) in enumerate([(3000, 5000), (90_000, 1000), (300_000, 50)]):
+        p = tmp_path / f"stale{j}"
+        p.write_bytes(rng.integers(0, 256, actual, dtype=np.uint8).tobytes())
+        paths.append(str(p)); sizes.append(size)
     keys, errs = eng.generate_cas_keys_from_paths(paths, sizes)
-    for i in range(7):
-        assert errs[i] == 0
-        assert f"{keys[i]:016x}" == oracle.generate_cas_id(paths[i], sizes[i])
+    for i in list(range(7)) + [9, 10, 11]:
+        assert errs[i] == 0, i
+        assert f"{keys[i]:016x}" == oracle.generate_cas_id(paths[i], sizes[i]), i
     assert errs[7] == 2  # ENOENT
     assert errs[8] == 5  # EIO (UnexpectedEof)
     # the single-file drop-in raises like io::Error
