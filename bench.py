@@ -43,8 +43,11 @@ HW_OPS = 680                 # VALU instructions per compression as compiled (ad
 SLOTS = 230 + 112 + 2 * (224 + 112)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 # grouping (group_hash.hip): hist read 8 + scatter read 8 / write 12 + refine read 12 /
-# write 12 + bucket read 12 + rep write 4 = 68 B/key when the refine level runs
-GROUP_BYTES_PER_KEY = 68
+# write 12 + bucket read 12 + rep write 4 = 68 B/key when the refine level runs (more
+# than 1,441,792 keys); 44 B/key below, where the 256 coarse buckets go straight to the
+# 8,192-slot tables (sd_bucket_min_big)
+def group_bytes_per_key(n: int) -> int:
+    return 44 if n <= 256 * 5632 else 68
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # 256 CUs x 4 SIMD32 x 32 lanes x 2.4 GHz = 78.6
 # full-rate wave64 VALU issue: 1024 SIMDs x 2.4 GHz / 2 cycles = 1228.8 G slots/s
 SLOT_PEAK_G = 1024 * 2.4e9 / 2 / 1e9
@@ -281,9 +284,9 @@ def main() -> None:
                 # Object grouping of one step's keys alone (K4h partition + K5h LDS hash
                 # min), HIP events around it on the stream it runs on, after the timed region
                 "ms": group_ms, "keys": F,
-                "algorithmic_bytes_per_key": GROUP_BYTES_PER_KEY,
-                "achieved_gb_s": F * GROUP_BYTES_PER_KEY / (group_ms / 1e3) / 1e9,
-                "hbm_frac": F * GROUP_BYTES_PER_KEY / (group_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                "algorithmic_bytes_per_key": group_bytes_per_key(F),
+                "achieved_gb_s": F * group_bytes_per_key(F) / (group_ms / 1e3) / 1e9,
+                "hbm_frac": F * group_bytes_per_key(F) / (group_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
             },
             "cpu_baseline": cpu,
         }

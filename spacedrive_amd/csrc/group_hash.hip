@@ -18,7 +18,10 @@
 //                           distinct keys with an atomic min of the value, then every
 //                           position looks its key up; it stores the min only where it
 //                           differs from the prefill (duplicates)            12 B read, <= 4 B write
-// = 68 B/key (44 without the refine level) in 7-8 launches.  Measured at 12.5M keys: 0.46 ms
+// = 68 B/key (44 without the refine level) in 7-8 launches.  Up to 1,441,792 keys (the
+// bench's 1.31 M per GPU) the refine level is skipped: the 256 coarse buckets (~5,100 keys)
+// go straight to 1,024-thread workgroups with 8,192-slot tables (sd_bucket_min_big):
+// 1.31 M keys 0.079 -> 0.062 ms.  Measured at 12.5M keys: 0.46 ms
 // vs 2.9 ms for the LSD path (profiles/r01_group_hash_v*.log).  The bucket is the top bits
 // of a bijective mix of the key, so any set of DISTINCT keys spreads evenly (BLAKE3 keys are
 // uniform anyway; test keys such as 0..n-1 are not), while duplicates — however many —
@@ -45,7 +48,9 @@ constexpr int ITEMS = 8;
 constexpr uint32_t PART_TILE = PART_THREADS * ITEMS;  // 4096 keys per block trip
 constexpr int MIN_THREADS = 512;
 constexpr uint32_t TABLE = 4096;          // LDS slots per bucket (48 KiB: 3 workgroups/CU)
-constexpr uint32_t TABLE_FILL = 3584;     // 7/8: above this the bucket goes to global memory
+constexpr uint32_t BIG_TABLE = 8192;      // sd_bucket_min_big: 96 KiB LDS, 1 workgroup/CU
+constexpr int BIG_THREADS = 1024;
+constexpr uint64_t BIG_MAX_KEYS = 256ull * 5632;  // mean coarse bucket <= 5,632 keys
 constexpr uint32_t MAX_BUCKETS = 16384;   // LDS cursor table of the partition kernels (64 KiB)
 constexpr uint64_t TARGET_PER_BUCKET = 1536;
 constexpr uint64_t MAX_TABLE_ENTRIES = 2ull << 20;  // [bucket][block] table (8 MiB)
@@ -349,9 +354,10 @@ sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict_
 
 // Linear-probing tables: LDS (the normal case) and global memory (overflow).  `fresh`
 // counts keys this thread inserted first.  Returns false if the table has no room.
+template <uint32_t TBL>
 __device__ __forceinline__ bool lds_insert(uint64_t* tk, uint32_t* tv, uint32_t slot, uint64_t k,
                                            uint32_t v, uint64_t empty, uint32_t& fresh) {
-  for (uint32_t probe = 0; probe < TABLE; ++probe) {
+  for (uint32_t probe = 0; probe < TBL; ++probe) {
     uint64_t cur = tk[slot];
     if (cur == empty) {
       const uint64_t old = atomicCAS((unsigned long long*)&tk[slot], (unsigned long long)empty,
@@ -362,13 +368,14 @@ __device__ __forceinline__ bool lds_insert(uint64_t* tk, uint32_t* tv, uint32_t 
       atomicMin(&tv[slot], v);
       return true;
     }
-    slot = (slot + 1) & (TABLE - 1);
+    slot = (slot + 1) & (TBL - 1);
   }
   return false;
 }
 
+template <uint32_t TBL>
 __device__ __forceinline__ uint32_t lds_find(const uint64_t* tk, uint32_t slot, uint64_t k) {
-  while (tk[slot] != k) slot = (slot + 1) & (TABLE - 1);  // present by construction
+  while (tk[slot] != k) slot = (slot + 1) & (TBL - 1);  // present by construction
   return slot;
 }
 
@@ -404,16 +411,21 @@ __device__ __forceinline__ uint64_t g_find(const uint64_t* tk, uint64_t cap, uin
 // out[pos] = min{ val(j) : key(j) == key(pos) }, val(j) = vals ? vals[j] : j, stored only
 // where it differs from val(pos): sd_part_hist_mix prefilled out[pos] = val(pos);
 // *objects += distinct keys.  gkeys/gvals: 2n-slot overflow tables (touched only on overflow).
-// A bucket of <= PART_TILE keys (all but pathological ones) is loaded once and kept in
-// registers for the lookup; larger buckets stream in PART_TILE trips.
-extern "C" __global__ void __launch_bounds__(MIN_THREADS)
-sd_bucket_min(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ ppos,
-              const uint32_t* __restrict__ vals, const uint32_t* __restrict__ starts, uint32_t nb,
-              uint32_t bits, uint64_t n, uint32_t* __restrict__ out,
-              unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
-              uint32_t* __restrict__ gvals) {
-  __shared__ uint64_t tk[TABLE];
-  __shared__ uint32_t tv[TABLE];
+// A bucket of <= TILE keys (all but pathological ones) is loaded once and kept in
+// registers for the lookup; larger buckets stream in TILE trips.
+template <uint32_t TBL, int THREADS>
+__device__ __forceinline__ void bucket_min(const uint64_t* __restrict__ pkeys,
+                                           const uint32_t* __restrict__ ppos,
+                                           const uint32_t* __restrict__ vals,
+                                           const uint32_t* __restrict__ starts, uint32_t nb,
+                                           uint32_t bits, uint64_t n, uint32_t* __restrict__ out,
+                                           unsigned long long* __restrict__ objects,
+                                           uint64_t* __restrict__ gkeys,
+                                           uint32_t* __restrict__ gvals) {
+  constexpr uint32_t TILE = THREADS * ITEMS;
+  constexpr uint32_t FILL = TBL / 8 * 7;  // above this the bucket goes to global memory
+  __shared__ uint64_t tk[TBL];
+  __shared__ uint32_t tv[TBL];
   __shared__ uint32_t distinct;
   __shared__ int overflow;
   const uint32_t b = blockIdx.x;
@@ -422,14 +434,14 @@ sd_bucket_min(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ p
   if (s == e) return;  // uniform for the whole workgroup
   // every stored key of this bucket has top bits == b, so a key from bucket b^1 is never stored
   const uint64_t empty = (uint64_t)(b ^ 1u) << (64 - bits);
-  for (uint32_t i = threadIdx.x; i < TABLE; i += MIN_THREADS) { tk[i] = empty; tv[i] = 0xFFFFFFFFu; }
+  for (uint32_t i = threadIdx.x; i < TBL; i += THREADS) { tk[i] = empty; tv[i] = 0xFFFFFFFFu; }
   if (threadIdx.x == 0) { distinct = 0; overflow = 0; }
   uint64_t k[ITEMS];
   uint32_t p[ITEMS], v[ITEMS];
-  for (uint64_t base = s; base < e; base += PART_TILE) {
+  for (uint64_t base = s; base < e; base += TILE) {
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
-      const uint64_t i = base + (uint64_t)j * MIN_THREADS + threadIdx.x;
+      const uint64_t i = base + (uint64_t)j * THREADS + threadIdx.x;
       k[j] = i < e ? pkeys[i] : empty;
       p[j] = i < e ? ppos[i] : 0u;
     }
@@ -441,31 +453,31 @@ sd_bucket_min(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ p
     bool ok = true;
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j)
-      if (k[j] != empty) ok &= lds_insert(tk, tv, (uint32_t)k[j] & (TABLE - 1), k[j], v[j], empty, fresh);
-    if (fresh && atomicAdd(&distinct, fresh) + fresh > TABLE_FILL) overflow = 1;
+      if (k[j] != empty) ok &= lds_insert<TBL>(tk, tv, (uint32_t)k[j] & (TBL - 1), k[j], v[j], empty, fresh);
+    if (fresh && atomicAdd(&distinct, fresh) + fresh > FILL) overflow = 1;
     if (!ok) overflow = 1;
   }
   __syncthreads();
   if (!overflow) {
-    if (e - s <= PART_TILE) {  // the one trip's keys are still in registers
+    if (e - s <= TILE) {  // the one trip's keys are still in registers
 #pragma unroll
       for (int j = 0; j < ITEMS; ++j)
         if (k[j] != empty) {
-          const uint32_t mv = tv[lds_find(tk, (uint32_t)k[j] & (TABLE - 1), k[j])];
+          const uint32_t mv = tv[lds_find<TBL>(tk, (uint32_t)k[j] & (TBL - 1), k[j])];
           if (mv != v[j]) out[p[j]] = mv;  // out[] was prefilled with the own value
         }
     } else {
-      for (uint64_t base = s; base < e; base += PART_TILE) {
+      for (uint64_t base = s; base < e; base += TILE) {
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
-          const uint64_t i = base + (uint64_t)j * MIN_THREADS + threadIdx.x;
+          const uint64_t i = base + (uint64_t)j * THREADS + threadIdx.x;
           k[j] = i < e ? pkeys[i] : empty;
           p[j] = i < e ? ppos[i] : 0u;
         }
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j)
           if (k[j] != empty) {
-            const uint32_t mv = tv[lds_find(tk, (uint32_t)k[j] & (TABLE - 1), k[j])];
+            const uint32_t mv = tv[lds_find<TBL>(tk, (uint32_t)k[j] & (TBL - 1), k[j])];
             if (mv != (vals ? vals[p[j]] : p[j])) out[p[j]] = mv;
           }
       }
@@ -477,12 +489,12 @@ sd_bucket_min(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ p
   const uint64_t m = e - s, cap = 2 * m;
   uint64_t* gk = gkeys + 2 * s;
   uint32_t* gv = gvals + 2 * s;
-  for (uint64_t i = threadIdx.x; i < cap; i += MIN_THREADS) { gk[i] = empty; gv[i] = 0xFFFFFFFFu; }
+  for (uint64_t i = threadIdx.x; i < cap; i += THREADS) { gk[i] = empty; gv[i] = 0xFFFFFFFFu; }
   if (threadIdx.x == 0) distinct = 0;
   __threadfence();
   __syncthreads();
   uint32_t fresh = 0;
-  for (uint64_t i = s + threadIdx.x; i < e; i += MIN_THREADS) {
+  for (uint64_t i = s + threadIdx.x; i < e; i += THREADS) {
     const uint64_t kk = pkeys[i];
     const uint32_t pp = ppos[i];
     g_insert(gk, gv, cap, (kk & 0xFFFFFFFFull) % cap, kk, vals ? vals[pp] : pp, empty, fresh);
@@ -490,7 +502,7 @@ sd_bucket_min(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ p
   if (fresh) atomicAdd(&distinct, fresh);
   __threadfence();
   __syncthreads();
-  for (uint64_t i = s + threadIdx.x; i < e; i += MIN_THREADS) {
+  for (uint64_t i = s + threadIdx.x; i < e; i += THREADS) {
     const uint64_t kk = pkeys[i];
     const uint32_t pp = ppos[i];
     const uint64_t slot = g_find(gk, cap, (kk & 0xFFFFFFFFull) % cap, kk);
@@ -498,6 +510,29 @@ sd_bucket_min(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ p
     if (mv != (vals ? vals[pp] : pp)) out[pp] = mv;
   }
   if (threadIdx.x == 0) atomicAdd(objects, (unsigned long long)distinct);
+}
+
+
+extern "C" __global__ void __launch_bounds__(MIN_THREADS)
+sd_bucket_min(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ ppos,
+              const uint32_t* __restrict__ vals, const uint32_t* __restrict__ starts, uint32_t nb,
+              uint32_t bits, uint64_t n, uint32_t* __restrict__ out,
+              unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
+              uint32_t* __restrict__ gvals) {
+  bucket_min<TABLE, MIN_THREADS>(pkeys, ppos, vals, starts, nb, bits, n, out, objects, gkeys, gvals);
+}
+
+// Small batches (<= BIG_MAX_KEYS): the 2^8 coarse buckets of the first partition level
+// (~5,100 keys at 1.31 M) go straight to 1,024-thread workgroups with an 8,192-slot table
+// (96 KiB LDS, one per CU) — no refine level, one launch and 24 B/key fewer.
+extern "C" __global__ void __launch_bounds__(BIG_THREADS)
+sd_bucket_min_big(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ ppos,
+                  const uint32_t* __restrict__ vals, const uint32_t* __restrict__ starts,
+                  uint32_t nb, uint32_t bits, uint64_t n, uint32_t* __restrict__ out,
+                  unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
+                  uint32_t* __restrict__ gvals) {
+  bucket_min<BIG_TABLE, BIG_THREADS>(pkeys, ppos, vals, starts, nb, bits, n, out, objects, gkeys,
+                                     gvals);
 }
 
 }  // namespace sdcas
@@ -533,6 +568,7 @@ static PartPlan part_plan(uint64_t n, uint32_t nb, uint32_t bits) {
 struct GroupPlan {
   PartPlan l1;
   uint32_t b1, b2;
+  bool big;  // coarse buckets straight to sd_bucket_min_big (no refine level)
   uint32_t nb() const { return 1u << (b1 + b2); }
 };
 
@@ -542,6 +578,8 @@ static GroupPlan group_plan(uint64_t n) {
   GroupPlan g;
   g.b1 = bits < 8 ? bits : 8;
   g.b2 = bits - g.b1;
+  g.big = g.b2 > 0 && n <= BIG_MAX_KEYS;
+  if (g.big) g.b2 = 0;
   g.l1 = part_plan(n, 1u << g.b1, g.b1);
   return g;
 }
@@ -618,8 +656,12 @@ hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n
     fk = k2;
     fp = p2;
   }
-  sd_bucket_min<<<g.nb(), MIN_THREADS, 0, s>>>(fk, fp, vals, starts, g.nb(), g.b1 + g.b2, n, out,
-                                               (unsigned long long*)d_objects, gkeys, gvals);
+  if (g.big)
+    sd_bucket_min_big<<<g.nb(), BIG_THREADS, 0, s>>>(fk, fp, vals, starts, g.nb(), g.b1, n, out,
+                                                     (unsigned long long*)d_objects, gkeys, gvals);
+  else
+    sd_bucket_min<<<g.nb(), MIN_THREADS, 0, s>>>(fk, fp, vals, starts, g.nb(), g.b1 + g.b2, n, out,
+                                                 (unsigned long long*)d_objects, gkeys, gvals);
   return hipGetLastError();
 }
 
