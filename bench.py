@@ -265,6 +265,9 @@ def main() -> None:
                 # roof is full-rate wave64 issue slots; the HBM view is in "hbm".
                 "kernel": "sd_cas_sampled_kernel",
                 "bound": "valu",
+                "bound_note": ("BLAKE3 is 32-bit integer ARX with no contraction: no MFMA path, and "
+                               "HBM runs at ~0.4 of peak (see 'hbm'); the binding roof is VALU "
+                               "issue (DESIGN.md 2.1, profiles/r01_ubench_*)"),
                 "achieved": slots,
                 "peak": SLOT_PEAK_G,
                 "unit": "G wave-issue-slots/s",
