@@ -76,15 +76,16 @@ size_t sd_cas_batch_quantum(const sd_cas_ctx* ctx);
  * for latency (~16 + log2(chunks) compression times per file instead of 953); larger
  * batches use one file per lane for throughput.  Both paths give identical keys.
  * 0 = always one file per lane;
- * SD_CAS_THRESHOLD_DEFAULT = the measured crossover (3/4 and 7/8 of the batch quantum). */
+ * SD_CAS_THRESHOLD_DEFAULT = the measured crossover (3/4 and 3x the batch quantum). */
 #define SD_CAS_THRESHOLD_DEFAULT ((size_t)-1)
 void sd_cas_set_latency_threshold(sd_cas_ctx* ctx, size_t sampled_files, size_t packed_files);
 /* Shape of the chunk-parallel path: batches of at least `sampled_files` / `packed_files`
  * files pack four files per wave (16 lanes per file, 4+ consecutive chunks per lane, lane
  * subtrees merged across lanes with DPP row shifts), smaller ones take one wave per file
  * (a lane per chunk, lowest latency).  Identical keys either way.  0 = always four per
- * wave; SD_CAS_THRESHOLD_DEFAULT = the measured crossover (sampled: 3/64 of the batch
- * quantum; whole files: never, four ragged lengths per wave run at the longest one's). */
+ * wave; SD_CAS_THRESHOLD_DEFAULT = the measured crossover (sampled: 3/64, whole files:
+ * 3/32 of the batch quantum; whole files are then visited by chunk count, one stable radix
+ * pass, so the four files of a wave share a chunks-per-lane class). */
 void sd_cas_set_chunkpar_split(sd_cas_ctx* ctx, size_t sampled_files, size_t packed_files);
 /* page-locked host staging for the gather (replaces the per-file Box<[u8]> of cas.rs:32) */
 int sd_cas_alloc_pinned(sd_cas_ctx* ctx, size_t bytes, void** out);

@@ -370,11 +370,13 @@ __device__ __forceinline__ void chunkpar_wave(const uint8_t* __restrict__ arena,
                                               const uint64_t* __restrict__ offs, uint64_t stride,
                                               const uint32_t* __restrict__ lens, uint32_t fixed_len,
                                               const uint64_t* __restrict__ sizes, uint64_t n,
+                                              const uint32_t* __restrict__ order,
                                               uint64_t* __restrict__ keys) {
   __shared__ uint32_t stk[CP_DEPTH][8][64];  // word-major per-lane columns: conflict-free
   const uint32_t lane = threadIdx.x;
   const uint32_t sl = lane % SEG;
-  const uint64_t f = (uint64_t)blockIdx.x * (64 / SEG) + lane / SEG;
+  const uint64_t slot = (uint64_t)blockIdx.x * (64 / SEG) + lane / SEG;
+  const uint64_t f = slot < n ? (order ? (uint64_t)order[slot] : slot) : n;
   uint32_t clen = 0, nchunks = 0;
   uint64_t size = 0;
   const uint4* q = nullptr;
@@ -426,14 +428,16 @@ __device__ __forceinline__ void chunkpar_wave(const uint8_t* __restrict__ arena,
 }
 
 // offs == nullptr: content i at arena + i*stride with length fixed_len (the sampled
-// layout); else arena + offs[i], lens[i] bytes.  One 64-lane workgroup = 64/SEG files.
+// layout); else arena + offs[i], lens[i] bytes.  One 64-lane workgroup = 64/SEG files,
+// visited in `order` (nullptr = identity): ragged files sorted by chunk count so the 4
+// files of a 16-lane-segment wave share one chunks-per-lane class.
 template <int SEG>
 __global__ void __launch_bounds__(64)
 sd_cas_chunkpar_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                        uint64_t stride, const uint32_t* __restrict__ lens, uint32_t fixed_len,
                        const uint64_t* __restrict__ sizes, uint64_t n,
-                       uint64_t* __restrict__ keys) {
-  chunkpar_wave<SEG>(arena, offs, stride, lens, fixed_len, sizes, n, keys);
+                       const uint32_t* __restrict__ order, uint64_t* __restrict__ keys) {
+  chunkpar_wave<SEG>(arena, offs, stride, lens, fixed_len, sizes, n, order, keys);
 }
 
 // K2: whole-file path, content length <= MAX_PACKED_CONTENT_LEN, files visited in `order`.
@@ -498,15 +502,16 @@ hipError_t hash_packed(const uint8_t* arena, const uint64_t* offs, const uint32_
 
 hipError_t hash_chunkpar(const uint8_t* arena, const uint64_t* offs, uint64_t stride,
                          const uint32_t* lens, uint32_t fixed_len, const uint64_t* sizes,
-                         uint64_t n, uint64_t* keys, int seg, hipStream_t s) {
+                         uint64_t n, uint64_t* keys, int seg, hipStream_t s,
+                         const uint32_t* order) {
   if (n == 0) return hipSuccess;
   if (n >= (1ull << 31)) return hipErrorInvalidValue;
   if (seg == 16)
-    sd_cas_chunkpar_kernel<16><<<(uint32_t)((n + 3) / 4), 64, 0, s>>>(arena, offs, stride, lens,
-                                                                      fixed_len, sizes, n, keys);
+    sd_cas_chunkpar_kernel<16><<<(uint32_t)((n + 3) / 4), 64, 0, s>>>(
+        arena, offs, stride, lens, fixed_len, sizes, n, order, keys);
   else
     sd_cas_chunkpar_kernel<64><<<(uint32_t)n, 64, 0, s>>>(arena, offs, stride, lens, fixed_len,
-                                                         sizes, n, keys);
+                                                         sizes, n, order, keys);
   return hipGetLastError();
 }
 

@@ -72,14 +72,14 @@ int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
 
 // Defaults = the measured crossovers on MI355X (profiles/r01_k1l_seg_sweep.log): K1L (four
 // files per wave) wins below ~0.75 of a batch quantum for sampled messages (49,152 files:
-// 1.12 vs 1.16 ms; 65,536: 1.48 vs 1.28) and K1L (a wave per file) below ~0.9 for ragged
-// whole files, where the lane-per-file path also pays the length sort and the 101-chunk
-// latency of its longest file.
+// 1.12 vs 1.16 ms; 65,536: 1.48 vs 1.28) and below ~3.5-4 quanta for ragged whole files
+// (131,072: 3.29 vs 3.46 ms; 262,144: 6.58 vs 6.51), where the lane-per-file K2 waits for
+// the 101-chunk latency of its longest files.
 void sd_cas_set_latency_threshold(sd_cas_ctx* c, size_t sampled_files, size_t packed_files) {
   if (!c) return;
   const size_t q = sd_cas_batch_quantum(c);
   c->latency_sampled = sampled_files == SD_CAS_THRESHOLD_DEFAULT ? q * 3 / 4 : sampled_files;
-  c->latency_packed = packed_files == SD_CAS_THRESHOLD_DEFAULT ? q * 7 / 8 : packed_files;
+  c->latency_packed = packed_files == SD_CAS_THRESHOLD_DEFAULT ? q * 3 : packed_files;
 }
 
 // Defaults = the measured crossovers between the two K1L shapes (profiles/
@@ -88,11 +88,11 @@ void sd_cas_set_latency_threshold(sd_cas_ctx* c, size_t sampled_files, size_t pa
 void sd_cas_set_chunkpar_split(sd_cas_ctx* c, size_t sampled_files, size_t packed_files) {
   if (!c) return;
   // sampled: crossover between 2,048 (0.078 vs 0.116 ms) and 4,096 files (0.139 vs 0.120);
-  // ragged whole files: 16-lane segments lose everywhere (four random lengths per wave run
-  // at the longest one's chunks-per-lane), so packed batches keep a wave per file
+  // ragged whole files (visited by chunk count, so a wave's 4 files share a chunks-per-lane
+  // class; the sort costs ~15 us): between 4,096 (0.216 vs 0.247) and 8,192 (0.364 vs 0.324)
   const size_t q = sd_cas_batch_quantum(c);
   c->seg16_sampled = sampled_files == SD_CAS_THRESHOLD_DEFAULT ? q * 3 / 64 : sampled_files;
-  c->seg16_packed = packed_files == SD_CAS_THRESHOLD_DEFAULT ? (size_t)-1 : packed_files;
+  c->seg16_packed = packed_files == SD_CAS_THRESHOLD_DEFAULT ? q * 3 / 32 : packed_files;
 }
 
 void sd_cas_ctx_destroy(sd_cas_ctx* c) {
@@ -193,11 +193,14 @@ int sd_cas_hash_packed_dev(sd_cas_ctx* c, const void* d_arena, const uint64_t* d
       n >= (1ull << 32))
     return fail(c, SD_CAS_EINVAL, "hash_packed: bad arguments");
   hipStream_t s = pick(c, stream);
-  if (n < c->latency_packed) {  // small batch: one wave per file (K1L), no length sort
+  const bool k1l = n < c->latency_packed;
+  if (k1l && c->chunkpar_seg(n, false) == 64) {  // small batch: a wave per file, no sort
     HIP_TRY(c, hash_chunkpar((const uint8_t*)d_arena, d_offs, 0, d_lens, 0, d_sizes, n, d_keys,
-                             c->chunkpar_seg(n, false), s));
+                             64, s));
     return SD_CAS_OK;
   }
+  // K2, and K1L with 4 files per wave: visit the files by descending chunk count (one
+  // stable radix pass) so the lanes of a wave (K2) / the files of a wave (K1L) match.
   // workspace: length keys | sorted keys | order | sort workspace
   const size_t kb = up256(n * 8), ob = up256(n * 4);
   int rc = ensure(c, c->ws, 2 * kb + ob + sort_workspace_bytes(n));
@@ -209,7 +212,11 @@ int sd_cas_hash_packed_dev(sd_cas_ctx* c, const void* d_arena, const uint64_t* d
   void* sws = p + 2 * kb + ob;
   HIP_TRY(c, length_keys(d_lens, n, lkeys, s));
   HIP_TRY(c, radix_sort_pairs(lkeys, nullptr, skeys, order, n, 0, length_key_bits(n), sws, s));
-  HIP_TRY(c, hash_packed((const uint8_t*)d_arena, d_offs, d_lens, d_sizes, order, n, d_keys, s));
+  if (k1l)
+    HIP_TRY(c, hash_chunkpar((const uint8_t*)d_arena, d_offs, 0, d_lens, 0, d_sizes, n, d_keys,
+                             16, s, order));
+  else
+    HIP_TRY(c, hash_packed((const uint8_t*)d_arena, d_offs, d_lens, d_sizes, order, n, d_keys, s));
   return SD_CAS_OK;
 }
 

@@ -34,6 +34,7 @@ hipError_t length_keys(const uint32_t* lens, uint64_t n, uint64_t* out, hipStrea
 // per wave, 4+ chunks per lane) (offs == nullptr: strided, fixed_len bytes each)
 hipError_t hash_chunkpar(const uint8_t* arena, const uint64_t* offs, uint64_t stride,
                          const uint32_t* lens, uint32_t fixed_len, const uint64_t* sizes,
-                         uint64_t n, uint64_t* keys, int seg, hipStream_t s);
+                         uint64_t n, uint64_t* keys, int seg, hipStream_t s,
+                         const uint32_t* order = nullptr);
 int length_key_bits(uint64_t n);  // significant bits of the length_keys sort key
 }  // namespace sdcas

@@ -63,6 +63,7 @@ def main():
         eng.set_latency_threshold()
         eng.set_chunkpar_split()
         row["sampled_auto_ms"] = round(timed(lambda: eng.hash_sampled(content, sizes[:n], keys, stride=SAMPLED, n=n)), 4)
+        row["packed_auto_ms"] = round(timed(lambda: eng.hash_packed(arena, soffs[:n], slens[:n], ssizes[:n], keys[:n])), 4)
         rows.append(row)
         print(json.dumps(row), flush=True)
     eng.set_latency_threshold()
