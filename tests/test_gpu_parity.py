@@ -400,6 +400,47 @@ def test_sampled_quantum_plus_remainder(eng, oracle):
         del content
 
 
+def test_headline_10m_files(eng, oracle):
+    """BASELINE's target at its full size: 10M sampled files with 30 % duplicate content,
+    hashed in 8 resident batches of 1.25M (71.7 GB each), cas_ids bit-exact vs the oracle on
+    400 random files of every batch, and the Object grouping of all 10M keys == the
+    generator's duplicate truth for every file — locally (K4h/K5h) and through the 8-way
+    key-range exchange of the multi-GPU path (8 shards on this device, sd_cas_multi_group)."""
+    from spacedrive_amd.multi import MultiEngine
+    n, batch, seed, dup = 10_000_000, 1_250_000, 0x5DCA50004, 300
+    content = torch.empty((batch, SAMPLED_CONTENT_LEN), dtype=torch.uint8, device="cuda")
+    sizes = torch.empty(batch, dtype=torch.int64, device="cuda")
+    keys = torch.empty(n, dtype=torch.int64, device="cuda")
+    rng = np.random.default_rng(100)
+    for f0 in range(0, n, batch):
+        eng.synth_sampled(seed, f0, batch, content, sizes, SAMPLED_CONTENT_LEN, dup_permille=dup)
+        eng.hash_sampled(content, sizes, keys[f0:f0 + batch])
+        idx = np.sort(rng.choice(batch, 400, replace=False))
+        sub = content[torch.from_numpy(idx).cuda()].cpu().numpy()
+        want = oracle.fast_cas_keys_strided(sub.reshape(-1), SAMPLED_CONTENT_LEN, SAMPLED_CONTENT_LEN,
+                                            host64(sizes)[idx], 8)
+        assert (host64(keys[f0:f0 + batch])[idx] == want).all(), f0
+    del content
+    roots = torch.empty(n, dtype=torch.int64, device="cuda")
+    eng.synth_roots(seed, 0, n, roots, dup_permille=dup)
+    r = roots.cpu().numpy()
+    del roots
+    uniq, inv = np.unique(r, return_inverse=True)
+    first = np.full(len(uniq), n, dtype=np.int64)
+    np.minimum.at(first, inv, np.arange(n))
+    truth = first[inv]
+    rep = torch.empty(n, dtype=torch.int32, device="cuda")
+    objects = eng.group(keys, rep)
+    assert objects == len(uniq)
+    assert (rep.cpu().numpy() == truth).all()
+    me = MultiEngine([0] * 8)
+    cuts = [n * i // 8 for i in range(9)]
+    reps, mobjects = me.group([keys[cuts[i]:cuts[i + 1]] for i in range(8)], cuts[:-1])
+    assert mobjects == len(uniq)
+    assert (np.concatenate([x.cpu().numpy() for x in reps]) == truth).all()
+    me.close()
+
+
 def test_identifier_job_step(eng, oracle, tmp_path):
     import spacedrive_amd as sd
     rng = np.random.default_rng(10)
