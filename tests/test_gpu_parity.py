@@ -400,6 +400,36 @@ def test_sampled_quantum_plus_remainder(eng, oracle):
         del content
 
 
+def test_random_cases_1e5(path_eng, oracle):
+    """SURVEY §7's minimum-slice bar on every kernel shape: 10^5 random whole-file messages
+    (sizes uniform in [0, 102,400]) and 10^5 random sampled files, every cas key vs the
+    oracle's SIMD restatement."""
+    eng = path_eng
+    n = 100_000
+    sz = torch.empty(n, dtype=torch.int64, device="cuda")
+    ln = torch.empty(n, dtype=torch.int32, device="cuda")
+    of = torch.empty(n, dtype=torch.int64, device="cuda")
+    nb = eng.synth_small(77, 0, n, sz, ln, of, None)
+    arena = torch.empty(nb + 64, dtype=torch.uint8, device="cuda")
+    eng.synth_small(77, 0, n, sz, ln, of, arena)
+    keys = torch.empty(n, dtype=torch.int64, device="cuda")
+    eng.hash_packed(arena, of, ln, sz, keys)
+    lens = ln.cpu().numpy().astype(np.uint32)
+    assert lens.min() < 1024 and lens.max() > 100_000  # the whole 1 B .. 100 KiB range
+    want = oracle.fast_cas_keys(arena.cpu().numpy(), of.cpu().numpy().astype(np.uint64), lens,
+                                host64(sz), 8)
+    assert (host64(keys) == want).all()
+    del arena
+    content = torch.empty((n, SAMPLED_CONTENT_LEN), dtype=torch.uint8, device="cuda")
+    sizes = torch.empty(n, dtype=torch.int64, device="cuda")
+    eng.synth_sampled(78, 0, n, content, sizes, SAMPLED_CONTENT_LEN)
+    eng.hash_sampled(content, sizes, keys)
+    want = oracle.fast_cas_keys_strided(content.cpu().numpy().reshape(-1), SAMPLED_CONTENT_LEN,
+                                        SAMPLED_CONTENT_LEN, host64(sizes), 8)
+    assert (host64(keys) == want).all()
+    del content
+
+
 def test_headline_10m_files(eng, oracle):
     """BASELINE's target at its full size: 10M sampled files with 30 % duplicate content,
     hashed in 8 resident batches of 1.25M (71.7 GB each), cas_ids bit-exact vs the oracle on
