@@ -8,10 +8,11 @@ their contiguous slice of files (no communication), then:
 
   1. key-range partition of the local keys, dest(k) = floor(k * G / 2^64)
      (BLAKE3 keys are uniform)                                   [HIP: sd_cas_partition_dev]
-  2. all_to_all_single of the part sizes, then of keys and global file idx  [RCCL]
+  2. all_to_all_single of the part sizes, then ONE all_to_all_single of 12-byte rows
+     (key u64, global file idx u32) — 12 B/key instead of two int64 exchanges' 16  [RCCL]
   3. grouping of the received pairs: rep = min global idx over equal keys
                                                                  [HIP: sd_cas_group_min_dev]
-  4. mirror all_to_all_single of the reps; scatter to local file order  [RCCL]
+  4. mirror all_to_all_single of the u32 reps (4 B/key); scatter to local file order [RCCL]
 
 Every key lives on exactly one rank after step 2, so step 3's minimum is the global one:
 rep(f) = min{ g : key(g) == key(f) } over all ranks, the single-GPU contract.
@@ -73,29 +74,31 @@ def sharded_group(local_keys: torch.Tensor, file0: int, ops: ShardOps,
     rank = dist.get_rank(group)
     dev = local_keys.device
     n = local_keys.numel()
+    if file0 + n > (1 << 32):
+        raise ValueError("sharded_group: global file idx must fit in u32")
     pkeys, ppos, send_counts = ops.partition(local_keys, world)     # 1
     recv_counts = torch.empty_like(send_counts)
     dist.all_to_all_single(recv_counts, send_counts, group=group)  # 2: sizes
     sc = send_counts.cpu().tolist()
     rc = recv_counts.cpu().tolist()
-    gidx = ppos.to(torch.int64) + file0
-    rkeys = torch.empty(sum(rc), dtype=torch.int64, device=dev)
-    ridx = torch.empty(sum(rc), dtype=torch.int64, device=dev)
-    dist.all_to_all_single(rkeys, pkeys, rc, sc, group=group)     # 2: keys, global idx
-    dist.all_to_all_single(ridx, gidx, rc, sc, group=group)
-    m = rkeys.numel()
+    # rows of 3 x int32: key (2 words, little-endian u64) and the u32 global idx (as int32 bits)
+    rows = torch.empty((n, 3), dtype=torch.int32, device=dev)
+    rows[:, :2] = pkeys.view(torch.int32).view(n, 2)
+    rows[:, 2] = (ppos.to(torch.int64) + file0).to(torch.int32)    # wraps to the u32's bits
+    m = sum(rc)
+    rrows = torch.empty((m, 3), dtype=torch.int32, device=dev)
+    dist.all_to_all_single(rrows, rows, rc, sc, group=group)        # 2: (key, idx) rows
     if m:
-        if int(ridx.max().item()) >= (1 << 32):
-            raise ValueError("sharded_group: global file idx must fit in u32")
-        rep_min, objects = ops.group_min(rkeys, ridx.to(torch.int32))  # 3
-        rep_global = rep_min.to(torch.int64) & 0xFFFFFFFF
+        rkeys = rrows[:, :2].contiguous().view(torch.int64).view(m)
+        ridx = rrows[:, 2].contiguous()
+        rep_min, objects = ops.group_min(rkeys, ridx)              # 3: u32 bits in int32
     else:
-        rep_global = torch.empty(0, dtype=torch.int64, device=dev)
+        rep_min = torch.empty(0, dtype=torch.int32, device=dev)
         objects = 0
-    back = torch.empty(n, dtype=torch.int64, device=dev)
-    dist.all_to_all_single(back, rep_global, sc, rc, group=group)  # 4
+    back = torch.empty(n, dtype=torch.int32, device=dev)
+    dist.all_to_all_single(back, rep_min, sc, rc, group=group)      # 4
     rep = torch.empty(n, dtype=torch.int64, device=dev)
-    rep[ppos.to(torch.int64)] = back
+    rep[ppos.to(torch.int64)] = back.to(torch.int64) & 0xFFFFFFFF
     tot = torch.tensor([objects], dtype=torch.int64, device=dev)
     dist.all_reduce(tot, group=group)
     return ShardResult(rep=rep, objects=int(tot.item()), sent=n - int(sc[rank]))
