@@ -156,6 +156,17 @@ int sd_cas_group_min_dev(sd_cas_ctx* ctx, const uint64_t* d_keys, const uint32_t
 int sd_cas_partition_dev(sd_cas_ctx* ctx, const uint64_t* d_keys, size_t n, uint32_t parts,
                          uint64_t* d_keys_out, uint32_t* d_pos_out, uint64_t* d_counts,
                          void* stream);
+/* Row packing of the per-process RCCL key-range exchange (one process per GPU,
+ * spacedrive_amd/shard.py): d_rows[3j..3j+2] = (key lo32, key hi32,
+ * u32(file0 + d_pos[j])) for the partition's output; split turns received rows back into
+ * keys + u32 vals; unpack scatters the mirrored u32 reps to local file order,
+ * d_rep[d_pos[j]] = d_back[j] (u64).  file0 + n must fit in u32. */
+int sd_cas_exchange_pack_dev(sd_cas_ctx* ctx, const uint64_t* d_keys, const uint32_t* d_pos,
+                             size_t n, uint64_t file0, uint32_t* d_rows, void* stream);
+int sd_cas_exchange_split_dev(sd_cas_ctx* ctx, const uint32_t* d_rows, size_t m,
+                              uint64_t* d_keys, uint32_t* d_vals, void* stream);
+int sd_cas_exchange_unpack_dev(sd_cas_ctx* ctx, const uint32_t* d_back, const uint32_t* d_pos,
+                               size_t n, uint64_t* d_rep, void* stream);
 /* Same on already-sorted pairs (keys ascending, vals = file idx, stable). */
 int sd_cas_group_sorted_dev(sd_cas_ctx* ctx, const uint64_t* d_sorted_keys,
                             const uint32_t* d_sorted_vals, size_t n, uint32_t* d_rep,

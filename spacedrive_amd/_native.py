@@ -42,6 +42,9 @@ SIGNATURES = [
     ("sd_cas_group_dev", _i, [_vp, _vp, _sz, _vp, _vp, _vp]),
     ("sd_cas_group_min_dev", _i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     ("sd_cas_partition_dev", _i, [_vp, _vp, _sz, _u32, _vp, _vp, _vp, _vp]),
+    ("sd_cas_exchange_pack_dev", _i, [_vp, _vp, _vp, _sz, _u64, _vp, _vp]),
+    ("sd_cas_exchange_split_dev", _i, [_vp, _vp, _sz, _vp, _vp, _vp]),
+    ("sd_cas_exchange_unpack_dev", _i, [_vp, _vp, _vp, _sz, _vp, _vp]),
     ("sd_cas_group_sorted_dev", _i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     ("sd_cas_group_chunked_dev", _i, [_vp, _vp, _sz, _u32, _vp, _vp, _vp, _vp]),
     ("sd_cas_sort_pairs_dev", _i, [_vp, _vp, _vp, _sz, _vp, _vp, _i, _i, _vp]),

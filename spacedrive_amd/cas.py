@@ -223,6 +223,20 @@ class CasEngine:
             ctypes.byref(obj) if want_objects else None, _stream(stream)), "group_min")
         return int(obj.value) if want_objects else None
 
+    def exchange_pack(self, keys, pos, file0: int, rows, stream: Optional[int] = None) -> None:
+        """rows int32 [n, 3] = (key lo, key hi, u32(file0 + pos)) for the RCCL exchange."""
+        self._check(self.L.sd_cas_exchange_pack_dev(self.h, _ptr(keys), _ptr(pos), int(keys.numel()),
+                                                    int(file0), _ptr(rows), _stream(stream)),
+                    "exchange_pack")
+
+    def exchange_split(self, rows, keys, vals, stream: Optional[int] = None) -> None:
+        self._check(self.L.sd_cas_exchange_split_dev(self.h, _ptr(rows), int(keys.numel()), _ptr(keys),
+                                                     _ptr(vals), _stream(stream)), "exchange_split")
+
+    def exchange_unpack(self, back, pos, rep, stream: Optional[int] = None) -> None:
+        self._check(self.L.sd_cas_exchange_unpack_dev(self.h, _ptr(back), _ptr(pos), int(back.numel()),
+                                                      _ptr(rep), _stream(stream)), "exchange_unpack")
+
     def partition(self, keys, parts: int, keys_out, pos_out, counts, stream: Optional[int] = None) -> None:
         """Key-range partition part(k) = floor(k * parts / 2^64), part-contiguous output."""
         n = int(keys.numel())

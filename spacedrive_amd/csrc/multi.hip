@@ -31,6 +31,40 @@ extern "C" __global__ void sd_multi_splits(const uint64_t* __restrict__ skeys, u
   splits[r] = lo;
 }
 
+// ---- the RCCL key-range exchange of spacedrive_amd/shard.py (one process per GPU) ----
+// rows[j] = (key lo32, key hi32, u32 global idx file0 + pos[j]): 12-byte rows, one
+// all-to-all instead of a key and an idx exchange
+extern "C" __global__ void __launch_bounds__(256)
+sd_exch_pack(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos, uint64_t n,
+             uint64_t file0, uint32_t* __restrict__ rows) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < n) {
+    const uint64_t k = keys[j];
+    rows[3 * j] = (uint32_t)k;
+    rows[3 * j + 1] = (uint32_t)(k >> 32);
+    rows[3 * j + 2] = (uint32_t)(file0 + pos[j]);
+  }
+}
+
+// received rows -> keys[m] u64 + vals[m] u32 (the grouping's inputs)
+extern "C" __global__ void __launch_bounds__(256)
+sd_exch_split(const uint32_t* __restrict__ rows, uint64_t m, uint64_t* __restrict__ keys,
+              uint32_t* __restrict__ vals) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < m) {
+    keys[j] = (uint64_t)rows[3 * j] | ((uint64_t)rows[3 * j + 1] << 32);
+    vals[j] = rows[3 * j + 2];
+  }
+}
+
+// rep[pos[j]] = back[j]: the mirrored u32 reps scattered to local file order (as u64)
+extern "C" __global__ void __launch_bounds__(256)
+sd_exch_unpack(const uint32_t* __restrict__ back, const uint32_t* __restrict__ pos, uint64_t n,
+               uint64_t* __restrict__ rep) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < n) rep[pos[j]] = back[j];
+}
+
 // gidx[j] = file0 + sidx[j]
 extern "C" __global__ void __launch_bounds__(256)
 sd_multi_gidx(const uint32_t* __restrict__ sidx, uint64_t n, uint64_t file0,
@@ -60,6 +94,27 @@ hipError_t multi_splits(const uint64_t* skeys, uint64_t n, uint32_t G, uint64_t*
                         hipStream_t s) {
   if (G == 0 || G > 1023) return hipErrorInvalidValue;
   sd_multi_splits<<<1, ((G + 1 + 63) / 64) * 64, 0, s>>>(skeys, n, G, splits);
+  return hipGetLastError();
+}
+
+hipError_t exch_pack(const uint64_t* keys, const uint32_t* pos, uint64_t n, uint64_t file0,
+                     uint32_t* rows, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  sd_exch_pack<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(keys, pos, n, file0, rows);
+  return hipGetLastError();
+}
+
+hipError_t exch_split(const uint32_t* rows, uint64_t m, uint64_t* keys, uint32_t* vals,
+                      hipStream_t s) {
+  if (m == 0) return hipSuccess;
+  sd_exch_split<<<(uint32_t)((m + 255) / 256), 256, 0, s>>>(rows, m, keys, vals);
+  return hipGetLastError();
+}
+
+hipError_t exch_unpack(const uint32_t* back, const uint32_t* pos, uint64_t n, uint64_t* rep,
+                       hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  sd_exch_unpack<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(back, pos, n, rep);
   return hipGetLastError();
 }
 

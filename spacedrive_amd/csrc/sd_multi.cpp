@@ -347,4 +347,31 @@ int sd_cas_multi_hash_group_sampled_host(sd_cas_multi* m, const void* h_content,
   return result;
 }
 
+// ---- row packing of the per-process RCCL exchange (spacedrive_amd/shard.py) ----------
+
+int sd_cas_exchange_pack_dev(sd_cas_ctx* c, const uint64_t* d_keys, const uint32_t* d_pos,
+                             size_t n, uint64_t file0, uint32_t* d_rows, void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (n && (!d_keys || !d_pos || !d_rows)) return sd_fail(c, SD_CAS_EINVAL, "exchange_pack: null");
+  if (file0 + n > (1ull << 32)) return sd_fail(c, SD_CAS_EINVAL, "exchange_pack: idx past u32");
+  HIP_TRY(c, exch_pack(d_keys, d_pos, n, file0, d_rows, sd_pick(c, stream)));
+  return SD_CAS_OK;
+}
+
+int sd_cas_exchange_split_dev(sd_cas_ctx* c, const uint32_t* d_rows, size_t m, uint64_t* d_keys,
+                              uint32_t* d_vals, void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (m && (!d_rows || !d_keys || !d_vals)) return sd_fail(c, SD_CAS_EINVAL, "exchange_split: null");
+  HIP_TRY(c, exch_split(d_rows, m, d_keys, d_vals, sd_pick(c, stream)));
+  return SD_CAS_OK;
+}
+
+int sd_cas_exchange_unpack_dev(sd_cas_ctx* c, const uint32_t* d_back, const uint32_t* d_pos,
+                               size_t n, uint64_t* d_rep, void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (n && (!d_back || !d_pos || !d_rep)) return sd_fail(c, SD_CAS_EINVAL, "exchange_unpack: null");
+  HIP_TRY(c, exch_unpack(d_back, d_pos, n, d_rep, sd_pick(c, stream)));
+  return SD_CAS_OK;
+}
+
 }  // extern "C"

@@ -14,4 +14,12 @@ hipError_t multi_gather(const uint32_t* rep_pos, const uint64_t* ridx, uint64_t 
 hipError_t multi_scatter(const uint32_t* sidx, const uint64_t* back, uint64_t n, uint64_t* rep,
                          hipStream_t s);
 
+// the per-process RCCL exchange (spacedrive_amd/shard.py): 12-byte (key, u32 idx) rows
+hipError_t exch_pack(const uint64_t* keys, const uint32_t* pos, uint64_t n, uint64_t file0,
+                     uint32_t* rows, hipStream_t s);
+hipError_t exch_split(const uint32_t* rows, uint64_t m, uint64_t* keys, uint32_t* vals,
+                      hipStream_t s);
+hipError_t exch_unpack(const uint32_t* back, const uint32_t* pos, uint64_t n, uint64_t* rep,
+                       hipStream_t s);
+
 }  // namespace sdcas

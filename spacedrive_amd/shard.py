@@ -38,6 +38,15 @@ class ShardOps(Protocol):
     def group_min(self, keys: torch.Tensor, vals: torch.Tensor) -> tuple[torch.Tensor, int]:
         """out[i] = min{ vals[j] : keys[j] == keys[i] } (int32), distinct keys"""
 
+    def pack(self, keys: torch.Tensor, pos: torch.Tensor, file0: int) -> torch.Tensor:
+        """int32 rows [n, 3] = (key lo32, key hi32, u32(file0 + pos))"""
+
+    def split(self, rows: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+        """received rows -> (int64 keys, int32 u32-bit vals)"""
+
+    def unpack(self, back: torch.Tensor, pos: torch.Tensor) -> torch.Tensor:
+        """int64 rep with rep[pos[j]] = u32(back[j])"""
+
 
 class HipShardOps:
     """The production ops: libsd_hip_cas.so on the rank's GPU."""
@@ -58,6 +67,23 @@ class HipShardOps:
         out = torch.empty(keys.numel(), dtype=torch.int32, device=keys.device)
         objects = self.eng.group_min(keys, vals, out, stream=torch.cuda.current_stream().cuda_stream)
         return out, objects
+
+    def pack(self, keys, pos, file0):
+        rows = torch.empty((keys.numel(), 3), dtype=torch.int32, device=keys.device)
+        self.eng.exchange_pack(keys, pos, file0, rows, stream=torch.cuda.current_stream().cuda_stream)
+        return rows
+
+    def split(self, rows):
+        m = rows.shape[0]
+        keys = torch.empty(m, dtype=torch.int64, device=rows.device)
+        vals = torch.empty(m, dtype=torch.int32, device=rows.device)
+        self.eng.exchange_split(rows, keys, vals, stream=torch.cuda.current_stream().cuda_stream)
+        return keys, vals
+
+    def unpack(self, back, pos):
+        rep = torch.empty(back.numel(), dtype=torch.int64, device=back.device)
+        self.eng.exchange_unpack(back, pos, rep, stream=torch.cuda.current_stream().cuda_stream)
+        return rep
 
 
 @dataclass
@@ -81,24 +107,19 @@ def sharded_group(local_keys: torch.Tensor, file0: int, ops: ShardOps,
     dist.all_to_all_single(recv_counts, send_counts, group=group)  # 2: sizes
     sc = send_counts.cpu().tolist()
     rc = recv_counts.cpu().tolist()
-    # rows of 3 x int32: key (2 words, little-endian u64) and the u32 global idx (as int32 bits)
-    rows = torch.empty((n, 3), dtype=torch.int32, device=dev)
-    rows[:, :2] = pkeys.view(torch.int32).view(n, 2)
-    rows[:, 2] = (ppos.to(torch.int64) + file0).to(torch.int32)    # wraps to the u32's bits
+    rows = ops.pack(pkeys, ppos, file0)  # int32 [n, 3]: key lo, key hi, u32 global idx
     m = sum(rc)
     rrows = torch.empty((m, 3), dtype=torch.int32, device=dev)
     dist.all_to_all_single(rrows, rows, rc, sc, group=group)        # 2: (key, idx) rows
     if m:
-        rkeys = rrows[:, :2].contiguous().view(torch.int64).view(m)
-        ridx = rrows[:, 2].contiguous()
+        rkeys, ridx = ops.split(rrows)
         rep_min, objects = ops.group_min(rkeys, ridx)              # 3: u32 bits in int32
     else:
         rep_min = torch.empty(0, dtype=torch.int32, device=dev)
         objects = 0
     back = torch.empty(n, dtype=torch.int32, device=dev)
     dist.all_to_all_single(back, rep_min, sc, rc, group=group)      # 4
-    rep = torch.empty(n, dtype=torch.int64, device=dev)
-    rep[ppos.to(torch.int64)] = back.to(torch.int64) & 0xFFFFFFFF
+    rep = ops.unpack(back, ppos)
     tot = torch.tensor([objects], dtype=torch.int64, device=dev)
     dist.all_reduce(tot, group=group)
     return ShardResult(rep=rep, objects=int(tot.item()), sent=n - int(sc[rank]))

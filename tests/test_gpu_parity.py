@@ -521,6 +521,30 @@ def test_sampled_host_pipeline(eng, oracle):
             oracle.cas_keys_strided(host, SAMPLED_CONTENT_LEN, SAMPLED_CONTENT_LEN, sizes)).all()
 
 
+def test_exchange_rows_vs_numpy(eng):
+    """sd_cas_exchange_{pack,split,unpack}_dev: the 12-byte (key, u32 idx) rows of the RCCL
+    exchange, with file0 near the top of the u32 range."""
+    rng = np.random.default_rng(61)
+    n = 100_003
+    keys = rng.integers(0, 2 ** 64, n, dtype=np.uint64)
+    pos = rng.permutation(n).astype(np.int32)
+    file0 = (1 << 32) - n
+    rows = torch.empty((n, 3), dtype=torch.int32, device="cuda")
+    eng.exchange_pack(dev64(keys), torch.from_numpy(pos).cuda(), file0, rows)
+    r = rows.cpu().numpy().view(np.uint32)
+    assert (r[:, 0] == (keys & 0xFFFFFFFF)).all() and (r[:, 1] == (keys >> np.uint64(32))).all()
+    assert (r[:, 2] == pos.astype(np.uint64) + file0).all()
+    k2 = torch.empty(n, dtype=torch.int64, device="cuda")
+    v2 = torch.empty(n, dtype=torch.int32, device="cuda")
+    eng.exchange_split(rows, k2, v2)
+    assert (host64(k2) == keys).all() and (v2.cpu().numpy().view(np.uint32) == r[:, 2]).all()
+    rep = torch.empty(n, dtype=torch.int64, device="cuda")
+    eng.exchange_unpack(v2, torch.from_numpy(pos).cuda(), rep)
+    want = np.empty(n, dtype=np.int64)
+    want[pos] = r[:, 2]
+    assert (rep.cpu().numpy() == want).all()
+
+
 def test_sharded_group_rccl_world1(eng, oracle):
     """The multi-GPU grouping path (spacedrive_amd/shard.py) on the GPU with the nccl (= RCCL)
     backend: world size 1 here (one GPU per box); the world-2/4 exchange logic is covered

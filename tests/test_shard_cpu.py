@@ -44,6 +44,25 @@ class HostOps:
         np.minimum.at(mins, inv, v)
         return torch.from_numpy(mins[inv].view(np.int32).copy()), len(uniq)
 
+    # the row contracts of sd_cas_exchange_{pack,split,unpack}_dev
+    def pack(self, keys, pos, file0):
+        k = keys.numpy().view(np.uint64)
+        rows = np.empty((len(k), 3), dtype=np.uint32)
+        rows[:, 0] = k & 0xFFFFFFFF
+        rows[:, 1] = k >> np.uint64(32)
+        rows[:, 2] = (pos.numpy().astype(np.uint64) + np.uint64(file0)) & 0xFFFFFFFF
+        return torch.from_numpy(rows.view(np.int32))
+
+    def split(self, rows):
+        r = rows.numpy().view(np.uint32)
+        k = r[:, 0].astype(np.uint64) | (r[:, 1].astype(np.uint64) << np.uint64(32))
+        return torch.from_numpy(k.view(np.int64).copy()), torch.from_numpy(r[:, 2].view(np.int32).copy())
+
+    def unpack(self, back, pos):
+        rep = np.empty(len(back), dtype=np.int64)
+        rep[pos.numpy()] = back.numpy().view(np.uint32)
+        return torch.from_numpy(rep)
+
 
 def _free_port():
     s = socket.socket()
