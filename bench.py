@@ -9,9 +9,10 @@ before the timed region (data: synthetic) and are resident in HBM when it starts
 Weak scaling: FILES_PER_GPU (default 1,310,720 = 20 x 65,536, the MI355X file-per-lane
 quantum; 75.2 GB/GPU) per rank per step, so one step at 8 GPUs is the 10M-file headline
 job (10.49 M files).  Steps are pipelined the way a production job
-would run them: step i's grouping (incl. its RCCL exchange) runs on a side stream while
-step i+1 is hashed; every step's hash AND grouping complete inside the timed region
-(--no-overlap serialises them).
+would run them: step i's grouping (incl. its RCCL exchange, issued from a worker thread
+so its host syncs never delay the next K1) runs on a side stream while steps i+1 and i+2
+are hashed (keys triple-buffered); every step's hash AND grouping complete inside the
+timed region (--no-overlap serialises them).
 
 Output: ONE JSON line on rank 0 (driver contract), with
   roofline      — K1 (sd_cas_sampled_kernel), timed by HIP events on its own stream:
