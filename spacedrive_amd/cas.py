@@ -290,6 +290,13 @@ class CasEngine:
                                                   ctypes.byref(out), _stream(stream)), "synth_small")
         return int(out.value)
 
+    def synth_small_content(self, seed: int, file0: int, n: int, offs, lens, arena,
+                            dup_permille: int = 0, stream: Optional[int] = None) -> None:
+        """Whole-file content at caller-chosen (16-B aligned) offsets."""
+        self._check(self.L.sd_cas_synth_small_content_dev(self.h, seed, file0, n, dup_permille,
+                                                          _ptr(offs), _ptr(lens), _ptr(arena),
+                                                          _stream(stream)), "synth_small_content")
+
     def synth_roots(self, seed: int, file0: int, n: int, roots, dup_permille: int = 0,
                     stream: Optional[int] = None) -> None:
         self._check(self.L.sd_cas_synth_roots_dev(self.h, seed, file0, n, dup_permille,

@@ -121,6 +121,8 @@ inline int sd_fail(sd_cas_ctx* c, int code, const char* fmt, ...) {
 // default stream (torch's default) must be ordered with our kernels.
 inline hipStream_t sd_pick(sd_cas_ctx*, void* s) { return (hipStream_t)s; }
 inline size_t up16(size_t x) { return (x + 15) & ~(size_t)15; }
+// packed whole-file contents start on 128-B lines: a K2 lane's line pair is one cache line
+inline size_t up128(size_t x) { return (x + 127) & ~(size_t)127; }
 inline size_t up256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // Grow a device buffer (on the CURRENT device).  Growing synchronises the device: call

@@ -328,7 +328,7 @@ int sd_cas_group_chunked_dev(sd_cas_ctx* c, const uint32_t* d_rep, size_t n, uin
 // ---- host-buffer cas (blocking) -----------------------------------------------------
 
 // Stage layout in pinned memory and on the device:
-//   [sampled contents, 57,344 B each, contiguous] [packed contents, 16-B aligned]
+//   [sampled contents, 57,344 B each, contiguous] [packed contents, 128-B aligned]
 //   [sizes_s u64][sizes_p u64][offs_p u64][lens_p u32]   (small metadata)
 struct Plan {
   std::vector<size_t> sampled, packed;  // file indices
@@ -351,7 +351,7 @@ static int plan_batch(sd_cas_ctx* c, const uint64_t* buf_lens, const uint64_t* s
                     (unsigned long long)buf_lens[i], MAX_PACKED_CONTENT_LEN);
       pl.packed.push_back(i);
       pl.poff.push_back(pl.packed_bytes);
-      pl.packed_bytes += up16(buf_lens[i]);
+      pl.packed_bytes += up128(buf_lens[i]);
     }
   }
   pl.sampled_bytes = pl.sampled.size() * (size_t)SAMPLED_CONTENT_LEN;
@@ -808,19 +808,31 @@ int sd_cas_synth_small_dev(sd_cas_ctx* c, uint64_t seed, uint64_t file0, size_t 
   hipStream_t s = pick(c, stream);
   if (n == 0) { if (out_arena_bytes) *out_arena_bytes = 16; return SD_CAS_OK; }
   HIP_TRY(c, synth_small_sizes(seed, file0, n, dup_permille, d_sizes, d_lens, s));
-  // offsets: 16-B aligned packing, computed on the host from the lens (small: 4 B/file)
+  // offsets: 128-B aligned packing (see up128), computed on the host from the lens
   std::vector<uint32_t> lens(n);
   HIP_TRY(c, hipMemcpyAsync(lens.data(), d_lens, n * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
   std::vector<uint64_t> offs(n);
   uint64_t o = 0;
-  for (size_t i = 0; i < n; i++) { offs[i] = o; o += up16(lens[i]); }
+  for (size_t i = 0; i < n; i++) { offs[i] = o; o += up128(lens[i]); }
   o += 16;
   if (out_arena_bytes) *out_arena_bytes = o;
   HIP_TRY(c, hipMemcpyAsync(d_offs, offs.data(), n * 8, hipMemcpyHostToDevice, s));
   if (d_arena) HIP_TRY(c, synth_small_content(seed, file0, n, dup_permille, d_offs, d_lens,
                                               (uint8_t*)d_arena, s));
   HIP_TRY(c, hipStreamSynchronize(s));
+  return SD_CAS_OK;
+}
+
+int sd_cas_synth_small_content_dev(sd_cas_ctx* c, uint64_t seed, uint64_t file0, size_t n,
+                                   uint32_t dup_permille, const uint64_t* d_offs,
+                                   const uint32_t* d_lens, void* d_arena, void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (!d_offs || !d_lens || !d_arena || dup_permille > 1000 || ((uintptr_t)d_arena & 15))
+    return fail(c, SD_CAS_EINVAL, "synth_small_content: bad arguments");
+  if (n == 0) return SD_CAS_OK;
+  HIP_TRY(c, synth_small_content(seed, file0, n, dup_permille, d_offs, d_lens,
+                                 (uint8_t*)d_arena, pick(c, stream)));
   return SD_CAS_OK;
 }
 

@@ -52,3 +52,20 @@ eng.synth_small(11, 0, m, sz, ln, of, arena)
 k = torch.empty(m, dtype=torch.int64, device="cuda")
 print(f"ragged 1M: K2 (windowed length sort) {timed(lambda: eng.hash_packed(arena, of, ln, sz, k)):.2f} ms",
       flush=True)
+
+# (c) packing-alignment A/B: the same 1M files with every content at a 16-B aligned offset
+# (the packing before this round's change) — a K2 line pair then straddles two 128-B
+# cache lines; synth_small itself packs at 128 B
+ref = k.clone()
+al = ((ln.to(torch.int64) + 15) // 16) * 16
+of16 = torch.cumsum(al, 0) - al
+nb16 = int(al.sum().item()) + 128
+del arena
+torch.cuda.empty_cache()
+arena16 = torch.empty(nb16, dtype=torch.uint8, device="cuda")
+eng.synth_small_content(11, 0, m, of16, ln, arena16)
+eng.hash_packed(arena16, of16, ln, sz, k)
+torch.cuda.synchronize()
+assert torch.equal(k, ref), "16-B packed layout changed the cas keys"
+print(f"ragged 1M, 16-B packed offsets: K2 {timed(lambda: eng.hash_packed(arena16, of16, ln, sz, k)):.2f} ms",
+      flush=True)
