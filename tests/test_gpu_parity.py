@@ -78,7 +78,7 @@ def packed_arena(contents):
     for c in contents:
         offs.append(o)
         o += (len(c) + 15) // 16 * 16
-    arena = np.zeros(o + 64, dtype=np.uint8)
+    arena = np.zeros(o + 128, dtype=np.uint8)  # readable to every content's 128-B round-up
     for c, off in zip(contents, offs):
         arena[off:off + len(c)] = np.frombuffer(c, np.uint8)
     return arena, np.array(offs, dtype=np.uint64)
