@@ -612,3 +612,37 @@ def test_multi_device_hash_group_host(eng, oracle):
     assert (keys == want).all()
     assert objects == oobj and (rep == orep.astype(np.uint64)).all()
     me.close()
+
+
+@pytest.mark.gpu
+def test_packed_layout_alignment_invariance(path_eng, oracle):
+    """synth_small packs whole-file contents at 128-B lines (K2's line pair = one cache
+    line); the same files at 16-B packed offsets (the ABI's minimum,
+    written by sd_cas_synth_small_content_dev) give identical cas keys, equal to the
+    oracle's, and so do the K1L shapes below the latency threshold."""
+    eng = path_eng
+    n = 20_000
+    sz = torch.empty(n, dtype=torch.int64, device="cuda")
+    ln = torch.empty(n, dtype=torch.int32, device="cuda")
+    of = torch.empty(n, dtype=torch.int64, device="cuda")
+    nb = eng.synth_small(91, 0, n, sz, ln, of, None)
+    arena = torch.empty(nb + 64, dtype=torch.uint8, device="cuda")
+    eng.synth_small(91, 0, n, sz, ln, of, arena)
+    assert bool((of % 128 == 0).all())
+    keys = torch.empty(n, dtype=torch.int64, device="cuda")
+    eng.hash_packed(arena, of, ln, sz, keys)
+    lens = ln.cpu().numpy().astype(np.uint32)
+    want = oracle.fast_cas_keys(arena.cpu().numpy(), of.cpu().numpy().astype(np.uint64), lens,
+                                host64(sz), 8)
+    assert (host64(keys) == want).all()
+    al = (ln.to(torch.int64) + 15) // 16 * 16
+    of16 = torch.cumsum(al, 0) - al
+    arena16 = torch.empty(int(al.sum().item()) + 64, dtype=torch.uint8, device="cuda")
+    eng.synth_small_content(91, 0, n, of16, ln, arena16)
+    keys16 = torch.empty(n, dtype=torch.int64, device="cuda")
+    eng.hash_packed(arena16, of16, ln, sz, keys16)
+    assert (host64(keys16) == want).all()
+    for m in (100, 5_000):  # K1L one wave per file / four files per wave
+        k = torch.empty(m, dtype=torch.int64, device="cuda")
+        eng.hash_packed(arena16, of16[:m].contiguous(), ln[:m].contiguous(), sz[:m].contiguous(), k)
+        assert (host64(k) == want[:m]).all()
