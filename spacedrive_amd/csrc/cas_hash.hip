@@ -90,9 +90,9 @@ __device__ __forceinline__ void compress_pair(uint32_t (&cv)[8], const uint4 (&A
 // The 5-deep chaining-value stack lives in LDS, word-major [depth][word][thread] so every
 // push/pop is a conflict-free dword access.  It is touched once per 1 KiB chunk (16
 // compressions), and moving its 40 words per lane out of VGPRs takes the kernel from 3
-// to 4 waves per SIMD (VGPR budget <= 128); 40 KiB per 256-lane block = 4 blocks/CU.
+// to 4 waves per SIMD (VGPR budget <= 128); 80 KiB per 512-lane block = 2 blocks/CU.
 constexpr int SAMPLED_DEPTH = 5;  // popcount(55) pending subtrees at most
-constexpr int SAMPLED_BLOCK = 256;
+constexpr int SAMPLED_BLOCK = 512;  // 256: 1-2 % slower, 128: 4 % (profiles/r01_k1_block_ab.log)
 
 struct LdsStack {
   uint32_t (*s)[8][SAMPLED_BLOCK];
@@ -486,8 +486,8 @@ int length_key_bits(uint64_t) { return (int)(LEN_BITS - BUCKET_SHIFT); }
 hipError_t hash_sampled(const uint8_t* content, uint64_t stride, const uint64_t* sizes,
                         uint64_t n, uint64_t* keys, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const uint64_t blocks = (n + 255) / 256;
-  sd_cas_sampled_kernel<<<(uint32_t)blocks, 256, 0, s>>>(content, stride, sizes, n, keys);
+  const uint64_t blocks = (n + SAMPLED_BLOCK - 1) / SAMPLED_BLOCK;
+  sd_cas_sampled_kernel<<<(uint32_t)blocks, SAMPLED_BLOCK, 0, s>>>(content, stride, sizes, n, keys);
   return hipGetLastError();
 }
 
