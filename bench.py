@@ -15,10 +15,18 @@ are hashed (keys triple-buffered); every step's hash AND grouping complete insid
 timed region (--no-overlap serialises them).
 
 Output: ONE JSON line on rank 0 (driver contract), with
-  roofline      — K1 (sd_cas_sampled_kernel), timed by HIP events on its own stream:
-                  VALU issue slots / kernel time vs the full-rate issue peak (the binding
-                  roof: BLAKE3's rotates and 3-input adds are half rate on gfx950), with the
-                  HBM byte view (vs 8 TB/s) and PMC traffic alongside;
+  roofline      — K1 (sd_cas_sampled_kernel), timed by HIP events on its own stream, priced
+                  as SURVEY.md §8(d) prices it: 953 compressions x 792 spec int32 ops per
+                  file / kernel time vs the guide's int32 VALU peak (256 CUs x 4 SIMDs x 32
+                  lanes x 2.4 GHz = 78.6 T lane-ops/s); secondary views: issue slots (rotates
+                  and 3-input adds issue at half rate on gfx950, measured), the measured
+                  compute-only ceiling of this instruction stream, the HBM byte view (vs
+                  8 TB/s) and PMC traffic;
+  sustained     — the same steps back to back for ~--sustain-seconds after the timed region
+                  (the DVFS-settled rate, long enough for an outside utilisation sampler);
+  e2e           — BASELINE config 3 as worded: sampled files streamed from pinned host
+                  memory (a pinned ring reused cyclically, every file copied H2D over PCIe)
+                  through K1, PCIe-inclusive; never `value` (rank 0, N=1);
   cpu_baseline  — the oracle's AVX-512 16-lane CPU path (oracle/cas_fast.c) on a bounded
                   sample of the SAME files on the host cores (rank 0, N=1 only); the sample's
                   keys are also checked against the GPU's.
@@ -50,6 +58,10 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 def group_bytes_per_key(n: int) -> int:
     return 44 if n <= 256 * 5632 else 68
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # 256 CUs x 4 SIMD32 x 32 lanes x 2.4 GHz = 78.6
+# measured ceiling of K1's own instruction stream (compute-only loop at 2.38 GHz, no loads):
+# profiles/r01_ubench_k1_clock.log
+K1_CEILING_FILES_S = 61.94e6
+PCIE_PEAK_GBS = 64.0         # PCIe Gen5 x16 per direction
 # full-rate wave64 VALU issue: 1024 SIMDs x 2.4 GHz / 2 cycles = 1228.8 G slots/s
 SLOT_PEAK_G = 1024 * 2.4e9 / 2 / 1e9
 
@@ -63,7 +75,13 @@ def main() -> None:
                     help="20 x 65,536 (the MI355X file-per-lane quantum): 10.49 M files per step at 8 GPUs")
     ap.add_argument("--dup-permille", type=int, default=300)
     ap.add_argument("--seed", type=int, default=0x5DCA50004)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=6.0)
+    ap.add_argument("--sustain-seconds", type=float, default=10.0,
+                    help="back-to-back steps after the timed region (0 = skip)")
+    ap.add_argument("--e2e-files", type=int, default=10_485_760,
+                    help="files streamed from pinned host memory for the e2e sub-object (0 = skip)")
+    ap.add_argument("--e2e-ring", type=int, default=131_072,
+                    help="pinned host ring (files) the e2e stream cycles through")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", dest="overlap", action="store_false",
                     help="group step i before hashing step i+1 (default: overlap them)")
@@ -182,7 +200,7 @@ def main() -> None:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    keys = keys[(args.steps - 1) % NBUF]
+    last_keys = keys[(args.steps - 1) % NBUF]
     res = results[-1] if results else None
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
@@ -195,7 +213,7 @@ def main() -> None:
 
     # objects (for the record) — outside the timed region
     if not sharded:
-        objects = eng.group(keys, rep)
+        objects = eng.group(last_keys, rep)
     else:
         objects = res.objects
     # the grouping alone (after the timed region: inside the steps it overlaps the next K1
@@ -206,11 +224,34 @@ def main() -> None:
         for _ in range(5):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(main)
-            eng.group(keys, rep, want_objects=False)
+            eng.group(last_keys, rep, want_objects=False)
             b.record(main)
             b.synchronize()
             gts.append(a.elapsed_time(b))
         group_ms = float(np.median(gts))
+
+    # sustained: the same pipelined steps back to back (DVFS-settled; long enough for an
+    # outside utilisation sampler to see the GPU busy), after the headline timed region
+    sustained = None
+    if args.sustain_seconds > 0:
+        n_sus = max(1, int(args.sustain_seconds / (dt / args.steps)))
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(n_sus, False)
+        torch.cuda.synchronize()
+        ts = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        if sharded:
+            dist.all_reduce(ts, op=dist.ReduceOp.MAX)
+        sus_dt = float(ts.item())
+        sustained = {"steps": n_sus, "seconds": sus_dt, "value": world * F * n_sus / sus_dt,
+                     "unit": "cas_ids/s", "ms_per_step": sus_dt / n_sus * 1e3}
+
+    e2e = None
+    if args.e2e_files > 0:
+        e2e = e2e_leg(eng, content, sizes, last_keys, args, world, rank, dev,
+                      dist if sharded else None)
 
     files_total = world * F * args.steps
     value = files_total / dt
@@ -232,7 +273,7 @@ def main() -> None:
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(content, sizes, keys, args.cpu_seconds)
+        cpu = cpu_baseline(content, sizes, last_keys, args.cpu_seconds)
 
     if rank == 0:
         line = {
@@ -261,22 +302,32 @@ def main() -> None:
                 "objects": objects,
             },
             "roofline": {
-                # K1 is bound by VALU issue, not HBM: BLAKE3's rotates (v_alignbit_b32) and
-                # 3-input adds (v_add3_u32) issue at half rate on gfx950 (measured), so the
-                # roof is full-rate wave64 issue slots; the HBM view is in "hbm".
+                # achieved = files x 953 compressions x 792 spec int32 ops /
+                # K1 time, vs the guide's int32 VALU peak (78.6 T lane-ops/s).  BLAKE3 is
+                # integer ARX with no contraction (no MFMA path) and K1 moves ~0.4 of HBM
+                # peak, so VALU is the binding roof.
                 "kernel": "sd_cas_sampled_kernel",
                 "bound": "valu",
                 "bound_note": ("BLAKE3 is 32-bit integer ARX with no contraction: no MFMA path, and "
                                "HBM runs at ~0.4 of peak (see 'hbm'); the binding roof is VALU "
-                               "issue (DESIGN.md 2.1, profiles/r01_ubench_*)"),
-                "achieved": slots,
-                "peak": SLOT_PEAK_G,
-                "unit": "G wave-issue-slots/s",
-                "frac": slots / SLOT_PEAK_G,
+                               "(DESIGN.md 2.1, profiles/r01_ubench_*)"),
+                "achieved": valu,
+                "peak": VALU_PEAK_TOPS,
+                "unit": "T int32 ops/s",
+                "frac": valu / VALU_PEAK_TOPS,
                 "traffic": traffic,
                 "kernel_ms": kern_ms,
                 "work_per_file": {"message_bytes": MSG_BYTES, "compressions": COMPRESSIONS,
+                                  "spec_ops_per_compression": SPEC_OPS,
                                   "issue_slots_per_wave_compression": SLOTS},
+                # secondary views of the same kernel time
+                "issue_slots": {"achieved": slots, "peak": SLOT_PEAK_G, "unit": "G wave-issue-slots/s",
+                                "frac": slots / SLOT_PEAK_G,
+                                "note": "v_alignbit_b32 / v_add3_u32 issue at half rate on gfx950 "
+                                        "(profiles/r01_ubench_valu_v2.log): 1,014 slots per compression"},
+                "measured_ceiling": {"files_per_s": K1_CEILING_FILES_S,
+                                     "frac": F / (kern_ms / 1e3) / K1_CEILING_FILES_S,
+                                     "source": "compute-only K1 loop at 2.38 GHz, profiles/r01_ubench_k1_clock.log"},
                 "hbm": {"achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS,
                         "algorithmic_bytes_per_launch": F * MSG_BYTES,
@@ -284,6 +335,8 @@ def main() -> None:
                 "int_ops": {"achieved_spec_tops": valu, "achieved_hw_instr_tops": valu_hw,
                             "peak_full_rate_tops": VALU_PEAK_TOPS},
             },
+            "sustained": sustained,
+            "e2e": e2e,
             "group": None if group_ms is None else {
                 # Object grouping of one step's keys alone (K4h partition + K5h LDS hash
                 # min), HIP events around it on the stream it runs on, after the timed region
@@ -299,6 +352,48 @@ def main() -> None:
         worker.shutdown()
     if sharded:
         dist.destroy_process_group()
+
+
+def e2e_leg(eng, content, sizes, keys, args, world, rank, dev, dist):
+    """BASELINE config 3 as worded (PCIe-inclusive): the job's 10.49M sampled files (split
+    over the ranks) streamed from pinned host memory through sd_cas_hash_sampled_host_ring —
+    H2D of batch k+1 on the side stream overlapping K1 on batch k.  The host ring holds the
+    first `ring` files of the resident batch (copied down once, untimed) and is reused
+    cyclically: every file's 57,344 B cross PCIe.  Parity: each ring pass equals the
+    resident K1 keys of the same files."""
+    import numpy as np
+    import torch
+    F = content.shape[0]
+    n = max(1, args.e2e_files // world)
+    ring = min(args.e2e_ring, F, n)
+    pinned = torch.empty((ring, 57344), dtype=torch.uint8, pin_memory=True)
+    pinned.copy_(content[:ring])
+    hs = sizes[:ring].cpu().numpy().view(np.uint64)
+    hsz = np.resize(hs, n)
+    want = keys[:ring].cpu().numpy().view(np.uint64)
+    eng.hash_sampled_host_ring(pinned.data_ptr(), ring, hsz[:65536])  # warm: staging buffers
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    got = eng.hash_sampled_host_ring(pinned.data_ptr(), ring, hsz)
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    parity = bool((got[:ring] == want).all() and (got == np.resize(want, n)).all())
+    ok = torch.tensor([1 if parity else 0], dtype=torch.int64, device=dev)
+    if dist is not None:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    del pinned
+    total = n * world
+    h2d = total * 57344 / dt / 1e9
+    return {"files": total, "files_per_gpu": n, "seconds": dt, "value": total / dt,
+            "unit": "cas_ids/s", "hashed_gb_per_s": total * MSG_BYTES / dt / 1e9,
+            "h2d_gb_per_s": h2d, "pcie_peak_gb_per_s_per_gpu": PCIE_PEAK_GBS,
+            "pcie_frac": h2d / world / PCIE_PEAK_GBS, "ring_files": ring,
+            "parity_vs_resident_k1": bool(ok.item()),
+            "note": "PCIe-inclusive: pinned host ring -> HBM (side stream) overlapped with K1; "
+                    "strong scaling of the 10.49M-file job over the ranks"}
 
 
 def cpu_baseline(content, sizes, keys, seconds: float):
@@ -324,10 +419,10 @@ def cpu_baseline(content, sizes, keys, seconds: float):
     dt = time.perf_counter() - t0
     files = reps * m
     # reference-faithful mode: one hashing thread, as one job's join_all
-    m1 = min(m, 4096)
+    m1 = min(m, 2048)
     t0 = time.perf_counter()
     r1 = 0
-    while time.perf_counter() - t0 < 2.0:
+    while time.perf_counter() - t0 < 1.0:
         orc.fast_cas_keys_strided(host[:m1].reshape(-1), 57344, 57344, hs[:m1], 1)
         r1 += 1
     one_thread = r1 * m1 / (time.perf_counter() - t0)

@@ -87,6 +87,17 @@ void sd_cas_set_latency_threshold(sd_cas_ctx* ctx, size_t sampled_files, size_t 
  * 3/32 of the batch quantum; whole files are then visited by chunk count, one stable radix
  * pass, so the four files of a wave share a chunks-per-lane class). */
 void sd_cas_set_chunkpar_split(sd_cas_ctx* ctx, size_t sampled_files, size_t packed_files);
+/* Object grouping method (sd_cas_group_dev / sd_cas_group_min_dev): AUTO = the bucket
+ * partition + LDS hash tables (K4h/K5h) up to SD_CAS_HASH_GROUP_MAX_KEYS keys per call and
+ * the LSD radix sort + runs (K4/K5) above; HASH / SORT force one (HASH fails beyond the
+ * limit).  bucket_target = mean keys per hash bucket (0 = the tuned 1,536; >= 16): smaller
+ * targets partition deeper — the plans of > 200M keys at small n, for tests.  Results
+ * are identical for every setting. */
+#define SD_CAS_GROUP_AUTO 0
+#define SD_CAS_GROUP_HASH 1
+#define SD_CAS_GROUP_SORT 2
+#define SD_CAS_HASH_GROUP_MAX_KEYS (1310720000ull) /* 2^19 buckets x 2,500 keys */
+int sd_cas_set_group_method(sd_cas_ctx* ctx, int method, uint64_t bucket_target);
 /* page-locked host staging for the gather (replaces the per-file Box<[u8]> of cas.rs:32) */
 int sd_cas_alloc_pinned(sd_cas_ctx* ctx, size_t bytes, void** out);
 int sd_cas_free_pinned(sd_cas_ctx* ctx, void* p);
@@ -120,6 +131,14 @@ int sd_cas_hash_sampled_host(sd_cas_ctx* ctx, const void* h_content, uint64_t st
                              const uint64_t* h_sizes, size_t n, uint64_t* h_keys,
                              size_t batch_files);
 
+/* Same over a host ring of ring_files contents reused cyclically: file i's 57,344 B are at
+ * h_ring + (i % ring_files) * stride; h_sizes / h_keys hold all n files.  Every file is
+ * copied host -> device (the E2E run of BASELINE config 3 over more files than fit in
+ * pinned memory).  Blocking. */
+int sd_cas_hash_sampled_host_ring(sd_cas_ctx* ctx, const void* h_ring, uint64_t stride,
+                                  size_t ring_files, const uint64_t* h_sizes, size_t n,
+                                  uint64_t* h_keys, size_t batch_files);
+
 /* 16 lowercase hex chars + NUL: the cas_id String of cas.rs:61 */
 void sd_cas_key_to_hex(uint64_t key, char out[17]);
 
@@ -148,7 +167,8 @@ int sd_cas_group_dev(sd_cas_ctx* ctx, const uint64_t* d_keys, size_t n, uint32_t
                      uint64_t* out_objects, void* stream);
 /* Generalised grouping (the receive side of the multi-GPU exchange):
  * d_out[i] = min{ vals[j] : key[j] == key[i] } (vals NULL = identity, i.e. sd_cas_group_dev);
- * *out_objects = distinct keys (blocks when non-NULL).  n <= ~41M per call. */
+ * *out_objects = distinct keys (blocks when non-NULL).  n < 2^32 (above
+ * SD_CAS_HASH_GROUP_MAX_KEYS: two stable LSD sorts, by value then by key). */
 int sd_cas_group_min_dev(sd_cas_ctx* ctx, const uint64_t* d_keys, const uint32_t* d_vals, size_t n,
                          uint32_t* d_out, uint64_t* out_objects, void* stream);
 /* Key-range partition for the exchange: part(k) = floor(k * parts / 2^64) (BLAKE3 keys are

@@ -25,7 +25,9 @@
  *   loop { read 10240 at file cursor; if current_pos >= 8192 + 3*seek_jump break;
  *          current_pos = seek(current_pos + seek_jump) }
  *   seek(End(-8192)); read 8192
- * The first sample read continues from the cursor after the header (offset 8192). */
+ * The first sample read continues from the cursor after the header (offset 8192).
+ * The footer entry is `size - 8192`, i.e. for a file whose actual length IS `size` (an
+ * in-memory image); orc_gather_path reads the footer from the actual end. */
 void orc_sample_plan(uint64_t size, uint64_t offs[6], uint64_t lens[6]) {
   const uint64_t H = ORC_HEADER_OR_FOOTER_SIZE, S = ORC_SAMPLE_SIZE;
   int k = 0;
@@ -89,11 +91,22 @@ int64_t orc_gather_path(const char* path, uint64_t size, uint8_t* out, size_t ou
     uint64_t offs[6], lens[6];
     orc_sample_plan(size, offs, lens);
     size_t w = 0;
-    for (int i = 0; i < 6; i++) {
+    /* header + 4 samples at the offsets derived from `size` (cas.rs:35-51) */
+    for (int i = 0; i < 5; i++) {
       int e = pread_exact(fd, out + w, lens[i], offs[i]);
       if (e) { ret = e; goto done; }
       w += lens[i];
     }
+    /* footer: seek(SeekFrom::End(-8192)) (cas.rs:54-55) is relative to the file's ACTUAL
+     * end, not to `size`: a file that grew or shrank since fs::metadata is footer-sampled
+     * at its current length.  lseek to a negative position is EINVAL. */
+    struct stat st;
+    if (fstat(fd, &st) != 0) { ret = -errno; goto done; }
+    if ((uint64_t)st.st_size < ORC_HEADER_OR_FOOTER_SIZE) { ret = -EINVAL; goto done; }
+    int e = pread_exact(fd, out + w, ORC_HEADER_OR_FOOTER_SIZE,
+                        (uint64_t)st.st_size - ORC_HEADER_OR_FOOTER_SIZE);
+    if (e) { ret = e; goto done; }
+    w += ORC_HEADER_OR_FOOTER_SIZE;
     ret = (int64_t)w;
   }
 done:

@@ -120,7 +120,9 @@ def py_derive_key(context: str, material: bytes) -> bytes:
 
 
 def py_sample_plan(size: int):
-    """cas.rs:35-58 simulated literally: [(offset, length)] x 6."""
+    """cas.rs:35-58 simulated literally: [(offset, length)] x 6, for a file whose actual
+    length is `size` (the footer is SeekFrom::End(-8192), i.e. relative to the actual end;
+    py_generate_cas_id_file covers files whose length differs from their metadata)."""
     H, S = HEADER_OR_FOOTER_SIZE, SAMPLE_SIZE
     plan = [(0, H)]
     cursor = H
@@ -135,6 +137,48 @@ def py_sample_plan(size: int):
         cursor = current_pos
     plan.append((size - H, H))
     return plan
+
+
+class UnexpectedEof(OSError):
+    """tokio read_exact's io::ErrorKind::UnexpectedEof (mapped to EIO by the C ABI)."""
+
+
+def py_generate_cas_id_file(path: str, size: int) -> str:
+    """cas.rs:23-62 executed literally on a real file with the same sequence of reads and
+    seeks (read_exact = read until full or EOF; seek(Start), seek(End(-8192))).  Unlike
+    py_sample_plan this follows the file's ACTUAL length for the footer, as the reference
+    does when the file changed after fs::metadata."""
+    H, S = HEADER_OR_FOOTER_SIZE, SAMPLE_SIZE
+    parts = [int(size).to_bytes(8, "little")]
+    if size <= MINIMUM_FILE_SIZE:
+        with open(path, "rb") as fh:  # fs::read: the whole file as it is now
+            parts.append(fh.read())
+        return py_blake3(b"".join(parts)).hex()[:16]
+
+    def read_exact(fh, n):
+        b = b""
+        while len(b) < n:
+            x = fh.read(n - len(b))
+            if not x:
+                raise UnexpectedEof(5, "failed to fill whole buffer")
+            b += x
+        return b
+
+    with open(path, "rb") as fh:
+        parts.append(read_exact(fh, H))
+        current_pos = H
+        seek_jump = (size - H * 2) // SAMPLE_COUNT
+        while True:
+            parts.append(read_exact(fh, S))
+            if current_pos >= H + seek_jump * (SAMPLE_COUNT - 1):
+                break
+            current_pos = fh.seek(current_pos + seek_jump, os.SEEK_SET)
+        end = os.fstat(fh.fileno()).st_size
+        if end < H:
+            raise OSError(22, "invalid seek to a negative or overflowing position")
+        fh.seek(-H, os.SEEK_END)
+        parts.append(read_exact(fh, H))
+    return py_blake3(b"".join(parts)).hex()[:16]
 
 
 def py_cas_message(content: bytes, size: int) -> bytes:

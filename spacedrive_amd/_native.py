@@ -31,11 +31,13 @@ SIGNATURES = [
     ("sd_cas_batch_quantum", _sz, [_vp]),
     ("sd_cas_set_latency_threshold", None, [_vp, _sz, _sz]),
     ("sd_cas_set_chunkpar_split", None, [_vp, _sz, _sz]),
+    ("sd_cas_set_group_method", _i, [_vp, _i, _u64]),
     ("sd_cas_alloc_pinned", _i, [_vp, _sz, ctypes.POINTER(_vp)]),
     ("sd_cas_free_pinned", _i, [_vp, _vp]),
     ("sd_cas_generate_cas_ids", _i, [_vp, _vp, _vp, _vp, _sz, _vp]),
     ("sd_cas_generate_cas_ids_from_paths", _i, [_vp, _vp, _vp, _sz, _vp, _vp]),
     ("sd_cas_hash_sampled_host", _i, [_vp, _vp, _u64, _vp, _sz, _vp, _sz]),
+    ("sd_cas_hash_sampled_host_ring", _i, [_vp, _vp, _u64, _sz, _vp, _sz, _vp, _sz]),
     ("sd_cas_key_to_hex", None, [_u64, _cp]),
     ("sd_cas_hash_sampled_dev", _i, [_vp, _vp, _u64, _vp, _sz, _vp, _vp]),
     ("sd_cas_hash_packed_dev", _i, [_vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp]),

@@ -126,6 +126,14 @@ class CasEngine:
         self.L.sd_cas_set_chunkpar_split(self.h, d if sampled is None else int(sampled),
                                          d if packed is None else int(packed))
 
+    GROUP_AUTO, GROUP_HASH, GROUP_SORT = 0, 1, 2
+
+    def set_group_method(self, method: int = 0, bucket_target: int = 0) -> None:
+        """Grouping method (GROUP_AUTO / GROUP_HASH / GROUP_SORT) and the hash grouping's
+        mean keys per bucket (0 = tuned default); identical results for every setting."""
+        self._check(self.L.sd_cas_set_group_method(self.h, int(method), int(bucket_target)),
+                    "set_group_method")
+
     # ---- host batches (blocking) -------------------------------------------------------
     def generate_cas_keys(self, items: Sequence[tuple[bytes, int]]) -> np.ndarray:
         """Batched ``generate_cas_id`` over already-gathered content: items = (buf, size)."""
@@ -179,6 +187,19 @@ class CasEngine:
         self._check(self.L.sd_cas_hash_sampled_host(self.h, int(content.ctypes.data), int(stride),
                                                     _np_ptr(sz), n, _np_ptr(keys), int(batch_files)),
                     "hash_sampled_host")
+        return keys
+
+    def hash_sampled_host_ring(self, ring_ptr: int, ring_files: int, sizes: np.ndarray,
+                               stride: int = SAMPLED_CONTENT_LEN, batch_files: int = 0) -> np.ndarray:
+        """End-to-end K1 over len(sizes) files whose contents cycle through a host ring of
+        ring_files x stride bytes at ring_ptr (every file is copied host -> device)."""
+        n = len(sizes)
+        sz = np.ascontiguousarray(sizes, dtype=np.uint64)
+        keys = np.zeros(n, dtype=np.uint64)
+        self._check(self.L.sd_cas_hash_sampled_host_ring(self.h, int(ring_ptr), int(stride),
+                                                         int(ring_files), _np_ptr(sz), n,
+                                                         _np_ptr(keys), int(batch_files)),
+                    "hash_sampled_host_ring")
         return keys
 
     def file_checksum(self, path: str) -> str:

@@ -85,6 +85,19 @@ struct sd_cas_ctx {
   void* pinned = nullptr;
   size_t pinned_bytes = 0;
   uint64_t* d_scalar = nullptr;  // 8 x u64 scratch for counters
+  // ws and d_scalar are shared by every device call of the context, whatever stream the
+  // caller passes: the last enqueued use is recorded here and a use on another stream
+  // waits for it first (sd_ws_acquire / sd_ws_release)
+  hipEvent_t ws_ev = nullptr;
+  hipStream_t ws_stream = nullptr;
+  bool ws_pending = false;
+  size_t quantum = 65536;  // files per full wave of the device (CUs x 4 SIMDs x 64 lanes)
+  int group_method = 0;       // SD_CAS_GROUP_* (sd_cas_set_group_method)
+  uint64_t group_target = 0;  // mean keys per hash-grouping bucket (0 = tuned default)
+  bool use_hash_group(uint64_t n) const {
+    return group_method == SD_CAS_GROUP_HASH ||
+           (group_method == SD_CAS_GROUP_AUTO && n <= SD_CAS_HASH_GROUP_MAX_KEYS);
+  }
   // batches below these sizes use the chunk-parallel K1L kernel (sd_cas_set_latency_threshold)
   size_t latency_sampled = 0, latency_packed = 0;
   // K1L batches of at least this many files pack 4 files per wave (16-lane segments),
@@ -120,6 +133,19 @@ inline int sd_fail(sd_cas_ctx* c, int code, const char* fmt, ...) {
 // NULL = the HIP null (default) stream, exactly as in HIP itself: a caller on the
 // default stream (torch's default) must be ordered with our kernels.
 inline hipStream_t sd_pick(sd_cas_ctx*, void* s) { return (hipStream_t)s; }
+
+// Order a use of the shared workspace (ws, d_scalar) on stream s after the previous use
+// on any other stream; release records this use.  Calls on one stream need no event wait
+// (stream order), so the single-stream pipelines pay one event record per call.
+inline hipError_t sd_ws_acquire(sd_cas_ctx* c, hipStream_t s) {
+  if (c->ws_pending && c->ws_stream != s) return hipStreamWaitEvent(s, c->ws_ev, 0);
+  return hipSuccess;
+}
+inline hipError_t sd_ws_release(sd_cas_ctx* c, hipStream_t s) {
+  c->ws_stream = s;
+  c->ws_pending = true;
+  return hipEventRecord(c->ws_ev, s);
+}
 inline size_t up16(size_t x) { return (x + 15) & ~(size_t)15; }
 // packed whole-file contents start on 128-B lines: a K2 lane's line pair is one cache line
 inline size_t up128(size_t x) { return (x + 127) & ~(size_t)127; }

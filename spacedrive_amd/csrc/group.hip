@@ -285,6 +285,26 @@ sd_group_chunked(const uint32_t* __restrict__ rep, uint64_t n, uint32_t chunk,
   if ((threadIdx.x & 63u) == 0 && b) atomicAdd(created, (unsigned long long)__popcll(b));
 }
 
+// helpers of group_min_by_sort: widen the values to sort keys, gather keys by position,
+// and out[i] = vals[rep[i]]
+extern "C" __global__ void __launch_bounds__(256)
+sd_widen_vals(const uint32_t* __restrict__ vals, uint64_t n, uint64_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = vals ? vals[i] : (uint32_t)i;
+}
+extern "C" __global__ void __launch_bounds__(256)
+sd_gather_keys(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ idx, uint64_t n,
+               uint64_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = keys[idx[i]];
+}
+extern "C" __global__ void __launch_bounds__(256)
+sd_gather_vals(const uint32_t* __restrict__ vals, const uint32_t* __restrict__ rep, uint64_t n,
+               uint32_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = vals ? vals[rep[i]] : rep[i];
+}
+
 }  // namespace sdcas
 
 // ---- host launchers ----------------------------------------------------------------
@@ -381,6 +401,38 @@ hipError_t group_keys(const uint64_t* keys, uint64_t n, uint32_t* rep, uint64_t*
   hipError_t e = radix_sort_pairs(keys, nullptr, skeys, svals, n, 0, 64, sort_ws, s);
   if (e != hipSuccess) return e;
   return group_sorted(skeys, svals, n, rep, d_objects, p, s);
+}
+
+size_t group_min_sorted_workspace_bytes(uint64_t n) {
+  return group_workspace_bytes(n) + 3 * align_up(n * 8, 256) + 3 * align_up(n * 4, 256) + 256;
+}
+
+// out[i] = min{ val(j) : keys[j] == keys[i] } through two stable LSD sorts: positions by
+// value (32 bits), then by key (64 bits) — inside every equal-key run the positions ascend
+// by value, so the run head holds the minimum (sd_cas_group_min_dev beyond the hash
+// grouping's range).
+hipError_t group_min_by_sort(const uint64_t* keys, const uint32_t* vals, uint64_t n, uint32_t* out,
+                             uint64_t* d_objects, void* ws, hipStream_t s) {
+  if (n == 0) return hipMemsetAsync(d_objects, 0, 8, s);
+  char* p = (char*)ws;
+  char* gws = p; p += group_workspace_bytes(n);
+  uint64_t* vkey = (uint64_t*)p; p += align_up(n * 8, 256);
+  uint64_t* k2 = (uint64_t*)p; p += align_up(n * 8, 256);
+  uint64_t* skeys = (uint64_t*)p; p += align_up(n * 8, 256);
+  uint32_t* order = (uint32_t*)p; p += align_up(n * 4, 256);
+  uint32_t* spos = (uint32_t*)p; p += align_up(n * 4, 256);
+  uint32_t* rep = (uint32_t*)p;
+  const uint32_t nb = tiles_of(n, 256);
+  sd_widen_vals<<<nb, 256, 0, s>>>(vals, n, vkey);
+  hipError_t e = radix_sort_pairs(vkey, nullptr, k2, order, n, 0, 32, gws, s);
+  if (e != hipSuccess) return e;
+  sd_gather_keys<<<nb, 256, 0, s>>>(keys, order, n, k2);
+  e = radix_sort_pairs(k2, order, skeys, spos, n, 0, 64, gws, s);
+  if (e != hipSuccess) return e;
+  e = group_sorted(skeys, spos, n, rep, d_objects, gws, s);
+  if (e != hipSuccess) return e;
+  sd_gather_vals<<<nb, 256, 0, s>>>(vals, rep, n, out);
+  return hipGetLastError();
 }
 
 hipError_t group_chunked(const uint32_t* rep, uint64_t n, uint32_t chunk, uint32_t* rep_chunked,

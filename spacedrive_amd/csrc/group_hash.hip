@@ -54,6 +54,11 @@ constexpr uint64_t BIG_MAX_KEYS = 256ull * 5632;  // mean coarse bucket <= 5,632
 constexpr uint32_t MAX_BUCKETS = 16384;   // LDS cursor table of the partition kernels (64 KiB)
 constexpr uint64_t TARGET_PER_BUCKET = 1536;
 constexpr uint64_t MAX_TABLE_ENTRIES = 2ull << 20;  // [bucket][block] table (8 MiB)
+// final buckets: 2^bits, bits = b1 (coarse, <= 10) + b2 (refine, <= 9); at the largest
+// plan the mean bucket may grow to MAX_MEAN_PER_BUCKET distinct keys (LDS table fill 3,584)
+constexpr uint32_t MAX_BITS = 19;
+constexpr uint32_t MAX_B2 = 9;
+constexpr uint64_t MAX_MEAN_PER_BUCKET = 2500;
 
 // splitmix64 finalizer: a bijection on u64, so distinct keys stay distinct
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -297,7 +302,7 @@ sd_part_starts(const uint32_t* __restrict__ offs, uint32_t nb, uint32_t nblk,
 // first position of fine bucket (c, j).  A single-level partition with 2^(b1+b2) buckets
 // writes runs of ~1-3 keys per bucket per block, which costs 5-10x in scattered stores
 // (tools/ubench_scatter.hip); two coalesced levels move more bytes in less time.
-constexpr uint32_t MAX_FINE = 64;
+constexpr uint32_t MAX_FINE = 1u << MAX_B2;
 extern "C" __global__ void __launch_bounds__(PART_THREADS)
 sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict__ in_pos,
                const uint32_t* __restrict__ offs1, uint32_t nb1, uint32_t nblk1, uint64_t n,
@@ -572,11 +577,14 @@ struct GroupPlan {
   uint32_t nb() const { return 1u << (b1 + b2); }
 };
 
-static GroupPlan group_plan(uint64_t n) {
+static GroupPlan group_plan(uint64_t n, uint64_t target) {
+  if (target == 0) target = TARGET_PER_BUCKET;
   uint32_t bits = 1;
-  while (bits < 14 && ((uint64_t)1 << bits) * TARGET_PER_BUCKET < n) ++bits;
+  while (bits < MAX_BITS && ((uint64_t)1 << bits) * target < n) ++bits;
   GroupPlan g;
-  g.b1 = bits < 8 ? bits : 8;
+  // coarse level: 2^8 buckets (runs of ~16 keys per 4,096-key trip), more only when the
+  // refine level would exceed 2^MAX_B2 fine buckets per coarse bucket (> ~200M keys)
+  g.b1 = bits < 8 ? bits : (bits - 8 > MAX_B2 ? bits - MAX_B2 : 8);
   g.b2 = bits - g.b1;
   g.big = g.b2 > 0 && n <= BIG_MAX_KEYS;
   if (g.big) g.b2 = 0;
@@ -585,8 +593,8 @@ static GroupPlan group_plan(uint64_t n) {
 }
 
 bool hash_group_supported(uint64_t n) {
-  // nb <= 16384 buckets at <= ~2,500 distinct keys each on average (table fill 3,584)
-  return n < (1ull << 32) && n <= (uint64_t)MAX_BUCKETS * 2500;
+  // <= 2^19 buckets at <= 2,500 distinct keys each on average (table fill 3,584): 1.31 G
+  return n < (1ull << 32) && n <= ((uint64_t)1 << MAX_BITS) * MAX_MEAN_PER_BUCKET;
 }
 
 static size_t table_ws(const PartPlan& p) {
@@ -594,8 +602,8 @@ static size_t table_ws(const PartPlan& p) {
   return 2 * al256(m * 4) + al256(((m + 4095) / 4096) * 4 + 4);
 }
 
-size_t hash_group_workspace_bytes(uint64_t n) {
-  const GroupPlan g = group_plan(n);
+size_t hash_group_workspace_bytes(uint64_t n, uint64_t target) {
+  const GroupPlan g = group_plan(n, target);
   return 2 * (al256(n * 8) + al256(n * 4)) + table_ws(g.l1) + al256((size_t)g.nb() * 4) +
          al256(2 * n * 8) + al256(2 * n * 4);
 }
@@ -627,11 +635,11 @@ static hipError_t run_partition(const uint64_t* keys, uint64_t n, const PartPlan
 }
 
 hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n, uint32_t* out,
-                          uint64_t* d_objects, void* ws, hipStream_t s) {
+                          uint64_t* d_objects, void* ws, hipStream_t s, uint64_t target) {
   hipError_t e = hipMemsetAsync(d_objects, 0, 8, s);
   if (e != hipSuccess || n == 0) return e;
   if (!hash_group_supported(n)) return hipErrorInvalidValue;
-  const GroupPlan g = group_plan(n);
+  const GroupPlan g = group_plan(n, target);
   const uint64_t m = (uint64_t)g.l1.nb * g.l1.nblk;
   char* q = (char*)ws;
   uint64_t* k1 = (uint64_t*)q; q += al256(n * 8);

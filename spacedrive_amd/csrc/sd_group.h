@@ -22,6 +22,12 @@ hipError_t radix_sort_pairs(const uint64_t* keys_in, const uint32_t* vals_in, ui
 hipError_t group_keys(const uint64_t* keys, uint64_t n, uint32_t* rep, uint64_t* d_objects,
                       void* ws, hipStream_t stream);
 
+// out[i] = min{ val(j) : keys[j] == keys[i] } by two stable LSD sorts (the fallback of
+// hash_group_min beyond its range); ws: group_min_sorted_workspace_bytes(n).
+size_t group_min_sorted_workspace_bytes(uint64_t n);
+hipError_t group_min_by_sort(const uint64_t* keys, const uint32_t* vals, uint64_t n, uint32_t* out,
+                             uint64_t* d_objects, void* ws, hipStream_t stream);
+
 // Group already-sorted pairs (keys ascending, vals = original idx, stable).
 hipError_t group_sorted(const uint64_t* skeys, const uint32_t* svals, uint64_t n, uint32_t* rep,
                         uint64_t* d_objects, void* ws, hipStream_t stream);
@@ -32,12 +38,14 @@ hipError_t exclusive_scan_u32(const uint32_t* in, uint32_t* out, uint64_t m, uin
 
 // ---- group_hash.hip: grouping without a full sort -------------------------------------
 bool hash_group_supported(uint64_t n);
-size_t hash_group_workspace_bytes(uint64_t n);
+// target = mean keys per final bucket (0 = the tuned default, 1,536); smaller targets give
+// deeper partitions (tests use them to reach the > 200M-key plan shapes at small n)
+size_t hash_group_workspace_bytes(uint64_t n, uint64_t target = 0);
 size_t partition_workspace_bytes(uint64_t n, uint32_t parts);
 // out[i] = min{ val(j) : keys[j] == keys[i] } with val(j) = vals ? vals[j] : j;
 // *d_objects = #distinct keys (written on the device).  n < 2^32.
 hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n, uint32_t* out,
-                          uint64_t* d_objects, void* ws, hipStream_t stream);
+                          uint64_t* d_objects, void* ws, hipStream_t stream, uint64_t target = 0);
 // Key-range partition: part(k) = floor(k * parts / 2^64); out_keys/out_pos hold the keys and
 // their input positions part-contiguous (order inside a part unspecified), d_counts[p] the
 // part sizes.  ws: partition_workspace_bytes(n, parts).

@@ -60,10 +60,12 @@ int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
       hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->h2d_done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ws_ev, hipEventDisableTiming) != hipSuccess ||
       hipMalloc((void**)&c->d_scalar, 64) != hipSuccess) {
     sd_cas_ctx_destroy(c);
     return SD_CAS_EHIP;
   }
+  c->quantum = (size_t)prop.multiProcessorCount * 4 * 64;
   sd_cas_set_latency_threshold(c, SD_CAS_THRESHOLD_DEFAULT, SD_CAS_THRESHOLD_DEFAULT);
   sd_cas_set_chunkpar_split(c, SD_CAS_THRESHOLD_DEFAULT, SD_CAS_THRESHOLD_DEFAULT);
   *out = c;
@@ -105,6 +107,7 @@ void sd_cas_ctx_destroy(sd_cas_ctx* c) {
   if (c->d_scalar) (void)hipFree(c->d_scalar);
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->h2d_done) (void)hipEventDestroy(c->h2d_done);
+  if (c->ws_ev) (void)hipEventDestroy(c->ws_ev);
   if (c->copy) (void)hipStreamDestroy(c->copy);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -114,11 +117,16 @@ const char* sd_cas_last_error(const sd_cas_ctx* c) { return c ? c->err.c_str() :
 
 void* sd_cas_ctx_stream(sd_cas_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
-size_t sd_cas_batch_quantum(const sd_cas_ctx* c) {
-  if (!c) return 0;
-  hipDeviceProp_t p;
-  if (hipGetDeviceProperties(&p, c->device) != hipSuccess) return 65536;
-  return (size_t)p.multiProcessorCount * 4 * 64;
+size_t sd_cas_batch_quantum(const sd_cas_ctx* c) { return c ? c->quantum : 0; }
+
+int sd_cas_set_group_method(sd_cas_ctx* c, int method, uint64_t bucket_target) {
+  if (!c) return SD_CAS_EINVAL;
+  if (method < SD_CAS_GROUP_AUTO || method > SD_CAS_GROUP_SORT || (bucket_target && bucket_target < 16))
+    return fail(c, SD_CAS_EINVAL, "set_group_method: method %d, bucket_target %llu", method,
+                (unsigned long long)bucket_target);
+  c->group_method = method;
+  c->group_target = bucket_target;
+  return SD_CAS_OK;
 }
 
 int sd_cas_synchronize(sd_cas_ctx* c) {
@@ -161,7 +169,7 @@ static hipError_t dispatch_sampled(sd_cas_ctx* c, const uint8_t* content, uint64
   if (n < c->latency_sampled)
     return hash_chunkpar(content, nullptr, stride, nullptr, SAMPLED_CONTENT_LEN, sizes, n, keys,
                          c->chunkpar_seg(n, true), s);
-  const size_t q = sd_cas_batch_quantum(c);
+  const size_t q = c->quantum;
   const size_t r = n % q;
   if (n < q || r == 0 || r >= c->latency_sampled) return hash_sampled(content, stride, sizes, n, keys, s);
   const size_t full = n - r;
@@ -210,6 +218,7 @@ int sd_cas_hash_packed_dev(sd_cas_ctx* c, const void* d_arena, const uint64_t* d
   uint64_t* skeys = (uint64_t*)(p + kb);
   uint32_t* order = (uint32_t*)(p + 2 * kb);
   void* sws = p + 2 * kb + ob;
+  HIP_TRY(c, sd_ws_acquire(c, s));
   HIP_TRY(c, length_keys(d_lens, n, lkeys, s));
   HIP_TRY(c, radix_sort_pairs(lkeys, nullptr, skeys, order, n, 0, length_key_bits(n), sws, s));
   if (k1l)
@@ -217,6 +226,7 @@ int sd_cas_hash_packed_dev(sd_cas_ctx* c, const void* d_arena, const uint64_t* d
                              16, s, order));
   else
     HIP_TRY(c, hash_packed((const uint8_t*)d_arena, d_offs, d_lens, d_sizes, order, n, d_keys, s));
+  HIP_TRY(c, sd_ws_release(c, s));
   return SD_CAS_OK;
 }
 
@@ -232,8 +242,11 @@ int sd_cas_sort_pairs_dev(sd_cas_ctx* c, const uint64_t* d_keys_in, const uint32
     return fail(c, SD_CAS_EINVAL, "sort_pairs: bad arguments");
   int rc = ensure(c, c->ws, sort_workspace_bytes(n));
   if (rc) return rc;
+  hipStream_t s = pick(c, stream);
+  HIP_TRY(c, sd_ws_acquire(c, s));
   HIP_TRY(c, radix_sort_pairs(d_keys_in, d_vals_in, d_keys_out, d_vals_out, n, begin_bit, end_bit,
-                              c->ws.p, pick(c, stream)));
+                              c->ws.p, s));
+  HIP_TRY(c, sd_ws_release(c, s));
   return SD_CAS_OK;
 }
 
@@ -242,16 +255,21 @@ int sd_cas_group_dev(sd_cas_ctx* c, const uint64_t* d_keys, size_t n, uint32_t* 
   if (!c) return SD_CAS_EINVAL;
   if (n >= (1ull << 32) || (n && (!d_keys || !d_rep)))
     return fail(c, SD_CAS_EINVAL, "group: bad arguments");
+  if (c->group_method == SD_CAS_GROUP_HASH && !hash_group_supported(n))
+    return fail(c, SD_CAS_EINVAL, "group: %zu keys exceed the hash grouping's range", n);
   hipStream_t s = pick(c, stream);
-  if (hash_group_supported(n)) {  // K4h/K5h: bucket partition + LDS hash min (no full sort)
-    int rc = ensure(c, c->ws, hash_group_workspace_bytes(n));
+  if (c->use_hash_group(n)) {  // K4h/K5h: bucket partition + LDS hash min (no full sort)
+    int rc = ensure(c, c->ws, hash_group_workspace_bytes(n, c->group_target));
     if (rc) return rc;
-    HIP_TRY(c, hash_group_min(d_keys, nullptr, n, d_rep, c->d_scalar, c->ws.p, s));
-  } else {  // beyond ~41M keys per call: LSD radix sort + run heads (K4 + K5)
+    HIP_TRY(c, sd_ws_acquire(c, s));
+    HIP_TRY(c, hash_group_min(d_keys, nullptr, n, d_rep, c->d_scalar, c->ws.p, s, c->group_target));
+  } else {  // beyond the hash grouping's range: LSD radix sort + run heads (K4 + K5)
     int rc = ensure(c, c->ws, group_workspace_bytes(n));
     if (rc) return rc;
+    HIP_TRY(c, sd_ws_acquire(c, s));
     HIP_TRY(c, group_keys(d_keys, n, d_rep, c->d_scalar, c->ws.p, s));
   }
+  HIP_TRY(c, sd_ws_release(c, s));
   if (out_objects) {
     HIP_TRY(c, hipMemcpyAsync(out_objects, c->d_scalar, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
@@ -264,11 +282,21 @@ int sd_cas_group_min_dev(sd_cas_ctx* c, const uint64_t* d_keys, const uint32_t* 
   if (!c) return SD_CAS_EINVAL;
   if (n >= (1ull << 32) || (n && (!d_keys || !d_out)))
     return fail(c, SD_CAS_EINVAL, "group_min: bad arguments");
-  if (!hash_group_supported(n)) return fail(c, SD_CAS_EINVAL, "group_min: batch too large");
+  if (c->group_method == SD_CAS_GROUP_HASH && !hash_group_supported(n))
+    return fail(c, SD_CAS_EINVAL, "group_min: %zu keys exceed the hash grouping's range", n);
   hipStream_t s = pick(c, stream);
-  int rc = ensure(c, c->ws, hash_group_workspace_bytes(n));
-  if (rc) return rc;
-  HIP_TRY(c, hash_group_min(d_keys, d_vals, n, d_out, c->d_scalar, c->ws.p, s));
+  if (c->use_hash_group(n)) {
+    int rc = ensure(c, c->ws, hash_group_workspace_bytes(n, c->group_target));
+    if (rc) return rc;
+    HIP_TRY(c, sd_ws_acquire(c, s));
+    HIP_TRY(c, hash_group_min(d_keys, d_vals, n, d_out, c->d_scalar, c->ws.p, s, c->group_target));
+  } else {  // beyond the hash grouping's range: stable LSD sort of (key, val) + run minima
+    int rc = ensure(c, c->ws, group_min_sorted_workspace_bytes(n));
+    if (rc) return rc;
+    HIP_TRY(c, sd_ws_acquire(c, s));
+    HIP_TRY(c, group_min_by_sort(d_keys, d_vals, n, d_out, c->d_scalar, c->ws.p, s));
+  }
+  HIP_TRY(c, sd_ws_release(c, s));
   if (out_objects) {
     HIP_TRY(c, hipMemcpyAsync(out_objects, c->d_scalar, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
@@ -286,7 +314,9 @@ int sd_cas_partition_dev(sd_cas_ctx* c, const uint64_t* d_keys, size_t n, uint32
   hipStream_t s = pick(c, stream);
   int rc = ensure(c, c->ws, partition_workspace_bytes(n, parts));
   if (rc) return rc;
+  HIP_TRY(c, sd_ws_acquire(c, s));
   HIP_TRY(c, partition_range(d_keys, n, parts, d_keys_out, d_pos_out, d_counts, c->ws.p, s));
+  HIP_TRY(c, sd_ws_release(c, s));
   return SD_CAS_OK;
 }
 
@@ -299,7 +329,9 @@ int sd_cas_group_sorted_dev(sd_cas_ctx* c, const uint64_t* d_sorted_keys,
   hipStream_t s = pick(c, stream);
   int rc = ensure(c, c->ws, group_workspace_bytes(n));
   if (rc) return rc;
+  HIP_TRY(c, sd_ws_acquire(c, s));
   HIP_TRY(c, group_sorted(d_sorted_keys, d_sorted_vals, n, d_rep, c->d_scalar, c->ws.p, s));
+  HIP_TRY(c, sd_ws_release(c, s));
   if (out_objects) {
     HIP_TRY(c, hipMemcpyAsync(out_objects, c->d_scalar, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
@@ -315,8 +347,10 @@ int sd_cas_group_chunked_dev(sd_cas_ctx* c, const uint32_t* d_rep, size_t n, uin
     return fail(c, SD_CAS_EINVAL, "group_chunked: bad arguments");
   hipStream_t s = pick(c, stream);
   uint64_t* d_created = c->d_scalar + 1;
+  HIP_TRY(c, sd_ws_acquire(c, s));
   HIP_TRY(c, hipMemsetAsync(d_created, 0, 8, s));
   HIP_TRY(c, group_chunked(d_rep, n, chunk, d_rep_chunked, d_created, s));
+  HIP_TRY(c, sd_ws_release(c, s));
   uint64_t created = 0;
   HIP_TRY(c, hipMemcpyAsync(&created, d_created, 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
@@ -508,20 +542,32 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
           if (fstat(fd, &st) != 0) { status[i] = -errno; close(fd); continue; }
           if ((uint64_t)st.st_size != lens[i]) { redo[i] = 1; close(fd); continue; }
         }
-        // cas.rs:35-58 offsets: header at 0, sample k at 8192 + k*jump, footer at size-8192
+        // cas.rs:35-58 offsets: header at 0, sample k at 8192 + k*jump (both from `size`,
+        // the metadata length), footer at the file's ACTUAL end - 8192: the reference
+        // seeks SeekFrom::End(-8192) (cas.rs:54-55), so it is located after the samples
+        // with fstat on the open descriptor (a grown or shrunk file keeps the reference's
+        // outcome: a cas_id while every read fits, UnexpectedEof = -EIO otherwise)
         uint64_t offs[6], lns[6];
         int parts;
-        if (sizes[i] > MINIMUM_FILE_SIZE) {
+        const bool sampled = sizes[i] > MINIMUM_FILE_SIZE;
+        if (sampled) {
           const uint64_t jump = (sizes[i] - 2 * HEADER_OR_FOOTER_SIZE) / SAMPLE_COUNT;
           offs[0] = 0; lns[0] = HEADER_OR_FOOTER_SIZE;
           for (int k = 0; k < 4; k++) { offs[1 + k] = HEADER_OR_FOOTER_SIZE + k * jump; lns[1 + k] = SAMPLE_SIZE; }
-          offs[5] = sizes[i] - HEADER_OR_FOOTER_SIZE; lns[5] = HEADER_OR_FOOTER_SIZE;
+          offs[5] = 0; lns[5] = HEADER_OR_FOOTER_SIZE;  // offset set below
           parts = 6;
         } else {
           offs[0] = 0; lns[0] = lens[i];
           parts = 1;
         }
         for (int k = 0; k < parts && !status[i] && !redo[i]; k++) {
+          if (sampled && k == 5) {
+            struct stat st;
+            if (fstat(fd, &st) != 0) { status[i] = -errno; break; }
+            // lseek to a negative position: EINVAL (io::ErrorKind::InvalidInput)
+            if ((uint64_t)st.st_size < HEADER_OR_FOOTER_SIZE) { status[i] = -EINVAL; break; }
+            offs[5] = (uint64_t)st.st_size - HEADER_OR_FOOTER_SIZE;
+          }
           size_t got = 0;
           while (got < lns[k]) {
             ssize_t r = pread(fd, dst + got, lns[k] - got, (off_t)(offs[k] + got));
@@ -620,29 +666,44 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
   return SD_CAS_OK;
 }
 
-int sd_cas_hash_sampled_host(sd_cas_ctx* c, const void* h_content, uint64_t stride,
-                             const uint64_t* h_sizes, size_t n, uint64_t* h_keys,
-                             size_t batch_files) {
+// File i's content is at h_content + (i % ring) * stride: ring == n is a plain batch, a
+// smaller ring re-sends the same host bytes cyclically (BASELINE config 3's E2E run over
+// more files than fit in pinned memory; the H2D volume is the full n files either way).
+static int hash_sampled_host_impl(sd_cas_ctx* c, const void* h_content, uint64_t stride,
+                                  size_t ring, const uint64_t* h_sizes, size_t n,
+                                  uint64_t* h_keys, size_t batch_files) {
   if (!c) return SD_CAS_EINVAL;
   if (n == 0) return SD_CAS_OK;
-  if (!h_content || !h_sizes || !h_keys || stride < SAMPLED_CONTENT_LEN || (stride & 15))
+  if (!h_content || !h_sizes || !h_keys || stride < SAMPLED_CONTENT_LEN || (stride & 15) || !ring)
     return fail(c, SD_CAS_EINVAL, "hash_sampled_host: bad arguments");
   HIP_TRY(c, hipSetDevice(c->device));
   if (batch_files == 0) batch_files = sd_cas_batch_quantum(c);
   batch_files = std::min(batch_files, n);
   // two device slots: [content | sizes | keys], ping-ponged between the copy stream (H2D of
-  // batch k+1) and the compute stream (K1 on batch k, then D2H of its keys)
+  // batch k+1) and the compute stream (K1 on batch k, then D2H of its keys).  Sizes and keys
+  // go through two pinned slots as well: a D2H into pageable caller memory would block this
+  // thread until K1 finished and serialise the next H2D behind it.
   const size_t cbytes = up256(batch_files * stride), sbytes = up256(batch_files * 8);
   const size_t slot = cbytes + 2 * sbytes;
   int rc = ensure(c, c->staging, 2 * slot);
   if (rc) return rc;
-  hipEvent_t h2d[2], done[2];
-  for (int i = 0; i < 2; i++) {
-    HIP_TRY(c, hipEventCreateWithFlags(&h2d[i], hipEventDisableTiming));
-    HIP_TRY(c, hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
-  }
+  if ((rc = ensure_pinned(c, 4 * sbytes))) return rc;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // h2d[0..1], done[0..1]
   int result = SD_CAS_OK;
+  for (int i = 0; i < 4 && result == SD_CAS_OK; i++)
+    if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess)
+      result = fail(c, SD_CAS_EHIP, "hash_sampled_host: event create");
+  hipEvent_t* h2d = ev;
+  hipEvent_t* done = ev + 2;
   const size_t nb = (n + batch_files - 1) / batch_files;
+  auto keys_out = [&](size_t k) -> int {  // batch k's keys: pinned slot -> caller
+    const int b = (int)(k & 1);
+    const size_t f0 = k * batch_files, m = std::min(batch_files, n - f0);
+    if (hipEventSynchronize(done[b]) != hipSuccess)
+      return fail(c, SD_CAS_EHIP, "hash_sampled_host: batch %zu", k);
+    memcpy(h_keys + f0, (const char*)c->pinned + (2 + b) * sbytes, m * 8);
+    return SD_CAS_OK;
+  };
   for (size_t k = 0; k < nb && result == SD_CAS_OK; k++) {
     const int b = (int)(k & 1);
     const size_t f0 = k * batch_files, m = std::min(batch_files, n - f0);
@@ -650,29 +711,43 @@ int sd_cas_hash_sampled_host(sd_cas_ctx* c, const void* h_content, uint64_t stri
     uint8_t* d_content = (uint8_t*)base;
     uint64_t* d_sizes = (uint64_t*)(base + cbytes);
     uint64_t* d_keys = (uint64_t*)(base + cbytes + sbytes);
+    uint64_t* p_sizes = (uint64_t*)((char*)c->pinned + b * sbytes);
+    uint64_t* p_keys = (uint64_t*)((char*)c->pinned + (2 + b) * sbytes);
+    if (k >= 2 && (result = keys_out(k - 2))) break;  // slot b (device + pinned) free again
+    memcpy(p_sizes, h_sizes + f0, m * 8);
     hipError_t e = hipSuccess;
-    if (k >= 2) e = hipStreamWaitEvent(c->copy, done[b], 0);  // slot b's previous batch done
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(d_content, (const char*)h_content + f0 * stride, m * stride,
-                         hipMemcpyHostToDevice, c->copy);
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(d_sizes, h_sizes + f0, m * 8, hipMemcpyHostToDevice, c->copy);
+    for (size_t done_f = 0; e == hipSuccess && done_f < m;) {  // <= 2 pieces per ring wrap
+      const size_t r0 = (f0 + done_f) % ring, piece = std::min(m - done_f, ring - r0);
+      e = hipMemcpyAsync(d_content + done_f * stride, (const char*)h_content + r0 * stride,
+                         piece * stride, hipMemcpyHostToDevice, c->copy);
+      done_f += piece;
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(d_sizes, p_sizes, m * 8, hipMemcpyHostToDevice, c->copy);
     if (e == hipSuccess) e = hipEventRecord(h2d[b], c->copy);
     if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, h2d[b], 0);
-    if (e == hipSuccess)
-      e = dispatch_sampled(c, d_content, stride, d_sizes, m, d_keys, c->stream);
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(h_keys + f0, d_keys, m * 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = dispatch_sampled(c, d_content, stride, d_sizes, m, d_keys, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(p_keys, d_keys, m * 8, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipEventRecord(done[b], c->stream);
     if (e != hipSuccess) result = fail(c, SD_CAS_EHIP, "hash_sampled_host: %s", hipGetErrorString(e));
   }
+  for (size_t k = nb >= 2 ? nb - 2 : 0; k < nb && result == SD_CAS_OK; k++) result = keys_out(k);
   (void)hipStreamSynchronize(c->stream);
   (void)hipStreamSynchronize(c->copy);
-  for (int i = 0; i < 2; i++) {
-    (void)hipEventDestroy(h2d[i]);
-    (void)hipEventDestroy(done[i]);
-  }
+  for (int i = 0; i < 4; i++)
+    if (ev[i]) (void)hipEventDestroy(ev[i]);
   return result;
+}
+
+int sd_cas_hash_sampled_host(sd_cas_ctx* c, const void* h_content, uint64_t stride,
+                             const uint64_t* h_sizes, size_t n, uint64_t* h_keys,
+                             size_t batch_files) {
+  return hash_sampled_host_impl(c, h_content, stride, n, h_sizes, n, h_keys, batch_files);
+}
+
+int sd_cas_hash_sampled_host_ring(sd_cas_ctx* c, const void* h_ring, uint64_t stride,
+                                  size_t ring_files, const uint64_t* h_sizes, size_t n,
+                                  uint64_t* h_keys, size_t batch_files) {
+  return hash_sampled_host_impl(c, h_ring, stride, ring_files, h_sizes, n, h_keys, batch_files);
 }
 
 // ---- file_checksum --------------------------------------------------------------------
@@ -686,8 +761,10 @@ int sd_cas_checksum_dev(sd_cas_ctx* c, const void* d_data, uint64_t len, uint8_t
   int rc = ensure(c, c->ws, checksum_workspace_bytes(len));
   if (rc) return rc;
   uint32_t* d_out = (uint32_t*)c->d_scalar;
+  HIP_TRY(c, sd_ws_acquire(c, s));
   HIP_TRY(c, checksum_device((const uint8_t*)d_data, len, 0, true, d_out, c->ws.p, s));
   HIP_TRY(c, hipMemcpyAsync(out, d_out, 32, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, sd_ws_release(c, s));
   HIP_TRY(c, hipStreamSynchronize(s));
   return SD_CAS_OK;
 }

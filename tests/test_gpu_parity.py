@@ -158,6 +158,26 @@ def test_generate_from_paths_and_errors(eng, oracle, tmp_path):
         sd.generate_cas_id(paths[7], 5000)
 
 
+def test_from_paths_stale_sampled_footer(eng, oracle, tmp_path):
+    """Sampled files whose length changed after fs::metadata: the footer comes from the
+    file's actual end (cas.rs:54-55 SeekFrom::End), samples from `size`; grown files and
+    shrunk-but-readable files get the reference's cas_id, files shrunk below a sample fail
+    with EIO — each vs the literal read/seek execution and the C oracle."""
+    from oracle.pyoracle import UnexpectedEof, py_generate_cas_id_file
+    from tests.test_oracle import stale_files
+    files = stale_files(tmp_path)
+    keys, errs = eng.generate_cas_keys_from_paths([p for p, _ in files], [s for _, s in files])
+    for (path, size), k, e in zip(files, keys, errs):
+        try:
+            want = py_generate_cas_id_file(path, size)
+        except UnexpectedEof:
+            want = None
+        if want is None:
+            assert e == 5 and k == 0, (path, size)
+        else:
+            assert e == 0 and f"{k:016x}" == want == oracle.generate_cas_id(path, size), (path, size)
+
+
 def test_from_paths_windowed_pipeline(eng, oracle, tmp_path):
     """> 2 gather windows (2,048 files each): slots reused, errors in several windows."""
     rng = np.random.default_rng(14)
@@ -269,6 +289,86 @@ def test_group_hash_adversarial_keys(eng, oracle):
         orep, oobj = oracle.group_canonical(keys)
         assert objects == oobj, name
         assert (rep.cpu().numpy().astype(np.uint32) == orep).all(), name
+
+
+@pytest.mark.parametrize("method,target,n", [
+    (2, 0, 300_001),          # LSD sort + run heads (the path above the hash range)
+    (1, 16, 300_001),         # hash plan b1 = 8, b2 = 7 with ~18-key buckets
+    (1, 16, 5_000_000),       # b1 = 9, b2 = 9: the > 200M-key plan shape
+    (1, 16, 9_000_000),       # b1 = 10, b2 = 9: the deepest plan (2^19 buckets)
+])
+def test_group_methods_and_deep_plans(eng, oracle, method, target, n):
+    """Every grouping method / partition depth gives the canonical grouping: forced LSD,
+    and hash plans with a small bucket target so that the partition shapes of >200M keys
+    (coarse levels of 2^9 / 2^10 buckets, 2^9-way refine) run at test sizes — for
+    sd_cas_group_dev vs the oracle and sd_cas_group_min_dev (random u32 vals) vs numpy."""
+    rng = np.random.default_rng(70 + n % 97)
+    pool = rng.integers(0, 2 ** 64, max(1, n * 2 // 3), dtype=np.uint64)
+    keys = pool[rng.integers(0, len(pool), n)]
+    eng.set_group_method(method, target)
+    try:
+        rep = torch.empty(n, dtype=torch.int32, device="cuda")
+        objects = eng.group(dev64(keys), rep)
+        orep, oobj = oracle.group_canonical(keys)
+        assert objects == oobj
+        assert (rep.cpu().numpy().astype(np.uint32) == orep).all()
+        vals = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+        out = torch.empty(n, dtype=torch.int32, device="cuda")
+        objects = eng.group_min(dev64(keys), torch.from_numpy(vals.view(np.int32)).cuda(), out)
+        uniq, inv = np.unique(keys, return_inverse=True)
+        mins = np.full(len(uniq), 0xFFFFFFFF, dtype=np.uint32)
+        np.minimum.at(mins, inv, vals)
+        assert objects == len(uniq)
+        assert (out.cpu().numpy().view(np.uint32) == mins[inv]).all()
+    finally:
+        eng.set_group_method()
+
+
+def test_workspace_ordered_across_streams(eng, oracle):
+    """One context, device calls on two streams with no host sync between them: grouping,
+    group_min and the packed hash's length sort share the context workspace, which the
+    library orders across streams (an event per use)."""
+    rng = np.random.default_rng(71)
+    n = 400_000
+    ka = rng.integers(0, 2 ** 64, n, dtype=np.uint64)
+    ka[::3] = ka[1::3][: len(ka[::3])]
+    kb = rng.integers(0, 2 ** 62, n, dtype=np.uint64)
+    kb[::2] = kb[1::2]
+    vb = rng.integers(0, 2 ** 31, n, dtype=np.uint64).astype(np.int32)
+    da, db, dvb = dev64(ka), dev64(kb), torch.from_numpy(vb).cuda()
+    sz = torch.empty(50_000, dtype=torch.int64, device="cuda")
+    ln = torch.empty(50_000, dtype=torch.int32, device="cuda")
+    of = torch.empty(50_000, dtype=torch.int64, device="cuda")
+    nb = eng.synth_small(72, 0, 50_000, sz, ln, of, None)
+    arena = torch.empty(nb + 64, dtype=torch.uint8, device="cuda")
+    eng.synth_small(72, 0, 50_000, sz, ln, of, arena)
+    want_p = torch.empty(50_000, dtype=torch.int64, device="cuda")
+    eng.set_latency_threshold(0, 0)  # K2 with its on-device length sort (workspace)
+    try:
+        eng.hash_packed(arena, of, ln, sz, want_p)
+        torch.cuda.synchronize()
+        orep_a, _ = oracle.group_canonical(ka)
+        uniq, inv = np.unique(kb, return_inverse=True)
+        mins = np.full(len(uniq), 2 ** 31, dtype=np.int64)
+        np.minimum.at(mins, inv, vb.astype(np.int64))
+        s1, s2, s3 = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+        for trial in range(4):
+            ra = torch.empty(n, dtype=torch.int32, device="cuda")
+            rb = torch.empty(n, dtype=torch.int32, device="cuda")
+            kp = torch.empty(50_000, dtype=torch.int64, device="cuda")
+            torch.cuda.synchronize()
+            with torch.cuda.stream(s1):
+                eng.group(da, ra, want_objects=False)
+            with torch.cuda.stream(s2):
+                eng.group_min(db, dvb, rb, want_objects=False)
+            with torch.cuda.stream(s3):
+                eng.hash_packed(arena, of, ln, sz, kp)
+            torch.cuda.synchronize()
+            assert (ra.cpu().numpy().astype(np.uint32) == orep_a).all(), trial
+            assert (rb.cpu().numpy() == mins[inv]).all(), trial
+            assert torch.equal(kp, want_p), trial
+    finally:
+        eng.set_latency_threshold()
 
 
 def test_group_min_vs_numpy(eng):
@@ -468,6 +568,57 @@ def test_headline_10m_files(eng, oracle):
     reps, mobjects = me.group([keys[cuts[i]:cuts[i + 1]] for i in range(8)], cuts[:-1])
     assert mobjects == len(uniq)
     assert (np.concatenate([x.cpu().numpy() for x in reps]) == truth).all()
+    me.close()
+
+
+def test_config4_100m_files(eng, oracle):
+    """BASELINE config 4 at its full size on one GPU: 100M sampled files with 30 % duplicate
+    content, hashed in 80 resident batches of 1.25M (content regenerated on the device per
+    batch), cas keys bit-exact vs the oracle on 200 random files of every batch, then the
+    Object grouping of ALL 100M keys in one call (hash partition plan b1 = 8, b2 = 8) ==
+    the generator's duplicate truth for every file — locally and through the 8-shard
+    key-range exchange of the multi-GPU path (sd_cas_multi_group, 8 shards on this device).
+    Truth: file f's content is that of synth_root(f), the first file of its duplicate
+    chain, so the canonical representative of f is exactly its root."""
+    import time as _t
+
+    from spacedrive_amd.multi import MultiEngine
+    n, batch, seed, dup = 100_000_000, 1_250_000, 0x5DCA50004 + 4, 300
+    content = torch.empty((batch, SAMPLED_CONTENT_LEN), dtype=torch.uint8, device="cuda")
+    sizes = torch.empty(batch, dtype=torch.int64, device="cuda")
+    keys = torch.empty(n, dtype=torch.int64, device="cuda")
+    rng = np.random.default_rng(101)
+    t0 = _t.time()
+    for f0 in range(0, n, batch):
+        eng.synth_sampled(seed, f0, batch, content, sizes, SAMPLED_CONTENT_LEN, dup_permille=dup)
+        eng.hash_sampled(content, sizes, keys[f0:f0 + batch])
+        idx = np.sort(rng.choice(batch, 200, replace=False))
+        sub = content[torch.from_numpy(idx).cuda()].cpu().numpy()
+        want = oracle.fast_cas_keys_strided(sub.reshape(-1), SAMPLED_CONTENT_LEN, SAMPLED_CONTENT_LEN,
+                                            host64(sizes)[idx], 8)
+        assert (host64(keys[f0:f0 + batch])[idx] == want).all(), f0
+        if f0 % (20 * batch) == 0:
+            print(f"  hashed {f0 + batch:,} files, {_t.time() - t0:.1f}s", flush=True)
+    del content
+    torch.cuda.empty_cache()
+    roots = torch.empty(n, dtype=torch.int64, device="cuda")
+    eng.synth_roots(seed, 0, n, roots, dup_permille=dup)
+    truth = roots.cpu().numpy()
+    del roots
+    n_obj = int(np.count_nonzero(truth == np.arange(n, dtype=np.int64)))
+    rep = torch.empty(n, dtype=torch.int32, device="cuda")
+    objects = eng.group(keys, rep)
+    assert objects == n_obj
+    assert (rep.cpu().numpy() == truth).all()
+    del rep
+    print(f"  grouped 100M keys locally: {objects:,} Objects, {_t.time() - t0:.1f}s", flush=True)
+    me = MultiEngine([0] * 8)
+    cuts = [n * i // 8 for i in range(9)]
+    reps, mobjects = me.group([keys[cuts[i]:cuts[i + 1]] for i in range(8)], cuts[:-1])
+    assert mobjects == n_obj
+    for i in range(8):
+        assert (reps[i].cpu().numpy() == truth[cuts[i]:cuts[i + 1]]).all(), i
+    del reps
     me.close()
 
 

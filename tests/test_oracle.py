@@ -117,6 +117,50 @@ def test_gather_short_file_is_eof_error(oracle, tmp_path):
         oracle.gather_path(str(p), 10 ** 7)  # size from stale metadata: read_exact -> EOF
 
 
+STALE_SAMPLED = [  # (actual length on disk, fs::metadata size the caller passes)
+    (300_000, 250_000),     # grew: samples from `size`, footer from the actual end
+    (5_000_000, 200_000),   # grew a lot
+    (240_000, 250_000),     # shrank, every sample still in bounds: a cas_id
+    (230_000, 1_000_000),   # shrank below the 2nd sample: UnexpectedEof
+    (60_000, 150_000),      # shrank below the last sample: UnexpectedEof
+    (150_000, 150_000),     # unchanged
+]
+
+
+def stale_files(tmp_path):
+    rng = np.random.default_rng(15)
+    out = []
+    for j, (actual, size) in enumerate(STALE_SAMPLED):
+        p = tmp_path / f"stale_sampled{j}"
+        p.write_bytes(rng.integers(0, 256, actual, dtype=np.uint8).tobytes())
+        out.append((str(p), size))
+    return out
+
+
+def test_sampled_footer_follows_actual_end(oracle, tmp_path):
+    """cas.rs:54-55 seeks SeekFrom::End(-8192): the footer of a file whose length changed
+    since fs::metadata comes from its ACTUAL end.  The C oracle's pread gather must agree
+    with a literal execution of the reference's read/seek sequence on the same files,
+    including which stale files fail with UnexpectedEof (-EIO)."""
+    from oracle.pyoracle import UnexpectedEof, py_generate_cas_id_file
+    for path, size in stale_files(tmp_path):
+        try:
+            want = py_generate_cas_id_file(path, size)
+        except UnexpectedEof:
+            want = None
+        if want is None:
+            with pytest.raises(OSError) as ei:
+                oracle.generate_cas_id(path, size)
+            assert ei.value.errno == 5, (path, size)
+        else:
+            assert oracle.generate_cas_id(path, size) == want, (path, size)
+    # the grown file's footer is NOT the one at size - 8192
+    path, size = stale_files(tmp_path)[0]
+    img = open(path, "rb").read()
+    at_size = oracle.cas_id(b"".join(img[o:o + ln] for o, ln in py_sample_plan(size)), size)
+    assert oracle.generate_cas_id(path, size) != at_size
+
+
 def test_file_checksum(oracle, tmp_path):
     for n in [0, 1, 1024, 1025, 1 << 20, (1 << 20) + 17]:
         d = np_content(9, n, n)
