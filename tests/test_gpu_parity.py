@@ -331,7 +331,7 @@ def test_workspace_ordered_across_streams(eng, oracle):
     rng = np.random.default_rng(71)
     n = 400_000
     ka = rng.integers(0, 2 ** 64, n, dtype=np.uint64)
-    ka[::3] = ka[1::3][: len(ka[::3])]
+    ka[1::3] = ka[0::3][: len(ka[1::3])]
     kb = rng.integers(0, 2 ** 62, n, dtype=np.uint64)
     kb[::2] = kb[1::2]
     vb = rng.integers(0, 2 ** 31, n, dtype=np.uint64).astype(np.int32)
