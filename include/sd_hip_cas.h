@@ -257,6 +257,11 @@ int sd_cas_synth_small_dev(sd_cas_ctx* ctx, uint64_t seed, uint64_t file0, size_
 int sd_cas_synth_small_content_dev(sd_cas_ctx* ctx, uint64_t seed, uint64_t file0, size_t n,
                                    uint32_t dup_permille, const uint64_t* d_offs,
                                    const uint32_t* d_lens, void* d_arena, void* stream);
+/* bytes [byte_off, byte_off + len) of synthetic file `file`'s content stream (the
+ * validator's multi-GiB files; byte_off and d_out 8-B aligned, d_out writable to the 8-B
+ * round-up of len) */
+int sd_cas_synth_stream_dev(sd_cas_ctx* ctx, uint64_t seed, uint64_t file, uint64_t byte_off,
+                            uint64_t len, void* d_out, void* stream);
 int sd_cas_synth_roots_dev(sd_cas_ctx* ctx, uint64_t seed, uint64_t file0, size_t n,
                            uint32_t dup_permille, uint64_t* d_roots, void* stream);
 

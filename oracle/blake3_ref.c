@@ -11,9 +11,14 @@
  * Three independent tree drivers are provided (incremental CV stack, recursive
  * left-balanced split, level-wise pair-and-promote); tests require they agree.
  */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <fcntl.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include "oracle.h"
 
@@ -215,4 +220,150 @@ void orc_blake3_pieces(const uint8_t* const* pieces, const size_t* lens, size_t 
   for (size_t i = 0; i < n; i++) { memcpy(buf + off, pieces[i], lens[i]); off += lens[i]; }
   orc_blake3(buf, total, out, 32);
   free(buf);
+}
+
+/* ---- tree-parallel driver (SURVEY §8d "multithreaded tree"; test infrastructure) ------
+ * The left-balanced tree over N chunks, level-wise: node i of level k covers chunks
+ * [i*2^k, min((i+1)*2^k, N)).  Threads compute the level-K nodes (complete subtrees of
+ * 2^K chunks, the last one possibly partial) independently; their CVs are then merged by
+ * pair-and-promote with ROOT on the final parent — the same tree as formulations 1-3. */
+#include <pthread.h>
+
+/* non-root CV of the subtree over in[0, len) (len > 0) whose first chunk is chunk0 */
+static void subtree_cv(const uint8_t* in, size_t len, uint64_t chunk0, uint32_t cv[8]) {
+  uint32_t stack[64][8];
+  int sp = 0;
+  const uint64_t nchunks = (len + B3_CHUNK - 1) / B3_CHUNK;
+  for (uint64_t c = 0; c < nchunks; c++) {
+    const size_t cl = len - c * B3_CHUNK < B3_CHUNK ? len - c * B3_CHUNK : B3_CHUNK;
+    b3_output o = chunk_output(IV, in + c * B3_CHUNK, cl, chunk0 + c, 0);
+    uint32_t x[8];
+    output_cv(&o, x);
+    for (uint64_t total = c + 1; (total & 1) == 0; total >>= 1) {
+      b3_output p = parent_output(IV, stack[--sp], x, 0);
+      output_cv(&p, x);
+    }
+    memcpy(stack[sp++], x, 32);
+  }
+  uint32_t cur[8];
+  memcpy(cur, stack[--sp], 32);
+  while (sp > 0) {
+    b3_output p = parent_output(IV, stack[--sp], cur, 0);
+    output_cv(&p, cur);
+  }
+  memcpy(cv, cur, 32);
+}
+
+/* source of the message bytes [off, off+len): returns a pointer to them (in `scratch`, of
+ * at least len bytes, or in place) */
+typedef const uint8_t* (*b3_src_fn)(void* ctx, uint64_t off, size_t len, uint8_t* scratch);
+
+#define MT_SUB_CHUNKS (1u << 14) /* 16 MiB subtrees */
+
+typedef struct {
+  b3_src_fn src; void* ctx; uint64_t len, nsub; uint32_t (*cvs)[8];
+  uint64_t next; int err;
+} mt_job;
+
+static void* mt_worker(void* p) {
+  mt_job* j = (mt_job*)p;
+  const size_t sub_bytes = (size_t)MT_SUB_CHUNKS * B3_CHUNK;
+  uint8_t* scratch = malloc(sub_bytes);
+  if (!scratch) { __atomic_store_n(&j->err, 1, __ATOMIC_RELAXED); return NULL; }
+  for (;;) {
+    const uint64_t s = __atomic_fetch_add(&j->next, 1, __ATOMIC_RELAXED);
+    if (s >= j->nsub) break;
+    const uint64_t off = s * sub_bytes;
+    const size_t n = (size_t)(j->len - off < sub_bytes ? j->len - off : sub_bytes);
+    const uint8_t* d = j->src(j->ctx, off, n, scratch);
+    if (!d) { __atomic_store_n(&j->err, 1, __ATOMIC_RELAXED); break; }
+    subtree_cv(d, n, s * MT_SUB_CHUNKS, j->cvs[s]);
+  }
+  free(scratch);
+  return NULL;
+}
+
+static int blake3_mt_src(b3_src_fn src, void* ctx, uint64_t len, int threads, uint8_t out[32]) {
+  const uint64_t sub_bytes = (uint64_t)MT_SUB_CHUNKS * B3_CHUNK;
+  if (len <= sub_bytes) { /* one subtree holds the root */
+    uint8_t* scratch = malloc(len ? len : 1);
+    const uint8_t* d = src(ctx, 0, (size_t)len, scratch);
+    if (d) orc_blake3(d, (size_t)len, out, 32);
+    free(scratch);
+    return d ? 0 : -1;
+  }
+  mt_job j = {src, ctx, len, (len + sub_bytes - 1) / sub_bytes, NULL, 0, 0};
+  j.cvs = malloc(j.nsub * 32);
+  if (threads < 1) threads = 1;
+  if ((uint64_t)threads > j.nsub) threads = (int)j.nsub;
+  pthread_t th[256];
+  if (threads > 256) threads = 256;
+  for (int t = 1; t < threads; t++) pthread_create(&th[t], NULL, mt_worker, &j);
+  mt_worker(&j);
+  for (int t = 1; t < threads; t++) pthread_join(th[t], NULL);
+  if (j.err) { free(j.cvs); return -1; }
+  uint64_t n = j.nsub;
+  while (n > 2) { /* pair-and-promote over the level-K nodes */
+    uint64_t m = 0;
+    for (uint64_t i = 0; i + 1 < n; i += 2) {
+      b3_output p = parent_output(IV, j.cvs[i], j.cvs[i + 1], 0);
+      output_cv(&p, j.cvs[m++]);
+    }
+    if (n & 1) memcpy(j.cvs[m++], j.cvs[n - 1], 32);
+    n = m;
+  }
+  b3_output root = parent_output(IV, j.cvs[0], j.cvs[1], 0);
+  output_root(&root, out, 32);
+  free(j.cvs);
+  return 0;
+}
+
+static const uint8_t* src_mem(void* ctx, uint64_t off, size_t len, uint8_t* scratch) {
+  (void)len; (void)scratch;
+  return (const uint8_t*)ctx + off;
+}
+
+void orc_blake3_mt(const uint8_t* in, size_t len, int threads, uint8_t out[32]) {
+  (void)blake3_mt_src(src_mem, (void*)in, len, threads, out);
+}
+
+typedef struct { uint64_t seed, file; } stream_ctx;
+static const uint8_t* src_stream(void* ctx, uint64_t off, size_t len, uint8_t* scratch) {
+  const stream_ctx* s = (const stream_ctx*)ctx;
+  orc_fill_content_range(s->seed, s->file, off, scratch, len);
+  return scratch;
+}
+
+void orc_stream_blake3_mt(uint64_t seed, uint64_t file, uint64_t len, int threads, uint8_t out[32]) {
+  stream_ctx s = {seed, file};
+  (void)blake3_mt_src(src_stream, &s, len, threads, out);
+}
+
+static const uint8_t* src_fd(void* ctx, uint64_t off, size_t len, uint8_t* scratch) {
+  const int fd = *(const int*)ctx;
+  size_t got = 0;
+  while (got < len) {
+    ssize_t r = pread(fd, scratch + got, len - got, (off_t)(off + got));
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) return NULL;
+    got += (size_t)r;
+  }
+  return scratch;
+}
+
+/* file_checksum of a regular file that does not change while it is read: the digest of its
+ * st_size bytes, subtrees read with pread by `threads` workers */
+int orc_file_checksum_mt(const char* path, int threads, char out[65]) {
+  int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return -errno;
+  struct stat st;
+  if (fstat(fd, &st) != 0) { int e = -errno; close(fd); return e; }
+  uint8_t h[32];
+  int rc = blake3_mt_src(src_fd, &fd, (uint64_t)st.st_size, threads, h);
+  close(fd);
+  if (rc) return -EIO;
+  static const char* hx = "0123456789abcdef";
+  for (int i = 0; i < 32; i++) { out[2 * i] = hx[h[i] >> 4]; out[2 * i + 1] = hx[h[i] & 15]; }
+  out[64] = 0;
+  return 0;
 }

@@ -232,22 +232,29 @@ void orc_generate_cas_keys_paths(const char* const* paths, const uint64_t* sizes
   free(th); free(jobs);
 }
 
-/* hash.rs:11-25: read 1 MiB at a time into one Hasher, stop at the first short read,
- * full 64-hex digest.  (The reference stops at the first read shorter than 1 MiB; on
- * regular files that is EOF, so this equals the full-file hash.) */
+/* hash.rs:11-25 literally: read(1 MiB) into one Hasher, update with what was read, stop at
+ * the first read that returned fewer than 1 MiB (EOF on a regular file).  The length is
+ * whatever the reads return, not st_size: a file that grew since it was stat'ed is hashed
+ * to its end.  Bytes are accumulated and hashed once (streaming `update` splits do not
+ * change the digest). */
 int orc_file_checksum(const char* path, char out[65]) {
+  enum { BLOCK_LEN = 1 << 20 };
   int fd = open(path, O_RDONLY | O_CLOEXEC);
   if (fd < 0) return -errno;
-  struct stat st;
-  if (fstat(fd, &st) != 0) { int e = -errno; close(fd); return e; }
-  size_t sz = (size_t)st.st_size;
-  uint8_t* buf = malloc(sz ? sz : 1);
-  size_t got = 0;
-  while (got < sz) {
-    ssize_t r = read(fd, buf + got, sz - got);
-    if (r < 0) { if (errno == EINTR) continue; int e = -errno; free(buf); close(fd); return e; }
-    if (r == 0) break;
+  size_t cap = BLOCK_LEN, got = 0;
+  uint8_t* buf = malloc(cap);
+  for (;;) {
+    if (got + BLOCK_LEN > cap) {
+      cap *= 2;
+      uint8_t* nb = realloc(buf, cap);
+      if (!nb) { free(buf); close(fd); return -ENOMEM; }
+      buf = nb;
+    }
+    ssize_t r;
+    do { r = read(fd, buf + got, BLOCK_LEN); } while (r < 0 && errno == EINTR);
+    if (r < 0) { int e = -errno; free(buf); close(fd); return e; }
     got += (size_t)r;
+    if (r != BLOCK_LEN) break;
   }
   close(fd);
   uint8_t h[32];
@@ -315,6 +322,22 @@ void orc_fill_content(uint64_t seed, uint64_t file, uint8_t* out, size_t len) {
   for (size_t w = 0; w * 8 < len; w++) {
     uint64_t v = orc_mix64(key + (w + 1) * 0x9E3779B97F4A7C15ull);
     for (int b = 0; b < 8 && w * 8 + b < len; b++) out[w * 8 + b] = (uint8_t)(v >> (8 * b));
+  }
+}
+
+void orc_fill_content_range(uint64_t seed, uint64_t file, uint64_t off, uint8_t* out, size_t len) {
+  const uint64_t key = orc_file_key(seed, file);
+  size_t w = 0;
+  while (w < len) {
+    const uint64_t pos = off + w, word = pos >> 3;
+    const uint64_t v = orc_mix64(key + (word + 1) * 0x9E3779B97F4A7C15ull);
+    if ((pos & 7) == 0 && len - w >= 8) {
+      memcpy(out + w, &v, 8); /* little-endian host */
+      w += 8;
+    } else {
+      out[w] = (uint8_t)(v >> (8 * (pos & 7)));
+      w += 1;
+    }
   }
 }
 

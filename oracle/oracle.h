@@ -39,6 +39,12 @@ void orc_blake3_levelwise(const uint8_t* in, size_t len, uint8_t out[32]);
 /* blake3::derive_key(context, material) -> 32 bytes. */
 void orc_blake3_derive_key(const char* context, const uint8_t* material, size_t len,
                            uint8_t out[32]);
+/* Same hash, tree-parallel over `threads` pthreads (16 MiB subtrees, then pair-and-promote;
+ * SURVEY §8d's "multithreaded tree" CPU mode). */
+void orc_blake3_mt(const uint8_t* in, size_t len, int threads, uint8_t out[32]);
+/* BLAKE3 of the first `len` bytes of synthetic file `file`'s content stream (the
+ * orc_fill_content stream, generated on the fly), tree-parallel. */
+void orc_stream_blake3_mt(uint64_t seed, uint64_t file, uint64_t len, int threads, uint8_t out[32]);
 /* BLAKE3 over a stream of pieces (== Hasher::update per piece). */
 void orc_blake3_pieces(const uint8_t* const* pieces, const size_t* lens, size_t n,
                        uint8_t out[32]);
@@ -75,8 +81,11 @@ void orc_generate_cas_keys_paths(const char* const* paths, const uint64_t* sizes
                                  int threads, uint64_t* keys, int32_t* status);
 void orc_fast_generate_cas_keys_paths(const char* const* paths, const uint64_t* sizes, size_t n,
                                       int threads, uint64_t* keys, int32_t* status);
-/* file_checksum(path) -> 0 and 64-hex, or -errno (hash.rs:11-25) */
+/* file_checksum(path) -> 0 and 64-hex, or -errno (hash.rs:11-25): the reference loop
+ * literally — 1 MiB reads into one hasher until the first read shorter than 1 MiB */
 int orc_file_checksum(const char* path, char out[65]);
+/* same digest for a regular file that does not change while read, tree-parallel */
+int orc_file_checksum_mt(const char* path, int threads, char out[65]);
 
 /* ---- grouping (core/src/object/file_identifier/mod.rs:98-350) ---------- */
 /* canonical: rep[i] = min{ j : key[j] == key[i] }; returns #objects (distinct keys). */
@@ -98,6 +107,8 @@ void orc_fast_cas_keys(const uint8_t* arena, const uint64_t* offs, const uint64_
 uint64_t orc_mix64(uint64_t z);
 uint64_t orc_file_key(uint64_t seed, uint64_t file);
 void orc_fill_content(uint64_t seed, uint64_t file, uint8_t* out, size_t len);
+/* bytes [off, off+len) of the same stream */
+void orc_fill_content_range(uint64_t seed, uint64_t file, uint64_t off, uint8_t* out, size_t len);
 /* duplicate chain root and synthetic size (kind 0 = sampled, 1 = whole-file) */
 uint64_t orc_synth_root(uint64_t seed, uint64_t f, uint32_t dup_permille);
 uint64_t orc_synth_size(uint64_t seed, uint64_t root, uint32_t kind);

@@ -258,6 +258,13 @@ class Oracle:
         L.orc_fast_generate_cas_keys_paths.restype = None
         L.orc_file_checksum.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
         L.orc_file_checksum.restype = ctypes.c_int
+        L.orc_blake3_mt.argtypes = [ctypes.c_void_p, sz, ctypes.c_int, ctypes.c_void_p]
+        L.orc_stream_blake3_mt.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                           ctypes.c_int, ctypes.c_void_p]
+        L.orc_file_checksum_mt.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p]
+        L.orc_file_checksum_mt.restype = ctypes.c_int
+        L.orc_fill_content_range.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                             ctypes.c_void_p, sz]
         L.orc_gather_path.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p, sz]
         L.orc_gather_path.restype = ctypes.c_int64
         L.orc_group_canonical.argtypes = [u64p, sz, u32p]
@@ -286,6 +293,33 @@ class Oracle:
         out = ctypes.create_string_buffer(32)
         self.L.orc_blake3_levelwise(data, len(data), out)
         return out.raw
+
+    def blake3_mt(self, data, threads: int = 8) -> bytes:
+        """Tree-parallel BLAKE3 (16 MiB subtrees); data: bytes or a contiguous uint8 array."""
+        out = ctypes.create_string_buffer(32)
+        if isinstance(data, np.ndarray):
+            self.L.orc_blake3_mt(data.ctypes.data, data.nbytes, threads, out)
+        else:
+            self.L.orc_blake3_mt(data, len(data), threads, out)
+        return out.raw
+
+    def stream_blake3_mt(self, seed: int, file: int, length: int, threads: int = 8) -> bytes:
+        """BLAKE3 of the first `length` bytes of the synthetic stream of (seed, file)."""
+        out = ctypes.create_string_buffer(32)
+        self.L.orc_stream_blake3_mt(seed, file, length, threads, out)
+        return out.raw
+
+    def fill_content_range(self, seed: int, file: int, off: int, length: int) -> np.ndarray:
+        out = np.empty(max(length, 1), dtype=np.uint8)
+        self.L.orc_fill_content_range(seed, file, off, out.ctypes.data, length)
+        return out[:length]
+
+    def file_checksum_mt(self, path: str, threads: int = 8) -> str:
+        out = ctypes.create_string_buffer(65)
+        rc = self.L.orc_file_checksum_mt(path.encode(), threads, out)
+        if rc != 0:
+            raise OSError(-rc, os.strerror(-rc), path)
+        return out.value.decode()
 
     def derive_key(self, context: str, material: bytes) -> bytes:
         out = ctypes.create_string_buffer(32)

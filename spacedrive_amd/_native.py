@@ -62,6 +62,7 @@ SIGNATURES = [
     ("sd_cas_synth_sampled_dev", _i, [_vp, _u64, _u64, _sz, _u32, _vp, _u64, _vp, _vp]),
     ("sd_cas_synth_small_dev", _i, [_vp, _u64, _u64, _sz, _u32, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("sd_cas_synth_small_content_dev", _i, [_vp, _u64, _u64, _sz, _u32, _vp, _vp, _vp, _vp]),
+    ("sd_cas_synth_stream_dev", _i, [_vp, _u64, _u64, _u64, _u64, _vp, _vp]),
     ("sd_cas_synth_roots_dev", _i, [_vp, _u64, _u64, _sz, _u32, _vp, _vp]),
 ]
 

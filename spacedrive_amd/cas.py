@@ -318,6 +318,12 @@ class CasEngine:
                                                           _ptr(offs), _ptr(lens), _ptr(arena),
                                                           _stream(stream)), "synth_small_content")
 
+    def synth_stream(self, seed: int, file: int, byte_off: int, length: int, out,
+                     stream: Optional[int] = None) -> None:
+        """Bytes [byte_off, byte_off + length) of synthetic file `file`'s content stream."""
+        self._check(self.L.sd_cas_synth_stream_dev(self.h, seed, file, byte_off, length, _ptr(out),
+                                                   _stream(stream)), "synth_stream")
+
     def synth_roots(self, seed: int, file0: int, n: int, roots, dup_permille: int = 0,
                     stream: Optional[int] = None) -> None:
         self._check(self.L.sd_cas_synth_roots_dev(self.h, seed, file0, n, dup_permille,

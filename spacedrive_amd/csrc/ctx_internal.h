@@ -82,6 +82,7 @@ struct sd_cas_ctx {
   DevBuf ws;       // kernel workspace
   DevBuf staging;  // device copy of a host batch
   DevBuf small;    // multi-device exchange buffers (sd_cas_multi_*)
+  DevBuf cvbuf;    // file_checksum: one 32-B CV per 64 MiB segment
   void* pinned = nullptr;
   size_t pinned_bytes = 0;
   uint64_t* d_scalar = nullptr;  // 8 x u64 scratch for counters

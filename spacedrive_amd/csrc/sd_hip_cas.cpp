@@ -104,6 +104,7 @@ void sd_cas_ctx_destroy(sd_cas_ctx* c) {
   if (c->ws.p) (void)hipFree(c->ws.p);
   if (c->staging.p) (void)hipFree(c->staging.p);
   if (c->small.p) (void)hipFree(c->small.p);
+  if (c->cvbuf.p) (void)hipFree(c->cvbuf.p);
   if (c->d_scalar) (void)hipFree(c->d_scalar);
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->h2d_done) (void)hipEventDestroy(c->h2d_done);
@@ -769,6 +770,32 @@ int sd_cas_checksum_dev(sd_cas_ctx* c, const void* d_data, uint64_t len, uint8_t
   return SD_CAS_OK;
 }
 
+// file_checksum(path) (validation/hash.rs:11-25): the reference reads 1 MiB blocks into one
+// hasher until the first read shorter than 1 MiB — i.e. to EOF on a regular file, whatever
+// the file's length was when it was opened.  Here the file streams through two pinned
+// segment buffers of up to 64 MiB (a segment = one complete 65,536-chunk subtree, hashed
+// on the GPU while the next segment is read by the pool) until a segment comes back short;
+// st_size only sizes the buffers (a file that outgrows its first buffer is re-read with
+// full-size segments).  The segment CVs are merged on the GPU (pair-and-promote, ROOT on
+// the last parent); a file of one segment is hashed with ROOT inside the segment.
+static int cv_capacity(sd_cas_ctx* c, DevBuf& cvb, size_t need_cvs, hipStream_t s) {
+  if (need_cvs * 32 <= cvb.bytes) return SD_CAS_OK;
+  DevBuf nb;
+  const size_t want = std::max<size_t>(need_cvs * 2 * 32, 1 << 16);
+  HIP_TRY(c, hipStreamSynchronize(s));
+  if (hipMalloc(&nb.p, want) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(c, SD_CAS_ENOMEM, "hipMalloc(%zu) failed", want);
+  }
+  nb.bytes = want;
+  if (cvb.p) {
+    HIP_TRY(c, hipMemcpy(nb.p, cvb.p, cvb.bytes, hipMemcpyDeviceToDevice));
+    HIP_TRY(c, hipFree(cvb.p));
+  }
+  cvb = nb;
+  return SD_CAS_OK;
+}
+
 int sd_cas_file_checksum(sd_cas_ctx* c, const char* path, char out_hex[65], int* err_no) {
   if (!c || !path || !out_hex) return SD_CAS_EINVAL;
   if (err_no) *err_no = 0;
@@ -784,77 +811,110 @@ int sd_cas_file_checksum(sd_cas_ctx* c, const char* path, char out_hex[65], int*
     close(fd);
     return fail(c, SD_CAS_EIO, "fstat(%s): %s", path, strerror(errno));
   }
-  const uint64_t len = (uint64_t)st.st_size;
   const uint64_t SEG = 64ull << 20;  // 65,536 chunks: a complete left subtree
-  const uint64_t nseg = len <= SEG ? 1 : (len + SEG - 1) / SEG;
-  const size_t seg_bytes = (size_t)std::min<uint64_t>(len ? len : 1, SEG);
-  // two pinned + two device segment buffers (double-buffered: read k+1 while hashing k)
-  int rc = ensure_pinned(c, 2 * up256(seg_bytes + 16));
-  if (rc) { close(fd); return rc; }
-  const size_t cvs_bytes = up256(nseg * 32);
-  rc = ensure(c, c->staging, 2 * up256(seg_bytes + 16) + cvs_bytes);
-  if (rc) { close(fd); return rc; }
-  // every kernel runs on c->stream, so segments and the final reduce share one workspace
-  rc = ensure(c, c->ws, std::max(checksum_workspace_bytes(std::min<uint64_t>(len, SEG)),
-                                 checksum_workspace_bytes(nseg * 1024)));
-  if (rc) { close(fd); return rc; }
-  char* pin[2] = {(char*)c->pinned, (char*)c->pinned + up256(seg_bytes + 16)};
-  char* dev[2] = {(char*)c->staging.p, (char*)c->staging.p + up256(seg_bytes + 16)};
-  uint32_t* d_cvs = (uint32_t*)((char*)c->staging.p + 2 * up256(seg_bytes + 16));
-  hipEvent_t done[2];
-  HIP_TRY(c, hipEventCreateWithFlags(&done[0], hipEventDisableTiming));
-  HIP_TRY(c, hipEventCreateWithFlags(&done[1], hipEventDisableTiming));
-  int result = SD_CAS_OK;
-  for (uint64_t sgi = 0; sgi < nseg && result == SD_CAS_OK; sgi++) {
-    const int b = (int)(sgi & 1);
-    const uint64_t off = sgi * SEG;
-    const uint64_t want = std::min<uint64_t>(SEG, len - off);
-    if (sgi >= 2) (void)hipEventSynchronize(done[b]);  // pinned[b] free again
-    // the segment is read as 4 MiB pieces by the pool (one reader tops out near 5-10 GB/s);
-    // hash.rs:16-20 reads until a short read — a file shorter than its stat is an error here
-    constexpr uint64_t PIECE = 4ull << 20;
-    const uint64_t npieces = (want + PIECE - 1) / PIECE;
-    std::atomic<uint64_t> next{0};
+  constexpr uint64_t PIECE = 4ull << 20;  // pool read unit (one reader tops out near 5-10 GB/s)
+  // segment capacity: the whole file plus room to see EOF, capped at one subtree
+  uint64_t cap = std::min<uint64_t>(SEG, (((uint64_t)st.st_size + 1 + 4095) / 4096) * 4096);
+  hipStream_t s = c->stream;
+  int rc = SD_CAS_OK;
+  hipEvent_t done[2] = {nullptr, nullptr};
+  for (int i = 0; i < 2; i++)
+    if (hipEventCreateWithFlags(&done[i], hipEventDisableTiming) != hipSuccess) {
+      close(fd);
+      for (int k = 0; k < i; k++) (void)hipEventDestroy(done[k]);
+      return fail(c, SD_CAS_EHIP, "file_checksum: event create");
+    }
+  // read segment `sgi` into pinned buffer b: returns its length (< cap at EOF), or -errno
+  auto read_seg = [&](uint64_t sgi, char* dst) -> int64_t {
+    const uint64_t off = sgi * cap;
+    const uint64_t npieces = (cap + PIECE - 1) / PIECE;
+    std::atomic<uint64_t> next{0}, eof{cap};
     std::atomic<int> rd_err{0};
     c->pool.run((unsigned)std::min<uint64_t>(8, npieces), [&]() {
       for (uint64_t p; (p = next.fetch_add(1)) < npieces && !rd_err.load();) {
-        const uint64_t p0 = p * PIECE, pn = std::min(PIECE, want - p0);
+        const uint64_t p0 = p * PIECE, pn = std::min(PIECE, cap - p0);
+        if (p0 >= eof.load()) break;
         uint64_t got = 0;
         while (got < pn) {
-          ssize_t r = pread(fd, pin[b] + p0 + got, pn - got, (off_t)(off + p0 + got));
+          ssize_t r = pread(fd, dst + p0 + got, pn - got, (off_t)(off + p0 + got));
           if (r < 0 && errno == EINTR) continue;
-          if (r <= 0) { rd_err.store(r < 0 ? errno : EIO); break; }
+          if (r < 0) { rd_err.store(errno); break; }
+          if (r == 0) break;  // EOF: the first short read ends the file (hash.rs:18-20)
           got += (uint64_t)r;
+        }
+        if (got < pn) {  // eof = min(eof, p0 + got)
+          uint64_t cur = eof.load();
+          while (p0 + got < cur && !eof.compare_exchange_weak(cur, p0 + got)) {}
         }
       }
     });
-    if (int e = rd_err.load()) {
-      if (err_no) *err_no = e;
-      result = fail(c, SD_CAS_EIO, "read(%s): %s", path, e == EIO ? "short read" : strerror(e));
+    if (int e = rd_err.load()) return -(int64_t)e;
+    return (int64_t)eof.load();
+  };
+  uint8_t digest[32];
+  for (int attempt = 0; attempt < 2; attempt++) {
+    const size_t sb = up256(cap + 16);
+    if ((rc = ensure_pinned(c, 2 * sb)) || (rc = ensure(c, c->staging, 2 * sb))) break;
+    if ((rc = ensure(c, c->ws, std::max(checksum_workspace_bytes(cap), checksum_workspace_bytes(1 << 20)))))
       break;
+    char* pin[2] = {(char*)c->pinned, (char*)c->pinned + sb};
+    char* dev[2] = {(char*)c->staging.p, (char*)c->staging.p + sb};
+    HIP_TRY(c, sd_ws_acquire(c, s));
+    // segment k is dispatched once it is known whether it is the only one (k == 0 waits for
+    // segment 1's read); ROOT sits inside it only then
+    auto dispatch = [&](uint64_t sgi, uint64_t len, bool only) -> int {
+      const int b = (int)(sgi & 1);
+      int r2 = cv_capacity(c, c->cvbuf, sgi + 1, s);
+      if (r2) return r2;
+      hipError_t e = hipMemcpyAsync(dev[b], pin[b], up16(len), hipMemcpyHostToDevice, s);
+      if (e == hipSuccess)
+        e = checksum_device((const uint8_t*)dev[b], len, (sgi * cap) >> 10, only,
+                            (uint32_t*)c->cvbuf.p + 8 * sgi, c->ws.p, s);
+      if (e == hipSuccess) e = hipEventRecord(done[b], s);
+      if (e != hipSuccess) return fail(c, SD_CAS_EHIP, "checksum segment: %s", hipGetErrorString(e));
+      return SD_CAS_OK;
+    };
+    int64_t len0 = read_seg(0, pin[0]);
+    if (len0 < 0) { if (err_no) *err_no = (int)-len0; rc = fail(c, SD_CAS_EIO, "read(%s): %s", path, strerror((int)-len0)); break; }
+    if ((uint64_t)len0 == cap && cap < SEG) { cap = SEG; continue; }  // grew past the buffer
+    uint64_t nseg = 1;
+    if ((uint64_t)len0 < cap) {
+      rc = dispatch(0, (uint64_t)len0, true);
+    } else {  // a full first segment: more may follow
+      uint64_t prev_len = (uint64_t)len0;
+      for (uint64_t sgi = 1;; sgi++) {
+        const int b = (int)(sgi & 1);
+        if (sgi >= 2 && hipEventSynchronize(done[b]) != hipSuccess) { rc = fail(c, SD_CAS_EHIP, "checksum: segment sync"); break; }
+        const int64_t ln = read_seg(sgi, pin[b]);
+        if (ln < 0) { if (err_no) *err_no = (int)-ln; rc = fail(c, SD_CAS_EIO, "read(%s): %s", path, strerror((int)-ln)); break; }
+        if (sgi == 1) {  // segment 0 is the only one iff nothing follows it
+          if ((rc = dispatch(0, prev_len, ln == 0))) break;
+        }
+        if (ln == 0) { nseg = sgi; break; }
+        if ((rc = dispatch(sgi, (uint64_t)ln, false))) break;
+        if ((uint64_t)ln < cap) { nseg = sgi + 1; break; }
+      }
     }
-    hipError_t e = hipMemcpyAsync(dev[b], pin[b], up16(want), hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess)
-      e = checksum_device((const uint8_t*)dev[b], want, off >> 10, nseg == 1, d_cvs + 8 * sgi,
-                          c->ws.p, c->stream);
-    if (e == hipSuccess) e = hipEventRecord(done[b], c->stream);
-    if (e != hipSuccess) result = fail(c, SD_CAS_EHIP, "checksum segment: %s", hipGetErrorString(e));
+    if (rc == SD_CAS_OK) {
+      uint32_t* d_out = (uint32_t*)c->d_scalar;
+      hipError_t e = hipSuccess;
+      // reduce_cvs_device ping-pongs ceil(nseg / 256) CVs per level through ws
+      const size_t red_ws = 2 * up256((nseg + 255) / 256 * 32) + 512;
+      if (nseg > 1 && (rc = ensure(c, c->ws, red_ws))) break;
+      if (nseg == 1) e = hipMemcpyAsync(d_out, c->cvbuf.p, 32, hipMemcpyDeviceToDevice, s);
+      else e = reduce_cvs_device((uint32_t*)c->cvbuf.p, nseg, d_out, c->ws.p, s);
+      if (e == hipSuccess) e = hipMemcpyAsync(digest, d_out, 32, hipMemcpyDeviceToHost, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      if (e != hipSuccess) rc = fail(c, SD_CAS_EHIP, "checksum reduce: %s", hipGetErrorString(e));
+    }
+    (void)sd_ws_release(c, s);
+    break;
   }
   close(fd);
-  uint8_t digest[32];
-  if (result == SD_CAS_OK) {
-    uint32_t* d_out = (uint32_t*)c->d_scalar;
-    hipError_t e = hipSuccess;
-    if (nseg == 1) e = hipMemcpyAsync(d_out, d_cvs, 32, hipMemcpyDeviceToDevice, c->stream);
-    else e = reduce_cvs_device(d_cvs, nseg, d_out, c->ws.p, c->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(digest, d_out, 32, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    if (e != hipSuccess) result = fail(c, SD_CAS_EHIP, "checksum reduce: %s", hipGetErrorString(e));
-  }
-  (void)hipStreamSynchronize(c->stream);
+  (void)hipStreamSynchronize(s);
   (void)hipEventDestroy(done[0]);
   (void)hipEventDestroy(done[1]);
-  if (result) return result;
+  if (rc) return rc;
   static const char* hx = "0123456789abcdef";
   for (int i = 0; i < 32; i++) { out_hex[2 * i] = hx[digest[i] >> 4]; out_hex[2 * i + 1] = hx[digest[i] & 15]; }
   out_hex[64] = 0;
@@ -910,6 +970,15 @@ int sd_cas_synth_small_content_dev(sd_cas_ctx* c, uint64_t seed, uint64_t file0,
   if (n == 0) return SD_CAS_OK;
   HIP_TRY(c, synth_small_content(seed, file0, n, dup_permille, d_offs, d_lens,
                                  (uint8_t*)d_arena, pick(c, stream)));
+  return SD_CAS_OK;
+}
+
+int sd_cas_synth_stream_dev(sd_cas_ctx* c, uint64_t seed, uint64_t file, uint64_t byte_off,
+                            uint64_t len, void* d_out, void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (len && (!d_out || (byte_off & 7) || ((uintptr_t)d_out & 7)))
+    return fail(c, SD_CAS_EINVAL, "synth_stream: bad arguments");
+  HIP_TRY(c, synth_stream(seed, file, byte_off, len, (uint8_t*)d_out, pick(c, stream)));
   return SD_CAS_OK;
 }
 

@@ -17,6 +17,10 @@ hipError_t synth_small_sizes(uint64_t seed, uint64_t file0, uint64_t n, uint32_t
 hipError_t synth_small_content(uint64_t seed, uint64_t file0, uint64_t n, uint32_t dup_permille,
                                const uint64_t* offs, const uint32_t* lens, uint8_t* arena,
                                hipStream_t s);
+// bytes [byte_off, byte_off + len) of file `file`'s stream (byte_off, out 8-B aligned; the
+// last word is written whole: out must hold the 8-B round-up of len)
+hipError_t synth_stream(uint64_t seed, uint64_t file, uint64_t byte_off, uint64_t len,
+                        uint8_t* out, hipStream_t s);
 hipError_t synth_roots(uint64_t seed, uint64_t file0, uint64_t n, uint32_t dup_permille,
                        uint64_t* roots, hipStream_t s);
 

@@ -92,6 +92,24 @@ sd_synth_roots(uint64_t seed, uint64_t file0, uint64_t n, uint32_t dup_permille,
   if (i < n) roots[i] = synth_root(seed, file0 + i, dup_permille);
 }
 
+// bytes [8*w0, 8*(w0+nw)) of file `file`'s content stream (the validator's multi-GiB files)
+extern "C" __global__ void __launch_bounds__(256)
+sd_synth_stream(uint64_t seed, uint64_t file, uint64_t w0, uint64_t nw, uint64_t* __restrict__ out) {
+  const uint64_t key = file_key(seed, file);
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw;
+       w += (uint64_t)gridDim.x * blockDim.x)
+    out[w] = mix64(key + (w0 + w + 1) * GAMMA);
+}
+
+hipError_t synth_stream(uint64_t seed, uint64_t file, uint64_t byte_off, uint64_t len,
+                        uint8_t* out, hipStream_t s) {
+  if (len == 0) return hipSuccess;
+  if ((byte_off & 7) || ((uintptr_t)out & 7)) return hipErrorInvalidValue;
+  sd_synth_stream<<<256 * 64, 256, 0, s>>>(seed, file, byte_off >> 3, (len + 7) >> 3,
+                                           reinterpret_cast<uint64_t*>(out));
+  return hipGetLastError();
+}
+
 hipError_t synth_sampled(uint64_t seed, uint64_t file0, uint64_t n, uint32_t dup_permille,
                          uint8_t* content, uint64_t stride, uint64_t* sizes, hipStream_t s) {
   if (n == 0) return hipSuccess;

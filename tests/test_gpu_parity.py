@@ -432,6 +432,53 @@ def test_file_checksum_streamed(eng, oracle, tmp_path):
         sd.file_checksum(str(tmp_path / "nope"))
 
 
+ORC_THREADS = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+
+
+def test_checksum_device_over_4gib(eng, oracle):
+    """BASELINE config 5 sizes on the device path: buffers past 4 GiB with odd tails — byte
+    offsets above 2^32, chunk counters above 2^22, and the multi-level CV reduce (> 256 x 256
+    1 MiB subtrees) — vs the oracle's tree-parallel hash of the same generated stream."""
+    for L in [(4 << 30) + 777, (5 << 30) + (1 << 20) + 3]:
+        buf = torch.empty(L + 64, dtype=torch.uint8, device="cuda")
+        eng.synth_stream(55, 3, 0, L, buf)
+        # the device generator is the oracle's stream, at the start and past 2^32
+        for off in (0, (L - 4096) & ~7):  # the last window lies past 2^32
+            assert (buf[off:off + 4096].cpu().numpy() == oracle.fill_content_range(55, 3, off, 4096)).all()
+        assert eng.checksum_dev(buf, L) == oracle.stream_blake3_mt(55, 3, L, ORC_THREADS).hex(), L
+        del buf
+        torch.cuda.empty_cache()
+
+
+def test_file_checksum_streamed_multi_gib(eng, oracle, tmp_path):
+    """file_checksum (hash.rs:11-25) of a > 4 GiB file streamed from tmpfs through the
+    pinned 64 MiB segments: 65 segment subtrees + the GPU CV reduce, vs the oracle (the
+    generated stream and the file read back, tree-parallel)."""
+    L = (4 << 30) + 12345
+    d = "/dev/shm" if os.path.isdir("/dev/shm") else str(tmp_path)
+    path = os.path.join(d, f"sdcas_checksum_{os.getpid()}.bin")
+    try:
+        with open(path, "wb") as fh:
+            piece = 256 << 20
+            for off in range(0, L, piece):
+                fh.write(oracle.fill_content_range(56, 4, off, min(piece, L - off)).tobytes())
+        want = oracle.stream_blake3_mt(56, 4, L, ORC_THREADS).hex()
+        assert eng.file_checksum(path) == want
+        assert oracle.file_checksum_mt(path, ORC_THREADS) == want
+    finally:
+        if os.path.exists(path):
+            os.unlink(path)
+
+
+def test_file_checksum_reads_to_eof(eng, oracle):
+    """hash.rs:15-21 hashes what the reads return until the first short read, not st_size: a
+    procfs file whose st_size is 0 but which has content is hashed over that content."""
+    p = "/proc/sys/kernel/ostype"
+    if not os.path.exists(p) or os.stat(p).st_size != 0:
+        pytest.skip("no procfs file with st_size 0")
+    assert eng.file_checksum(p) == oracle.file_checksum(p) == oracle.blake3(open(p, "rb").read()).hex()
+
+
 def test_synth_matches_oracle_generator(eng, oracle):
     n, seed = 64, 12345
     content = torch.empty((n, SAMPLED_CONTENT_LEN), dtype=torch.uint8, device="cuda")

@@ -169,6 +169,37 @@ def test_file_checksum(oracle, tmp_path):
         assert oracle.file_checksum(str(p)) == oracle.blake3(d).hex()
 
 
+def test_tree_parallel_modes_agree(oracle, tmp_path):
+    """The multithreaded tree (16 MiB subtrees merged by pair-and-promote) equals the
+    sequential hash at lengths around the subtree and chunk boundaries; the generated
+    stream mode equals hashing the materialised stream; the file mode equals the literal
+    file_checksum loop."""
+    sub = 16 << 20
+    for L in [0, 1, 1024, sub - 1, sub, sub + 1, sub + 1024, 2 * sub, 3 * sub + 777, 5 * sub - 1025]:
+        d = oracle.fill_content_range(41, 2, 0, L)
+        want = oracle.blake3(d.tobytes())
+        assert oracle.blake3_mt(d, 4) == want, L
+        assert oracle.stream_blake3_mt(41, 2, L, 3) == want, L
+        if L in (sub + 1, 3 * sub + 777):
+            p = tmp_path / "mt.bin"
+            p.write_bytes(d.tobytes())
+            assert oracle.file_checksum_mt(str(p), 4) == want.hex() == oracle.file_checksum(str(p))
+    # the stream at an unaligned offset equals the slice of the materialised stream
+    d = oracle.fill_content_range(41, 2, 0, 5000)
+    assert (oracle.fill_content_range(41, 2, 13, 4000) == d[13:4013]).all()
+    assert oracle.fill_content(41, 2, 5000) == d.tobytes()
+
+
+def test_file_checksum_reads_to_eof_not_stat(oracle):
+    """hash.rs:15-21 reads until the first short read, whatever fstat says: a procfs file
+    with st_size 0 but content is hashed over its content."""
+    p = "/proc/sys/kernel/ostype"
+    if not os.path.exists(p) or os.stat(p).st_size != 0:
+        pytest.skip("no procfs file with st_size 0")
+    content = open(p, "rb").read()
+    assert content and oracle.file_checksum(p) == oracle.blake3(content).hex()
+
+
 def test_grouping_golden(oracle, golden):
     g = golden["grouping"]
     for name, lay in g["layouts"].items():

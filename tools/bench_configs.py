@@ -226,47 +226,65 @@ def config4(eng, orc, n_total: int, batch: int, dup: int):
 
 
 def config5(eng, orc, gib: float, file_mb: int):
+    """Validator (file_checksum, validation/hash.rs:11-25) at BASELINE size: (a) one 64 GiB
+    resident buffer, (b) 64 GiB as 16 resident multi-GiB files (4 GiB each), every digest
+    verified IN FULL against the oracle's tree-parallel CPU hash of the same generated
+    stream, (c) a streamed file_checksum of a multi-GiB tmpfs file."""
     import torch
     n = int(gib * (1 << 30))
-    buf = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
-    # fill on device with the synthetic generator: n // 57,344 whole 57,344-B records
-    # (never past the buffer); the < 57,344-B tail is zeroed
-    files = n // 57344
-    sz = torch.empty(max(files, 1), dtype=torch.int64, device="cuda")
-    eng.synth_sampled(5, 0, files, buf, sz, 57344)
-    buf[files * 57344:].zero_()
+    buf = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    eng.synth_stream(5, 0, 0, n, buf)
     torch.cuda.synchronize()
     eng.checksum_dev(buf, min(n, 1 << 30))
     t = time.perf_counter()
     digest = eng.checksum_dev(buf, n)
     dt = time.perf_counter() - t
-    # parity on a 1 GiB prefix (full 64 GiB on one CPU thread would take minutes)
-    pre = 1 << 30
-    d1 = eng.checksum_dev(buf, pre)
-    ok = d1 == orc.blake3(buf[:pre].cpu().numpy().tobytes()).hex()
+    t = time.perf_counter()
+    want = orc.stream_blake3_mt(5, 0, n, THREADS).hex()
+    cpu_mt = time.perf_counter() - t
     comps = n // 64 + n // 1024
     emit({"config": 5, "bytes": n, "seconds": dt, "gb_per_s": n / dt / 1e9, "digest": digest,
-          "valu_slot_frac": comps * 1014 / 64 / dt / (1024 * 2.4e9 / 2), "hbm_frac": n / dt / 8e12,
-          "parity_1gib_prefix": ok})
+          "valu_slot_frac": comps * 1014 / 64 / dt / (1024 * 2.4e9 / 2),
+          "spec_op_frac": comps * 792 / dt / 78.6432e12, "hbm_frac": n / dt / 8e12,
+          "parity_full": digest == want, "cpu_tree_parallel_gb_per_s": n / cpu_mt / 1e9,
+          "cpu_threads": THREADS})
+    # (b) 16 multi-GiB files of the same 64 GiB, each its own stream and its own digest
+    nf = 16
+    fl = n // nf
+    ts, digs = [], []
+    for f in range(nf):
+        eng.synth_stream(5, 100 + f, 0, fl, buf[f * fl:])
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for f in range(nf):
+        digs.append(eng.checksum_dev(buf[f * fl:], fl))
+    dtf = time.perf_counter() - t
+    ok = all(d == orc.stream_blake3_mt(5, 100 + f, fl, THREADS).hex() for f, d in enumerate(digs))
+    emit({"config": "5-files", "files": nf, "file_bytes": fl, "bytes": nf * fl, "seconds": dtf,
+          "gb_per_s": nf * fl / dtf / 1e9, "hbm_frac": nf * fl / dtf / 8e12, "parity_full": ok})
     del buf
     torch.cuda.empty_cache()
-    # streamed file_checksum through pinned staging (tmpfs file)
+    # (c) streamed file_checksum through pinned staging (tmpfs file)
     path = "/dev/shm/sdcas_validator.bin"
+    L = file_mb << 20
     try:
-        rng = np.random.default_rng(5)
         with open(path, "wb") as fh:
-            for _ in range(file_mb // 64):
-                fh.write(rng.integers(0, 256, 64 << 20, dtype=np.uint8).tobytes())
+            for off in range(0, L, 256 << 20):
+                fh.write(orc.fill_content_range(6, 0, off, min(256 << 20, L - off)).tobytes())
         eng.file_checksum(path)
         t = time.perf_counter()
         h = eng.file_checksum(path)
         dt = time.perf_counter() - t
         t = time.perf_counter()
-        w = orc.file_checksum(path)
-        cpu = time.perf_counter() - t
-        emit({"config": "5-file", "bytes": os.path.getsize(path), "gpu_seconds": dt,
-              "gpu_gb_per_s": os.path.getsize(path) / dt / 1e9, "cpu_oracle_1thread_gb_per_s":
-              os.path.getsize(path) / cpu / 1e9, "parity": h == w})
+        w1 = orc.file_checksum(path)
+        cpu1 = time.perf_counter() - t
+        t = time.perf_counter()
+        wm = orc.file_checksum_mt(path, THREADS)
+        cpum = time.perf_counter() - t
+        emit({"config": "5-file", "bytes": L, "gpu_seconds": dt, "gpu_gb_per_s": L / dt / 1e9,
+              "cpu_oracle_1thread_gb_per_s": L / cpu1 / 1e9,
+              "cpu_oracle_tree_parallel_gb_per_s": L / cpum / 1e9, "cpu_threads": THREADS,
+              "parity_full": h == w1 == wm})
     finally:
         if os.path.exists(path):
             os.unlink(path)
