@@ -200,6 +200,52 @@ int sd_cas_group_sorted_dev(sd_cas_ctx* ctx, const uint64_t* d_sorted_keys,
 int sd_cas_group_chunked_dev(sd_cas_ctx* ctx, const uint32_t* d_rep, size_t n, uint32_t chunk,
                              uint32_t* d_rep_chunked, uint64_t* out_created,
                              uint64_t* out_linked, void* stream);
+/* ---- Object-link emission of a file-identifier job ------------------
+ * The decisions of file_identifier_job.rs:180-236 (the step loop) and identifier_job_step
+ * (mod.rs:98-350) over n orphan file_path rows in ascending id order on a fresh library,
+ * `chunk` rows per step (CHUNK_SIZE = 100, mod.rs:34), with the reference's cursor: step k
+ * queries the orphan rows with `id >= cursor` (file_identifier_job.rs:268, 307-315) and
+ * the next cursor is the chunk's LAST row (mod.rs:401-405), so a last row that stays
+ * orphan (an error, or an empty file: no cas_id) is queried again by the next step; the
+ * job runs at most ceil(n / chunk) steps (file_identifier_job.rs:146) and ends early when
+ * a query comes back empty.
+ *   d_keys[i]  cas key of row i (read for hashed rows only)
+ *   d_state[i] SD_CAS_ROW_* (u8; NULL = every row hashed): HASHED = cas_id computed,
+ *              NO_CAS = metadata length 0 (mod.rs:78-86), ERROR = FileMetadata::new failed
+ *              (the row is dropped from its step, mod.rs:125-141)
+ * Outputs (device, n entries each):
+ *   d_step[i]   the (last) step that processed row i, SD_CAS_NO_STEP if none;
+ *   d_object[i] the row whose new Object row i is connected to: i when row i created one
+ *               (create_many, mod.rs:246-347), the key's first row when it linked to an
+ *               existing Object (mod.rs:202-238; find() = the lowest Object id), and
+ *               SD_CAS_NO_OBJECT when dropped or not reached;
+ *   d_action[i] SD_CAS_LINK_*.
+ * h_step_counts (host, 2 x max_steps u64): per step (total_created, total_linked) as
+ * identifier_job_step returns them (mod.rs:349); an empty row queried again counts one
+ * creation in every step that processed it.  *out_steps = steps executed.  Ties inside a
+ * step follow HashMap order := ascending row.  Blocking; n < 2^32. */
+#define SD_CAS_ROW_HASHED 0
+#define SD_CAS_ROW_NO_CAS 1
+#define SD_CAS_ROW_ERROR 2
+#define SD_CAS_LINK_CREATED 0
+#define SD_CAS_LINK_LINKED 1
+#define SD_CAS_LINK_DROPPED 2
+#define SD_CAS_LINK_NOT_REACHED 3
+#define SD_CAS_NO_STEP 0xFFFFFFFFu
+#define SD_CAS_NO_OBJECT 0xFFFFFFFFu
+size_t sd_cas_identifier_max_steps(size_t n, uint32_t chunk);
+int sd_cas_identifier_links_dev(sd_cas_ctx* ctx, const uint64_t* d_keys, const uint8_t* d_state,
+                                size_t n, uint32_t chunk, uint32_t* d_step, uint32_t* d_object,
+                                uint8_t* d_action, uint64_t* h_step_counts, size_t max_steps,
+                                uint64_t* out_steps, void* stream);
+/* Same with every array in host memory (the DB layer's side of the boundary: keys and
+ * per-file status come from sd_cas_generate_cas_ids_from_paths, the decisions go into the
+ * create_many / link batches).  h_state NULL = every row hashed.  Blocking. */
+int sd_cas_identifier_links(sd_cas_ctx* ctx, const uint64_t* h_keys, const uint8_t* h_state,
+                            size_t n, uint32_t chunk, uint32_t* h_step, uint32_t* h_object,
+                            uint8_t* h_action, uint64_t* h_step_counts, size_t max_steps,
+                            uint64_t* out_steps);
+
 /* Stable LSD radix sort of (u64 key, u32 val) on bits [begin_bit, end_bit).
  * d_vals_in == NULL sorts the identity 0..n-1. */
 int sd_cas_sort_pairs_dev(sd_cas_ctx* ctx, const uint64_t* d_keys_in, const uint32_t* d_vals_in,

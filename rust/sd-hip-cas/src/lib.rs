@@ -1,26 +1,130 @@
-//! Safe wrapper over libsd_hip_cas: the batched drop-in for
-//! `generate_cas_id` (core/src/object/cas.rs:23-62) and `file_checksum`
-//! (core/src/object/validation/hash.rs:11-25).  See INTEGRATION.md.
-use std::{ffi::{c_char, c_int, c_void, CStr, CString}, io, path::Path, ptr};
+//! Safe wrapper over libsd_hip_cas: the batched drop-in for `generate_cas_id`
+//! (core/src/object/cas.rs:23-62), the Object-link decisions of the file identifier job
+//! (core/src/object/file_identifier/file_identifier_job.rs:180-236, mod.rs:98-350) and
+//! `file_checksum` (core/src/object/validation/hash.rs:11-25).  See INTEGRATION.md.
+//!
+//! The `extern "C"` block declares every entry point of include/sd_hip_cas.h;
+//! tests/test_rust_binding.py checks it against the header (names, argument and return
+//! types) on every CPU test run, since cargo is not available where this repo is built.
+#![allow(non_camel_case_types)]
+use std::{
+    ffi::{c_char, c_int, c_void, CStr, CString},
+    io,
+    path::Path,
+    ptr,
+};
 
 #[repr(C)]
 pub struct sd_cas_ctx {
     _p: [u8; 0],
 }
 
+#[repr(C)]
+pub struct sd_cas_multi {
+    _p: [u8; 0],
+}
+
+pub const SD_CAS_ROW_HASHED: u8 = 0;
+pub const SD_CAS_ROW_NO_CAS: u8 = 1;
+pub const SD_CAS_ROW_ERROR: u8 = 2;
+pub const SD_CAS_LINK_CREATED: u8 = 0;
+pub const SD_CAS_LINK_LINKED: u8 = 1;
+pub const SD_CAS_LINK_DROPPED: u8 = 2;
+pub const SD_CAS_LINK_NOT_REACHED: u8 = 3;
+pub const SD_CAS_NO_OBJECT: u32 = 0xFFFF_FFFF;
+pub const SD_CAS_CHUNK_SIZE: u32 = 100;
+
 extern "C" {
-    fn sd_cas_ctx_create(device: c_int, out: *mut *mut sd_cas_ctx) -> c_int;
-    fn sd_cas_ctx_destroy(ctx: *mut sd_cas_ctx);
-    fn sd_cas_last_error(ctx: *const sd_cas_ctx) -> *const c_char;
-    fn sd_cas_generate_cas_ids(ctx: *mut sd_cas_ctx, bufs: *const *const u8, buf_lens: *const u64,
-                               sizes: *const u64, n: usize, out_keys: *mut u64) -> c_int;
-    fn sd_cas_generate_cas_ids_from_paths(ctx: *mut sd_cas_ctx, paths: *const *const c_char,
-                                          sizes: *const u64, n: usize, out_keys: *mut u64,
-                                          status: *mut i32) -> c_int;
-    fn sd_cas_file_checksum(ctx: *mut sd_cas_ctx, path: *const c_char, out_hex: *mut c_char,
-                            err_no: *mut c_int) -> c_int;
-    fn sd_cas_group_dev(ctx: *mut sd_cas_ctx, d_keys: *const u64, n: usize, d_rep: *mut u32,
-                        out_objects: *mut u64, stream: *mut c_void) -> c_int;
+    pub fn sd_cas_abi_version() -> c_int;
+    pub fn sd_cas_ctx_create(device: c_int, out: *mut *mut sd_cas_ctx) -> c_int;
+    pub fn sd_cas_ctx_destroy(ctx: *mut sd_cas_ctx);
+    pub fn sd_cas_last_error(ctx: *const sd_cas_ctx) -> *const c_char;
+    pub fn sd_cas_ctx_stream(ctx: *mut sd_cas_ctx) -> *mut c_void;
+    pub fn sd_cas_synchronize(ctx: *mut sd_cas_ctx) -> c_int;
+    pub fn sd_cas_batch_quantum(ctx: *const sd_cas_ctx) -> usize;
+    pub fn sd_cas_set_latency_threshold(ctx: *mut sd_cas_ctx, sampled_files: usize, packed_files: usize);
+    pub fn sd_cas_set_chunkpar_split(ctx: *mut sd_cas_ctx, sampled_files: usize, packed_files: usize);
+    pub fn sd_cas_set_group_method(ctx: *mut sd_cas_ctx, method: c_int, bucket_target: u64) -> c_int;
+    pub fn sd_cas_alloc_pinned(ctx: *mut sd_cas_ctx, bytes: usize, out: *mut *mut c_void) -> c_int;
+    pub fn sd_cas_free_pinned(ctx: *mut sd_cas_ctx, p: *mut c_void) -> c_int;
+    pub fn sd_cas_generate_cas_ids(ctx: *mut sd_cas_ctx, bufs: *const *const u8, buf_lens: *const u64,
+                                   sizes: *const u64, n: usize, out_keys: *mut u64) -> c_int;
+    pub fn sd_cas_generate_cas_ids_from_paths(ctx: *mut sd_cas_ctx, paths: *const *const c_char,
+                                              sizes: *const u64, n: usize, out_keys: *mut u64,
+                                              status: *mut i32) -> c_int;
+    pub fn sd_cas_hash_sampled_host(ctx: *mut sd_cas_ctx, h_content: *const c_void, stride: u64,
+                                    h_sizes: *const u64, n: usize, h_keys: *mut u64,
+                                    batch_files: usize) -> c_int;
+    pub fn sd_cas_hash_sampled_host_ring(ctx: *mut sd_cas_ctx, h_ring: *const c_void, stride: u64,
+                                         ring_files: usize, h_sizes: *const u64, n: usize,
+                                         h_keys: *mut u64, batch_files: usize) -> c_int;
+    pub fn sd_cas_key_to_hex(key: u64, out: *mut c_char);
+    pub fn sd_cas_hash_sampled_dev(ctx: *mut sd_cas_ctx, d_content: *const c_void, stride: u64,
+                                   d_sizes: *const u64, n: usize, d_keys: *mut u64,
+                                   stream: *mut c_void) -> c_int;
+    pub fn sd_cas_hash_packed_dev(ctx: *mut sd_cas_ctx, d_arena: *const c_void, d_offs: *const u64,
+                                  d_lens: *const u32, d_sizes: *const u64, n: usize, d_keys: *mut u64,
+                                  stream: *mut c_void) -> c_int;
+    pub fn sd_cas_group_dev(ctx: *mut sd_cas_ctx, d_keys: *const u64, n: usize, d_rep: *mut u32,
+                            out_objects: *mut u64, stream: *mut c_void) -> c_int;
+    pub fn sd_cas_group_min_dev(ctx: *mut sd_cas_ctx, d_keys: *const u64, d_vals: *const u32, n: usize,
+                                d_out: *mut u32, out_objects: *mut u64, stream: *mut c_void) -> c_int;
+    pub fn sd_cas_partition_dev(ctx: *mut sd_cas_ctx, d_keys: *const u64, n: usize, parts: u32,
+                                d_keys_out: *mut u64, d_pos_out: *mut u32, d_counts: *mut u64,
+                                stream: *mut c_void) -> c_int;
+    pub fn sd_cas_exchange_pack_dev(ctx: *mut sd_cas_ctx, d_keys: *const u64, d_pos: *const u32,
+                                    n: usize, file0: u64, d_rows: *mut u32, stream: *mut c_void) -> c_int;
+    pub fn sd_cas_exchange_split_dev(ctx: *mut sd_cas_ctx, d_rows: *const u32, m: usize,
+                                     d_keys: *mut u64, d_vals: *mut u32, stream: *mut c_void) -> c_int;
+    pub fn sd_cas_exchange_unpack_dev(ctx: *mut sd_cas_ctx, d_back: *const u32, d_pos: *const u32,
+                                      n: usize, d_rep: *mut u64, stream: *mut c_void) -> c_int;
+    pub fn sd_cas_group_sorted_dev(ctx: *mut sd_cas_ctx, d_sorted_keys: *const u64,
+                                   d_sorted_vals: *const u32, n: usize, d_rep: *mut u32,
+                                   out_objects: *mut u64, stream: *mut c_void) -> c_int;
+    pub fn sd_cas_group_chunked_dev(ctx: *mut sd_cas_ctx, d_rep: *const u32, n: usize, chunk: u32,
+                                    d_rep_chunked: *mut u32, out_created: *mut u64,
+                                    out_linked: *mut u64, stream: *mut c_void) -> c_int;
+    pub fn sd_cas_identifier_max_steps(n: usize, chunk: u32) -> usize;
+    pub fn sd_cas_identifier_links_dev(ctx: *mut sd_cas_ctx, d_keys: *const u64, d_state: *const u8,
+                                       n: usize, chunk: u32, d_step: *mut u32, d_object: *mut u32,
+                                       d_action: *mut u8, h_step_counts: *mut u64, max_steps: usize,
+                                       out_steps: *mut u64, stream: *mut c_void) -> c_int;
+    pub fn sd_cas_identifier_links(ctx: *mut sd_cas_ctx, h_keys: *const u64, h_state: *const u8,
+                                   n: usize, chunk: u32, h_step: *mut u32, h_object: *mut u32,
+                                   h_action: *mut u8, h_step_counts: *mut u64, max_steps: usize,
+                                   out_steps: *mut u64) -> c_int;
+    pub fn sd_cas_sort_pairs_dev(ctx: *mut sd_cas_ctx, d_keys_in: *const u64, d_vals_in: *const u32,
+                                 n: usize, d_keys_out: *mut u64, d_vals_out: *mut u32, begin_bit: c_int,
+                                 end_bit: c_int, stream: *mut c_void) -> c_int;
+    pub fn sd_cas_checksum_dev(ctx: *mut sd_cas_ctx, d_data: *const c_void, len: u64, out: *mut u8,
+                               stream: *mut c_void) -> c_int;
+    pub fn sd_cas_file_checksum(ctx: *mut sd_cas_ctx, path: *const c_char, out_hex: *mut c_char,
+                                err_no: *mut c_int) -> c_int;
+    pub fn sd_cas_multi_create(devices: *const c_int, ndev: c_int, out: *mut *mut sd_cas_multi) -> c_int;
+    pub fn sd_cas_multi_destroy(m: *mut sd_cas_multi);
+    pub fn sd_cas_multi_count(m: *const sd_cas_multi) -> c_int;
+    pub fn sd_cas_multi_ctx(m: *mut sd_cas_multi, i: c_int) -> *mut sd_cas_ctx;
+    pub fn sd_cas_multi_last_error(m: *const sd_cas_multi) -> *const c_char;
+    pub fn sd_cas_multi_group(m: *mut sd_cas_multi, d_keys: *const *const u64, n: *const usize,
+                              file0: *const u64, d_rep: *const *mut u64, out_objects: *mut u64) -> c_int;
+    pub fn sd_cas_multi_hash_group_sampled_host(m: *mut sd_cas_multi, h_content: *const c_void,
+                                                stride: u64, h_sizes: *const u64, n: usize,
+                                                h_keys: *mut u64, h_rep: *mut u64,
+                                                out_objects: *mut u64) -> c_int;
+    pub fn sd_cas_synth_sampled_dev(ctx: *mut sd_cas_ctx, seed: u64, file0: u64, n: usize,
+                                    dup_permille: u32, d_content: *mut c_void, stride: u64,
+                                    d_sizes: *mut u64, stream: *mut c_void) -> c_int;
+    pub fn sd_cas_synth_small_dev(ctx: *mut sd_cas_ctx, seed: u64, file0: u64, n: usize,
+                                  dup_permille: u32, d_sizes: *mut u64, d_lens: *mut u32,
+                                  d_offs: *mut u64, d_arena: *mut c_void, out_arena_bytes: *mut u64,
+                                  stream: *mut c_void) -> c_int;
+    pub fn sd_cas_synth_small_content_dev(ctx: *mut sd_cas_ctx, seed: u64, file0: u64, n: usize,
+                                          dup_permille: u32, d_offs: *const u64, d_lens: *const u32,
+                                          d_arena: *mut c_void, stream: *mut c_void) -> c_int;
+    pub fn sd_cas_synth_stream_dev(ctx: *mut sd_cas_ctx, seed: u64, file: u64, byte_off: u64,
+                                   len: u64, d_out: *mut c_void, stream: *mut c_void) -> c_int;
+    pub fn sd_cas_synth_roots_dev(ctx: *mut sd_cas_ctx, seed: u64, file0: u64, n: usize,
+                                  dup_permille: u32, d_roots: *mut u64, stream: *mut c_void) -> c_int;
 }
 
 /// A cas_id: the big-endian u64 of BLAKE3(le64(size) || content)[0..8].
@@ -32,6 +136,27 @@ impl std::fmt::Display for CasId {
     fn fmt(&self, f: &mut std::fmt::Formatter<'_>) -> std::fmt::Result {
         write!(f, "{:016x}", self.0)
     }
+}
+
+/// What happens to one orphan row in the job (sd_cas_identifier_links).
+#[derive(Clone, Copy, Debug, PartialEq, Eq)]
+pub enum RowState {
+    /// cas_id computed
+    Hashed(CasId),
+    /// fs::metadata length 0: no cas_id, its own Object (mod.rs:78-86)
+    NoCas,
+    /// FileMetadata::new failed: logged and dropped from the step (mod.rs:125-141)
+    Error,
+}
+
+/// One job step's DB batches (mod.rs:157-347): `creates` feed `create_many` + the link
+/// updates of the new Objects, `links` connect rows to the Object created for `.1`.
+#[derive(Clone, Debug, Default, PartialEq, Eq)]
+pub struct StepBatch {
+    pub creates: Vec<usize>,
+    pub links: Vec<(usize, usize)>,
+    pub total_created: u64,
+    pub total_linked: u64,
 }
 
 /// One context per (job thread, device).  Not Sync; Send is fine.
@@ -97,6 +222,45 @@ impl HipCas {
             .collect())
     }
 
+    /// The Object decisions of a whole file-identifier job over `rows` (orphan file_paths in
+    /// ascending id order, fresh library), `chunk` rows per step with the reference's cursor:
+    /// the batches each step hands to the DB (file_identifier_job.rs:180-236, mod.rs:157-347).
+    pub fn identifier_links(&mut self, rows: &[RowState], chunk: u32) -> io::Result<Vec<StepBatch>> {
+        let n = rows.len();
+        let keys: Vec<u64> = rows.iter().map(|r| if let RowState::Hashed(k) = r { k.0 } else { 0 }).collect();
+        let state: Vec<u8> = rows
+            .iter()
+            .map(|r| match r {
+                RowState::Hashed(_) => SD_CAS_ROW_HASHED,
+                RowState::NoCas => SD_CAS_ROW_NO_CAS,
+                RowState::Error => SD_CAS_ROW_ERROR,
+            })
+            .collect();
+        let max_steps = unsafe { sd_cas_identifier_max_steps(n, chunk) };
+        let (mut step, mut object, mut action) = (vec![0u32; n], vec![0u32; n], vec![0u8; n]);
+        let mut counts = vec![0u64; 2 * max_steps.max(1)];
+        let mut steps = 0u64;
+        let rc = unsafe {
+            sd_cas_identifier_links(self.ctx, keys.as_ptr(), state.as_ptr(), n, chunk, step.as_mut_ptr(),
+                                    object.as_mut_ptr(), action.as_mut_ptr(), counts.as_mut_ptr(),
+                                    max_steps, &mut steps)
+        };
+        if rc != 0 {
+            return Err(self.err(rc));
+        }
+        let mut out: Vec<StepBatch> = (0..steps as usize)
+            .map(|k| StepBatch { total_created: counts[2 * k], total_linked: counts[2 * k + 1], ..Default::default() })
+            .collect();
+        for i in 0..n {
+            match action[i] {
+                SD_CAS_LINK_CREATED => out[step[i] as usize].creates.push(i),
+                SD_CAS_LINK_LINKED => out[step[i] as usize].links.push((i, object[i] as usize)),
+                _ => {}
+            }
+        }
+        Ok(out)
+    }
+
     /// `file_checksum(path)` (validation/hash.rs:11).
     pub fn file_checksum(&mut self, path: &Path) -> io::Result<String> {
         let c = CString::new(path.as_os_str().as_encoded_bytes()).expect("NUL in path");
@@ -125,6 +289,22 @@ impl HipCas {
             return Err(self.err(rc));
         }
         Ok(objects)
+    }
+
+    /// The 100-row chunk replay of a canonical grouping (`sd_cas_group_chunked_dev`):
+    /// returns the summed (total_created, total_linked) of mod.rs:349.
+    ///
+    /// # Safety
+    /// `d_rep` / `d_rep_chunked` must point to `n` u32 in device memory of this context's GPU.
+    pub unsafe fn group_chunked_dev(&mut self, d_rep: *const u32, n: usize, chunk: u32,
+                                    d_rep_chunked: *mut u32) -> io::Result<(u64, u64)> {
+        let (mut created, mut linked) = (0u64, 0u64);
+        let rc = sd_cas_group_chunked_dev(self.ctx, d_rep, n, chunk, d_rep_chunked, &mut created,
+                                          &mut linked, ptr::null_mut());
+        if rc != 0 {
+            return Err(self.err(rc));
+        }
+        Ok((created, linked))
     }
 }
 

@@ -49,6 +49,9 @@ SIGNATURES = [
     ("sd_cas_exchange_unpack_dev", _i, [_vp, _vp, _vp, _sz, _vp, _vp]),
     ("sd_cas_group_sorted_dev", _i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     ("sd_cas_group_chunked_dev", _i, [_vp, _vp, _sz, _u32, _vp, _vp, _vp, _vp]),
+    ("sd_cas_identifier_max_steps", _sz, [_sz, _u32]),
+    ("sd_cas_identifier_links_dev", _i, [_vp, _vp, _vp, _sz, _u32, _vp, _vp, _vp, _vp, _sz, _vp, _vp]),
+    ("sd_cas_identifier_links", _i, [_vp, _vp, _vp, _sz, _u32, _vp, _vp, _vp, _vp, _sz, _vp]),
     ("sd_cas_sort_pairs_dev", _i, [_vp, _vp, _vp, _sz, _vp, _vp, _i, _i, _vp]),
     ("sd_cas_checksum_dev", _i, [_vp, _vp, _u64, _vp, _vp]),
     ("sd_cas_file_checksum", _i, [_vp, _cp, _cp, ctypes.POINTER(_i)]),

@@ -282,6 +282,48 @@ class CasEngine:
                                                      ctypes.byref(ln), _stream(stream)), "group_chunked")
         return int(c.value), int(ln.value)
 
+    def identifier_links(self, keys, state=None, chunk: int = CHUNK_SIZE,
+                         stream: Optional[int] = None):
+        """Object-link emission of one file-identifier job over the rows (ascending
+        file_path.id) — sd_cas_identifier_links_dev: returns (step, object, action) device
+        tensors (int32, int32, uint8) and the per-step (created, linked) counts as an
+        int64 numpy array [steps, 2].  state: uint8 ROW_* per row (None = all hashed)."""
+        import torch
+        n = int(keys.numel())
+        dev = keys.device
+        step = torch.empty(n, dtype=torch.int32, device=dev)
+        obj = torch.empty(n, dtype=torch.int32, device=dev)
+        act = torch.empty(n, dtype=torch.uint8, device=dev)
+        ms = int(self.L.sd_cas_identifier_max_steps(n, int(chunk)))
+        counts = np.zeros(2 * max(ms, 1), dtype=np.uint64)
+        steps = ctypes.c_uint64(0)
+        self._check(self.L.sd_cas_identifier_links_dev(
+            self.h, _ptr(keys), _ptr(state) if state is not None else None, n, int(chunk),
+            _ptr(step), _ptr(obj), _ptr(act), _np_ptr(counts), ms, ctypes.byref(steps),
+            _stream(stream)), "identifier_links")
+        k = int(steps.value)
+        return step, obj, act, counts[:2 * k].reshape(k, 2).astype(np.int64)
+
+    def identifier_links_host(self, keys: np.ndarray, state: Optional[np.ndarray] = None,
+                              chunk: int = CHUNK_SIZE):
+        """sd_cas_identifier_links (host arrays): (step u32, object u32, action u8, counts
+        int64 [steps, 2]) — the DB layer's view of the same emission."""
+        n = len(keys)
+        k = np.ascontiguousarray(keys, dtype=np.uint64)
+        st = None if state is None else np.ascontiguousarray(state, dtype=np.uint8)
+        step = np.zeros(n, dtype=np.uint32)
+        obj = np.zeros(n, dtype=np.uint32)
+        act = np.zeros(n, dtype=np.uint8)
+        ms = int(self.L.sd_cas_identifier_max_steps(n, int(chunk)))
+        counts = np.zeros(2 * max(ms, 1), dtype=np.uint64)
+        steps = ctypes.c_uint64(0)
+        self._check(self.L.sd_cas_identifier_links(
+            self.h, _np_ptr(k), _np_ptr(st) if st is not None else None, n, int(chunk),
+            _np_ptr(step), _np_ptr(obj), _np_ptr(act), _np_ptr(counts), ms, ctypes.byref(steps)),
+            "identifier_links")
+        s = int(steps.value)
+        return step, obj, act, counts[:2 * s].reshape(s, 2).astype(np.int64)
+
     def sort_pairs(self, keys_in, vals_in, keys_out, vals_out, begin_bit: int = 0,
                    end_bit: int = 64, stream: Optional[int] = None) -> None:
         n = int(keys_in.numel())
@@ -366,27 +408,45 @@ class FileMetadata:
     size: int
 
 
+ROW_HASHED, ROW_NO_CAS, ROW_ERROR = 0, 1, 2                          # SD_CAS_ROW_*
+LINK_CREATED, LINK_LINKED, LINK_DROPPED, LINK_NOT_REACHED = 0, 1, 2, 3  # SD_CAS_LINK_*
+
+
+@dataclass
+class StepBatch:
+    """One job step's DB batches as identifier_job_step issues them (mod.rs:157-347)."""
+    step: int
+    creates: list = field(default_factory=list)   # rows getting a new Object (create_many)
+    links: list = field(default_factory=list)     # (row, row owning the existing Object)
+    total_created: int = 0                        # mod.rs:349 (total_created, total_linked)
+    total_linked: int = 0
+
+
 @dataclass
 class StepResult:
-    """What identifier_job_step (mod.rs:98-350) decides for one batch of file_paths."""
+    """What one file-identifier job (file_identifier_job.rs:180-236 over identifier_job_step,
+    mod.rs:98-350) decides for its orphan file_paths."""
     metadata: dict = field(default_factory=dict)   # idx -> FileMetadata (errors dropped)
     object_of: dict = field(default_factory=dict)  # idx -> idx of the file owning its Object
     total_created: int = 0
     total_linked: int = 0
     errors: dict = field(default_factory=dict)     # idx -> errno (logged + dropped, :125-141)
+    steps: list = field(default_factory=list)      # StepBatch per executed step
+    not_reached: list = field(default_factory=list)  # rows past the job's last step
 
 
 def identifier_job_step(paths: Sequence[str], chunk: int = CHUNK_SIZE,
                         eng: Optional[CasEngine] = None) -> StepResult:
-    """Run the file identifier over ``paths`` (ascending file_path.id order) on a fresh
-    library, CHUNK_SIZE rows per step, as mod.rs:98-350 would: cas_ids from the GPU,
-    Objects from the GPU grouping in its chunk-replay form (HashMap order := ascending
-    idx).  Empty files get no cas_id and their own Object (mod.rs:78-86,
-    :246-311).  Returns the per-file decisions and the summed (created, linked)."""
-    import torch
-
+    """Run the file identifier over ``paths`` (ascending file_path.id order, all orphan) on a
+    fresh library, as file_identifier_job.rs:180-236 / mod.rs:98-350 would: fs::metadata
+    per row (mod.rs:63), cas_ids from the GPU (len 0 -> no cas_id, mod.rs:78-86; an I/O
+    error drops the row, :125-141), and the Object decisions of every step from the GPU
+    link emission (sd_cas_identifier_links: grouping + the cursor walk, a last row that
+    stays orphan is queried again by the next step).  Returns the per-file decisions, the
+    per-step batches and the summed (created, linked)."""
     eng = eng or engine()
     res = StepResult()
+    n = len(paths)
     sizes = []
     for i, p in enumerate(paths):
         try:
@@ -394,40 +454,40 @@ def identifier_job_step(paths: Sequence[str], chunk: int = CHUNK_SIZE,
         except OSError as e:
             res.errors[i] = e.errno
             sizes.append(-1)
-    live = [i for i in range(len(paths)) if sizes[i] > 0]
+    live = [i for i in range(n) if sizes[i] > 0]
     keys, errs = eng.generate_cas_keys_from_paths([paths[i] for i in live], [sizes[i] for i in live])
+    all_keys = np.zeros(n, dtype=np.uint64)
+    state = np.full(n, ROW_NO_CAS, dtype=np.uint8)
     for j, i in enumerate(live):
         if errs[j]:
             res.errors[i] = int(errs[j])
-    for i in range(len(paths)):
-        if i in res.errors:
-            continue
-        res.metadata[i] = FileMetadata(None, sizes[i])  # cas_id filled below for hashed files
-    ok = [j for j, i in enumerate(live) if not errs[j]]
-    for j in ok:
-        res.metadata[live[j]].cas_id = key_to_cas_id(keys[j])
-    # rows that survive into the step, in id order (errors are dropped from the chunk but
-    # still occupy their row of the 100-row query, so chunk membership uses the row index)
-    rows = sorted(res.metadata)
-    hashed = [i for i in rows if res.metadata[i].cas_id is not None]
-    if hashed:
-        dev = torch.device("cuda", eng.device)
-        # key per hashed file; rows without cas are not grouped (each gets its own Object)
-        k = torch.tensor(np.array([cas_id_to_key(res.metadata[i].cas_id) for i in hashed],
-                                  dtype=np.uint64).view(np.int64), device=dev)
-        rep = torch.empty(len(hashed), dtype=torch.int32, device=dev)
-        eng.group(k, rep)
-        rep = rep.cpu().numpy().astype(np.int64)
-        canon = {hashed[a]: hashed[int(rep[a])] for a in range(len(hashed))}
-    else:
-        canon = {}
-    for i in rows:
-        if i in canon and canon[i] // chunk != i // chunk:
-            res.object_of[i] = canon[i]
-            res.total_linked += 1
         else:
-            res.object_of[i] = i
-            res.total_created += 1
+            all_keys[i] = keys[j]
+            state[i] = ROW_HASHED
+    for i in res.errors:
+        state[i] = ROW_ERROR
+    if n == 0:
+        return res
+    step, obj, act, counts = eng.identifier_links_host(all_keys, state, chunk)
+    res.steps = [StepBatch(k, total_created=int(c), total_linked=int(ln))
+                 for k, (c, ln) in enumerate(counts)]
+    for i in range(n):
+        a = int(act[i])
+        if a == LINK_NOT_REACHED:
+            res.not_reached.append(i)
+            continue
+        if a == LINK_DROPPED:
+            continue
+        res.metadata[i] = FileMetadata(key_to_cas_id(all_keys[i]) if state[i] == ROW_HASHED else None,
+                                       sizes[i])
+        res.object_of[i] = int(obj[i])
+        b = res.steps[int(step[i])]
+        if a == LINK_CREATED:
+            b.creates.append(i)
+        else:
+            b.links.append((i, int(obj[i])))
+    res.total_created = int(counts[:, 0].sum()) if len(counts) else 0
+    res.total_linked = int(counts[:, 1].sum()) if len(counts) else 0
     return res
 
 

@@ -83,6 +83,7 @@ struct sd_cas_ctx {
   DevBuf staging;  // device copy of a host batch
   DevBuf small;    // multi-device exchange buffers (sd_cas_multi_*)
   DevBuf cvbuf;    // file_checksum: one 32-B CV per 64 MiB segment
+  DevBuf io;       // device copies of host arrays (sd_cas_identifier_links)
   void* pinned = nullptr;
   size_t pinned_bytes = 0;
   uint64_t* d_scalar = nullptr;  // 8 x u64 scratch for counters

@@ -27,6 +27,7 @@
 #include "sd_checksum.h"
 #include "sd_group.h"
 #include "sd_kernels.h"
+#include "sd_links.h"
 #include "sd_synth.h"
 
 using namespace sdcas;
@@ -105,6 +106,7 @@ void sd_cas_ctx_destroy(sd_cas_ctx* c) {
   if (c->staging.p) (void)hipFree(c->staging.p);
   if (c->small.p) (void)hipFree(c->small.p);
   if (c->cvbuf.p) (void)hipFree(c->cvbuf.p);
+  if (c->io.p) (void)hipFree(c->io.p);
   if (c->d_scalar) (void)hipFree(c->d_scalar);
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->h2d_done) (void)hipEventDestroy(c->h2d_done);
@@ -357,6 +359,145 @@ int sd_cas_group_chunked_dev(sd_cas_ctx* c, const uint32_t* d_rep, size_t n, uin
   HIP_TRY(c, hipStreamSynchronize(s));
   if (out_created) *out_created = created;
   if (out_linked) *out_linked = n - created;
+  return SD_CAS_OK;
+}
+
+// ---- Object-link emission (file_identifier_job.rs:180-236, mod.rs:98-350) -------------
+
+static_assert(SD_CAS_ROW_HASHED == SD_LINKS_HASHED && SD_CAS_ROW_NO_CAS == SD_LINKS_NO_CAS &&
+                  SD_CAS_ROW_ERROR == SD_LINKS_ERROR && SD_CAS_LINK_CREATED == SD_LINKS_CREATED &&
+                  SD_CAS_LINK_LINKED == SD_LINKS_LINKED && SD_CAS_LINK_DROPPED == SD_LINKS_DROPPED &&
+                  SD_CAS_LINK_NOT_REACHED == SD_LINKS_NOT_REACHED &&
+                  SD_CAS_NO_STEP == SD_LINKS_NO_STEP && SD_CAS_NO_OBJECT == SD_LINKS_NO_OBJECT,
+              "link constants");
+
+size_t sd_cas_identifier_max_steps(size_t n, uint32_t chunk) {
+  return chunk ? (n + chunk - 1) / chunk : 0;
+}
+
+int sd_cas_identifier_links_dev(sd_cas_ctx* c, const uint64_t* d_keys, const uint8_t* d_state,
+                                size_t n, uint32_t chunk, uint32_t* d_step, uint32_t* d_object,
+                                uint8_t* d_action, uint64_t* h_step_counts, size_t max_steps,
+                                uint64_t* out_steps, void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  const size_t steps_total = sd_cas_identifier_max_steps(n, chunk);
+  if (chunk == 0 || n >= (1ull << 32) || !out_steps || max_steps < steps_total ||
+      (n && (!d_keys || !d_step || !d_object || !d_action || !h_step_counts)))
+    return fail(c, SD_CAS_EINVAL, "identifier_links: bad arguments");
+  *out_steps = 0;
+  for (size_t k = 0; k < 2 * steps_total; k++) h_step_counts[k] = 0;
+  if (n == 0) return SD_CAS_OK;
+  hipStream_t s = pick(c, stream);
+  // staging (this call is blocking): rep | hkeys | hrows | minrow | orphans | starts | counts | 2 counters
+  const size_t b_rep = up256(n * 4), b_hk = up256(n * 8), b_hr = up256(n * 4), b_mr = up256(n * 4),
+               b_or = up256(n * 8), b_st = up256((steps_total + 1) * 4), b_ct = up256(steps_total * 8);
+  int rc = ensure(c, c->staging, b_rep + b_hk + b_hr + b_mr + b_or + b_st + b_ct + 256);
+  if (rc) return rc;
+  char* p = (char*)c->staging.p;
+  uint32_t* rep = (uint32_t*)p; p += b_rep;
+  uint64_t* hkeys = (uint64_t*)p; p += b_hk;
+  uint32_t* hrows = (uint32_t*)p; p += b_hr;
+  uint32_t* minrow = (uint32_t*)p; p += b_mr;
+  uint64_t* orphans = (uint64_t*)p; p += b_or;
+  uint32_t* starts = (uint32_t*)p; p += b_st;
+  uint32_t* counts = (uint32_t*)p; p += b_ct;
+  uint64_t* counters = (uint64_t*)p;
+  // 1. grouping over the hashed rows (rep = the key's first row), and the rows that stay
+  //    orphan after being processed (they steer the cursor)
+  std::vector<uint64_t> stay;  // row << 8 | state, ascending
+  if (d_state) {
+    uint64_t cnt[2] = {0, 0};
+    HIP_TRY(c, hipMemsetAsync(counters, 0, 16, s));
+    HIP_TRY(c, links_split(d_keys, d_state, n, hkeys, hrows, counters, orphans, counters + 1, s));
+    HIP_TRY(c, hipMemcpyAsync(cnt, counters, 16, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    stay.resize(cnt[1]);
+    if (cnt[1]) {
+      HIP_TRY(c, hipMemcpyAsync(stay.data(), orphans, cnt[1] * 8, hipMemcpyDeviceToHost, s));
+    }
+    if (cnt[0]) {
+      if ((rc = sd_cas_group_min_dev(c, hkeys, hrows, cnt[0], minrow, nullptr, s))) return rc;
+      HIP_TRY(c, links_scatter(minrow, hrows, cnt[0], rep, s));
+    }
+    HIP_TRY(c, hipStreamSynchronize(s));
+    std::sort(stay.begin(), stay.end());
+  } else {
+    if ((rc = sd_cas_group_dev(c, d_keys, n, rep, nullptr, s))) return rc;
+  }
+  // 2. the cursor walk (host; O(steps + orphans)): step k covers [start, start + chunk);
+  //    the next cursor is its last row, which the next query returns again iff it is
+  //    still orphan; an empty query ends the job
+  auto stays = [&](uint64_t row, uint8_t* st) {
+    auto it = std::lower_bound(stay.begin(), stay.end(), row << 8);
+    if (it == stay.end() || (*it >> 8) != row) return false;
+    *st = (uint8_t)(*it & 0xFF);
+    return true;
+  };
+  std::vector<uint32_t> h_starts;
+  h_starts.reserve(steps_total + 1);
+  std::vector<uint64_t> extra(steps_total, 0);  // re-queried empty rows: one creation per step
+  uint64_t start = 0, reached = 0;
+  for (size_t k = 0; k < steps_total && start < n; k++) {
+    h_starts.push_back((uint32_t)start);
+    const uint64_t end = std::min<uint64_t>(start + chunk, n), last = end - 1;
+    reached = end;
+    uint8_t st = 0;
+    if (stays(last, &st)) {
+      if (st == SD_CAS_ROW_NO_CAS && k + 1 < steps_total) extra[k] += 1;
+      start = last;
+    } else {
+      start = end;
+    }
+  }
+  const size_t nsteps = h_starts.size();
+  h_starts.push_back(0xFFFFFFFFu);  // sentinel
+  // 3. per-row decisions + per-step counts (device)
+  HIP_TRY(c, hipMemcpyAsync(starts, h_starts.data(), h_starts.size() * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemsetAsync(counts, 0, std::max<size_t>(nsteps, 1) * 8, s));
+  HIP_TRY(c, links_decide(d_state, rep, n, starts, (uint32_t)nsteps, reached, d_step, d_object,
+                          d_action, counts, s));
+  std::vector<uint32_t> hc(2 * std::max<size_t>(nsteps, 1));
+  HIP_TRY(c, hipMemcpyAsync(hc.data(), counts, hc.size() * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  for (size_t k = 0; k < nsteps; k++) {
+    h_step_counts[2 * k] = hc[2 * k] + extra[k];
+    h_step_counts[2 * k + 1] = hc[2 * k + 1];
+  }
+  *out_steps = nsteps;
+  return SD_CAS_OK;
+}
+
+int sd_cas_identifier_links(sd_cas_ctx* c, const uint64_t* h_keys, const uint8_t* h_state,
+                            size_t n, uint32_t chunk, uint32_t* h_step, uint32_t* h_object,
+                            uint8_t* h_action, uint64_t* h_step_counts, size_t max_steps,
+                            uint64_t* out_steps) {
+  if (!c) return SD_CAS_EINVAL;
+  if (n && (!h_keys || !h_step || !h_object || !h_action))
+    return fail(c, SD_CAS_EINVAL, "identifier_links: bad arguments");
+  if (n == 0 || n >= (1ull << 32))
+    return sd_cas_identifier_links_dev(c, nullptr, nullptr, n, chunk, nullptr, nullptr, nullptr,
+                                       h_step_counts, max_steps, out_steps, c->stream);
+  HIP_TRY(c, hipSetDevice(c->device));
+  // device copies (c->io): keys | state | step | object | action
+  const size_t bk = up256(n * 8), bs = up256(n), b4 = up256(n * 4);
+  int rc = ensure(c, c->io, bk + 2 * bs + 2 * b4);
+  if (rc) return rc;
+  char* p = (char*)c->io.p;
+  uint64_t* d_keys = (uint64_t*)p; p += bk;
+  uint8_t* d_state = h_state ? (uint8_t*)p : nullptr; p += bs;
+  uint32_t* d_step = (uint32_t*)p; p += b4;
+  uint32_t* d_object = (uint32_t*)p; p += b4;
+  uint8_t* d_action = (uint8_t*)p;
+  hipStream_t s = c->stream;
+  HIP_TRY(c, hipMemcpyAsync(d_keys, h_keys, n * 8, hipMemcpyHostToDevice, s));
+  if (h_state) HIP_TRY(c, hipMemcpyAsync(d_state, h_state, n, hipMemcpyHostToDevice, s));
+  rc = sd_cas_identifier_links_dev(c, d_keys, d_state, n, chunk, d_step, d_object, d_action,
+                                   h_step_counts, max_steps, out_steps, s);
+  if (rc) return rc;
+  HIP_TRY(c, hipMemcpyAsync(h_step, d_step, n * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipMemcpyAsync(h_object, d_object, n * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipMemcpyAsync(h_action, d_action, n, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
   return SD_CAS_OK;
 }
 

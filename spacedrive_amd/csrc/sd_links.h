@@ -1,0 +1,33 @@
+// sd_links.h — launchers of the Object-link emission kernels (links.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// row states / actions / sentinels: the same values as include/sd_hip_cas.h
+#define SD_LINKS_HASHED 0
+#define SD_LINKS_NO_CAS 1
+#define SD_LINKS_ERROR 2
+#define SD_LINKS_CREATED 0
+#define SD_LINKS_LINKED 1
+#define SD_LINKS_DROPPED 2
+#define SD_LINKS_NOT_REACHED 3
+#define SD_LINKS_NO_STEP 0xFFFFFFFFu
+#define SD_LINKS_NO_OBJECT 0xFFFFFFFFu
+
+namespace sdcas {
+
+// hashed rows -> (hkeys, hrows) (unordered), other rows -> orphans[] = row << 8 | state;
+// *d_hcount / *d_ocount (u64, zeroed by the caller) = counts
+hipError_t links_split(const uint64_t* keys, const uint8_t* state, uint64_t n, uint64_t* hkeys,
+                       uint32_t* hrows, uint64_t* d_hcount, uint64_t* orphans, uint64_t* d_ocount,
+                       hipStream_t s);
+// rep[hrows[i]] = minrow[i]
+hipError_t links_scatter(const uint32_t* minrow, const uint32_t* hrows, uint64_t m, uint32_t* rep,
+                         hipStream_t s);
+// per-row decisions; counts[2k], counts[2k+1] (u32, zeroed by the caller) += created, linked
+hipError_t links_decide(const uint8_t* state, const uint32_t* rep, uint64_t n,
+                        const uint32_t* starts, uint32_t nsteps, uint64_t reached,
+                        uint32_t* step_out, uint32_t* object_out, uint8_t* action_out,
+                        uint32_t* counts, hipStream_t s);
+
+}  // namespace sdcas

@@ -90,6 +90,84 @@ def replay_identifier(keys: list[int], chunk: int = 100):
     return rep_chunked, created_total, linked_total
 
 
+ROW_HASHED, ROW_NO_CAS, ROW_ERROR = 0, 1, 2
+LINK_CREATED, LINK_LINKED, LINK_DROPPED, LINK_NOT_REACHED = 0, 1, 2, 3
+NO_STEP = NO_OBJECT = 0xFFFFFFFF
+
+
+def replay_identifier_job(keys, states, chunk: int = 100):
+    """Literal replay of one file-identifier job over a fresh library, DB state included:
+    file_identifier_job.rs:86-178 (init: orphan count, ceil(n/chunk) steps, cursor = first
+    orphan id), :180-236 (execute_step: get_orphan_file_paths = orphan rows with id >=
+    cursor, ascending, LIMIT chunk (:251-319); an empty query ends the job), mod.rs:98-350
+    (identifier_job_step: FileMetadata per row, errors dropped; cas_id written; Objects
+    found by cas; links to the first; one new Object per remaining row, HashMap order :=
+    ascending row) and mod.rs:401-405 (the next cursor = the chunk's last row).
+    Rows: file_path ids 0..n-1, all orphan at init (object_id and cas_id NULL).
+    Returns (step[], object[], action[], [(created, linked)] per step) where object[i] is
+    the row that created the Object row i is connected to."""
+    n = len(keys)
+    cas_col = [None] * n         # file_path.cas_id
+    obj_col = [None] * n         # file_path.object_id
+    creator = []                 # Object table: id -> creating row
+    cas_objects = {}             # cas -> Object ids having a file_path with that cas, in id order
+    step = [NO_STEP] * n
+    processed_ok = [False] * n   # last processing of the row succeeded
+    processed = [False] * n
+    counts = []
+    cursor = 0
+    for k in range(-(-n // chunk) if chunk else 0):
+        rows = []
+        r = cursor
+        while r < n and len(rows) < chunk:          # orphan: object_id NULL or cas_id NULL
+            if obj_col[r] is None or cas_col[r] is None:
+                rows.append(r)
+            r += 1
+        if not rows:
+            break                                    # JobError::EarlyFinish
+        meta = {}
+        for r in rows:                               # FileMetadata::new (mod.rs:105-147)
+            step[r] = k
+            processed[r] = True
+            processed_ok[r] = states[r] != ROW_ERROR
+            if states[r] == ROW_ERROR:
+                continue
+            meta[r] = None if states[r] == ROW_NO_CAS else keys[r]
+        for r, c in meta.items():                    # cas_id write (mod.rs:157-178)
+            cas_col[r] = c
+        unique = {c for c in meta.values() if c is not None}
+        existing = {c: cas_objects[c] for c in unique if c in cas_objects}  # :181-198
+        linked = 0
+        for r in sorted(meta):                       # :202-238 link to the FIRST Object
+            c = meta[r]
+            if c is not None and c in existing:
+                obj_col[r] = existing[c][0]
+                linked += 1
+        created = 0
+        for r in sorted(meta):                       # :246-347 one new Object per remaining row
+            c = meta[r]
+            if c is None or c not in existing:
+                oid = len(creator)
+                creator.append(r)
+                obj_col[r] = oid
+                if c is not None:
+                    cas_objects.setdefault(c, []).append(oid)
+                created += 1
+        counts.append((created, linked))
+        cursor = rows[-1]                            # mod.rs:401-405
+    obj = [NO_OBJECT] * n
+    act = [LINK_NOT_REACHED] * n
+    for r in range(n):
+        if not processed[r]:
+            continue
+        if not processed_ok[r]:
+            act[r] = LINK_DROPPED
+            continue
+        obj[r] = creator[obj_col[r]]
+        act[r] = LINK_CREATED if obj[r] == r else LINK_LINKED
+    return step, obj, act, counts
+
+
 def canonical(keys: list[int]):
     first = {}
     rep = []

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 from oracle.pyoracle import MINIMUM_FILE_SIZE, SAMPLED_CONTENT_LEN, np_content, py_sample_plan
-from tests.golden.make_golden import canonical, gather_virtual, replay_identifier
+from tests.golden.make_golden import canonical, gather_virtual, replay_identifier, replay_identifier_job
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -683,19 +683,74 @@ def test_identifier_job_step(eng, oracle, tmp_path):
             p.write_bytes(blobs[int(rng.integers(0, len(blobs)))] if rng.random() < 0.5
                           else rng.integers(0, 256, int(rng.integers(1, 200_000)), dtype=np.uint8).tobytes())
         paths.append(str(p))
+    # an empty file at a chunk's last row (re-queried by the next step) and a missing one
+    open(paths[198], "wb").close()
+    os.unlink(paths[99])
     res = sd.identifier_job_step(paths, eng=eng)
-    keys = []
+    keys, states = [], []
     for p in paths:
+        if not os.path.exists(p):
+            keys.append(0); states.append(2)
+            continue
         size = os.path.getsize(p)
-        keys.append(None if size == 0 else int(oracle.generate_cas_id(p, size), 16))
-    for i, p in enumerate(paths):
-        want = None if keys[i] is None else f"{keys[i]:016x}"
+        keys.append(0 if size == 0 else int(oracle.generate_cas_id(p, size), 16))
+        states.append(1 if size == 0 else 0)
+    assert res.errors == {99: 2}
+    for i in range(len(paths)):
+        if i in res.errors:
+            continue
+        want = None if states[i] else f"{keys[i]:016x}"
         assert res.metadata[i].cas_id == want
-    # replay with unique sentinels for the cas-less rows (each gets its own Object)
-    rk = [k if k is not None else -(i + 1) for i, k in enumerate(keys)]
-    rc, created, linked = replay_identifier(rk, 100)
-    assert [res.object_of[i] for i in range(len(paths))] == rc
-    assert (res.total_created, res.total_linked) == (created, linked)
+    step, obj, act, counts = replay_identifier_job(keys, states, 100)
+    assert {i: o for i, (o, a) in enumerate(zip(obj, act)) if a in (0, 1)} == res.object_of
+    assert [(b.total_created, b.total_linked) for b in res.steps] == counts
+    assert (res.total_created, res.total_linked) == tuple(map(sum, zip(*counts)))
+    assert 99 in [r for b in res.steps for r in b.creates] or step[99] == 1  # re-queried row
+    for b in res.steps:
+        assert all(step[r] == b.step and act[r] == 0 for r in b.creates)
+        assert all(step[r] == b.step and obj[r] == o and act[r] == 1 for r, o in b.links)
+
+
+@pytest.mark.parametrize("chunk", [100, 7, 2, 1])
+def test_identifier_links_vs_replay(eng, chunk):
+    """sd_cas_identifier_links_dev vs the literal DB replay of a whole job
+    (file_identifier_job.rs:180-236, mod.rs:98-350) with the reference's cursor: rows that
+    stay orphan (errors, empty files) at a chunk's last row are queried again by the next
+    step (mod.rs:401-405, file_identifier_job.rs:268), the job stops after ceil(n/chunk)
+    steps, duplicates inside and across steps, and error/empty runs at the table's end."""
+    rng = np.random.default_rng(80 + chunk)
+    n = 20_000 if chunk > 2 else 3_000
+    pool = rng.integers(1, 2 ** 64, n // 3, dtype=np.uint64)
+    keys = pool[rng.integers(0, len(pool), n)]
+    states = rng.choice(np.array([0, 1, 2], dtype=np.uint8), n, p=[0.9, 0.05, 0.05])
+    last_rows = np.arange(chunk - 1, n, chunk)  # chunk ends: many stay-orphan rows
+    states[last_rows[rng.random(len(last_rows)) < 0.3]] = 2
+    states[last_rows[rng.random(len(last_rows)) < 0.2]] = 1
+    states[-5:] = [0, 1, 2, 1, 2]
+    want_step, want_obj, want_act, want_counts = replay_identifier_job(
+        [int(k) for k in keys], [int(s) for s in states], chunk)
+    step, obj, act, counts = eng.identifier_links(dev64(keys), torch.from_numpy(states).cuda(), chunk)
+    assert [tuple(c) for c in counts.tolist()] == want_counts
+    assert (step.cpu().numpy().view(np.uint32) == np.array(want_step, dtype=np.uint32)).all()
+    assert (obj.cpu().numpy().view(np.uint32) == np.array(want_obj, dtype=np.uint32)).all()
+    assert (act.cpu().numpy() == np.array(want_act, dtype=np.uint8)).all()
+
+
+def test_identifier_links_all_hashed_1m(eng, oracle):
+    """Without per-row states (every row hashed, the device-resident re-identify batch) the
+    emission equals the chunk replay (sd_cas_group_chunked_dev / the oracle) at 1M rows."""
+    rng = np.random.default_rng(90)
+    n = 1 << 20
+    pool = rng.integers(0, 2 ** 64, 700_000, dtype=np.uint64)
+    keys = pool[rng.integers(0, len(pool), n)]
+    step, obj, act, counts = eng.identifier_links(dev64(keys), None, 100)
+    crep, cc, cl = oracle.group_chunked(keys, 100)
+    assert len(counts) == (n + 99) // 100
+    assert (int(counts[:, 0].sum()), int(counts[:, 1].sum())) == (cc, cl)
+    assert (obj.cpu().numpy().view(np.uint32) == crep).all()
+    assert (step.cpu().numpy() == np.arange(n) // 100).all()
+    a = act.cpu().numpy()
+    assert ((a == 0) == (crep == np.arange(n, dtype=np.uint32))).all()
 
 
 def test_sampled_host_pipeline(eng, oracle):

@@ -224,6 +224,33 @@ def test_grouping_random_vs_replay(oracle):
         assert list(crep) == rc and (cc, cl) == (c, ln)
 
 
+def test_job_replay_cursor_semantics():
+    """The literal job replay (DB state + cursor): with every row hashed it equals the
+    chunk replay; a row that stays orphan at a chunk's end (error / empty file) is queried
+    again by the next step (mod.rs:401-405 + `id >= cursor`, file_identifier_job.rs:268),
+    shifting every later chunk by one, and the job still runs only ceil(n/chunk) steps."""
+    from tests.golden.make_golden import replay_identifier_job
+    rng = np.random.default_rng(12)
+    keys = [int(k) for k in rng.integers(0, 2 ** 63, 350)]
+    keys[150] = keys[20]
+    keys[260] = keys[120]
+    step, obj, act, counts = replay_identifier_job(keys, [0] * 350, 100)
+    rc, created, linked = replay_identifier(keys, 100)
+    assert obj == rc and tuple(map(sum, zip(*counts))) == (created, linked)
+    assert step == [i // 100 for i in range(350)]
+    # row 99 errors: step 1 re-queries it and covers rows 99..198; row 198 is empty: step 2
+    # re-queries it (a second new Object), rows 198..297; step 3 covers 298..349 only
+    states = [0] * 300
+    states[99], states[198] = 2, 1
+    step, obj, act, counts = replay_identifier_job(keys[:300], states, 100)
+    assert step[99] == 1 and act[99] == 2 and obj[99] == 0xFFFFFFFF
+    assert step[198] == 2 and act[198] == 0 and obj[198] == 198
+    assert step[199] == 2 and step[297] == 2 and len(counts) == 3
+    assert step[298] == 0xFFFFFFFF and act[298] == act[299] == 3  # past the 3 steps: not reached
+    assert counts[0] == (99, 0) and counts[1][0] + counts[1][1] == 99
+    assert counts[2][0] + counts[2][1] == 100 + 0  # 198 again (new Object) + 199..297
+
+
 def test_simd_baseline_matches_scalar(oracle):
     rng = np.random.default_rng(2)
     n = 48
