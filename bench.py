@@ -118,7 +118,7 @@ def main() -> None:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from spacedrive_amd import CasEngine
-    from spacedrive_amd.shard import HipShardOps, sharded_group
+    from spacedrive_amd.shard import HipShardOps, fixed_capacity, sharded_group
 
     eng = CasEngine(local)
     F = args.files_per_gpu
@@ -141,7 +141,10 @@ def main() -> None:
     pending = [None] * NBUF
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
-    results = []
+    results = []      # the last step's ShardResult (sharded runs)
+    overflows = []    # per-step overflow flags of the fixed-capacity exchange (device)
+    # fixed per-peer capacity: the exchange needs no host sync (spacedrive_amd/shard.py)
+    capacity = fixed_capacity(F, world) if sharded else None
     # The exchange path reads part sizes back to the host (all_to_all_single needs host
     # split lists), so it blocks its caller: it runs on a worker thread, and the main
     # thread only ever waits on it when it reuses that step's key buffer.
@@ -157,7 +160,10 @@ def main() -> None:
             if not sharded:
                 eng.group(keys[b], rep, want_objects=False)  # K4h + K5h, async
             else:
-                results.append(sharded_group(keys[b], file0, ops))
+                r = sharded_group(keys[b], file0, ops, capacity=capacity)
+                results[:] = [r]
+                if r.overflow is not None:
+                    overflows.append(r.overflow)
             grouped[b].record(side)
 
     def launch_group(i: int):
@@ -193,6 +199,7 @@ def main() -> None:
         dist.barrier()
     torch.cuda.synchronize()
     results.clear()
+    overflows.clear()
     t0 = time.perf_counter()
     run(args.steps, True)
     torch.cuda.synchronize()
@@ -215,6 +222,9 @@ def main() -> None:
     if not sharded:
         objects = eng.group(last_keys, rep)
     else:
+        # every timed step's fixed-capacity exchange must have fit (else it would have been
+        # redone exactly outside the timed region, and the step time would not stand)
+        n_overflow = sum(int(f.item()) for f in overflows)
         objects = res.objects
     # the grouping alone (after the timed region: inside the steps it overlaps the next K1
     # on a side stream and shares the CUs with it, so its own speed is measured serially)
@@ -300,6 +310,9 @@ def main() -> None:
                              "overlaps hashing of steps i+1 and i+2" if args.overlap
                              else "hash then group, serial"),
                 "objects": objects,
+                "exchange": None if not sharded else {
+                    "capacity_per_peer": capacity[0], "spill_per_peer": capacity[1],
+                    "host_syncs_per_step": 0, "timed_steps_overflowed": n_overflow},
             },
             "roofline": {
                 # achieved = files x 953 compressions x 792 spec int32 ops /

@@ -189,6 +189,30 @@ int sd_cas_exchange_split_dev(sd_cas_ctx* ctx, const uint32_t* d_rows, size_t m,
                               uint64_t* d_keys, uint32_t* d_vals, void* stream);
 int sd_cas_exchange_unpack_dev(sd_cas_ctx* ctx, const uint32_t* d_back, const uint32_t* d_pos,
                                size_t n, uint64_t* d_rep, void* stream);
+/* Fixed-capacity form of the exchange rows (no host read of the part sizes): G blocks of
+ * `cap` rows (d_rows, 3 u32 each) and G spill blocks of `spill` rows (d_spill_rows) are
+ * always written — part p's first cap rows, its next spill rows, and in every unused slot a
+ * sentinel row whose key is the first key of range p+1 (outside receiver p's range) and
+ * whose value is 0xFFFFFFFF.  d_counts = the partition's part sizes (device).  A part
+ * larger than cap + spill sets *d_overflow (u32, device; zero it first): the caller then
+ * falls back to the exact exchange.  G <= 1024. */
+int sd_cas_exchange_pack_fixed_dev(sd_cas_ctx* ctx, const uint64_t* d_keys, const uint32_t* d_pos,
+                                   const uint64_t* d_counts, uint32_t G, uint64_t cap,
+                                   uint64_t spill, uint64_t file0, uint32_t* d_rows,
+                                   uint32_t* d_spill_rows, uint32_t* d_overflow, void* stream);
+/* received rows -> keys + vals; *d_has_sentinel |= 1 if any key equals `sentinel` (this
+ * receiver's sentinel: the first key of range rank+1; zero it first). */
+int sd_cas_exchange_split_fixed_dev(sd_cas_ctx* ctx, const uint32_t* d_rows, size_t m,
+                                    uint64_t sentinel, uint64_t* d_keys, uint32_t* d_vals,
+                                    uint64_t* d_has_sentinel, void* stream);
+/* mirror of pack_fixed: d_rep[d_pos[o_p + t]] = (main or spill block) rep for t < count_p. */
+int sd_cas_exchange_unpack_fixed_dev(sd_cas_ctx* ctx, const uint32_t* d_back,
+                                     const uint32_t* d_spill_back, const uint32_t* d_pos,
+                                     const uint64_t* d_counts, uint32_t G, uint64_t cap,
+                                     uint64_t spill, uint64_t* d_rep, void* stream);
+/* Enqueue a copy of the Object count of this context's last grouping call (sd_cas_group*_dev)
+ * to device memory — for callers that keep the count on the device (no host sync). */
+int sd_cas_copy_objects_dev(sd_cas_ctx* ctx, uint64_t* d_dst, void* stream);
 /* Same on already-sorted pairs (keys ascending, vals = file idx, stable). */
 int sd_cas_group_sorted_dev(sd_cas_ctx* ctx, const uint64_t* d_sorted_keys,
                             const uint32_t* d_sorted_vals, size_t n, uint32_t* d_rep,
@@ -268,6 +292,8 @@ int sd_cas_file_checksum(sd_cas_ctx* ctx, const char* path, char out_hex[65], in
  * xGMI (hipMemcpyPeerAsync, event-ordered across devices), then groups locally; the
  * multi-process form of the same exchange uses RCCL all-to-all (spacedrive_amd/shard.py). */
 typedef struct sd_cas_multi sd_cas_multi;
+/* Fails with SD_CAS_ENODEV when a device is not a gfx950 or when peer access between two
+ * distinct devices cannot be enabled (sd_cas_multi_last_error(NULL) says which). */
 int sd_cas_multi_create(const int* devices, int ndev, sd_cas_multi** out);
 void sd_cas_multi_destroy(sd_cas_multi* m);
 int sd_cas_multi_count(const sd_cas_multi* m);

@@ -78,6 +78,18 @@ extern "C" {
                                      d_keys: *mut u64, d_vals: *mut u32, stream: *mut c_void) -> c_int;
     pub fn sd_cas_exchange_unpack_dev(ctx: *mut sd_cas_ctx, d_back: *const u32, d_pos: *const u32,
                                       n: usize, d_rep: *mut u64, stream: *mut c_void) -> c_int;
+    pub fn sd_cas_exchange_pack_fixed_dev(ctx: *mut sd_cas_ctx, d_keys: *const u64, d_pos: *const u32,
+                                          d_counts: *const u64, G: u32, cap: u64, spill: u64,
+                                          file0: u64, d_rows: *mut u32, d_spill_rows: *mut u32,
+                                          d_overflow: *mut u32, stream: *mut c_void) -> c_int;
+    pub fn sd_cas_exchange_split_fixed_dev(ctx: *mut sd_cas_ctx, d_rows: *const u32, m: usize,
+                                           sentinel: u64, d_keys: *mut u64, d_vals: *mut u32,
+                                           d_has_sentinel: *mut u64, stream: *mut c_void) -> c_int;
+    pub fn sd_cas_exchange_unpack_fixed_dev(ctx: *mut sd_cas_ctx, d_back: *const u32,
+                                            d_spill_back: *const u32, d_pos: *const u32,
+                                            d_counts: *const u64, G: u32, cap: u64, spill: u64,
+                                            d_rep: *mut u64, stream: *mut c_void) -> c_int;
+    pub fn sd_cas_copy_objects_dev(ctx: *mut sd_cas_ctx, d_dst: *mut u64, stream: *mut c_void) -> c_int;
     pub fn sd_cas_group_sorted_dev(ctx: *mut sd_cas_ctx, d_sorted_keys: *const u64,
                                    d_sorted_vals: *const u32, n: usize, d_rep: *mut u32,
                                    out_objects: *mut u64, stream: *mut c_void) -> c_int;

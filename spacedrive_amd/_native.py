@@ -47,6 +47,10 @@ SIGNATURES = [
     ("sd_cas_exchange_pack_dev", _i, [_vp, _vp, _vp, _sz, _u64, _vp, _vp]),
     ("sd_cas_exchange_split_dev", _i, [_vp, _vp, _sz, _vp, _vp, _vp]),
     ("sd_cas_exchange_unpack_dev", _i, [_vp, _vp, _vp, _sz, _vp, _vp]),
+    ("sd_cas_exchange_pack_fixed_dev", _i, [_vp, _vp, _vp, _vp, _u32, _u64, _u64, _u64, _vp, _vp, _vp, _vp]),
+    ("sd_cas_exchange_split_fixed_dev", _i, [_vp, _vp, _sz, _u64, _vp, _vp, _vp, _vp]),
+    ("sd_cas_exchange_unpack_fixed_dev", _i, [_vp, _vp, _vp, _vp, _vp, _u32, _u64, _u64, _vp, _vp]),
+    ("sd_cas_copy_objects_dev", _i, [_vp, _vp, _vp]),
     ("sd_cas_group_sorted_dev", _i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     ("sd_cas_group_chunked_dev", _i, [_vp, _vp, _sz, _u32, _vp, _vp, _vp, _vp]),
     ("sd_cas_identifier_max_steps", _sz, [_sz, _u32]),

@@ -65,6 +65,109 @@ sd_exch_unpack(const uint32_t* __restrict__ back, const uint32_t* __restrict__ p
   if (j < n) rep[pos[j]] = back[j];
 }
 
+// ---- fixed-capacity exchange (no host round trip for the part sizes) -----------------
+// Every rank sends G blocks of `cap` rows (+ G spill blocks of `spill` rows) whatever its
+// part sizes are: BLAKE3 keys are uniform, so a part of a rank's n keys is n/G +- a few
+// sqrt(n/G) and fits a capacity fixed up front; all_to_all then needs no split lists and
+// the step no host sync.  Unused slots carry a sentinel key that lies outside the
+// receiver's key range (the first key of the next range), so it never merges with a real
+// key; a part larger than cap + spill raises `overflow` (the caller then redoes the step
+// with the exact, size-exchanging path).
+
+// first key of range r of G: ceil(r * 2^64 / G) (r = G wraps to 0)
+__device__ __forceinline__ uint64_t range_start(uint32_t r, uint32_t G) {
+  if (r == 0 || r >= G) return 0;
+  const uint64_t q1 = ~0ull / G, r1 = ~0ull % G;  // 2^64 - 1 = q1*G + r1
+  const uint64_t Q = (r1 + 1 == G) ? q1 + 1 : q1, R = (r1 + 1 == G) ? 0 : r1 + 1;
+  return (uint64_t)r * Q + ((uint64_t)r * R + G - 1) / G;
+}
+
+constexpr uint32_t FIXED_MAX_G = 1024;
+
+// Part offsets o_p = sum_{q<p} counts[q] into LDS (G <= FIXED_MAX_G).
+__device__ __forceinline__ void part_offsets(const uint64_t* counts, uint32_t G, uint64_t* off) {
+  if (threadIdx.x == 0) {
+    uint64_t run = 0;
+    for (uint32_t p = 0; p < G; ++p) { off[p] = run; run += counts[p]; }
+  }
+  __syncthreads();
+}
+
+extern "C" __global__ void __launch_bounds__(256)
+sd_exch_pack_fixed(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
+                   const uint64_t* __restrict__ counts, uint32_t G, uint64_t cap, uint64_t spill,
+                   uint64_t file0, uint32_t* __restrict__ rows, uint32_t* __restrict__ srows,
+                   uint32_t* __restrict__ overflow) {
+  __shared__ uint64_t off[FIXED_MAX_G];
+  part_offsets(counts, G, off);
+  const uint64_t total = (uint64_t)G * (cap + spill);
+  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < total;
+       s += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t p;
+    uint64_t t;
+    uint32_t* dst;
+    if (s < (uint64_t)G * cap) {
+      p = (uint32_t)(s / cap); t = s % cap; dst = rows + 3 * s;
+    } else {
+      const uint64_t s2 = s - (uint64_t)G * cap;
+      p = (uint32_t)(s2 / spill); t = cap + s2 % spill; dst = srows + 3 * s2;
+    }
+    uint64_t k;
+    uint32_t v;
+    if (t < counts[p]) {
+      const uint64_t j = off[p] + t;
+      k = keys[j];
+      v = (uint32_t)(file0 + pos[j]);
+    } else {
+      k = range_start(p + 1, G);  // outside receiver p's range [start(p), start(p+1))
+      v = 0xFFFFFFFFu;
+    }
+    dst[0] = (uint32_t)k;
+    dst[1] = (uint32_t)(k >> 32);
+    dst[2] = v;
+    if (t == cap + spill - 1 && counts[p] > cap + spill) atomicOr(overflow, 1u);
+  }
+}
+
+// received rows -> keys/vals, has_sentinel |= any key == sentinel (this receiver's)
+extern "C" __global__ void __launch_bounds__(256)
+sd_exch_split_fixed(const uint32_t* __restrict__ rows, uint64_t m, uint64_t sentinel,
+                    uint64_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                    unsigned long long* __restrict__ has_sentinel) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool hit = false;
+  if (j < m) {
+    const uint64_t k = (uint64_t)rows[3 * j] | ((uint64_t)rows[3 * j + 1] << 32);
+    keys[j] = k;
+    vals[j] = rows[3 * j + 2];
+    hit = k == sentinel;
+  }
+  if (__ballot(hit) && (threadIdx.x & 63u) == 0) atomicOr(has_sentinel, 1ull);
+}
+
+// rep[pos[o_p + t]] = back (main block t < cap, spill block otherwise) for t < counts[p]
+extern "C" __global__ void __launch_bounds__(256)
+sd_exch_unpack_fixed(const uint32_t* __restrict__ back, const uint32_t* __restrict__ sback,
+                     const uint32_t* __restrict__ pos, const uint64_t* __restrict__ counts,
+                     uint32_t G, uint64_t cap, uint64_t spill, uint64_t* __restrict__ rep) {
+  __shared__ uint64_t off[FIXED_MAX_G];
+  part_offsets(counts, G, off);
+  const uint64_t total = (uint64_t)G * (cap + spill);
+  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < total;
+       s += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t p;
+    uint64_t t;
+    uint32_t b;
+    if (s < (uint64_t)G * cap) {
+      p = (uint32_t)(s / cap); t = s % cap; b = back[s];
+    } else {
+      const uint64_t s2 = s - (uint64_t)G * cap;
+      p = (uint32_t)(s2 / spill); t = cap + s2 % spill; b = sback[s2];
+    }
+    if (t < counts[p]) rep[pos[off[p] + t]] = b;
+  }
+}
+
 // gidx[j] = file0 + sidx[j]
 extern "C" __global__ void __launch_bounds__(256)
 sd_multi_gidx(const uint32_t* __restrict__ sidx, uint64_t n, uint64_t file0,
@@ -115,6 +218,37 @@ hipError_t exch_unpack(const uint32_t* back, const uint32_t* pos, uint64_t n, ui
                        hipStream_t s) {
   if (n == 0) return hipSuccess;
   sd_exch_unpack<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(back, pos, n, rep);
+  return hipGetLastError();
+}
+
+static uint32_t grid_for(uint64_t total) {
+  const uint64_t b = (total + 255) / 256;
+  return (uint32_t)(b < 65536 ? (b ? b : 1) : 65536);
+}
+
+hipError_t exch_pack_fixed(const uint64_t* keys, const uint32_t* pos, const uint64_t* counts,
+                           uint32_t G, uint64_t cap, uint64_t spill, uint64_t file0, uint32_t* rows,
+                           uint32_t* srows, uint32_t* overflow, hipStream_t s) {
+  if (G == 0 || G > FIXED_MAX_G || cap == 0) return hipErrorInvalidValue;
+  sd_exch_pack_fixed<<<grid_for((uint64_t)G * (cap + spill)), 256, 0, s>>>(
+      keys, pos, counts, G, cap, spill, file0, rows, srows, overflow);
+  return hipGetLastError();
+}
+
+hipError_t exch_split_fixed(const uint32_t* rows, uint64_t m, uint64_t sentinel, uint64_t* keys,
+                            uint32_t* vals, uint64_t* has_sentinel, hipStream_t s) {
+  if (m == 0) return hipSuccess;
+  sd_exch_split_fixed<<<(uint32_t)((m + 255) / 256), 256, 0, s>>>(
+      rows, m, sentinel, keys, vals, (unsigned long long*)has_sentinel);
+  return hipGetLastError();
+}
+
+hipError_t exch_unpack_fixed(const uint32_t* back, const uint32_t* sback, const uint32_t* pos,
+                             const uint64_t* counts, uint32_t G, uint64_t cap, uint64_t spill,
+                             uint64_t* rep, hipStream_t s) {
+  if (G == 0 || G > FIXED_MAX_G || cap == 0) return hipErrorInvalidValue;
+  sd_exch_unpack_fixed<<<grid_for((uint64_t)G * (cap + spill)), 256, 0, s>>>(
+      back, sback, pos, counts, G, cap, spill, rep);
   return hipGetLastError();
 }
 

@@ -39,6 +39,9 @@ static int mfail(sd_cas_multi* m, int code, const std::string& what) {
   return code;
 }
 
+// why the last sd_cas_multi_create on this thread failed (sd_cas_multi_last_error(NULL))
+static thread_local std::string g_create_err;
+
 #define MTRY(m, i, expr)                                                                   \
   do {                                                                                     \
     int rc_ = (expr);                                                                      \
@@ -88,25 +91,38 @@ extern "C" {
 int sd_cas_multi_create(const int* devices, int ndev, sd_cas_multi** out) {
   if (!devices || ndev <= 0 || ndev > 64 || !out) return SD_CAS_EINVAL;
   *out = nullptr;
+  g_create_err.clear();
   sd_cas_multi* m = new sd_cas_multi();
   m->G = ndev;
   for (int i = 0; i < ndev; i++) {
     sd_cas_ctx* c = nullptr;
     int rc = sd_cas_ctx_create(devices[i], &c);
-    if (rc) { sd_cas_multi_destroy(m); return rc; }
+    if (rc) {
+      g_create_err = "shard " + std::to_string(i) + ": no gfx950 device " + std::to_string(devices[i]);
+      sd_cas_multi_destroy(m);
+      return rc;
+    }
     m->ctx.push_back(c);
   }
-  // peer access between distinct devices (xGMI); a shard pair on one device copies D2D
+  // peer access between distinct devices (the exchange pulls over xGMI); a shard pair on
+  // one device copies D2D.  Without peer access the pulls would silently stage through
+  // host memory, so a pair that cannot be enabled fails the creation.
   for (int i = 0; i < ndev; i++)
     for (int j = 0; j < ndev; j++) {
       if (devices[i] == devices[j]) continue;
       int can = 0;
-      (void)hipDeviceCanAccessPeer(&can, devices[i], devices[j]);
-      if (can) {
-        (void)hipSetDevice(devices[i]);
-        hipError_t e = hipDeviceEnablePeerAccess(devices[j], 0);
-        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
-        else (void)hipGetLastError();
+      hipError_t e = hipDeviceCanAccessPeer(&can, devices[i], devices[j]);
+      if (e == hipSuccess && can) {
+        e = hipSetDevice(devices[i]);
+        if (e == hipSuccess) e = hipDeviceEnablePeerAccess(devices[j], 0);
+        if (e == hipErrorPeerAccessAlreadyEnabled) e = hipSuccess;
+      }
+      (void)hipGetLastError();
+      if (e != hipSuccess || !can) {
+        g_create_err = "peer access " + std::to_string(devices[i]) + " -> " + std::to_string(devices[j]) +
+                       (e != hipSuccess ? std::string(": ") + hipGetErrorString(e) : ": not supported");
+        sd_cas_multi_destroy(m);
+        return SD_CAS_ENODEV;
       }
     }
   m->ev_a.resize(ndev);
@@ -147,7 +163,7 @@ sd_cas_ctx* sd_cas_multi_ctx(sd_cas_multi* m, int i) {
 }
 
 const char* sd_cas_multi_last_error(const sd_cas_multi* m) {
-  return m ? m->err.c_str() : "null multi context";
+  return m ? m->err.c_str() : g_create_err.c_str();
 }
 
 int sd_cas_multi_group(sd_cas_multi* m, const uint64_t* const* d_keys, const size_t* n,
@@ -371,6 +387,51 @@ int sd_cas_exchange_unpack_dev(sd_cas_ctx* c, const uint32_t* d_back, const uint
   if (!c) return SD_CAS_EINVAL;
   if (n && (!d_back || !d_pos || !d_rep)) return sd_fail(c, SD_CAS_EINVAL, "exchange_unpack: null");
   HIP_TRY(c, exch_unpack(d_back, d_pos, n, d_rep, sd_pick(c, stream)));
+  return SD_CAS_OK;
+}
+
+int sd_cas_exchange_pack_fixed_dev(sd_cas_ctx* c, const uint64_t* d_keys, const uint32_t* d_pos,
+                                   const uint64_t* d_counts, uint32_t G, uint64_t cap,
+                                   uint64_t spill, uint64_t file0, uint32_t* d_rows,
+                                   uint32_t* d_spill_rows, uint32_t* d_overflow, void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (G == 0 || G > 1024 || cap == 0 || !d_counts || !d_rows || !d_overflow || (spill && !d_spill_rows))
+    return sd_fail(c, SD_CAS_EINVAL, "exchange_pack_fixed: bad arguments");
+  if (file0 >= (1ull << 32))  // file0 + every local position must fit in u32 (the caller checks n)
+    return sd_fail(c, SD_CAS_EINVAL, "exchange_pack_fixed: idx past u32");
+  HIP_TRY(c, exch_pack_fixed(d_keys, d_pos, d_counts, G, cap, spill, file0, d_rows, d_spill_rows,
+                             d_overflow, sd_pick(c, stream)));
+  return SD_CAS_OK;
+}
+
+int sd_cas_exchange_split_fixed_dev(sd_cas_ctx* c, const uint32_t* d_rows, size_t m,
+                                    uint64_t sentinel, uint64_t* d_keys, uint32_t* d_vals,
+                                    uint64_t* d_has_sentinel, void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (m && (!d_rows || !d_keys || !d_vals || !d_has_sentinel))
+    return sd_fail(c, SD_CAS_EINVAL, "exchange_split_fixed: null");
+  HIP_TRY(c, exch_split_fixed(d_rows, m, sentinel, d_keys, d_vals, d_has_sentinel, sd_pick(c, stream)));
+  return SD_CAS_OK;
+}
+
+int sd_cas_exchange_unpack_fixed_dev(sd_cas_ctx* c, const uint32_t* d_back,
+                                     const uint32_t* d_spill_back, const uint32_t* d_pos,
+                                     const uint64_t* d_counts, uint32_t G, uint64_t cap,
+                                     uint64_t spill, uint64_t* d_rep, void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (G == 0 || G > 1024 || cap == 0 || !d_back || !d_pos || !d_counts || !d_rep || (spill && !d_spill_back))
+    return sd_fail(c, SD_CAS_EINVAL, "exchange_unpack_fixed: bad arguments");
+  HIP_TRY(c, exch_unpack_fixed(d_back, d_spill_back, d_pos, d_counts, G, cap, spill, d_rep,
+                               sd_pick(c, stream)));
+  return SD_CAS_OK;
+}
+
+int sd_cas_copy_objects_dev(sd_cas_ctx* c, uint64_t* d_dst, void* stream) {
+  if (!c || !d_dst) return SD_CAS_EINVAL;
+  hipStream_t s = sd_pick(c, stream);
+  HIP_TRY(c, sd_ws_acquire(c, s));
+  HIP_TRY(c, hipMemcpyAsync(d_dst, c->d_scalar, 8, hipMemcpyDeviceToDevice, s));
+  HIP_TRY(c, sd_ws_release(c, s));
   return SD_CAS_OK;
 }
 

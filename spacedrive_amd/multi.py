@@ -21,7 +21,9 @@ class MultiEngine:
         h = ctypes.c_void_p()
         rc = self.L.sd_cas_multi_create(arr, len(self.devices), ctypes.byref(h))
         if rc != 0:
-            raise CasError(rc, f"sd_cas_multi_create({self.devices}) failed")
+            why = self.L.sd_cas_multi_last_error(None)
+            raise CasError(rc, f"sd_cas_multi_create({self.devices}) failed: "
+                               f"{why.decode() if why else ''}")
         self.h = h
 
     def close(self) -> None:

@@ -8,8 +8,7 @@ their contiguous slice of files (no communication), then:
 
   1. key-range partition of the local keys, dest(k) = floor(k * G / 2^64)
      (BLAKE3 keys are uniform)                                   [HIP: sd_cas_partition_dev]
-  2. all_to_all_single of the part sizes, then ONE all_to_all_single of 12-byte rows
-     (key u64, global file idx u32) — 12 B/key instead of two int64 exchanges' 16  [RCCL]
+  2. ONE all_to_all_single of 12-byte rows (key u64, global file idx u32)          [RCCL]
   3. grouping of the received pairs: rep = min global idx over equal keys
                                                                  [HIP: sd_cas_group_min_dev]
   4. mirror all_to_all_single of the u32 reps (4 B/key); scatter to local file order [RCCL]
@@ -17,14 +16,25 @@ their contiguous slice of files (no communication), then:
 Every key lives on exactly one rank after step 2, so step 3's minimum is the global one:
 rep(f) = min{ g : key(g) == key(f) } over all ranks, the single-GPU contract.
 
+Two forms of step 2:
+  * fixed capacity (``capacity=`` given, the production form): every rank sends G blocks of
+    `cap` rows + G spill blocks whatever its part sizes are — uniform keys put n/G +- a few
+    sqrt(n/G) keys in each part, so no part sizes travel to the host and the step has NO
+    host synchronisation (equal-split all_to_all); unused slots carry a sentinel key outside
+    the receiver's range.  A part larger than cap + spill (heavily duplicated libraries: the
+    copies of one file all go to one rank) raises a device flag; :meth:`ShardResult.resolve`
+    (called by ``.objects``) reads it once and redoes the step with the exact form;
+  * exact: the part sizes are exchanged first and read on the host for the split lists.
+
 ``ops`` supplies the device primitives; in production it is the HIP engine
 (:class:`HipShardOps`).  Tests on CPU pass a host implementation to check the exchange
 logic with the gloo backend — that is a test double for the kernels, not a fallback.
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
-from typing import Protocol
+import math
+from dataclasses import dataclass, field
+from typing import Optional, Protocol
 
 import torch
 import torch.distributed as dist
@@ -38,6 +48,9 @@ class ShardOps(Protocol):
     def group_min(self, keys: torch.Tensor, vals: torch.Tensor) -> tuple[torch.Tensor, int]:
         """out[i] = min{ vals[j] : keys[j] == keys[i] } (int32), distinct keys"""
 
+    def group_min_dev(self, keys: torch.Tensor, vals: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+        """same, the distinct-key count as an int64 [1] device tensor (no host sync)"""
+
     def pack(self, keys: torch.Tensor, pos: torch.Tensor, file0: int) -> torch.Tensor:
         """int32 rows [n, 3] = (key lo32, key hi32, u32(file0 + pos))"""
 
@@ -47,61 +60,156 @@ class ShardOps(Protocol):
     def unpack(self, back: torch.Tensor, pos: torch.Tensor) -> torch.Tensor:
         """int64 rep with rep[pos[j]] = u32(back[j])"""
 
+    def pack_fixed(self, keys, pos, counts, parts: int, cap: int, spill: int, file0: int):
+        """(rows [parts*cap, 3], spill rows [parts*spill, 3], overflow int32 [1])"""
+
+    def split_fixed(self, rows, sentinel: int) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """(int64 keys, int32 vals, int64 [1] = 1 if any key == sentinel)"""
+
+    def unpack_fixed(self, back, spill_back, pos, counts, parts: int, cap: int, spill: int) -> torch.Tensor:
+        """int64 rep: mirror of pack_fixed"""
+
+
+def _cs(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
 
 class HipShardOps:
     """The production ops: libsd_hip_cas.so on the rank's GPU."""
 
     def __init__(self, eng):
         self.eng = eng
+        self.L = eng.L
+
+    def _chk(self, rc: int, what: str) -> None:
+        self.eng._check(rc, what)
 
     def partition(self, keys, parts):
         n = keys.numel()
         ko = torch.empty_like(keys)
         po = torch.empty(n, dtype=torch.int32, device=keys.device)
         counts = torch.empty(parts, dtype=torch.int64, device=keys.device)
-        self.eng.partition(keys, parts, ko, po, counts,
-                           stream=torch.cuda.current_stream().cuda_stream)
+        self.eng.partition(keys, parts, ko, po, counts, stream=_cs(keys))
         return ko, po, counts
 
     def group_min(self, keys, vals):
         out = torch.empty(keys.numel(), dtype=torch.int32, device=keys.device)
-        objects = self.eng.group_min(keys, vals, out, stream=torch.cuda.current_stream().cuda_stream)
+        objects = self.eng.group_min(keys, vals, out, stream=_cs(keys))
         return out, objects
+
+    def group_min_dev(self, keys, vals):
+        out = torch.empty(keys.numel(), dtype=torch.int32, device=keys.device)
+        obj = torch.empty(1, dtype=torch.int64, device=keys.device)
+        self.eng.group_min(keys, vals, out, stream=_cs(keys), want_objects=False)
+        self._chk(self.L.sd_cas_copy_objects_dev(self.eng.h, obj.data_ptr(), _cs(keys)), "copy_objects")
+        return out, obj
 
     def pack(self, keys, pos, file0):
         rows = torch.empty((keys.numel(), 3), dtype=torch.int32, device=keys.device)
-        self.eng.exchange_pack(keys, pos, file0, rows, stream=torch.cuda.current_stream().cuda_stream)
+        self.eng.exchange_pack(keys, pos, file0, rows, stream=_cs(keys))
         return rows
 
     def split(self, rows):
         m = rows.shape[0]
         keys = torch.empty(m, dtype=torch.int64, device=rows.device)
         vals = torch.empty(m, dtype=torch.int32, device=rows.device)
-        self.eng.exchange_split(rows, keys, vals, stream=torch.cuda.current_stream().cuda_stream)
+        self.eng.exchange_split(rows, keys, vals, stream=_cs(rows))
         return keys, vals
 
     def unpack(self, back, pos):
         rep = torch.empty(back.numel(), dtype=torch.int64, device=back.device)
-        self.eng.exchange_unpack(back, pos, rep, stream=torch.cuda.current_stream().cuda_stream)
+        self.eng.exchange_unpack(back, pos, rep, stream=_cs(back))
         return rep
+
+    def pack_fixed(self, keys, pos, counts, parts, cap, spill, file0):
+        dev = keys.device
+        rows = torch.empty((parts * cap, 3), dtype=torch.int32, device=dev)
+        srows = torch.empty((max(parts * spill, 1), 3), dtype=torch.int32, device=dev)
+        overflow = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._chk(self.L.sd_cas_exchange_pack_fixed_dev(
+            self.eng.h, keys.data_ptr(), pos.data_ptr(), counts.data_ptr(), parts, cap, spill,
+            file0, rows.data_ptr(), srows.data_ptr(), overflow.data_ptr(), _cs(keys)), "pack_fixed")
+        return rows, srows[:parts * spill], overflow
+
+    def split_fixed(self, rows, sentinel):
+        m = rows.shape[0]
+        keys = torch.empty(m, dtype=torch.int64, device=rows.device)
+        vals = torch.empty(m, dtype=torch.int32, device=rows.device)
+        flag = torch.zeros(1, dtype=torch.int64, device=rows.device)
+        self._chk(self.L.sd_cas_exchange_split_fixed_dev(
+            self.eng.h, rows.data_ptr(), m, sentinel & 0xFFFFFFFFFFFFFFFF, keys.data_ptr(),
+            vals.data_ptr(), flag.data_ptr(), _cs(rows)), "split_fixed")
+        return keys, vals, flag
+
+    def unpack_fixed(self, back, spill_back, pos, counts, parts, cap, spill):
+        n = pos.numel()
+        rep = torch.empty(n, dtype=torch.int64, device=pos.device)
+        sb = spill_back if spill_back.numel() else back
+        self._chk(self.L.sd_cas_exchange_unpack_fixed_dev(
+            self.eng.h, back.data_ptr(), sb.data_ptr(), pos.data_ptr(), counts.data_ptr(), parts,
+            cap, spill, rep.data_ptr(), _cs(pos)), "unpack_fixed")
+        return rep
+
+
+def range_start(r: int, parts: int) -> int:
+    """First key of range r of `parts`: ceil(r * 2^64 / parts) (r = parts wraps to 0)."""
+    r %= parts
+    return -((-(r << 64)) // parts) if r else 0
+
+
+def fixed_capacity(n_per_rank: int, parts: int) -> tuple[int, int]:
+    """(cap, spill) of the fixed-capacity exchange for ranks holding <= n_per_rank uniform
+    keys: the mean part plus 8 standard deviations (binomial), and a spill block of 1/16
+    more — overflow then needs > 8 sigma (uniform keys) or heavy duplication."""
+    mean = n_per_rank / parts
+    sd = math.sqrt(max(mean * (1 - 1 / parts), 1.0))
+    cap = int(math.ceil(mean + 8 * sd)) + 64
+    return cap, max(256, cap // 16)
 
 
 @dataclass
 class ShardResult:
     rep: torch.Tensor        # int64 global idx of the file owning each local file's Object
-    objects: int             # Objects over all ranks (= distinct keys)
-    sent: int                # keys this rank sent to other ranks
+    objects_dev: torch.Tensor  # int64 [1]: Objects over all ranks (= distinct keys), device
+    sent: Optional[int] = None  # keys this rank sent to other ranks (exact form only)
+    overflow: Optional[torch.Tensor] = None  # int32 [1] (fixed form): a part exceeded cap+spill
+    _redo: Optional[object] = field(default=None, repr=False)
+
+    def resolve(self) -> "ShardResult":
+        """Read the overflow flag (one host sync) and, if any rank's part overflowed its fixed
+        capacity, redo the grouping with the exact exchange.  Collective: every rank calls it
+        (the flag was max-reduced, so all ranks agree)."""
+        if self.overflow is not None:
+            if int(self.overflow.item()):
+                exact = self._redo()
+                self.rep, self.objects_dev, self.sent = exact.rep, exact.objects_dev, exact.sent
+            self.overflow = None
+            self._redo = None
+        return self
+
+    @property
+    def objects(self) -> int:
+        self.resolve()
+        return int(self.objects_dev.item())
 
 
-def sharded_group(local_keys: torch.Tensor, file0: int, ops: ShardOps,
-                  group=None) -> ShardResult:
-    """Canonical grouping across all ranks: rep(f) = min{ g : key(g) == key(f) }."""
+def sharded_group(local_keys: torch.Tensor, file0: int, ops: ShardOps, group=None,
+                  capacity: Optional[tuple[int, int]] = None) -> ShardResult:
+    """Canonical grouping across all ranks: rep(f) = min{ g : key(g) == key(f) }.
+    capacity = (cap, spill) selects the sync-free fixed-capacity exchange (every rank must
+    pass the same values, e.g. fixed_capacity(max files per rank, world)); None = exact."""
+    if file0 + local_keys.numel() > (1 << 32):
+        raise ValueError("sharded_group: global file idx must fit in u32")
+    if capacity is None:
+        return _sharded_group_exact(local_keys, file0, ops, group)
+    return _sharded_group_fixed(local_keys, file0, ops, group, capacity)
+
+
+def _sharded_group_exact(local_keys, file0, ops, group) -> ShardResult:
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = local_keys.device
     n = local_keys.numel()
-    if file0 + n > (1 << 32):
-        raise ValueError("sharded_group: global file idx must fit in u32")
     pkeys, ppos, send_counts = ops.partition(local_keys, world)     # 1
     recv_counts = torch.empty_like(send_counts)
     dist.all_to_all_single(recv_counts, send_counts, group=group)  # 2: sizes
@@ -122,4 +230,34 @@ def sharded_group(local_keys: torch.Tensor, file0: int, ops: ShardOps,
     rep = ops.unpack(back, ppos)
     tot = torch.tensor([objects], dtype=torch.int64, device=dev)
     dist.all_reduce(tot, group=group)
-    return ShardResult(rep=rep, objects=int(tot.item()), sent=n - int(sc[rank]))
+    return ShardResult(rep=rep, objects_dev=tot, sent=n - int(sc[rank]))
+
+
+def _sharded_group_fixed(local_keys, file0, ops, group, capacity) -> ShardResult:
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if world == 1:  # one range: no slot can hold a key outside it, nothing to exchange
+        return _sharded_group_exact(local_keys, file0, ops, group)
+    cap, spill = capacity
+    dev = local_keys.device
+    pkeys, ppos, counts = ops.partition(local_keys, world)                    # 1
+    rows, srows, overflow = ops.pack_fixed(pkeys, ppos, counts, world, cap, spill, file0)
+    rrows = torch.empty_like(rows)
+    dist.all_to_all_single(rrows, rows, group=group)                          # 2: equal splits
+    if spill:
+        rsrows = torch.empty_like(srows)
+        dist.all_to_all_single(rsrows, srows, group=group)
+        rrows = torch.cat([rrows, rsrows])
+    rkeys, ridx, has_sentinel = ops.split_fixed(rrows, range_start(rank + 1, world))
+    rep_min, obj = ops.group_min_dev(rkeys, ridx)                             # 3
+    tot = obj - has_sentinel                      # the sentinel rows form one extra key
+    back = torch.empty(world * cap, dtype=torch.int32, device=dev)
+    dist.all_to_all_single(back, rep_min[:world * cap].contiguous(), group=group)   # 4
+    sback = torch.empty(world * spill, dtype=torch.int32, device=dev)
+    if spill:
+        dist.all_to_all_single(sback, rep_min[world * cap:].contiguous(), group=group)
+    rep = ops.unpack_fixed(back, sback, ppos, counts, world, cap, spill)
+    dist.all_reduce(tot, group=group)
+    dist.all_reduce(overflow, op=dist.ReduceOp.MAX, group=group)
+    return ShardResult(rep=rep, objects_dev=tot, overflow=overflow,
+                       _redo=lambda: _sharded_group_exact(local_keys, file0, ops, group))

@@ -825,6 +825,74 @@ def test_sharded_group_rccl_world1(eng, oracle):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_fixed_capacity_exchange_kernels(eng, oracle, world):
+    """The HIP kernels of the sync-free exchange (sd_cas_exchange_{pack,split,unpack}_
+    fixed_dev + sd_cas_copy_objects_dev) with `world` ranks emulated in one process: the
+    all_to_all of equal blocks is a block transpose.  Grouping == the oracle's canonical,
+    keys equal to the sentinels included; then an overflowing part sets the flag."""
+    from spacedrive_amd.shard import HipShardOps, fixed_capacity, range_start
+    ops = HipShardOps(eng)
+    rng = np.random.default_rng(50 + world)
+    pool = rng.integers(0, 2 ** 64, 60_000, dtype=np.uint64)
+    for r in range(world):
+        b = range_start(r, world)
+        pool[2 * r: 2 * r + 2] = [b, (b - 1) % 2 ** 64]
+    keys = pool[rng.integers(0, len(pool), 200_003)]
+    cuts = [len(keys) * r // world for r in range(world + 1)]
+    cap, spill = fixed_capacity(max(cuts[r + 1] - cuts[r] for r in range(world)), world)
+    sent = []
+    for r in range(world):
+        k = dev64(keys[cuts[r]:cuts[r + 1]])
+        pk, pp, cnt = ops.partition(k, world)
+        rows, srows, ovf = ops.pack_fixed(pk, pp, cnt, world, cap, spill, cuts[r])
+        sent.append((pp, cnt, rows.view(world, cap, 3), srows.view(world, spill, 3), ovf))
+    assert all(int(s[4].item()) == 0 for s in sent)
+    backs = []
+    objects = 0
+    for d in range(world):  # receiver d: block d of every sender, main then spill
+        rr = torch.cat([s[2][d] for s in sent] + [s[3][d] for s in sent])
+        rk, rv, hit = ops.split_fixed(rr, range_start(d + 1, world))
+        out, obj = ops.group_min_dev(rk, rv)
+        objects += int(obj.item()) - int(hit.item())
+        backs.append(out)
+    orep, oobj = oracle.group_canonical(keys)
+    assert objects == oobj
+    for r in range(world):  # mirror: sender r gets block r of every receiver's reps
+        back = torch.cat([b[:world * cap].view(world, cap)[r] for b in backs])
+        sback = torch.cat([b[world * cap:].view(world, spill)[r] for b in backs])
+        rep = ops.unpack_fixed(back, sback, sent[r][0], sent[r][1], world, cap, spill)
+        assert (rep.cpu().numpy() == orep[cuts[r]:cuts[r + 1]].astype(np.int64)).all(), r
+    # a part beyond cap + spill raises the overflow flag
+    k = dev64(np.full(5000, keys[0], dtype=np.uint64))
+    pk, pp, cnt = ops.partition(k, world)
+    _, _, ovf = ops.pack_fixed(pk, pp, cnt, world, 100, 100, 0)
+    assert int(ovf.item()) == 1
+
+
+def test_multi_device_create_across_devices(eng, oracle):
+    """sd_cas_multi_create over two distinct devices: on a one-GPU box it fails loudly
+    (ENODEV, with the reason); with two or more GPUs peer access must be enabled and the
+    cross-device exchange (hipMemcpyPeerAsync over xGMI) must match the oracle."""
+    from spacedrive_amd import CasError
+    from spacedrive_amd.multi import MultiEngine
+    if torch.cuda.device_count() < 2:
+        with pytest.raises(CasError, match="ENODEV.*device 1"):
+            MultiEngine([0, 1])
+        return
+    rng = np.random.default_rng(24)
+    pool = rng.integers(0, 2 ** 64, 40_000, dtype=np.uint64)
+    keys = pool[rng.integers(0, len(pool), 100_000)]
+    me = MultiEngine([0, 1])
+    parts = [torch.from_numpy(keys[:50_000].view(np.int64)).to("cuda:0"),
+             torch.from_numpy(keys[50_000:].view(np.int64)).to("cuda:1")]
+    reps, objects = me.group(parts, [0, 50_000])
+    orep, oobj = oracle.group_canonical(keys)
+    assert objects == oobj
+    assert (np.concatenate([r.cpu().numpy() for r in reps]) == orep.astype(np.int64)).all()
+    me.close()
+
+
 @pytest.mark.parametrize("shards", [1, 2, 3, 4])
 def test_multi_device_group(eng, oracle, shards):
     """Single-process multi-device grouping (sd_cas_multi_group): `shards` shards on

@@ -63,6 +63,45 @@ class HostOps:
         rep[pos.numpy()] = back.numpy().view(np.uint32)
         return torch.from_numpy(rep)
 
+    def group_min_dev(self, keys, vals):
+        out, objects = self.group_min(keys, vals)
+        return out, torch.tensor([objects], dtype=torch.int64)
+
+    # the contracts of sd_cas_exchange_{pack,split,unpack}_fixed_dev
+    def pack_fixed(self, keys, pos, counts, parts, cap, spill, file0):
+        from spacedrive_amd.shard import range_start
+        k = keys.numpy().view(np.uint64)
+        p = pos.numpy().astype(np.uint64)
+        c = counts.numpy()
+        off = np.concatenate([[0], np.cumsum(c)[:-1]])
+        rows = np.empty((parts * (cap + spill), 3), dtype=np.uint32)
+        for q in range(parts):
+            sent = np.uint64(range_start(q + 1, parts))
+            for t in range(cap + spill):
+                slot = q * cap + t if t < cap else parts * cap + q * spill + (t - cap)
+                if t < c[q]:
+                    kk, vv = k[off[q] + t], (p[off[q] + t] + np.uint64(file0)) & np.uint64(0xFFFFFFFF)
+                else:
+                    kk, vv = sent, np.uint64(0xFFFFFFFF)
+                rows[slot] = [kk & np.uint64(0xFFFFFFFF), kk >> np.uint64(32), vv]
+        overflow = torch.tensor([int((c > cap + spill).any())], dtype=torch.int32)
+        r = torch.from_numpy(rows.view(np.int32))
+        return r[:parts * cap].contiguous(), r[parts * cap:].contiguous(), overflow
+
+    def split_fixed(self, rows, sentinel):
+        k, v = self.split(rows)
+        hit = bool((k.numpy().view(np.uint64) == np.uint64(sentinel)).any())
+        return k, v, torch.tensor([int(hit)], dtype=torch.int64)
+
+    def unpack_fixed(self, back, spill_back, pos, counts, parts, cap, spill):
+        b, sb, p, c = back.numpy().view(np.uint32), spill_back.numpy().view(np.uint32), pos.numpy(), counts.numpy()
+        off = np.concatenate([[0], np.cumsum(c)[:-1]])
+        rep = np.empty(len(p), dtype=np.int64)
+        for q in range(parts):
+            for t in range(min(int(c[q]), cap + spill)):
+                rep[p[off[q] + t]] = b[q * cap + t] if t < cap else sb[q * spill + t - cap]
+        return torch.from_numpy(rep)
+
 
 def _free_port():
     s = socket.socket()
@@ -72,25 +111,28 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, all_keys, per, q):
+def _worker(rank, world, port, all_keys, per, q, capacity):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from spacedrive_amd.shard import sharded_group
     lo, hi = rank * per, min(len(all_keys), (rank + 1) * per)
     keys = torch.from_numpy(all_keys[lo:hi].view(np.int64).copy())
-    res = sharded_group(keys, lo, HostOps())
-    q.put((rank, res.rep.numpy().tolist(), res.objects))
+    res = sharded_group(keys, lo, HostOps(rank), capacity=capacity)
+    overflowed = None if res.overflow is None else int(res.overflow.item())
+    res.resolve()
+    q.put((rank, res.rep.numpy().tolist(), res.objects, overflowed))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def run_sharded(all_keys: np.ndarray, world: int):
+def run_sharded(all_keys: np.ndarray, world: int, capacity=None, want_overflow=None):
     per = (len(all_keys) + world - 1) // world
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, all_keys, per, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, all_keys, per, q, capacity))
+             for r in range(world)]
     for p in procs:
         p.start()
     out = [q.get(timeout=120) for _ in range(world)]
@@ -100,16 +142,56 @@ def run_sharded(all_keys: np.ndarray, world: int):
     out.sort()
     rep = sum((o[1] for o in out), [])
     assert len({o[2] for o in out}) == 1
+    if want_overflow is not None:
+        assert {o[3] for o in out} == {int(want_overflow)}
     return np.array(rep), out[0][2]
 
 
-@pytest.mark.parametrize("world", [2, 4])
+def boundary_keys(rng, world, n_pool, n):
+    pool = rng.integers(0, 2 ** 64, n_pool, dtype=np.uint64)
+    pool[:5] = [0, 1, 2 ** 63, 2 ** 63 - 1, 2 ** 64 - 1]  # range-boundary keys
+    from spacedrive_amd.shard import range_start
+    for r in range(1, world):  # every range's first key, its predecessor (= sentinels)
+        b = range_start(r, world)
+        pool[5 + 2 * r: 7 + 2 * r] = [b, b - 1]
+    return pool[rng.integers(0, len(pool), n)]
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_sharded_group_matches_canonical(world, oracle):
     rng = np.random.default_rng(world)
-    pool = rng.integers(0, 2 ** 64, 900, dtype=np.uint64)
-    pool[:5] = [0, 1, 2 ** 63, 2 ** 63 - 1, 2 ** 64 - 1]  # range-boundary keys
-    keys = pool[rng.integers(0, len(pool), 2500)]
+    keys = boundary_keys(rng, world, 900, 2500)
     rep, objects = run_sharded(keys, world)
+    orep, oobj = oracle.group_canonical(keys)
+    assert objects == oobj
+    assert (rep == orep.astype(np.int64)).all()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_group_fixed_capacity(world, oracle):
+    """The sync-free exchange (fixed per-peer capacity, sentinel rows in unused slots,
+    spill blocks): same grouping as the canonical one, keys equal to every sentinel
+    (the first key of each range) included, no overflow for uniform keys."""
+    from spacedrive_amd.shard import fixed_capacity
+    rng = np.random.default_rng(10 + world)
+    keys = boundary_keys(rng, world, 1500, 4000)
+    per = (len(keys) + world - 1) // world
+    rep, objects = run_sharded(keys, world, capacity=fixed_capacity(per, world), want_overflow=0)
+    orep, oobj = oracle.group_canonical(keys)
+    assert objects == oobj
+    assert (rep == orep.astype(np.int64)).all()
+
+
+def test_sharded_group_fixed_capacity_overflow_falls_back(oracle):
+    """A heavily duplicated library (many copies of one file: all on one rank's range)
+    overflows the fixed capacity; the max-reduced flag makes every rank redo the step with
+    the exact exchange, and the result is still the canonical grouping."""
+    rng = np.random.default_rng(33)
+    keys = rng.integers(0, 2 ** 64, 3000, dtype=np.uint64)
+    keys[::2] = keys[7]  # half the files are one content
+    world = 4
+    per = (len(keys) + world - 1) // world
+    rep, objects = run_sharded(keys, world, capacity=(per // world + 20, 16), want_overflow=1)
     orep, oobj = oracle.group_canonical(keys)
     assert objects == oobj
     assert (rep == orep.astype(np.int64)).all()
