@@ -51,12 +51,12 @@ HW_OPS = 680                 # VALU instructions per compression as compiled (ad
 # 224 v_alignbit + 112 v_add3 (half rate on gfx950, 2 slots; profiles/r01_ubench_valu.log)
 SLOTS = 230 + 112 + 2 * (224 + 112)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
-# grouping (group_hash.hip): hist read 8 + scatter read 8 / write 12 + refine read 12 /
-# write 12 + bucket read 12 + rep write 4 = 68 B/key when the refine level runs (more
-# than 1,441,792 keys); 44 B/key below, where the 256 coarse buckets go straight to the
-# 8,192-slot tables (sd_bucket_min_big)
+# grouping (group_hash.hip): totals read 8 + prefill write 4 + scatter read 8 / write 12 +
+# bucket read 12 = 44 B/key up to 1,441,792 keys (the 256 coarse buckets go straight to
+# the 8,192-slot tables, sd_bucket_min_big); above, the refine level adds count read 8 +
+# read 12 / write 12 = 76 B/key (the minima of duplicates are the only other stores)
 def group_bytes_per_key(n: int) -> int:
-    return 44 if n <= 256 * 5632 else 68
+    return 44 if n <= 256 * 5632 else 76
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # 256 CUs x 4 SIMD32 x 32 lanes x 2.4 GHz = 78.6
 # measured ceiling of K1's own instruction stream (compute-only loop at 2.38 GHz, no loads):
 # profiles/r01_ubench_k1_clock.log

@@ -7,28 +7,28 @@
 //
 // The grouping never needs the keys in order — only equal keys side by side — so instead
 // of an 8-pass LSD sort (256 B/key of HBM traffic, ~40 launches) it is:
-//   K4h-a  sd_part_hist     per-block coarse-bucket histogram, [bucket][block] table,
-//                           and the prefill out[i] = val(i)                  8 B read, 4 B write
-//          exclusive scan of the table (sd_group.h exclusive_scan_u32)
+//   K4h-a  sd_part_totals   per-block coarse-bucket histogram in LDS, added to the bucket
+//                           totals (one atomic per bucket per block), and the prefill
+//                           out[i] = val(i)                                  8 B read, 4 B write
 //   K4h-b  sd_part_scatter  keys -> coarse-bucket-contiguous (mixed key, position),
-//                           LDS-staged so stores are coalesced runs          8 B read, 12 B write
+//                           LDS-staged so stores are coalesced runs; each trip reserves its
+//                           run in a bucket with one atomic per bucket     8 B read, 12 B write
 //   K4h-c  sd_part_refine   one workgroup per coarse bucket splits it by the next bits
-//                           (only when > 2^8 buckets are needed)             12 B read, 12 B write
+//                           (only above 1.44M keys)                     20 B read, 12 B write
 //   K5h    sd_bucket_min    one workgroup per fine bucket: LDS hash table of the bucket's
 //                           distinct keys with an atomic min of the value, then every
-//                           position looks its key up; it stores the min only where it
+//                           position reads its slot's minimum; it stores only where it
 //                           differs from the prefill (duplicates)            12 B read, <= 4 B write
-// = 68 B/key (44 without the refine level) in 7-8 launches.  Up to 1,441,792 keys (the
-// bench's 1.31 M per GPU) the refine level is skipped: the 256 coarse buckets (~5,100 keys)
-// go straight to 1,024-thread workgroups with 8,192-slot tables (sd_bucket_min_big):
-// 1.31 M keys 0.079 -> 0.062 ms.  Measured at 12.5M keys: 0.46 ms
-// vs 2.9 ms for the LSD path (profiles/r01_group_hash_v*.log).  The bucket is the top bits
+// = 76 B/key (44 without the refine level) in 4-5 launches (a memset of the totals + the
+// kernels; no [bucket][block] table and no scan: the order inside a bucket is arbitrary and
+// the results do not depend on it).  Up to 1,441,792 keys (the bench's 1.31 M per GPU) the
+// refine level is skipped: the 256 coarse buckets (~5,100 keys) go straight to 1,024-thread
+// workgroups with 8,192-slot tables (sd_bucket_min_big).  The bucket is the top bits
 // of a bijective mix of the key, so any set of DISTINCT keys spreads evenly (BLAKE3 keys are
 // uniform anyway; test keys such as 0..n-1 are not), while duplicates — however many —
 // share one table slot.  A bucket whose distinct keys overflow the LDS table (never for
 // uniform keys: mean <= 1,536 distinct per bucket vs 3,584 allowed) is redone by the same
-// workgroup in a global-memory table; results do not depend on the order the scatter wrote
-// the bucket in.
+// workgroup in a global-memory table.
 //
 // The same two kernels give the key-RANGE partition of the multi-GPU exchange (SURVEY §8e:
 // dest = floor(key * G / 2^64)), with the bucket function applied to the raw key.
@@ -53,7 +53,8 @@ constexpr int BIG_THREADS = 1024;
 constexpr uint64_t BIG_MAX_KEYS = 256ull * 5632;  // mean coarse bucket <= 5,632 keys
 constexpr uint32_t MAX_BUCKETS = 16384;   // LDS cursor table of the partition kernels (64 KiB)
 constexpr uint64_t TARGET_PER_BUCKET = 1536;
-constexpr uint64_t MAX_TABLE_ENTRIES = 2ull << 20;  // [bucket][block] table (8 MiB)
+constexpr uint64_t MAX_TABLE_ENTRIES = 2ull << 20;  // bucket-count atomics per partition pass
+constexpr uint32_t TOTALS_REPL = 16;                  // interleaved copies of the bucket totals
 // final buckets: 2^bits, bits = b1 (coarse, <= 10) + b2 (refine, <= 9); at the largest
 // plan the mean bucket may grow to MAX_MEAN_PER_BUCKET distinct keys (LDS table fill 3,584)
 constexpr uint32_t MAX_BITS = 19;
@@ -81,13 +82,28 @@ __device__ __forceinline__ uint32_t bucket_of(uint64_t stored, uint32_t nb) {
 // read, so that sd_bucket_min only stores where a key's minimum differs from the
 // position's own value — a scattered 4-B store costs a 32-B HBM write (PMC:
 // profiles/r01_pmc_group.json), and most positions are their key's first occurrence.
+//
+// Bucket totals: each block counts its slice in LDS and adds its counts to totals[nb]
+// (one global atomic per non-empty bucket per block).  The scatter then reserves each
+// trip's run inside a bucket with one atomic per bucket (order inside a bucket is
+// arbitrary — the grouping never depends on it), so no [bucket][block] table and no scan
+// pass are needed (measured: the scan was 3 launches / ~15 us per grouping call).  Block
+// 0 also zeroes the scatter's reservation cursors and the Object counter (both are used
+// only by later kernels of the chain).
+// totals are kept in `repl` interleaved copies (block b adds into copy b % repl): a single
+// copy took 1,024 same-address atomics per bucket at 12.5M keys (+8 us, measured); the
+// scatter sums the copies.
 template <int MODE>
-__device__ void part_hist_body(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb,
-                               uint64_t per_block, uint32_t* __restrict__ hist, uint32_t nblk,
-                               const uint32_t* __restrict__ vals = nullptr,
-                               uint32_t* __restrict__ prefill = nullptr) {
+__device__ void part_totals_body(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb,
+                                 uint64_t per_block, uint32_t* __restrict__ totals, uint32_t repl,
+                                 uint32_t* __restrict__ fill, unsigned long long* __restrict__ objects,
+                                 const uint32_t* __restrict__ vals, uint32_t* __restrict__ prefill) {
   extern __shared__ uint32_t cnt[];
   for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS) cnt[b] = 0;
+  if (blockIdx.x == 0) {
+    for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS) fill[b] = 0;
+    if (objects && threadIdx.x == 0) *objects = 0;
+  }
   __syncthreads();
   const uint64_t lo = (uint64_t)blockIdx.x * per_block;
   const uint64_t hi = lo + per_block < n ? lo + per_block : n;
@@ -112,8 +128,9 @@ __device__ void part_hist_body(const uint64_t* __restrict__ keys, uint64_t n, ui
     }
   }
   __syncthreads();
+  uint32_t* mine = totals + (uint64_t)(blockIdx.x % repl) * nb;
   for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS)
-    hist[(uint64_t)b * nblk + blockIdx.x] = cnt[b];
+    if (cnt[b]) atomicAdd(&mine[b], cnt[b]);
 }
 
 // Exclusive scan of cnt[0..nb) into out (both LDS) by the whole PART_THREADS block.
@@ -141,14 +158,17 @@ __device__ void lds_exclusive_scan(const uint32_t* cnt, uint32_t* out, uint32_t 
 // LDS-staged scatter of one trip (<= PART_TILE keys at trip indices [0, trip_n)): the
 // keys are first counting-sorted by bucket in LDS, then written so that consecutive
 // lanes store consecutive slots of one bucket's run — coalesced, instead of 64 buckets
-// (= 64 cache lines) per store instruction.  gcur[b] = next global slot of bucket b for
-// this block.  tcnt must be zero on entry and is left zero.
+// (= 64 cache lines) per store instruction.  RESERVE: the trip's run in bucket b starts at
+// bstart[b] + atomicAdd(&fill[b], count) (the coarse level: many blocks share a bucket);
+// otherwise gcur[b] is this workgroup's running cursor (the refine level: one workgroup
+// owns the segment).  tcnt must be zero on entry and is left zero.
 constexpr uint32_t STAGED_MAX_NB = 1024;
-template <typename BucketFn>
+template <bool RESERVE, typename BucketFn>
 __device__ __forceinline__ void staged_trip(const uint64_t (&k)[ITEMS], const uint32_t (&pos)[ITEMS],
                                             uint32_t trip_n, uint32_t nb, BucketFn bfn,
                                             uint32_t* gcur, uint32_t* tcnt, uint32_t* tstart,
                                             uint64_t* skey, uint32_t* spos,
+                                            const uint32_t* bstart, uint32_t* __restrict__ fill,
                                             uint64_t* __restrict__ out_keys,
                                             uint32_t* __restrict__ out_pos) {
   uint32_t bk[ITEMS], r[ITEMS];
@@ -159,7 +179,11 @@ __device__ __forceinline__ void staged_trip(const uint64_t (&k)[ITEMS], const ui
     r[j] = t < trip_n ? atomicAdd(&tcnt[bk[j]], 1u) : 0u;
   }
   __syncthreads();
-  lds_exclusive_scan(tcnt, tstart, nb);
+  if (RESERVE) {
+    for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS)
+      if (tcnt[b]) gcur[b] = bstart[b] + atomicAdd(&fill[b], tcnt[b]);
+  }
+  lds_exclusive_scan(tcnt, tstart, nb);  // (its barriers also publish gcur)
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const uint32_t t = (uint32_t)j * PART_THREADS + threadIdx.x;
@@ -183,31 +207,54 @@ __device__ __forceinline__ void staged_trip(const uint64_t (&k)[ITEMS], const ui
   }
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS) {
-    gcur[b] += tcnt[b];
+    if (!RESERVE) gcur[b] += tcnt[b];
     tcnt[b] = 0;
   }
   __syncthreads();
 }
 
-// dynamic LDS of the scatter kernels: staged = gcur | tcnt | tstart | skey | spos
+// dynamic LDS of the scatter kernels: staged = bstart | gcur | tcnt | tstart | skey | spos;
+// above STAGED_MAX_NB buckets (range partitions into > 1,024 parts) bstart only
 __host__ __device__ constexpr size_t scatter_lds_bytes(uint32_t nb) {
-  return nb <= STAGED_MAX_NB ? (size_t)(3 * nb + 1) * 4 + (size_t)PART_TILE * 12 : (size_t)nb * 4;
+  return nb <= STAGED_MAX_NB ? (size_t)(4 * nb + 2) * 4 + (size_t)PART_TILE * 12 : (size_t)nb * 4;
 }
 
+// Bucket-contiguous scatter.  Every block derives the bucket starts from the totals (an
+// LDS scan); block 0 publishes them (starts_out, the coarse level's segments) and, for the
+// range partition, the part sizes (counts_out, u64).
 template <int MODE>
 __device__ void part_scatter_body(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb,
-                                  uint64_t per_block, const uint32_t* __restrict__ offs,
-                                  uint32_t nblk, uint64_t* __restrict__ out_keys,
-                                  uint32_t* __restrict__ out_pos) {
-  extern __shared__ uint32_t cur[];
-  for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS)
-    cur[b] = offs[(uint64_t)b * nblk + blockIdx.x];
+                                  uint64_t per_block, const uint32_t* __restrict__ totals,
+                                  uint32_t repl, uint32_t* __restrict__ fill,
+                                  uint64_t* __restrict__ out_keys,
+                                  uint32_t* __restrict__ out_pos, uint32_t* __restrict__ starts_out,
+                                  uint64_t* __restrict__ counts_out) {
+  extern __shared__ uint32_t lds[];
+  uint32_t* bstart = lds;
+  uint32_t* tcnt = lds + nb;  // staged only; the scan below reads totals through tcnt
+  const bool staged = nb <= STAGED_MAX_NB;
+  for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS) {
+    uint32_t x = 0;
+    for (uint32_t r = 0; r < repl; ++r) x += totals[(uint64_t)r * nb + b];
+    if (staged) tcnt[b] = x;
+    if (blockIdx.x == 0 && counts_out) counts_out[b] = x;
+  }
+  __syncthreads();
+  if (staged) {
+    lds_exclusive_scan(tcnt, bstart, nb);
+  } else if (threadIdx.x == 0) {  // > 1,024 parts (range mode only, repl = 1): sequential, rare
+    uint32_t run = 0;
+    for (uint32_t b = 0; b < nb; ++b) { bstart[b] = run; run += totals[b]; }
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && starts_out)
+    for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS) starts_out[b] = bstart[b];
   const uint64_t lo = (uint64_t)blockIdx.x * per_block;
   const uint64_t hi = lo + per_block < n ? lo + per_block : n;
-  if (nb <= STAGED_MAX_NB) {
-    uint32_t* tcnt = cur + nb;
-    uint32_t* tstart = cur + 2 * nb;
-    uint64_t* skey = reinterpret_cast<uint64_t*>(cur + 3 * nb + (nb & 1u));  // 8-B aligned
+  if (staged) {
+    uint32_t* gcur = lds + 2 * nb;  // tcnt (lds + nb) is zeroed below for the trips
+    uint32_t* tstart = lds + 3 * nb;
+    uint64_t* skey = reinterpret_cast<uint64_t*>(lds + 4 * nb + 2);  // 16nb + 8 B: 8-B aligned
     uint32_t* spos = reinterpret_cast<uint32_t*>(skey + PART_TILE);
     for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS) tcnt[b] = 0;
     __syncthreads();
@@ -222,12 +269,11 @@ __device__ void part_scatter_body(const uint64_t* __restrict__ keys, uint64_t n,
         q[j] = (uint32_t)i;
       }
       const uint64_t left = hi - base;
-      staged_trip(k, q, left < PART_TILE ? (uint32_t)left : PART_TILE, nb, bfn, cur, tcnt, tstart,
-                  skey, spos, out_keys, out_pos);
+      staged_trip<true>(k, q, left < PART_TILE ? (uint32_t)left : PART_TILE, nb, bfn, gcur, tcnt,
+                        tstart, skey, spos, bstart, fill, out_keys, out_pos);
     }
     return;
   }
-  __syncthreads();
   for (uint64_t base = lo; base < hi; base += PART_TILE) {
     uint64_t k[ITEMS];
 #pragma unroll
@@ -235,65 +281,46 @@ __device__ void part_scatter_body(const uint64_t* __restrict__ keys, uint64_t n,
       const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
       k[j] = i < hi ? stored_key<MODE>(keys[i]) : 0;
     }
-    uint32_t p[ITEMS];
-#pragma unroll
-    for (int j = 0; j < ITEMS; ++j) {
-      const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
-      p[j] = i < hi ? atomicAdd(&cur[bucket_of(k[j], nb)], 1u) : 0u;
-    }
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
       const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
       if (i < hi) {
-        out_keys[p[j]] = k[j];
-        out_pos[p[j]] = (uint32_t)i;
+        const uint32_t b = bucket_of(k[j], nb);
+        const uint32_t d = bstart[b] + atomicAdd(&fill[b], 1u);
+        out_keys[d] = k[j];
+        out_pos[d] = (uint32_t)i;
       }
     }
   }
 }
 
 extern "C" __global__ void __launch_bounds__(PART_THREADS)
-sd_part_hist_mix(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb, uint64_t per_block,
-                 uint32_t* __restrict__ hist, uint32_t nblk, const uint32_t* __restrict__ vals,
-                 uint32_t* __restrict__ prefill) {
-  part_hist_body<0>(keys, n, nb, per_block, hist, nblk, vals, prefill);
+sd_part_totals_mix(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb, uint64_t per_block,
+                   uint32_t* __restrict__ totals, uint32_t repl, uint32_t* __restrict__ fill,
+                   unsigned long long* __restrict__ objects, const uint32_t* __restrict__ vals,
+                   uint32_t* __restrict__ prefill) {
+  part_totals_body<0>(keys, n, nb, per_block, totals, repl, fill, objects, vals, prefill);
 }
 extern "C" __global__ void __launch_bounds__(PART_THREADS)
-sd_part_hist_range(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb, uint64_t per_block,
-                   uint32_t* __restrict__ hist, uint32_t nblk) {
-  part_hist_body<1>(keys, n, nb, per_block, hist, nblk);
+sd_part_totals_range(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb, uint64_t per_block,
+                     uint32_t* __restrict__ totals, uint32_t repl, uint32_t* __restrict__ fill) {
+  part_totals_body<1>(keys, n, nb, per_block, totals, repl, fill, nullptr, nullptr, nullptr);
 }
 extern "C" __global__ void __launch_bounds__(PART_THREADS)
 sd_part_scatter_mix(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb, uint64_t per_block,
-                    const uint32_t* __restrict__ offs, uint32_t nblk, uint64_t* __restrict__ out_keys,
-                    uint32_t* __restrict__ out_pos) {
-  part_scatter_body<0>(keys, n, nb, per_block, offs, nblk, out_keys, out_pos);
+                    const uint32_t* __restrict__ totals, uint32_t repl, uint32_t* __restrict__ fill,
+                    uint64_t* __restrict__ out_keys, uint32_t* __restrict__ out_pos,
+                    uint32_t* __restrict__ starts_out) {
+  part_scatter_body<0>(keys, n, nb, per_block, totals, repl, fill, out_keys, out_pos, starts_out,
+                       nullptr);
 }
 extern "C" __global__ void __launch_bounds__(PART_THREADS)
 sd_part_scatter_range(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb, uint64_t per_block,
-                      const uint32_t* __restrict__ offs, uint32_t nblk, uint64_t* __restrict__ out_keys,
-                      uint32_t* __restrict__ out_pos) {
-  part_scatter_body<1>(keys, n, nb, per_block, offs, nblk, out_keys, out_pos);
-}
-
-// counts[b] = size of part b (from the scanned [bucket][block] table)
-extern "C" __global__ void __launch_bounds__(256)
-sd_part_counts(const uint32_t* __restrict__ offs, uint32_t nb, uint32_t nblk, uint64_t n,
-               uint64_t* __restrict__ counts) {
-  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
-  if (b < nb) {
-    const uint64_t s = offs[(uint64_t)b * nblk];
-    const uint64_t e = b + 1 < nb ? offs[(uint64_t)(b + 1) * nblk] : n;
-    counts[b] = e - s;
-  }
-}
-
-// starts[b] = first position of bucket b (single-level partition)
-extern "C" __global__ void __launch_bounds__(256)
-sd_part_starts(const uint32_t* __restrict__ offs, uint32_t nb, uint32_t nblk,
-               uint32_t* __restrict__ starts) {
-  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
-  if (b < nb) starts[b] = offs[(uint64_t)b * nblk];
+                      const uint32_t* __restrict__ totals, uint32_t repl, uint32_t* __restrict__ fill,
+                      uint64_t* __restrict__ out_keys, uint32_t* __restrict__ out_pos,
+                      uint64_t* __restrict__ counts_out) {
+  part_scatter_body<1>(keys, n, nb, per_block, totals, repl, fill, out_keys, out_pos, nullptr,
+                       counts_out);
 }
 
 // Second partition level: one workgroup per coarse bucket (top b1 bits of the stored key)
@@ -305,15 +332,15 @@ sd_part_starts(const uint32_t* __restrict__ offs, uint32_t nb, uint32_t nblk,
 constexpr uint32_t MAX_FINE = 1u << MAX_B2;
 extern "C" __global__ void __launch_bounds__(PART_THREADS)
 sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict__ in_pos,
-               const uint32_t* __restrict__ offs1, uint32_t nb1, uint32_t nblk1, uint64_t n,
-               uint32_t b1, uint32_t b2, uint64_t* __restrict__ out_keys,
-               uint32_t* __restrict__ out_pos, uint32_t* __restrict__ starts) {
+               const uint32_t* __restrict__ starts1, uint32_t nb1, uint64_t n, uint32_t b1,
+               uint32_t b2, uint64_t* __restrict__ out_keys, uint32_t* __restrict__ out_pos,
+               uint32_t* __restrict__ starts) {
   __shared__ uint32_t cnt[MAX_FINE], gcur[MAX_FINE], tcnt[MAX_FINE], tstart[MAX_FINE];
   __shared__ uint64_t skey[PART_TILE];
   __shared__ uint32_t spos[PART_TILE];
   const uint32_t c = blockIdx.x, nb2 = 1u << b2;
-  const uint64_t s = offs1[(uint64_t)c * nblk1];
-  const uint64_t e = c + 1 < nb1 ? offs1[(uint64_t)(c + 1) * nblk1] : n;
+  const uint64_t s = starts1[c];
+  const uint64_t e = c + 1 < nb1 ? starts1[c + 1] : n;
   if (threadIdx.x < nb2) cnt[threadIdx.x] = 0;
   __syncthreads();
   for (uint64_t base = s; base < e; base += PART_TILE) {
@@ -352,15 +379,15 @@ sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict_
       q[j] = i < e ? in_pos[i] : 0;
     }
     const uint64_t left = e - base;
-    staged_trip(k, q, left < PART_TILE ? (uint32_t)left : PART_TILE, nb2, bfn, gcur, tcnt, tstart,
-                skey, spos, out_keys, out_pos);
+    staged_trip<false>(k, q, left < PART_TILE ? (uint32_t)left : PART_TILE, nb2, bfn, gcur, tcnt,
+                       tstart, skey, spos, nullptr, nullptr, out_keys, out_pos);
   }
 }
 
 // Linear-probing tables: LDS (the normal case) and global memory (overflow).  `fresh`
 // counts keys this thread inserted first.  Returns false if the table has no room.
 template <uint32_t TBL>
-__device__ __forceinline__ bool lds_insert(uint64_t* tk, uint32_t* tv, uint32_t slot, uint64_t k,
+__device__ __forceinline__ bool lds_insert(uint64_t* tk, uint32_t* tv, uint32_t& slot, uint64_t k,
                                            uint32_t v, uint64_t empty, uint32_t& fresh) {
   for (uint32_t probe = 0; probe < TBL; ++probe) {
     uint64_t cur = tk[slot];
@@ -414,11 +441,15 @@ __device__ __forceinline__ uint64_t g_find(const uint64_t* tk, uint64_t cap, uin
 
 // One workgroup per bucket of the mixed-key partition (nb = 2^bits, bits >= 1).
 // out[pos] = min{ val(j) : key(j) == key(pos) }, val(j) = vals ? vals[j] : j, stored only
-// where it differs from val(pos): sd_part_hist_mix prefilled out[pos] = val(pos);
+// where it differs from val(pos): sd_part_totals_mix prefilled out[pos] = val(pos);
 // *objects += distinct keys.  gkeys/gvals: 2n-slot overflow tables (touched only on overflow).
 // A bucket of <= TILE keys (all but pathological ones) is loaded once and kept in
 // registers for the lookup; larger buckets stream in TILE trips.
-template <uint32_t TBL, int THREADS>
+// KEEP_SLOT: the one-trip lookup reads the slot each key landed in during the insert
+// instead of probing again — faster for the 8,192-slot tables (1.31M keys: 0.064 -> 0.060
+// ms), slower for the 4,096-slot ones (12.5M keys: 0.369 -> 0.398 ms; A/B in
+// profiles/r02_group_ab.log), so only sd_bucket_min_big keeps it.
+template <uint32_t TBL, int THREADS, bool KEEP_SLOT>
 __device__ __forceinline__ void bucket_min(const uint64_t* __restrict__ pkeys,
                                            const uint32_t* __restrict__ ppos,
                                            const uint32_t* __restrict__ vals,
@@ -442,7 +473,7 @@ __device__ __forceinline__ void bucket_min(const uint64_t* __restrict__ pkeys,
   for (uint32_t i = threadIdx.x; i < TBL; i += THREADS) { tk[i] = empty; tv[i] = 0xFFFFFFFFu; }
   if (threadIdx.x == 0) { distinct = 0; overflow = 0; }
   uint64_t k[ITEMS];
-  uint32_t p[ITEMS], v[ITEMS];
+  uint32_t p[ITEMS], v[ITEMS], sl[ITEMS];
   for (uint64_t base = s; base < e; base += TILE) {
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
@@ -457,18 +488,21 @@ __device__ __forceinline__ void bucket_min(const uint64_t* __restrict__ pkeys,
     uint32_t fresh = 0;
     bool ok = true;
 #pragma unroll
-    for (int j = 0; j < ITEMS; ++j)
-      if (k[j] != empty) ok &= lds_insert<TBL>(tk, tv, (uint32_t)k[j] & (TBL - 1), k[j], v[j], empty, fresh);
+    for (int j = 0; j < ITEMS; ++j) {
+      sl[j] = (uint32_t)k[j] & (TBL - 1);  // -> the key's slot (kept for the one-trip lookup)
+      if (k[j] != empty) ok &= lds_insert<TBL>(tk, tv, sl[j], k[j], v[j], empty, fresh);
+    }
     if (fresh && atomicAdd(&distinct, fresh) + fresh > FILL) overflow = 1;
     if (!ok) overflow = 1;
   }
   __syncthreads();
   if (!overflow) {
-    if (e - s <= TILE) {  // the one trip's keys are still in registers
+    if (e - s <= TILE) {  // the one trip's keys and their slots are still in registers
 #pragma unroll
       for (int j = 0; j < ITEMS; ++j)
         if (k[j] != empty) {
-          const uint32_t mv = tv[lds_find<TBL>(tk, (uint32_t)k[j] & (TBL - 1), k[j])];
+          const uint32_t mv =
+              tv[KEEP_SLOT ? sl[j] : lds_find<TBL>(tk, (uint32_t)k[j] & (TBL - 1), k[j])];
           if (mv != v[j]) out[p[j]] = mv;  // out[] was prefilled with the own value
         }
     } else {
@@ -524,7 +558,7 @@ sd_bucket_min(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ p
               uint32_t bits, uint64_t n, uint32_t* __restrict__ out,
               unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
               uint32_t* __restrict__ gvals) {
-  bucket_min<TABLE, MIN_THREADS>(pkeys, ppos, vals, starts, nb, bits, n, out, objects, gkeys, gvals);
+  bucket_min<TABLE, MIN_THREADS, false>(pkeys, ppos, vals, starts, nb, bits, n, out, objects, gkeys, gvals);
 }
 
 // Small batches (<= BIG_MAX_KEYS): the 2^8 coarse buckets of the first partition level
@@ -536,7 +570,7 @@ sd_bucket_min_big(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict
                   uint32_t nb, uint32_t bits, uint64_t n, uint32_t* __restrict__ out,
                   unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
                   uint32_t* __restrict__ gvals) {
-  bucket_min<BIG_TABLE, BIG_THREADS>(pkeys, ppos, vals, starts, nb, bits, n, out, objects, gkeys,
+  bucket_min<BIG_TABLE, BIG_THREADS, true>(pkeys, ppos, vals, starts, nb, bits, n, out, objects, gkeys,
                                      gvals);
 }
 
@@ -548,14 +582,14 @@ namespace sdcas {
 static inline size_t al256(size_t x) { return (x + 255) / 256 * 256; }
 
 struct PartPlan {
-  uint32_t nb, bits, nblk;
+  uint32_t nb, nblk;
   uint64_t per_block;
 };
 
-// blocks: whole PART_TILE trips, at most ~1024 blocks (4 per CU) and a [bucket][block]
-// table of at most MAX_TABLE_ENTRIES (written, scanned and read once per partition)
-static PartPlan part_plan(uint64_t n, uint32_t nb, uint32_t bits) {
-  PartPlan p{nb, bits, 1, PART_TILE};
+// blocks: whole PART_TILE trips, at most ~1024 blocks (4 per CU) and nb x blocks <= 2M
+// (each block adds its nb counts to the totals with atomics)
+static PartPlan part_plan(uint64_t n, uint32_t nb) {
+  PartPlan p{nb, 1, PART_TILE};
   const uint64_t trips = n ? (n + PART_TILE - 1) / PART_TILE : 1;
   uint64_t maxblk = MAX_TABLE_ENTRIES / nb;
   if (maxblk > 1024) maxblk = 1024;
@@ -588,7 +622,7 @@ static GroupPlan group_plan(uint64_t n, uint64_t target) {
   g.b2 = bits - g.b1;
   g.big = g.b2 > 0 && n <= BIG_MAX_KEYS;
   if (g.big) g.b2 = 0;
-  g.l1 = part_plan(n, 1u << g.b1, g.b1);
+  g.l1 = part_plan(n, 1u << g.b1);
   return g;
 }
 
@@ -597,78 +631,80 @@ bool hash_group_supported(uint64_t n) {
   return n < (1ull << 32) && n <= ((uint64_t)1 << MAX_BITS) * MAX_MEAN_PER_BUCKET;
 }
 
-static size_t table_ws(const PartPlan& p) {
-  const uint64_t m = (uint64_t)p.nb * p.nblk;
-  return 2 * al256(m * 4) + al256(((m + 4095) / 4096) * 4 + 4);
-}
+static uint32_t totals_repl(uint32_t nb) { return nb <= STAGED_MAX_NB ? TOTALS_REPL : 1; }
 
+// workspace: k1 | p1 | k2 | p2 | totals (repl copies) | fill | starts1 | starts | overflow tables
 size_t hash_group_workspace_bytes(uint64_t n, uint64_t target) {
   const GroupPlan g = group_plan(n, target);
-  return 2 * (al256(n * 8) + al256(n * 4)) + table_ws(g.l1) + al256((size_t)g.nb() * 4) +
-         al256(2 * n * 8) + al256(2 * n * 4);
+  const size_t nb1 = g.l1.nb;
+  return 2 * (al256(n * 8) + al256(n * 4)) + al256(totals_repl(nb1) * nb1 * 4) +
+         2 * al256(nb1 * 4) + al256((size_t)g.nb() * 4) + al256(2 * n * 8) + al256(2 * n * 4);
 }
 
 size_t partition_workspace_bytes(uint64_t n, uint32_t parts) {
-  return table_ws(part_plan(n, parts, 0));
+  (void)n;
+  return al256((size_t)totals_repl(parts) * parts * 4) + al256((size_t)parts * 4);
 }
 
+// totals (zeroed here) -> bucket-contiguous (out_keys, out_pos); starts_out / counts_out
 static hipError_t run_partition(const uint64_t* keys, uint64_t n, const PartPlan& p, int mode,
-                                uint64_t* out_keys, uint32_t* out_pos, uint32_t* hist,
-                                uint32_t* offs, uint32_t* partial, hipStream_t s,
+                                uint64_t* out_keys, uint32_t* out_pos, uint32_t* totals,
+                                uint32_t* fill, uint32_t* starts_out, uint64_t* counts_out,
+                                unsigned long long* objects, hipStream_t s,
                                 const uint32_t* vals = nullptr, uint32_t* prefill = nullptr) {
-  const uint64_t m = (uint64_t)p.nb * p.nblk;
-  const size_t lds = (size_t)p.nb * 4, slds = scatter_lds_bytes(p.nb);
-  if (mode == 0)
-    sd_part_hist_mix<<<p.nblk, PART_THREADS, lds, s>>>(keys, n, p.nb, p.per_block, hist, p.nblk,
-                                                       vals, prefill);
-  else
-    sd_part_hist_range<<<p.nblk, PART_THREADS, lds, s>>>(keys, n, p.nb, p.per_block, hist, p.nblk);
-  hipError_t e = exclusive_scan_u32(hist, offs, m, partial, s);
+  const uint32_t repl = totals_repl(p.nb);
+  hipError_t e = hipMemsetAsync(totals, 0, (size_t)repl * p.nb * 4, s);
   if (e != hipSuccess) return e;
-  if (mode == 0)
-    sd_part_scatter_mix<<<p.nblk, PART_THREADS, slds, s>>>(keys, n, p.nb, p.per_block, offs, p.nblk,
-                                                           out_keys, out_pos);
-  else
-    sd_part_scatter_range<<<p.nblk, PART_THREADS, slds, s>>>(keys, n, p.nb, p.per_block, offs,
-                                                             p.nblk, out_keys, out_pos);
+  const size_t lds = (size_t)p.nb * 4, slds = scatter_lds_bytes(p.nb);
+  if (mode == 0) {
+    sd_part_totals_mix<<<p.nblk, PART_THREADS, lds, s>>>(keys, n, p.nb, p.per_block, totals, repl,
+                                                         fill, objects, vals, prefill);
+    sd_part_scatter_mix<<<p.nblk, PART_THREADS, slds, s>>>(keys, n, p.nb, p.per_block, totals, repl,
+                                                           fill, out_keys, out_pos, starts_out);
+  } else {
+    sd_part_totals_range<<<p.nblk, PART_THREADS, lds, s>>>(keys, n, p.nb, p.per_block, totals, repl,
+                                                           fill);
+    sd_part_scatter_range<<<p.nblk, PART_THREADS, slds, s>>>(keys, n, p.nb, p.per_block, totals,
+                                                             repl, fill, out_keys, out_pos, counts_out);
+  }
   return hipGetLastError();
 }
 
 hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n, uint32_t* out,
                           uint64_t* d_objects, void* ws, hipStream_t s, uint64_t target) {
-  hipError_t e = hipMemsetAsync(d_objects, 0, 8, s);
-  if (e != hipSuccess || n == 0) return e;
+  if (n == 0) return hipMemsetAsync(d_objects, 0, 8, s);
   if (!hash_group_supported(n)) return hipErrorInvalidValue;
   const GroupPlan g = group_plan(n, target);
-  const uint64_t m = (uint64_t)g.l1.nb * g.l1.nblk;
+  const size_t nb1 = g.l1.nb;
   char* q = (char*)ws;
   uint64_t* k1 = (uint64_t*)q; q += al256(n * 8);
   uint32_t* p1 = (uint32_t*)q; q += al256(n * 4);
   uint64_t* k2 = (uint64_t*)q; q += al256(n * 8);
   uint32_t* p2 = (uint32_t*)q; q += al256(n * 4);
-  uint32_t* hist = (uint32_t*)q; q += al256(m * 4);
-  uint32_t* offs = (uint32_t*)q; q += al256(m * 4);
-  uint32_t* partial = (uint32_t*)q; q += al256(((m + 4095) / 4096) * 4 + 4);
+  uint32_t* totals = (uint32_t*)q; q += al256(totals_repl(nb1) * nb1 * 4);
+  uint32_t* fill = (uint32_t*)q; q += al256(nb1 * 4);
+  uint32_t* starts1 = (uint32_t*)q; q += al256(nb1 * 4);
   uint32_t* starts = (uint32_t*)q; q += al256((size_t)g.nb() * 4);
   uint64_t* gkeys = (uint64_t*)q; q += al256(2 * n * 8);
   uint32_t* gvals = (uint32_t*)q;
-  e = run_partition(keys, n, g.l1, 0, k1, p1, hist, offs, partial, s, vals, out);
+  hipError_t e = run_partition(keys, n, g.l1, 0, k1, p1, totals, fill, starts1, nullptr,
+                               (unsigned long long*)d_objects, s, vals, out);
   if (e != hipSuccess) return e;
   const uint64_t* fk = k1;
   const uint32_t* fp = p1;
-  if (g.b2 == 0) {
-    sd_part_starts<<<(g.l1.nb + 255) / 256, 256, 0, s>>>(offs, g.l1.nb, g.l1.nblk, starts);
-  } else {
-    sd_part_refine<<<g.l1.nb, PART_THREADS, 0, s>>>(k1, p1, offs, g.l1.nb, g.l1.nblk, n, g.b1, g.b2,
-                                                    k2, p2, starts);
+  const uint32_t* fstarts = starts1;
+  if (g.b2 > 0) {
+    sd_part_refine<<<(uint32_t)nb1, PART_THREADS, 0, s>>>(k1, p1, starts1, (uint32_t)nb1, n, g.b1,
+                                                          g.b2, k2, p2, starts);
     fk = k2;
     fp = p2;
+    fstarts = starts;
   }
   if (g.big)
-    sd_bucket_min_big<<<g.nb(), BIG_THREADS, 0, s>>>(fk, fp, vals, starts, g.nb(), g.b1, n, out,
+    sd_bucket_min_big<<<g.nb(), BIG_THREADS, 0, s>>>(fk, fp, vals, fstarts, g.nb(), g.b1, n, out,
                                                      (unsigned long long*)d_objects, gkeys, gvals);
   else
-    sd_bucket_min<<<g.nb(), MIN_THREADS, 0, s>>>(fk, fp, vals, starts, g.nb(), g.b1 + g.b2, n, out,
+    sd_bucket_min<<<g.nb(), MIN_THREADS, 0, s>>>(fk, fp, vals, fstarts, g.nb(), g.b1 + g.b2, n, out,
                                                  (unsigned long long*)d_objects, gkeys, gvals);
   return hipGetLastError();
 }
@@ -677,16 +713,10 @@ hipError_t partition_range(const uint64_t* keys, uint64_t n, uint32_t parts, uin
                            uint32_t* out_pos, uint64_t* d_counts, void* ws, hipStream_t s) {
   if (parts == 0 || parts > MAX_BUCKETS || n >= (1ull << 32)) return hipErrorInvalidValue;
   if (n == 0) return hipMemsetAsync(d_counts, 0, (size_t)parts * 8, s);
-  const PartPlan p = part_plan(n, parts, 0);
-  const uint64_t m = (uint64_t)p.nb * p.nblk;
-  char* q = (char*)ws;
-  uint32_t* hist = (uint32_t*)q; q += al256(m * 4);
-  uint32_t* offs = (uint32_t*)q; q += al256(m * 4);
-  uint32_t* partial = (uint32_t*)q;
-  hipError_t e = run_partition(keys, n, p, 1, out_keys, out_pos, hist, offs, partial, s);
-  if (e != hipSuccess) return e;
-  sd_part_counts<<<(parts + 255) / 256, 256, 0, s>>>(offs, p.nb, p.nblk, n, d_counts);
-  return hipGetLastError();
+  const PartPlan p = part_plan(n, parts);
+  uint32_t* totals = (uint32_t*)ws;
+  uint32_t* fill = (uint32_t*)((char*)ws + al256((size_t)totals_repl(parts) * parts * 4));
+  return run_partition(keys, n, p, 1, out_keys, out_pos, totals, fill, nullptr, d_counts, nullptr, s);
 }
 
 }  // namespace sdcas
