@@ -199,16 +199,45 @@ __device__ __forceinline__ uint32_t block_inclusive_max(uint32_t x, uint32_t* to
   return max(pre, inc);
 }
 
+// Run heads of one SCAN_TILE of sorted keys, in blocked order (thread t owns items
+// t*SCAN_ITEMS ..): bit k of the result = item k starts a run.  The keys are loaded striped
+// (coalesced) into LDS, one padding slot per SCAN_ITEMS so the blocked reads hit distinct
+// banks; a blocked global load made every load instruction touch 64 cache lines and read
+// 107-150 B/key from HBM for 8 (PMC, profiles/r01_pmc_group.json).
+constexpr uint32_t PADDED_TILE = SCAN_TILE + SCAN_TILE / SCAN_ITEMS + 1;
+__device__ __forceinline__ uint32_t padded(uint32_t i) { return i + i / SCAN_ITEMS; }
+
+__device__ __forceinline__ uint32_t tile_head_bits(const uint64_t* __restrict__ skeys, uint64_t n,
+                                                   uint64_t tile0, uint64_t* sk) {
+  // sk[padded(i) + 1] = key tile0 + i; sk[0] = the previous tile's last key
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const uint32_t i = (uint32_t)k * SCAN_THREADS + threadIdx.x;
+    const uint64_t g = tile0 + i;
+    sk[padded(i) + 1] = g < n ? skeys[g] : 0;
+  }
+  if (threadIdx.x == 0) sk[0] = tile0 ? skeys[tile0 - 1] : 0;
+  __syncthreads();
+  uint32_t bits = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const uint32_t i = threadIdx.x * SCAN_ITEMS + k;
+    const uint64_t g = tile0 + i;
+    const uint64_t prev = i ? sk[padded(i - 1) + 1] : sk[0];
+    if (g < n && (g == 0 || sk[padded(i) + 1] != prev)) bits |= 1u << k;
+  }
+  return bits;
+}
+
 // +1-encoded head positions (0 = no head seen in this prefix of the tile)
 extern "C" __global__ void __launch_bounds__(SCAN_THREADS)
 sd_group_tile_heads(const uint64_t* __restrict__ skeys, uint64_t n,
                     uint32_t* __restrict__ tile_last_head, uint32_t* __restrict__ tile_heads) {
-  const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
-  uint32_t hmax = 0, hcnt = 0;
-  for (int k = 0; k < SCAN_ITEMS; ++k) {
-    const uint64_t i = base + k;
-    if (i < n && (i == 0 || skeys[i] != skeys[i - 1])) { hmax = (uint32_t)i + 1u; ++hcnt; }
-  }
+  __shared__ uint64_t sk[PADDED_TILE];
+  const uint64_t tile0 = (uint64_t)blockIdx.x * SCAN_TILE;
+  const uint32_t bits = tile_head_bits(skeys, n, tile0, sk);
+  const uint32_t hmax = bits ? (uint32_t)(tile0 + threadIdx.x * SCAN_ITEMS + 31 - __clz(bits)) + 1u : 0u;
+  const uint32_t hcnt = (uint32_t)__popc(bits);
   uint32_t tmax, tsum;
   (void)block_inclusive_max(hmax, &tmax);
   (void)block_exclusive_sum(hcnt, &tsum);
@@ -238,17 +267,26 @@ sd_group_carry(const uint32_t* __restrict__ tile_last_head, uint32_t ntiles,
   if (threadIdx.x == 0) *objects = stot;
 }
 
-// rep[vals[i]] = vals[head(i)]
+// rep[vals[i]] = vals[head(i)]; keys and vals staged through LDS like sd_group_tile_heads
 extern "C" __global__ void __launch_bounds__(SCAN_THREADS)
 sd_group_emit(const uint64_t* __restrict__ skeys, const uint32_t* __restrict__ svals,
               uint64_t n, const uint32_t* __restrict__ carry, uint32_t* __restrict__ rep) {
-  const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+  __shared__ uint64_t sk[PADDED_TILE];
+  __shared__ uint32_t sv[PADDED_TILE];
+  const uint64_t tile0 = (uint64_t)blockIdx.x * SCAN_TILE;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const uint32_t i = (uint32_t)k * SCAN_THREADS + threadIdx.x;
+    const uint64_t g = tile0 + i;
+    sv[padded(i)] = g < n ? svals[g] : 0u;
+  }
+  const uint32_t bits = tile_head_bits(skeys, n, tile0, sk);  // (its barrier publishes sv)
+  const uint64_t base = tile0 + (uint64_t)threadIdx.x * SCAN_ITEMS;
   uint32_t hm[SCAN_ITEMS];
   uint32_t run = 0;
 #pragma unroll
   for (int k = 0; k < SCAN_ITEMS; ++k) {
-    const uint64_t i = base + k;
-    if (i < n && (i == 0 || skeys[i] != skeys[i - 1])) run = (uint32_t)i + 1u;
+    if ((bits >> k) & 1u) run = (uint32_t)(base + k) + 1u;
     hm[k] = run;
   }
   uint32_t tot;
@@ -264,7 +302,8 @@ sd_group_emit(const uint64_t* __restrict__ skeys, const uint32_t* __restrict__ s
     const uint64_t i = base + k;
     if (i < n) {
       const uint32_t h = max(prev, hm[k]) - 1u;  // always >= 1 because i==0 is a head
-      rep[svals[i]] = svals[h];
+      const uint32_t hv = h >= tile0 ? sv[padded((uint32_t)(h - tile0))] : svals[h];
+      rep[sv[padded(threadIdx.x * SCAN_ITEMS + k)]] = hv;
     }
   }
 }
