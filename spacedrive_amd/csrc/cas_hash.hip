@@ -172,8 +172,40 @@ sd_cas_sampled_kernel(const uint8_t* __restrict__ content, uint64_t stride,
 // Same line-batched loads as K1 (a 128-B block pair per batch, prefetched one pair
 // ahead; quads past the content are not loaded, bytes past the message are masked) and
 // an LDS CV stack (per-lane depth, word-major).
-constexpr int PACKED_DEPTH = 6;    // popcount(c) for c <= 103 completed chunks
+// popcount(c) <= 6 pending subtrees for c <= 103 completed chunks: the bottom one (the
+// largest subtree) stays in VGPRs and the other 5 live in LDS, 160 B per lane = 40 KiB per
+// 256-lane block, so 4 blocks fill a CU's 160 KiB and K2 runs 4 waves per SIMD (a 6-deep
+// LDS stack, 48 KiB per block, held it to 3).
+constexpr int PACKED_DEPTH = 6;
+constexpr int PACKED_LDS_DEPTH = PACKED_DEPTH - 1;
 constexpr int PACKED_BLOCK = 256;
+
+struct PackedStack {
+  uint32_t (*s)[8][PACKED_BLOCK];
+  uint32_t t;
+  uint32_t sp = 0;
+  uint32_t bottom[8];
+  __device__ __forceinline__ void push(const uint32_t (&cv)[8]) {
+    if (sp == 0) {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) bottom[w] = cv[w];
+    } else {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) s[sp - 1][w][t] = cv[w];
+    }
+    ++sp;
+  }
+  __device__ __forceinline__ void pop(uint32_t (&out)[8]) {
+    --sp;
+    if (sp == 0) {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) out[w] = bottom[w];
+    } else {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) out[w] = s[sp - 1][w][t];
+    }
+  }
+};
 
 // Always 8 x 16-B loads: a quad past the content is re-pointed at quad 0 (in bounds; an
 // empty content still has 16 readable bytes, see the ABI) instead of being predicated off
@@ -194,9 +226,37 @@ __device__ __forceinline__ void mask_tail(uint32_t (&m)[16], uint32_t blen) {
   }
 }
 
+// One FULL 1 KiB chunk (not the message's last) of a K2 lane: 16 blocks of 64 B with the
+// chunk flags on blocks 0 and 15 — none of the generic loop's per-block length, mask and
+// flag logic, and unclamped loads for the chunk's own pairs (a full chunk's content quads
+// are readable: clen > 1024c + 1016 puts its 16-B round-up past the chunk).  Only the
+// prefetch of the next chunk's first pair is clamped.  A holds pair 8c on entry and pair
+// 8(c+1) on exit.  Lanes of a wave share the chunk count (the visiting order is sorted on
+// it), so this loop is wave-uniform.
+__device__ __forceinline__ void packed_full_chunk(const uint4* __restrict__ q, uint32_t clen,
+                                                  uint32_t c, uint32_t (&cv)[8], uint4 (&A)[8],
+                                                  uint4 (&B)[8], uint32_t& c0, uint32_t& c1) {
+  set_iv(cv);
+  // K1's ping-pong schedule (no register moves): pairs 0..5 in the loop, 6 and 7 peeled so
+  // that the clamped prefetch of the next chunk's first pair does not merge with the
+  // unclamped loads into per-dword select loads (that merge measured 2.8x slower)
+#pragma unroll 1
+  for (uint32_t pp = 0; pp < 3; ++pp) {
+    const uint32_t P = 8u * c + 2u * pp;
+    load_pair(q, P + 1, B);
+    compress_pair(cv, A, c0, c1, c, pp == 0 ? (uint32_t)CHUNK_START : 0u, 0u);
+    load_pair(q, P + 2, A);
+    compress_pair(cv, B, c0, c1, c, 0u, 0u);
+  }
+  load_pair(q, 8u * c + 7u, B);
+  compress_pair(cv, A, c0, c1, c, 0u, 0u);
+  load_pair_pred(q, 8u * c + 8u, clen, A);
+  compress_pair(cv, B, c0, c1, c, 0u, CHUNK_END);
+}
+
 __device__ __forceinline__ uint64_t cas_lane_packed(const uint4* __restrict__ q, uint32_t clen,
                                                     uint64_t size,
-                                                    uint32_t (*stk)[8][PACKED_BLOCK], uint32_t t) {
+                                                    PackedStack& stk) {
   const uint32_t mlen = clen + 8u;
   const uint32_t nblocks = (mlen + 63u) >> 6;   // >= 1
   const uint32_t nchunks = (mlen + 1023u) >> 10;
@@ -204,17 +264,28 @@ __device__ __forceinline__ uint64_t cas_lane_packed(const uint4* __restrict__ q,
   uint32_t c0 = (uint32_t)size, c1 = (uint32_t)(size >> 32);
   uint4 A[8], B[8];
   load_pair_pred(q, 0, clen, A);
-  uint32_t sp = 0;
   uint32_t cv[8];
-  for (uint32_t c = 0; c < nchunks; ++c) {
-    const bool last = (c + 1 == nchunks);
-    const uint32_t cblocks = last ? (nblocks - 16u * c) : 16u;
+  for (uint32_t c = 0; c + 1 < nchunks; ++c) {
+    packed_full_chunk(q, clen, c, cv, A, B, c0, c1);
+    uint32_t total = c + 1;
+    while ((total & 1u) == 0u) {
+      uint32_t left[8];
+      stk.pop(left);
+      parent(cv, left, cv, 0u);
+      total >>= 1;
+    }
+    stk.push(cv);
+  }
+  {
+    // the message's last chunk: generic blocks with length, tail mask and ROOT flags
+    const uint32_t c = nchunks - 1;
+    const uint32_t cblocks = nblocks - 16u * c;
     set_iv(cv);
     for (uint32_t b = 0; b < cblocks; b += 2) {
       const uint32_t P = 8u * c + (b >> 1);
       if (P + 1 < npairs) load_pair_pred(q, P + 1, clen, B);
       const uint32_t j = 16u * c + b;  // global block index of the pair's first block
-      const bool root1 = last && c == 0;
+      const bool root1 = c == 0;
       {
         uint32_t m[16] = {c0, c1, A[0].x, A[0].y, A[0].z, A[0].w, A[1].x, A[1].y,
                           A[1].z, A[1].w, A[2].x, A[2].y, A[2].z, A[2].w, A[3].x, A[3].y};
@@ -239,27 +310,11 @@ __device__ __forceinline__ uint64_t cas_lane_packed(const uint4* __restrict__ q,
 #pragma unroll
       for (int i = 0; i < 8; ++i) A[i] = B[i];
     }
-    if (!last) {
-      uint32_t total = c + 1;
-      while ((total & 1u) == 0u) {
-        uint32_t left[8];
-        --sp;
-#pragma unroll
-        for (int w = 0; w < 8; ++w) left[w] = stk[sp][w][t];
-        parent(cv, left, cv, 0u);
-        total >>= 1;
-      }
-#pragma unroll
-      for (int w = 0; w < 8; ++w) stk[sp][w][t] = cv[w];
-      ++sp;
-    }
   }
-  while (sp > 0) {
+  while (stk.sp > 0) {
     uint32_t left[8];
-    --sp;
-#pragma unroll
-    for (int w = 0; w < 8; ++w) left[w] = stk[sp][w][t];
-    parent(cv, left, cv, sp == 0 ? (uint32_t)ROOT : 0u);
+    stk.pop(left);
+    parent(cv, left, cv, stk.sp == 0 ? (uint32_t)ROOT : 0u);
   }
   return key_of(cv);
 }
@@ -446,12 +501,13 @@ sd_cas_packed_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restri
                      const uint32_t* __restrict__ lens, const uint64_t* __restrict__ sizes,
                      const uint32_t* __restrict__ order, uint64_t n,
                      uint64_t* __restrict__ keys) {
-  __shared__ uint32_t stack_lds[PACKED_DEPTH][8][PACKED_BLOCK];
+  __shared__ uint32_t stack_lds[PACKED_LDS_DEPTH][8][PACKED_BLOCK];
   const uint64_t t = (uint64_t)blockIdx.x * PACKED_BLOCK + threadIdx.x;
   if (t >= n) return;
   const uint32_t f = order ? order[t] : (uint32_t)t;
   const uint4* q = reinterpret_cast<const uint4*>(arena + offs[f]);
-  keys[f] = cas_lane_packed(q, lens[f], sizes[f], stack_lds, threadIdx.x);
+  PackedStack stk{stack_lds, threadIdx.x};
+  keys[f] = cas_lane_packed(q, lens[f], sizes[f], stk);
 }
 
 }  // namespace sdcas
@@ -464,24 +520,25 @@ namespace sdcas {
 // window keeps a wave's 64 lanes inside ~LEN_WINDOW files of the arena instead of spread
 // over all of it (a global length sort scattered every wave over the whole arena and
 // thrashed address translation: 4x slower on 1M files / 51 GB).
-// Visiting order = STABLE sort on the descending chunk count only (blocks >> 4): the
-// longest messages start first (no tail of late long waves) and, the sort being stable,
-// the files of one bucket keep their arena order, so a wave's 64 lanes stay close in
-// memory.  Measured on 1M ragged files (profiles/r01_k2_order.txt): exact-length global
-// sort 41 ms, per-window exact sort 31.7 ms, chunk buckets 17.4 ms.
-constexpr uint32_t LEN_BITS = 11;    // block count <= 1664 < 2048
-constexpr uint32_t BUCKET_SHIFT = 4; // 16 blocks = one BLAKE3 chunk
+// Visiting order = STABLE sort on the descending exact BLAKE3 chunk count of the message
+// (ceil((len + 8) / 1024)): the longest messages start first (no tail of late long waves),
+// the lanes of a wave share the chunk count (so K2's full-chunk loop is wave-uniform and
+// only the last chunk runs the generic per-block code) and, the sort being stable, the
+// files of one bucket keep their arena order, so a wave's 64 lanes stay close in memory.
+// Measured on 1M ragged files (profiles/r01_k2_order.txt): exact-length global sort 41 ms,
+// per-window exact sort 31.7 ms, chunk buckets 17.4 ms.
+constexpr uint32_t CHUNK_KEY_BITS = 7;  // chunk count <= 104 < 128
 
 extern "C" __global__ void __launch_bounds__(256)
 sd_cas_length_keys(const uint32_t* __restrict__ lens, uint64_t n, uint64_t* __restrict__ out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
-    const uint64_t nb = ((uint64_t)lens[i] + 8u + 63u) >> 6;
-    out[i] = (((1ull << LEN_BITS) - 1) - nb) >> BUCKET_SHIFT;
+    const uint64_t nchunks = ((uint64_t)lens[i] + 8u + 1023u) >> 10;
+    out[i] = ((1ull << CHUNK_KEY_BITS) - 1) - nchunks;
   }
 }
 
-int length_key_bits(uint64_t) { return (int)(LEN_BITS - BUCKET_SHIFT); }
+int length_key_bits(uint64_t) { return (int)CHUNK_KEY_BITS; }
 
 hipError_t hash_sampled(const uint8_t* content, uint64_t stride, const uint64_t* sizes,
                         uint64_t n, uint64_t* keys, hipStream_t s) {
