@@ -10,6 +10,8 @@
               H2D of batch k+1 overlapping hashing of batch k.
   --config 4  one rank's share of the 100M-file library (12.5M files, 30 % duplicates):
               K1 over resident batches, then Object grouping of all 12.5M keys.
+  --config 4full  the whole 100M-file library on one GPU: K1 over 80 resident batches,
+              grouping of all 100M keys, and the 8-shard key-range exchange path.
   --config 5  validator: full BLAKE3 of a resident buffer (default 64 GiB) with K3, and a
               streamed file_checksum of a file on tmpfs (read + H2D + K3).
 Every GPU result is checked against the oracle on (a sample of) the same input.
@@ -176,7 +178,7 @@ def config3e(eng, orc, n: int, batch: int):
         eng.free_pinned(pinned)
 
 
-def config4(eng, orc, n_total: int, batch: int, dup: int):
+def config4(eng, orc, n_total: int, batch: int, dup: int, shards: int = 1):
     """One rank's share of the 100M-file / 8-GPU library (12.5M files): hash in resident
     batches of `batch` files (content regenerated per batch on the device, untimed), keep
     all keys, then group all of them (K4h/K5h: bucket partition + LDS hash min).  Grouping is checked against the
@@ -215,14 +217,36 @@ def config4(eng, orc, n_total: int, batch: int, dup: int):
     first = np.full(len(uniq), n_total, dtype=np.int64)
     np.minimum.at(first, inv, np.arange(n_total))
     ok = objects == len(uniq) and bool((rep.cpu().numpy() == first[inv]).all())
-    # K4h/K5h algorithmic bytes: hist read 8 + scatter read 8 / write 12 + refine read 12 /
-    # write 12 + bucket read 12 + rep write 4 = 68 B/key
-    group_bytes = 68 * n_total
-    emit({"config": "4-rank-share", "files": n_total, "dup_permille": dup,
-          "hash_kernel_s": hash_s, "hash_files_per_s": n_total / hash_s,
-          "group_s": gs, "group_keys_per_s": n_total / gs,
-          "group_hbm_gb_per_s_algorithmic": group_bytes / gs / 1e9, "objects": objects,
-          "grouping_equals_duplicate_truth": ok})
+    del roots, r, inv, first
+    # K4h/K5h algorithmic bytes per key (bench.group_bytes_per_key): totals read 8 + rep
+    # prefill 4 + scatter 8/12 + bucket read 12 = 44 up to 1,441,792 keys; above, the refine
+    # level adds count read 8 + read 12 / write 12 = 76
+    bpk = 44 if n_total <= 256 * 5632 else 76
+    out = {"config": "4-rank-share" if n_total < 100_000_000 else "4-full-library",
+           "files": n_total, "dup_permille": dup,
+           "hash_kernel_s": hash_s, "hash_files_per_s": n_total / hash_s,
+           "group_s": gs, "group_keys_per_s": n_total / gs, "group_bytes_per_key": bpk,
+           "group_hbm_gb_per_s_algorithmic": bpk * n_total / gs / 1e9,
+           "group_hbm_frac": bpk * n_total / gs / 1e9 / 8000.0, "objects": objects,
+           "grouping_equals_duplicate_truth": ok}
+    if shards > 1:
+        # the multi-GPU key-range exchange path, all shards on this device (peer copies are
+        # device-local here): rep of every file == the local grouping's
+        from spacedrive_amd.multi import MultiEngine
+        me = MultiEngine([0] * shards)
+        cuts = [n_total * i // shards for i in range(shards + 1)]
+        parts = [keys[cuts[i]:cuts[i + 1]] for i in range(shards)]
+        me.group(parts, cuts[:-1])  # warm
+        t = time.perf_counter()
+        reps, mobjects = me.group(parts, cuts[:-1])
+        torch.cuda.synchronize()
+        out["multi_group_shards"] = shards
+        out["multi_group_s_one_device"] = time.perf_counter() - t
+        out["multi_group_equals_local"] = mobjects == objects and all(
+            bool(torch.equal(reps[i], rep[cuts[i]:cuts[i + 1]])) for i in range(shards))
+        del reps
+        me.close()
+    emit(out)
 
 
 def config5(eng, orc, gib: float, file_mb: int):
@@ -317,6 +341,8 @@ def main():
             config3e(eng, orc, a.c3_files, a.c3_batch)
         elif c == "4":
             config4(eng, orc, a.c4_files, a.c4_batch, 300)
+        elif c == "4full":
+            config4(eng, orc, 100_000_000, a.c4_batch, 300, shards=8)
         elif c == "5":
             config5(eng, orc, a.c5_gib, a.c5_file_mb)
 
