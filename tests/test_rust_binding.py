@@ -103,3 +103,18 @@ def test_type_mapping_examples():
     assert c_type_to_rust("char out[17]") == "*mut c_char"
     assert c_type_to_rust("const void* h") == "*const c_void"
     assert c_type_to_rust("size_t n") == "usize"
+
+
+def test_rust_constants_match_header():
+    """Every `pub const SD_CAS_*` of the crate equals the header's #define of that name."""
+    hdr = open(os.path.join(ROOT, "include", "sd_hip_cas.h")).read()
+    rs = open(os.path.join(ROOT, "rust", "sd-hip-cas", "src", "lib.rs")).read()
+
+    def cint(v: str) -> int:
+        return int(v.replace("_", "").rstrip("uUlL"), 0)
+    defines = {m.group(1): m.group(2) for m in re.finditer(r"#define\s+(SD_CAS_\w+)\s+(\S+)", hdr)}
+    consts = re.findall(r"pub const (SD_CAS_\w+):\s*\w+\s*=\s*([0-9xXa-fA-F_]+);", rs)
+    assert len(consts) >= 8
+    for name, val in consts:
+        assert name in defines, name
+        assert cint(defines[name]) == cint(val), (name, defines[name], val)
