@@ -142,6 +142,31 @@ int sd_cas_hash_sampled_host_ring(sd_cas_ctx* ctx, const void* h_ring, uint64_t 
 /* 16 lowercase hex chars + NUL: the cas_id String of cas.rs:61 */
 void sd_cas_key_to_hex(uint64_t key, char out[17]);
 
+/* ---- cas_id string consumers: thumbnails -----------------------------
+ * get_shard_hex (core/src/object/media/thumbnail/shard.rs:10-13): the first 3 chars of the
+ * cas_id (4,096 directories "000".."fff") + NUL. */
+void sd_cas_shard_hex(uint64_t key, char out[4]);
+/* get_thumbnail_path (thumbnail/mod.rs:67-82): PathBuf pushes of
+ *   data_dir / "thumbnails" / (library_id | "ephemeral") / shard / cas_id, extension "webp"
+ * library_id NULL = ThumbnailKind::Ephemeral, else the library's UUID string
+ * (ThumbnailKind::Indexed).  snprintf-like: writes at most cap bytes incl. the NUL and returns
+ * the full path length without it (>= cap: truncated); SD_CAS_EINVAL on a NULL data_dir. */
+int64_t sd_cas_thumbnail_path(const char* data_dir, const char* library_id, uint64_t key,
+                              char* out, size_t cap);
+/* get_thumb_key (thumbnail/mod.rs:94-103): the three strings [library_id | "ephemeral",
+ * shard, cas_id], each NUL-terminated, back to back in out.  Returns the bytes needed
+ * (written only if <= cap). */
+int64_t sd_cas_thumb_key(const char* library_id, uint64_t key, char* out, size_t cap);
+/* Device batches (async on stream).  keys_to_hex: d_out[16 i .. 16 i + 16) = the cas_id of
+ * key i (no NUL; d_out 16-B aligned).  thumbnail_paths: d_out[stride i ..] = prefix ‖ shard ‖
+ * '/' ‖ cas_id ‖ ".webp", NUL-padded to stride, where prefix is one kind's directory with its
+ * trailing '/' (sd_cas_thumbnail_path's result minus its last 25 chars, <= 1,024 B);
+ * stride a multiple of 16, <= 2,048, >= strlen(prefix) + 26. */
+int sd_cas_keys_to_hex_dev(sd_cas_ctx* ctx, const uint64_t* d_keys, size_t n, char* d_out,
+                           void* stream);
+int sd_cas_thumbnail_paths_dev(sd_cas_ctx* ctx, const uint64_t* d_keys, size_t n,
+                               const char* prefix, uint32_t stride, char* d_out, void* stream);
+
 /* ---- cas_id: device-resident batches (async on stream) --------------------------------
  * K1 sampled path: n contents of exactly 57,344 B at d_content + i*stride
  * (stride >= 57,344, multiple of 16; d_content 16-B aligned). */

@@ -191,6 +191,55 @@ def py_cas_id(content: bytes, size: int) -> str:
 
 
 # ---------------------------------------------------------------------------
+# cas_id string consumers: thumbnails (core/src/object/media/thumbnail/)
+# ---------------------------------------------------------------------------
+THUMBNAIL_CACHE_DIR_NAME = "thumbnails"  # mod.rs:37
+WEBP_EXTENSION = "webp"                  # mod.rs:40
+EPHEMERAL_DIR = "ephemeral"              # mod.rs:41
+
+
+def py_shard_hex(cas_id: str) -> str:
+    """get_shard_hex (shard.rs:10-13): &cas_id[0..3]."""
+    return cas_id[0:3]
+
+
+def _pathbuf_push(base: str, comp: str) -> str:
+    """std PathBuf::push on Unix: an absolute component replaces the path; otherwise one '/'
+    separates the components unless the base is empty or already ends in '/'."""
+    if comp.startswith("/"):
+        return comp
+    if not base:
+        return comp
+    return base + ("" if base.endswith("/") else "/") + comp
+
+
+def _pathbuf_set_extension(path: str, ext: str) -> str:
+    """std PathBuf::set_extension: replace the file name's extension (the part after its
+    last '.', a leading '.' of a dot-file not counting) with `ext`."""
+    d, sep, name = path.rpartition("/")
+    stem = name
+    i = name.rfind(".")
+    if i > 0:
+        stem = name[:i]
+    name = stem + ("." + ext if ext else "")
+    return d + sep + name
+
+
+def py_thumbnail_path(data_dir: str, cas_id: str, library_id=None) -> str:
+    """get_thumbnail_path (mod.rs:67-82); library_id None = ThumbnailKind::Ephemeral."""
+    p = _pathbuf_push(data_dir, THUMBNAIL_CACHE_DIR_NAME)
+    p = _pathbuf_push(p, EPHEMERAL_DIR if library_id is None else str(library_id))
+    p = _pathbuf_push(p, py_shard_hex(cas_id))
+    p = _pathbuf_push(p, cas_id)
+    return _pathbuf_set_extension(p, WEBP_EXTENSION)
+
+
+def py_thumb_key(cas_id: str, library_id=None) -> list:
+    """get_thumb_key (mod.rs:94-103)."""
+    return [EPHEMERAL_DIR if library_id is None else str(library_id), py_shard_hex(cas_id), cas_id]
+
+
+# ---------------------------------------------------------------------------
 # synthetic content (same counter-based splitmix64 as oracle/cas_ref.c and the device)
 # ---------------------------------------------------------------------------
 _G = np.uint64(0x9E3779B97F4A7C15)

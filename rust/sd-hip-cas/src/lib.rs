@@ -10,7 +10,8 @@
 use std::{
     ffi::{c_char, c_int, c_void, CStr, CString},
     io,
-    path::Path,
+    os::unix::ffi::OsStrExt,
+    path::{Path, PathBuf},
     ptr,
 };
 
@@ -59,6 +60,15 @@ extern "C" {
                                          ring_files: usize, h_sizes: *const u64, n: usize,
                                          h_keys: *mut u64, batch_files: usize) -> c_int;
     pub fn sd_cas_key_to_hex(key: u64, out: *mut c_char);
+    pub fn sd_cas_shard_hex(key: u64, out: *mut c_char);
+    pub fn sd_cas_thumbnail_path(data_dir: *const c_char, library_id: *const c_char, key: u64,
+                                 out: *mut c_char, cap: usize) -> i64;
+    pub fn sd_cas_thumb_key(library_id: *const c_char, key: u64, out: *mut c_char, cap: usize) -> i64;
+    pub fn sd_cas_keys_to_hex_dev(ctx: *mut sd_cas_ctx, d_keys: *const u64, n: usize, d_out: *mut c_char,
+                                  stream: *mut c_void) -> c_int;
+    pub fn sd_cas_thumbnail_paths_dev(ctx: *mut sd_cas_ctx, d_keys: *const u64, n: usize,
+                                      prefix: *const c_char, stride: u32, d_out: *mut c_char,
+                                      stream: *mut c_void) -> c_int;
     pub fn sd_cas_hash_sampled_dev(ctx: *mut sd_cas_ctx, d_content: *const c_void, stride: u64,
                                    d_sizes: *const u64, n: usize, d_keys: *mut u64,
                                    stream: *mut c_void) -> c_int;
@@ -147,6 +157,27 @@ pub struct CasId(pub u64);
 impl std::fmt::Display for CasId {
     fn fmt(&self, f: &mut std::fmt::Formatter<'_>) -> std::fmt::Result {
         write!(f, "{:016x}", self.0)
+    }
+}
+
+impl CasId {
+    /// get_shard_hex (thumbnail/shard.rs:10-13) through sd_cas_shard_hex.
+    pub fn shard_hex(&self) -> String {
+        let mut out = [0 as c_char; 4];
+        unsafe { sd_cas_shard_hex(self.0, out.as_mut_ptr()) };
+        unsafe { CStr::from_ptr(out.as_ptr()) }.to_string_lossy().into_owned()
+    }
+
+    /// get_thumbnail_path (thumbnail/mod.rs:67-82): `library` None = ThumbnailKind::Ephemeral.
+    pub fn thumbnail_path(&self, data_dir: &Path, library: Option<&str>) -> PathBuf {
+        let dd = CString::new(data_dir.as_os_str().as_encoded_bytes()).expect("NUL in path");
+        let lib = library.map(|l| CString::new(l).expect("NUL in library id"));
+        let lp = lib.as_ref().map_or(ptr::null(), |l| l.as_ptr());
+        let need = unsafe { sd_cas_thumbnail_path(dd.as_ptr(), lp, self.0, ptr::null_mut(), 0) };
+        let mut buf = vec![0 as c_char; need as usize + 1];
+        unsafe { sd_cas_thumbnail_path(dd.as_ptr(), lp, self.0, buf.as_mut_ptr(), buf.len()) };
+        let s = unsafe { CStr::from_ptr(buf.as_ptr()) };
+        PathBuf::from(std::ffi::OsStr::from_bytes(s.to_bytes()))  // Unix paths are bytes
     }
 }
 

@@ -17,9 +17,14 @@ from .cas import (  # noqa: F401
     file_checksum,
     generate_cas_id,
     generate_cas_ids,
+    get_ephemeral_thumb_key,
+    get_ephemeral_thumbnail_path,
+    get_indexed_thumb_key,
+    get_indexed_thumbnail_path,
     get_shard_hex,
     identifier_job_step,
     key_to_cas_id,
+    thumbnail_dir,
 )
 
 __all__ = [n for n in dir() if not n.startswith("_")]

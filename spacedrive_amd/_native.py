@@ -39,6 +39,11 @@ SIGNATURES = [
     ("sd_cas_hash_sampled_host", _i, [_vp, _vp, _u64, _vp, _sz, _vp, _sz]),
     ("sd_cas_hash_sampled_host_ring", _i, [_vp, _vp, _u64, _sz, _vp, _sz, _vp, _sz]),
     ("sd_cas_key_to_hex", None, [_u64, _cp]),
+    ("sd_cas_shard_hex", None, [_u64, _cp]),
+    ("sd_cas_thumbnail_path", ctypes.c_int64, [_cp, _cp, _u64, _cp, _sz]),
+    ("sd_cas_thumb_key", ctypes.c_int64, [_cp, _u64, _cp, _sz]),
+    ("sd_cas_keys_to_hex_dev", _i, [_vp, _vp, _sz, _vp, _vp]),
+    ("sd_cas_thumbnail_paths_dev", _i, [_vp, _vp, _sz, _cp, _u32, _vp, _vp]),
     ("sd_cas_hash_sampled_dev", _i, [_vp, _vp, _u64, _vp, _sz, _vp, _vp]),
     ("sd_cas_hash_packed_dev", _i, [_vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp]),
     ("sd_cas_group_dev", _i, [_vp, _vp, _sz, _vp, _vp, _vp]),
@@ -94,6 +99,15 @@ def lib() -> ctypes.CDLL:
             raise RuntimeError(
                 f"{LIB_PATH} is missing: the HIP extension is the only implementation. "
                 "Run spacedrive_amd._native.build() (or __graft_entry__.build()).")
+        # One HIP/HSA runtime per process: torch ships its own libamdhip64.so.7, and if this
+        # library were loaded first its DT_NEEDED would pull /opt/rocm's copy too — two HSA
+        # runtimes in one process, and whichever opens the GPU second finds none (measured:
+        # ENODEV here or "No HIP GPUs" in torch).  Loading torch first makes our SONAME
+        # lookup bind to the copy already mapped.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
             if os.environ.get("SD_HIP_CAS_LIB") and not hasattr(L, name):

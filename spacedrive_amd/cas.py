@@ -324,6 +324,18 @@ class CasEngine:
         s = int(steps.value)
         return step, obj, act, counts[:2 * s].reshape(s, 2).astype(np.int64)
 
+    def keys_to_hex(self, keys, out, stream: Optional[int] = None) -> None:
+        """The cas_id column of a device batch: out (uint8, 16 per key, 16-B aligned)."""
+        self._check(self.L.sd_cas_keys_to_hex_dev(self.h, _ptr(keys), keys.numel(), _ptr(out),
+                                                  _stream(stream)), "keys_to_hex_dev")
+
+    def thumbnail_paths(self, keys, prefix: str, stride: int, out, stream: Optional[int] = None) -> None:
+        """Thumbnail path records of a device batch: out[i*stride ..] = prefix + shard + '/' +
+        cas_id + '.webp', NUL-padded (prefix from :func:`thumbnail_dir`)."""
+        self._check(self.L.sd_cas_thumbnail_paths_dev(self.h, _ptr(keys), keys.numel(),
+                                                      os.fsencode(prefix), stride, _ptr(out),
+                                                      _stream(stream)), "thumbnail_paths_dev")
+
     def sort_pairs(self, keys_in, vals_in, keys_out, vals_out, begin_bit: int = 0,
                    end_bit: int = 64, stream: Optional[int] = None) -> None:
         n = int(keys_in.numel())
@@ -491,7 +503,65 @@ def identifier_job_step(paths: Sequence[str], chunk: int = CHUNK_SIZE,
     return res
 
 
+# ---- cas_id string consumers: thumbnails (core/src/object/media/thumbnail/) ---------------
+
+def _key_of(cas_id: str) -> int:
+    if len(cas_id) != 16:
+        raise ValueError(f"a cas_id is 16 hex chars (cas.rs:61), got {cas_id!r}")
+    return cas_id_to_key(cas_id)
+
+
 def get_shard_hex(cas_id: str) -> str:
     """Thumbnail shard directory of a cas_id: its first three hex chars
-    (core/src/object/media/thumbnail/shard.rs:10-13), 4096 shards 000..fff."""
-    return cas_id[0:3]
+    (thumbnail/shard.rs:10-13), 4,096 shards 000..fff — sd_cas_shard_hex."""
+    out = ctypes.create_string_buffer(4)
+    _native.lib().sd_cas_shard_hex(_key_of(cas_id), out)
+    return out.value.decode()
+
+
+def _thumbnail_path(data_dir: str, cas_id: str, library_id: Optional[str]) -> str:
+    L = _native.lib()
+    dd = os.fsencode(data_dir)
+    lib = None if library_id is None else str(library_id).encode()
+    need = L.sd_cas_thumbnail_path(dd, lib, _key_of(cas_id), None, 0)
+    if need < 0:
+        raise CasError(int(need), "sd_cas_thumbnail_path")
+    out = ctypes.create_string_buffer(need + 1)
+    L.sd_cas_thumbnail_path(dd, lib, _key_of(cas_id), out, need + 1)
+    return os.fsdecode(out.value)
+
+
+def get_indexed_thumbnail_path(data_dir: str, cas_id: str, library_id: str) -> str:
+    """get_indexed_thumbnail_path (thumbnail/mod.rs:62-64): data_dir / "thumbnails" /
+    library_id / shard / cas_id.webp (``node.config.data_directory()`` given as data_dir)."""
+    return _thumbnail_path(data_dir, cas_id, library_id)
+
+
+def get_ephemeral_thumbnail_path(data_dir: str, cas_id: str) -> str:
+    """get_thumbnail_path(.., ThumbnailKind::Ephemeral) (thumbnail/mod.rs:67-82)."""
+    return _thumbnail_path(data_dir, cas_id, None)
+
+
+def _thumb_key(cas_id: str, library_id: Optional[str]) -> list[str]:
+    L = _native.lib()
+    lib = None if library_id is None else str(library_id).encode()
+    need = L.sd_cas_thumb_key(lib, _key_of(cas_id), None, 0)
+    out = ctypes.create_string_buffer(need)
+    L.sd_cas_thumb_key(lib, _key_of(cas_id), out, need)
+    return [x.decode() for x in out.raw[:need].split(b"\0")[:3]]
+
+
+def get_indexed_thumb_key(cas_id: str, library_id: str) -> list[str]:
+    """get_indexed_thumb_key (thumbnail/mod.rs:84-86): [library_id, shard, cas_id]."""
+    return _thumb_key(cas_id, library_id)
+
+
+def get_ephemeral_thumb_key(cas_id: str) -> list[str]:
+    """get_ephemeral_thumb_key (thumbnail/mod.rs:88-90, 94-103): ["ephemeral", shard, cas_id]."""
+    return _thumb_key(cas_id, None)
+
+
+def thumbnail_dir(data_dir: str, library_id: Optional[str] = None) -> str:
+    """The batch prefix of sd_cas_thumbnail_paths_dev: one kind's thumbnail directory with
+    its trailing '/' (the thumbnail path minus "<shard>/<cas_id>.webp")."""
+    return _thumbnail_path(data_dir, "0" * 16, library_id)[:-25]

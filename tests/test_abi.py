@@ -61,3 +61,18 @@ def test_null_context_rejected():
     L = _native.lib()
     assert L.sd_cas_generate_cas_ids(None, None, None, None, 0, None) == -1
     assert L.sd_cas_group_dev(None, None, 0, None, None, None) == -1
+
+
+def test_one_hip_runtime_per_process():
+    """Loading the library before torch must not map a second HIP/HSA runtime (torch ships
+    its own libamdhip64.so.7; two runtimes in one process leave the second without a GPU)."""
+    import subprocess
+    import sys
+    code = ("import re, spacedrive_amd._native as n; n.lib(); import torch; "
+            "m = open('/proc/self/maps').read(); "
+            "print(len(set(re.findall(r'/\\S*libamdhip64\\S*', m))), "
+            "len(set(re.findall(r'/\\S*libhsa-runtime64\\S*', m))))")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.split() == ["1", "1"], out.stdout

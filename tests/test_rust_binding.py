@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 C_TO_RUST = {
     "void": "()", "int": "c_int", "size_t": "usize", "uint64_t": "u64", "uint32_t": "u32",
-    "int32_t": "i32", "uint8_t": "u8", "char": "c_char", "sd_cas_ctx": "sd_cas_ctx",
+    "int32_t": "i32", "int64_t": "i64", "uint8_t": "u8", "char": "c_char", "sd_cas_ctx": "sd_cas_ctx",
     "sd_cas_multi": "sd_cas_multi",
 }
 
