@@ -53,7 +53,7 @@ SLOTS = 230 + 112 + 2 * (224 + 112)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 # grouping (group_hash.hip): totals read 8 + prefill write 4 + scatter read 8 / write 12 +
 # bucket read 12 = 44 B/key up to 1,441,792 keys (the 256 coarse buckets go straight to
-# the 8,192-slot tables, sd_bucket_min_big); above, the refine level adds count read 8 +
+# the 12,288-slot tables, sd_bucket_min_big); above, the refine level adds count read 8 +
 # read 12 / write 12 = 76 B/key (the minima of duplicates are the only other stores)
 def group_bytes_per_key(n: int) -> int:
     return 44 if n <= 256 * 5632 else 76

@@ -23,7 +23,7 @@
 // kernels; no [bucket][block] table and no scan: the order inside a bucket is arbitrary and
 // the results do not depend on it).  Up to 1,441,792 keys (the bench's 1.31 M per GPU) the
 // refine level is skipped: the 256 coarse buckets (~5,100 keys) go straight to 1,024-thread
-// workgroups with 8,192-slot tables (sd_bucket_min_big).  The bucket is the top bits
+// workgroups with 12,288-slot tables (sd_bucket_min_big).  The bucket is the top bits
 // of a bijective mix of the key, so any set of DISTINCT keys spreads evenly (BLAKE3 keys are
 // uniform anyway; test keys such as 0..n-1 are not), while duplicates — however many —
 // share one table slot.  A bucket whose distinct keys overflow the LDS table (never for
@@ -48,7 +48,7 @@ constexpr int ITEMS = 8;
 constexpr uint32_t PART_TILE = PART_THREADS * ITEMS;  // 4096 keys per block trip
 constexpr int MIN_THREADS = 512;
 constexpr uint32_t TABLE = 4096;          // LDS slots per bucket (48 KiB: 3 workgroups/CU)
-constexpr uint32_t BIG_TABLE = 8192;      // sd_bucket_min_big: 96 KiB LDS, 1 workgroup/CU
+constexpr uint32_t BIG_TABLE = 12288;     // sd_bucket_min_big: 144 KiB LDS, 1 workgroup/CU
 constexpr int BIG_THREADS = 1024;
 constexpr uint64_t BIG_MAX_KEYS = 256ull * 5632;  // mean coarse bucket <= 5,632 keys
 constexpr uint32_t MAX_BUCKETS = 16384;   // LDS cursor table of the partition kernels (64 KiB)
@@ -92,7 +92,11 @@ __device__ __forceinline__ uint32_t bucket_of(uint64_t stored, uint32_t nb) {
 // only by later kernels of the chain).
 // totals are kept in `repl` interleaved copies (block b adds into copy b % repl): a single
 // copy took 1,024 same-address atomics per bucket at 12.5M keys (+8 us, measured); the
-// scatter sums the copies.
+// scatter sums the copies.  The scatter's block b covers the same slice as the totals'
+// block b, so bucket c's run is split into repl sub-runs, sub-run r sized by copy r, and
+// block b reserves inside sub-run b % repl with its own cursor fill[b % repl][c]: 1/repl
+// of the blocks contend on each cursor (all of them did: every block's reservation waited
+// behind ~nblk same-address returning atomics).
 template <int MODE>
 __device__ void part_totals_body(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb,
                                  uint64_t per_block, uint32_t* __restrict__ totals, uint32_t repl,
@@ -101,7 +105,7 @@ __device__ void part_totals_body(const uint64_t* __restrict__ keys, uint64_t n, 
   extern __shared__ uint32_t cnt[];
   for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS) cnt[b] = 0;
   if (blockIdx.x == 0) {
-    for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS) fill[b] = 0;
+    for (uint32_t b = threadIdx.x; b < repl * nb; b += PART_THREADS) fill[b] = 0;
     if (objects && threadIdx.x == 0) *objects = 0;
   }
   __syncthreads();
@@ -213,10 +217,10 @@ __device__ __forceinline__ void staged_trip(const uint64_t (&k)[ITEMS], const ui
   __syncthreads();
 }
 
-// dynamic LDS of the scatter kernels: staged = bstart | gcur | tcnt | tstart | skey | spos;
-// above STAGED_MAX_NB buckets (range partitions into > 1,024 parts) bstart only
+// dynamic LDS of the scatter kernels: staged = bstart | tcnt | gcur | tstart | rbase | pad |
+// skey | spos; above STAGED_MAX_NB buckets (range partitions into > 1,024 parts) bstart only
 __host__ __device__ constexpr size_t scatter_lds_bytes(uint32_t nb) {
-  return nb <= STAGED_MAX_NB ? (size_t)(4 * nb + 2) * 4 + (size_t)PART_TILE * 12 : (size_t)nb * 4;
+  return nb <= STAGED_MAX_NB ? (size_t)(5 * nb + 2) * 4 + (size_t)PART_TILE * 12 : (size_t)nb * 4;
 }
 
 // Bucket-contiguous scatter.  Every block derives the bucket starts from the totals (an
@@ -232,16 +236,37 @@ __device__ void part_scatter_body(const uint64_t* __restrict__ keys, uint64_t n,
   extern __shared__ uint32_t lds[];
   uint32_t* bstart = lds;
   uint32_t* tcnt = lds + nb;  // staged only; the scan below reads totals through tcnt
+  uint32_t* rbase = lds + 4 * nb;  // staged: bucket start + this block's sub-run offset
   const bool staged = nb <= STAGED_MAX_NB;
+  const uint32_t mine = blockIdx.x % repl;
+  const uint64_t lo = (uint64_t)blockIdx.x * per_block;
+  const uint64_t hi = lo + per_block < n ? lo + per_block : n;
+  // the first trip's keys are loaded before the totals, so both latencies overlap
+  uint64_t k[ITEMS];
+  uint32_t q[ITEMS];
+  auto load_trip = [&](uint64_t base) {
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
+      k[j] = i < hi ? stored_key<MODE>(keys[i]) : 0;
+      q[j] = (uint32_t)i;
+    }
+  };
+  if (staged) load_trip(lo);
   for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS) {
-    uint32_t x = 0;
-    for (uint32_t r = 0; r < repl; ++r) x += totals[(uint64_t)r * nb + b];
-    if (staged) tcnt[b] = x;
+    uint32_t x = 0, pre = 0;
+    for (uint32_t r = 0; r < repl; ++r) {
+      const uint32_t t = totals[(uint64_t)r * nb + b];
+      pre += r < mine ? t : 0u;
+      x += t;
+    }
+    if (staged) { tcnt[b] = x; rbase[b] = pre; }
     if (blockIdx.x == 0 && counts_out) counts_out[b] = x;
   }
   __syncthreads();
   if (staged) {
     lds_exclusive_scan(tcnt, bstart, nb);
+    for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS) rbase[b] += bstart[b];
   } else if (threadIdx.x == 0) {  // > 1,024 parts (range mode only, repl = 1): sequential, rare
     uint32_t run = 0;
     for (uint32_t b = 0; b < nb; ++b) { bstart[b] = run; run += totals[b]; }
@@ -249,28 +274,20 @@ __device__ void part_scatter_body(const uint64_t* __restrict__ keys, uint64_t n,
   __syncthreads();
   if (blockIdx.x == 0 && starts_out)
     for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS) starts_out[b] = bstart[b];
-  const uint64_t lo = (uint64_t)blockIdx.x * per_block;
-  const uint64_t hi = lo + per_block < n ? lo + per_block : n;
   if (staged) {
     uint32_t* gcur = lds + 2 * nb;  // tcnt (lds + nb) is zeroed below for the trips
     uint32_t* tstart = lds + 3 * nb;
-    uint64_t* skey = reinterpret_cast<uint64_t*>(lds + 4 * nb + 2);  // 16nb + 8 B: 8-B aligned
+    uint64_t* skey = reinterpret_cast<uint64_t*>(lds + 5 * nb + 2);  // 20nb + 8 B: 8-B aligned
     uint32_t* spos = reinterpret_cast<uint32_t*>(skey + PART_TILE);
+    uint32_t* myfill = fill + (uint64_t)mine * nb;
     for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS) tcnt[b] = 0;
     __syncthreads();
     auto bfn = [nb](uint64_t x) { return bucket_of(x, nb); };
     for (uint64_t base = lo; base < hi; base += PART_TILE) {
-      uint64_t k[ITEMS];
-      uint32_t q[ITEMS];
-#pragma unroll
-      for (int j = 0; j < ITEMS; ++j) {
-        const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
-        k[j] = i < hi ? stored_key<MODE>(keys[i]) : 0;
-        q[j] = (uint32_t)i;
-      }
+      if (base != lo) load_trip(base);
       const uint64_t left = hi - base;
       staged_trip<true>(k, q, left < PART_TILE ? (uint32_t)left : PART_TILE, nb, bfn, gcur, tcnt,
-                        tstart, skey, spos, bstart, fill, out_keys, out_pos);
+                        tstart, skey, spos, rbase, myfill, out_keys, out_pos);
     }
     return;
   }
@@ -384,6 +401,19 @@ sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict_
   }
 }
 
+// Home slot of a (mixed, uniform) key in a TBL-slot table — its low bits for a power of two,
+// else the high half of low32 x TBL — and the linear-probing successor.
+template <uint32_t TBL>
+__device__ __forceinline__ uint32_t home_slot(uint64_t k) {
+  if ((TBL & (TBL - 1)) == 0) return (uint32_t)k & (TBL - 1);
+  return (uint32_t)(((k & 0xFFFFFFFFull) * TBL) >> 32);
+}
+template <uint32_t TBL>
+__device__ __forceinline__ uint32_t next_slot(uint32_t s) {
+  if ((TBL & (TBL - 1)) == 0) return (s + 1) & (TBL - 1);
+  return s + 1 == TBL ? 0u : s + 1;
+}
+
 // Linear-probing tables: LDS (the normal case) and global memory (overflow).  `fresh`
 // counts keys this thread inserted first.  Returns false if the table has no room.
 template <uint32_t TBL>
@@ -400,14 +430,14 @@ __device__ __forceinline__ bool lds_insert(uint64_t* tk, uint32_t* tv, uint32_t&
       atomicMin(&tv[slot], v);
       return true;
     }
-    slot = (slot + 1) & (TBL - 1);
+    slot = next_slot<TBL>(slot);
   }
   return false;
 }
 
 template <uint32_t TBL>
 __device__ __forceinline__ uint32_t lds_find(const uint64_t* tk, uint32_t slot, uint64_t k) {
-  while (tk[slot] != k) slot = (slot + 1) & (TBL - 1);  // present by construction
+  while (tk[slot] != k) slot = next_slot<TBL>(slot);  // present by construction
   return slot;
 }
 
@@ -446,7 +476,7 @@ __device__ __forceinline__ uint64_t g_find(const uint64_t* tk, uint64_t cap, uin
 // A bucket of <= TILE keys (all but pathological ones) is loaded once and kept in
 // registers for the lookup; larger buckets stream in TILE trips.
 // KEEP_SLOT: the one-trip lookup reads the slot each key landed in during the insert
-// instead of probing again — faster for the 8,192-slot tables (1.31M keys: 0.064 -> 0.060
+// instead of probing again — faster for the big tables (1.31M keys: 0.064 -> 0.060
 // ms), slower for the 4,096-slot ones (12.5M keys: 0.369 -> 0.398 ms; A/B in
 // profiles/r02_group_ab.log), so only sd_bucket_min_big keeps it.
 template <uint32_t TBL, int THREADS, bool KEEP_SLOT>
@@ -489,7 +519,7 @@ __device__ __forceinline__ void bucket_min(const uint64_t* __restrict__ pkeys,
     bool ok = true;
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
-      sl[j] = (uint32_t)k[j] & (TBL - 1);  // -> the key's slot (kept for the one-trip lookup)
+      sl[j] = home_slot<TBL>(k[j]);  // -> the key's slot (kept for the one-trip lookup)
       if (k[j] != empty) ok &= lds_insert<TBL>(tk, tv, sl[j], k[j], v[j], empty, fresh);
     }
     if (fresh && atomicAdd(&distinct, fresh) + fresh > FILL) overflow = 1;
@@ -502,7 +532,7 @@ __device__ __forceinline__ void bucket_min(const uint64_t* __restrict__ pkeys,
       for (int j = 0; j < ITEMS; ++j)
         if (k[j] != empty) {
           const uint32_t mv =
-              tv[KEEP_SLOT ? sl[j] : lds_find<TBL>(tk, (uint32_t)k[j] & (TBL - 1), k[j])];
+              tv[KEEP_SLOT ? sl[j] : lds_find<TBL>(tk, home_slot<TBL>(k[j]), k[j])];
           if (mv != v[j]) out[p[j]] = mv;  // out[] was prefilled with the own value
         }
     } else {
@@ -516,7 +546,7 @@ __device__ __forceinline__ void bucket_min(const uint64_t* __restrict__ pkeys,
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j)
           if (k[j] != empty) {
-            const uint32_t mv = tv[lds_find<TBL>(tk, (uint32_t)k[j] & (TBL - 1), k[j])];
+            const uint32_t mv = tv[lds_find<TBL>(tk, home_slot<TBL>(k[j]), k[j])];
             if (mv != (vals ? vals[p[j]] : p[j])) out[p[j]] = mv;
           }
       }
@@ -562,8 +592,10 @@ sd_bucket_min(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ p
 }
 
 // Small batches (<= BIG_MAX_KEYS): the 2^8 coarse buckets of the first partition level
-// (~5,100 keys at 1.31 M) go straight to 1,024-thread workgroups with an 8,192-slot table
-// (96 KiB LDS, one per CU) — no refine level, one launch and 24 B/key fewer.
+// (~5,100 keys at 1.31 M) go straight to 1,024-thread workgroups with a 12,288-slot table
+// (144 KiB LDS, one per CU; fill ~0.42 — 8,192 slots at fill 0.625 probed ~4 times per
+// insert and ran 3 % slower, profiles/r02_group_ab2.log) — no refine level, one launch and
+// 24 B/key fewer.
 extern "C" __global__ void __launch_bounds__(BIG_THREADS)
 sd_bucket_min_big(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ ppos,
                   const uint32_t* __restrict__ vals, const uint32_t* __restrict__ starts,
@@ -633,17 +665,18 @@ bool hash_group_supported(uint64_t n) {
 
 static uint32_t totals_repl(uint32_t nb) { return nb <= STAGED_MAX_NB ? TOTALS_REPL : 1; }
 
-// workspace: k1 | p1 | k2 | p2 | totals (repl copies) | fill | starts1 | starts | overflow tables
+// workspace: k1 | p1 | k2 | p2 | totals (repl copies) | fill (repl copies) | starts1 | starts |
+// overflow tables
 size_t hash_group_workspace_bytes(uint64_t n, uint64_t target) {
   const GroupPlan g = group_plan(n, target);
   const size_t nb1 = g.l1.nb;
-  return 2 * (al256(n * 8) + al256(n * 4)) + al256(totals_repl(nb1) * nb1 * 4) +
-         2 * al256(nb1 * 4) + al256((size_t)g.nb() * 4) + al256(2 * n * 8) + al256(2 * n * 4);
+  return 2 * (al256(n * 8) + al256(n * 4)) + 2 * al256(totals_repl(nb1) * nb1 * 4) +
+         al256(nb1 * 4) + al256((size_t)g.nb() * 4) + al256(2 * n * 8) + al256(2 * n * 4);
 }
 
 size_t partition_workspace_bytes(uint64_t n, uint32_t parts) {
   (void)n;
-  return al256((size_t)totals_repl(parts) * parts * 4) + al256((size_t)parts * 4);
+  return 2 * al256((size_t)totals_repl(parts) * parts * 4);
 }
 
 // totals (zeroed here) -> bucket-contiguous (out_keys, out_pos); starts_out / counts_out
@@ -682,7 +715,7 @@ hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n
   uint64_t* k2 = (uint64_t*)q; q += al256(n * 8);
   uint32_t* p2 = (uint32_t*)q; q += al256(n * 4);
   uint32_t* totals = (uint32_t*)q; q += al256(totals_repl(nb1) * nb1 * 4);
-  uint32_t* fill = (uint32_t*)q; q += al256(nb1 * 4);
+  uint32_t* fill = (uint32_t*)q; q += al256(totals_repl(nb1) * nb1 * 4);
   uint32_t* starts1 = (uint32_t*)q; q += al256(nb1 * 4);
   uint32_t* starts = (uint32_t*)q; q += al256((size_t)g.nb() * 4);
   uint64_t* gkeys = (uint64_t*)q; q += al256(2 * n * 8);

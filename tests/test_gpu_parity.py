@@ -277,7 +277,7 @@ def test_group_hash_adversarial_keys(eng, oracle):
     # whose mixed top 14 bits are 0, among 1M uniform keys
     deep = np.array([unmix64(int(x) >> 14) for x in rng.integers(0, 2 ** 63, 10_000, dtype=np.uint64)],
                     dtype=np.uint64)
-    # <= 1.44M keys: one level into 256 coarse buckets, 8,192-slot tables (sd_bucket_min_big);
+    # <= 1.44M keys: one level into 256 coarse buckets, 12,288-slot tables (sd_bucket_min_big);
     # above: the refine level and 4,096-slot tables — one overflowing bucket in each
     big = np.concatenate([rng.integers(0, 2 ** 64, 990_000, dtype=np.uint64), deep])
     cases["big-table overflow"] = big[rng.permutation(len(big))]
