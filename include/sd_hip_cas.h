@@ -11,7 +11,8 @@
  *
  * Conventions
  *   - Every function returns an int status: SD_CAS_OK (0) or a negative SD_CAS_E*.
- *     The message of the last failure on a context is sd_cas_last_error(ctx).
+ *     The message of the last failure on a context is sd_cas_last_error(ctx);
+ *     sd_cas_last_error(NULL) says why this thread's last sd_cas_ctx_create failed.
  *   - A "cas key" is the big-endian u64 of BLAKE3(le64(size) || content)[0..8]:
  *     sd_cas_key_to_hex(key) is exactly the 16-char cas_id String of cas.rs:61, and
  *     numeric key order equals the string order of cas_ids.

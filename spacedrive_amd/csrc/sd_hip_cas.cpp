@@ -44,17 +44,30 @@ extern "C" {
 
 int sd_cas_abi_version(void) { return SD_CAS_ABI_VERSION; }
 
+// why the calling thread's last sd_cas_ctx_create failed: sd_cas_last_error(NULL)
+static thread_local std::string g_ctx_create_err;
+
 int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
   if (!out) return SD_CAS_EINVAL;
   *out = nullptr;
+  g_ctx_create_err.clear();
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
     (void)hipGetLastError();
+    g_ctx_create_err = "no HIP device " + std::to_string(device) + " (" + std::to_string(ndev) +
+                       " visible)";
     return SD_CAS_ENODEV;
   }
   hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return SD_CAS_ENODEV;
-  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return SD_CAS_ENODEV;  // gfx950 only
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+    g_ctx_create_err = "hipGetDeviceProperties(" + std::to_string(device) + ") failed";
+    return SD_CAS_ENODEV;
+  }
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {  // gfx950 only
+    g_ctx_create_err = std::string("device ") + std::to_string(device) + " is " + prop.gcnArchName +
+                       ", not gfx950 (MI355X)";
+    return SD_CAS_ENODEV;
+  }
   sd_cas_ctx* c = new sd_cas_ctx();
   c->device = device;
   if (hipSetDevice(device) != hipSuccess ||
@@ -64,6 +77,7 @@ int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
       hipEventCreateWithFlags(&c->ws_ev, hipEventDisableTiming) != hipSuccess ||
       hipMalloc((void**)&c->d_scalar, 64) != hipSuccess) {
     sd_cas_ctx_destroy(c);
+    g_ctx_create_err = "stream/event/scratch creation failed on device " + std::to_string(device);
     return SD_CAS_EHIP;
   }
   c->quantum = (size_t)prop.multiProcessorCount * 4 * 64;
@@ -116,7 +130,9 @@ void sd_cas_ctx_destroy(sd_cas_ctx* c) {
   delete c;
 }
 
-const char* sd_cas_last_error(const sd_cas_ctx* c) { return c ? c->err.c_str() : "null context"; }
+const char* sd_cas_last_error(const sd_cas_ctx* c) {
+  return c ? c->err.c_str() : g_ctx_create_err.empty() ? "null context" : g_ctx_create_err.c_str();
+}
 
 void* sd_cas_ctx_stream(sd_cas_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
