@@ -7,6 +7,9 @@
  *
  * 1. walks <dir> (regular files, sorted by path = the file_path id order of a fresh
  *    library) and takes fs::metadata().len() of each (file_identifier/mod.rs:63,78-79);
+ *    the job's orphan query skips file_paths indexed with size 0
+ *    (orphan_path_filters, file_identifier_job.rs:264), so empty files are reported but
+ *    are not rows of the job;
  * 2. one batched generate_cas_id over all of them (sd_cas_generate_cas_ids_from_paths —
  *    cas.rs:23-62 with the reference's reads/seeks; per-file errno like mod.rs:125-141);
  * 3. the Object decisions of the whole identifier job, `chunk` rows per step with the
@@ -88,58 +91,54 @@ int main(int argc, char** argv) {
     fprintf(stderr, "sd_cas_ctx_create: %d (%s)\n", rc, sd_cas_last_error(NULL));
     return 1;
   }
+  /* the job's rows: the non-empty files (orphan_path_filters), in id order */
   const size_t n = g_n;
-  uint64_t* keys = calloc(n ? n : 1, 8);
-  int32_t* status = calloc(n ? n : 1, 4);
-  uint8_t* state = calloc(n ? n : 1, 1);
-  /* empty files get no cas_id (mod.rs:78-86): not hashed, NO_CAS rows */
   size_t m = 0;
   const char** hp = malloc((n ? n : 1) * sizeof *hp);
   uint64_t* hs = malloc((n ? n : 1) * 8);
-  size_t* hi = malloc((n ? n : 1) * sizeof *hi);
-  for (size_t i = 0; i < n; i++) {
-    if (sizes[i] == 0) {
-      state[i] = SD_CAS_ROW_NO_CAS;
-      continue;
+  for (size_t i = 0; i < n; i++)
+    if (sizes[i] != 0) {
+      hp[m] = paths[i];
+      hs[m++] = sizes[i];
     }
-    hp[m] = paths[i];
-    hs[m] = sizes[i];
-    hi[m++] = i;
-  }
-  uint64_t* hk = calloc(m ? m : 1, 8);
-  int32_t* hst = calloc(m ? m : 1, 4);
-  if (m && (rc = sd_cas_generate_cas_ids_from_paths(ctx, hp, hs, m, hk, hst)) != SD_CAS_OK) {
+  uint64_t* keys = calloc(m ? m : 1, 8);
+  int32_t* status = calloc(m ? m : 1, 4);
+  uint8_t* state = calloc(m ? m : 1, 1);
+  if (m && (rc = sd_cas_generate_cas_ids_from_paths(ctx, hp, hs, m, keys, status)) != SD_CAS_OK) {
     fprintf(stderr, "generate_cas_ids_from_paths: %d (%s)\n", rc, sd_cas_last_error(ctx));
     return 1;
   }
-  for (size_t j = 0; j < m; j++) {
-    keys[hi[j]] = hk[j];
-    status[hi[j]] = hst[j];
-    state[hi[j]] = hst[j] ? SD_CAS_ROW_ERROR : SD_CAS_ROW_HASHED;
-  }
-  const size_t max_steps = sd_cas_identifier_max_steps(n, chunk);
-  uint32_t* step = calloc(n ? n : 1, 4);
-  uint32_t* object = calloc(n ? n : 1, 4);
-  uint8_t* action = calloc(n ? n : 1, 1);
+  /* a row whose length is 0 by now gets no cas_id (mod.rs:78-86): the gather reports the
+   * file as it is, so a failed read is an ERROR row (dropped from its step, mod.rs:125-141) */
+  for (size_t j = 0; j < m; j++) state[j] = status[j] ? SD_CAS_ROW_ERROR : SD_CAS_ROW_HASHED;
+  const size_t max_steps = sd_cas_identifier_max_steps(m, chunk);
+  uint32_t* step = calloc(m ? m : 1, 4);
+  uint32_t* object = calloc(m ? m : 1, 4);
+  uint8_t* action = calloc(m ? m : 1, 1);
   uint64_t* counts = calloc(2 * (max_steps ? max_steps : 1), 8);
   uint64_t steps = 0;
-  if ((rc = sd_cas_identifier_links(ctx, keys, state, n, chunk, step, object, action, counts,
+  if ((rc = sd_cas_identifier_links(ctx, keys, state, m, chunk, step, object, action, counts,
                                     max_steps, &steps)) != SD_CAS_OK) {
     fprintf(stderr, "identifier_links: %d (%s)\n", rc, sd_cas_last_error(ctx));
     return 1;
   }
   static const char* act[] = {"created", "linked", "dropped", "not_reached"};
-  for (size_t i = 0; i < n; i++) {
-    printf("{\"row\": %zu, \"path\": ", i);
+  for (size_t i = 0, j = 0; i < n; i++) {
+    printf("{\"path\": ");
     json_str(paths[i]);
     printf(", \"size\": %llu", (unsigned long long)sizes[i]);
-    if (state[i] == SD_CAS_ROW_HASHED) {
+    if (sizes[i] == 0) {  /* not an orphan row of the job */
+      printf(", \"row\": null, \"cas_id\": null, \"action\": \"not_queried\"}\n");
+      continue;
+    }
+    printf(", \"row\": %zu", j);
+    if (state[j] == SD_CAS_ROW_HASHED) {
       char hex[17];
-      sd_cas_key_to_hex(keys[i], hex);
+      sd_cas_key_to_hex(keys[j], hex);
       printf(", \"cas_id\": \"%s\"", hex);
       if (data_dir) {
         char tp[4096];
-        if (sd_cas_thumbnail_path(data_dir, library, keys[i], tp, sizeof tp) < (int64_t)sizeof tp) {
+        if (sd_cas_thumbnail_path(data_dir, library, keys[j], tp, sizeof tp) < (int64_t)sizeof tp) {
           printf(", \"thumbnail\": ");
           json_str(tp);
         }
@@ -147,12 +146,13 @@ int main(int argc, char** argv) {
     } else {
       printf(", \"cas_id\": null");
     }
-    printf(", \"errno\": %d", status[i] ? -status[i] : 0);
-    if (step[i] == SD_CAS_NO_STEP) printf(", \"step\": null");
-    else printf(", \"step\": %u", step[i]);
-    if (object[i] == SD_CAS_NO_OBJECT) printf(", \"object\": null");
-    else printf(", \"object\": %u", object[i]);
-    printf(", \"action\": \"%s\"}\n", action[i] < 4 ? act[action[i]] : "?");
+    printf(", \"errno\": %d", status[j] ? -status[j] : 0);
+    if (step[j] == SD_CAS_NO_STEP) printf(", \"step\": null");
+    else printf(", \"step\": %u", step[j]);
+    if (object[j] == SD_CAS_NO_OBJECT) printf(", \"object\": null");
+    else printf(", \"object\": %u", object[j]);
+    printf(", \"action\": \"%s\"}\n", action[j] < 4 ? act[action[j]] : "?");
+    j++;
   }
   for (uint64_t k = 0; k < steps; k++)
     printf("{\"step\": %llu, \"total_created\": %llu, \"total_linked\": %llu}\n",

@@ -260,8 +260,12 @@ int sd_cas_group_chunked_dev(sd_cas_ctx* ctx, const uint32_t* d_rep, size_t n, u
  * job runs at most ceil(n / chunk) steps (file_identifier_job.rs:146) and ends early when
  * a query comes back empty.
  *   d_keys[i]  cas key of row i (read for hashed rows only)
+ *   rows       the file_paths the job's orphan query returns: object_id or cas_id NULL,
+ *              not a directory, and indexed size_in_bytes != 0 (orphan_path_filters,
+ *              file_identifier_job.rs:251-277) — a file indexed empty is never a row
  *   d_state[i] SD_CAS_ROW_* (u8; NULL = every row hashed): HASHED = cas_id computed,
- *              NO_CAS = metadata length 0 (mod.rs:78-86), ERROR = FileMetadata::new failed
+ *              NO_CAS = fs::metadata length 0 at identification time (a file emptied
+ *              after indexing: no cas_id, mod.rs:78-86), ERROR = FileMetadata::new failed
  *              (the row is dropped from its step, mod.rs:125-141)
  * Outputs (device, n entries each):
  *   d_step[i]   the (last) step that processed row i, SD_CAS_NO_STEP if none;

@@ -449,8 +449,10 @@ class StepResult:
 
 def identifier_job_step(paths: Sequence[str], chunk: int = CHUNK_SIZE,
                         eng: Optional[CasEngine] = None) -> StepResult:
-    """Run the file identifier over ``paths`` (ascending file_path.id order, all orphan) on a
-    fresh library, as file_identifier_job.rs:180-236 / mod.rs:98-350 would: fs::metadata
+    """Run the file identifier over ``paths`` (ascending file_path.id order: the rows the
+    job's orphan query returns — object/cas NULL and indexed size != 0, orphan_path_filters,
+    file_identifier_job.rs:251-277) on a fresh library, as file_identifier_job.rs:180-236 /
+    mod.rs:98-350 would: fs::metadata
     per row (mod.rs:63), cas_ids from the GPU (len 0 -> no cas_id, mod.rs:78-86; an I/O
     error drops the row, :125-141), and the Object decisions of every step from the GPU
     link emission (sd_cas_identifier_links: grouping + the cursor walk, a last row that

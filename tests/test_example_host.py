@@ -45,7 +45,7 @@ def test_example_job_vs_oracle_and_replay(exe, oracle, tmp_path):
     for i in range(230):
         p = d / ("sub" if i % 3 == 0 else ".") / f"f{i:04d}"
         if i % 29 == 3:
-            p.write_bytes(b"")  # no cas_id: its own Object, re-queried at a chunk end
+            p.write_bytes(b"")  # indexed with size 0: not an orphan row of the job
         elif rng.random() < 0.4:
             p.write_bytes(blobs[int(rng.integers(0, len(blobs)))])
         else:
@@ -56,18 +56,24 @@ def test_example_job_vs_oracle_and_replay(exe, oracle, tmp_path):
     r = subprocess.run([exe, str(d), "7", data_dir, LIB], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     lines = [json.loads(x) for x in r.stdout.splitlines()]
-    rows = [x for x in lines if "row" in x]
-    steps = [x for x in lines if "row" not in x]
+    files = [x for x in lines if "path" in x]
+    steps = [x for x in lines if "path" not in x]
     paths = sorted(str(p) for p in d.rglob("*") if p.is_file())
-    assert [x["path"] for x in rows] == paths
+    assert [x["path"] for x in files] == paths
+    # the job's rows: file_paths indexed with size 0 are not orphans of the job
+    # (orphan_path_filters, file_identifier_job.rs:264)
+    rows = []
+    for x in files:
+        if os.path.getsize(x["path"]) == 0:
+            assert x["row"] is None and x["action"] == "not_queried"
+        else:
+            assert x["row"] == len(rows)
+            rows.append(x)
     keys, states = [], []
     for x in rows:
         size = os.path.getsize(x["path"])
         assert x["size"] == size
-        if size == 0:
-            keys.append(0); states.append(1)
-            assert x["cas_id"] is None
-        elif not os.access(x["path"], os.R_OK):
+        if not os.access(x["path"], os.R_OK):
             keys.append(0); states.append(2)
             assert x["cas_id"] is None and x["errno"] == 13
         else:
