@@ -259,9 +259,10 @@ def unmix64(m: int) -> int:
 
 
 def test_group_hash_adversarial_keys(eng, oracle):
-    """K4h/K5h on key sets that are not uniform: small integers, one key repeated, and
+    """K4h/K5h on key sets that are not uniform: small integers, one key repeated,
     8,000 distinct keys crafted (inverse mix) into ONE bucket so its LDS table overflows
-    and the global-memory table takes over — every case vs the oracle's canonical grouping."""
+    and the global-memory table takes over, and keys ordered by bucket (maximally unequal
+    per-replica sub-runs in the scatter) — every case vs the oracle's canonical grouping."""
     rng = np.random.default_rng(40)
     crafted = np.array([unmix64(int(x) >> 3) for x in rng.integers(0, 2 ** 63, 8000, dtype=np.uint64)],
                        dtype=np.uint64)  # mix64(key) has top 3 bits 0: all in bucket 0 of 8
@@ -283,6 +284,17 @@ def test_group_hash_adversarial_keys(eng, oracle):
     cases["big-table overflow"] = big[rng.permutation(len(big))]
     big = np.concatenate([rng.integers(0, 2 ** 64, 1_600_000, dtype=np.uint64), deep])
     cases["two-level overflow"] = big[rng.permutation(len(big))]
+    # keys ordered by their mixed value: every partition block's slice falls in a few
+    # buckets, so the per-replica sub-runs of a bucket (the scatter's reservation ranges)
+    # are as unequal as they can be — one level (1.2M) and two levels (3M), ascending and
+    # descending
+    from oracle.pyoracle import np_mix64
+    for label, m in (("1 level", 1_200_000), ("2 levels", 3_000_000)):
+        sk = rng.integers(0, 2 ** 64, m, dtype=np.uint64)
+        sk[1::4] = sk[0::4][: len(sk[1::4])]
+        order = np.argsort(np_mix64(sk), kind="stable")
+        cases[f"bucket-sorted {label}"] = sk[order]
+        cases[f"bucket-sorted desc {label}"] = sk[order[::-1]]
     for name, keys in cases.items():
         rep = torch.empty(len(keys), dtype=torch.int32, device="cuda")
         objects = eng.group(dev64(keys), rep)
