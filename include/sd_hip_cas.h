@@ -77,7 +77,7 @@ size_t sd_cas_batch_quantum(const sd_cas_ctx* ctx);
  * for latency (~16 + log2(chunks) compression times per file instead of 953); larger
  * batches use one file per lane for throughput.  Both paths give identical keys.
  * 0 = always one file per lane;
- * SD_CAS_THRESHOLD_DEFAULT = the measured crossover (3/4 and 3x the batch quantum). */
+ * SD_CAS_THRESHOLD_DEFAULT = the measured crossover (3/4 and 2x the batch quantum). */
 #define SD_CAS_THRESHOLD_DEFAULT ((size_t)-1)
 void sd_cas_set_latency_threshold(sd_cas_ctx* ctx, size_t sampled_files, size_t packed_files);
 /* Shape of the chunk-parallel path: batches of at least `sampled_files` / `packed_files`

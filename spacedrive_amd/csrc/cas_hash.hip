@@ -94,8 +94,9 @@ __device__ __forceinline__ void compress_pair(uint32_t (&cv)[8], const uint4 (&A
 constexpr int SAMPLED_DEPTH = 5;  // popcount(55) pending subtrees at most
 constexpr int SAMPLED_BLOCK = 512;  // 256: 1-2 % slower, 128: 4 % (profiles/r01_k1_block_ab.log)
 
+template <int B = SAMPLED_BLOCK>
 struct LdsStack {
-  uint32_t (*s)[8][SAMPLED_BLOCK];
+  uint32_t (*s)[8][B];
   uint32_t t;
   uint32_t sp = 0;  // wave-uniform on the sampled path
   __device__ __forceinline__ void push(const uint32_t (&cv)[8]) {
@@ -110,9 +111,9 @@ struct LdsStack {
   }
 };
 
-template <bool NT = false, int L = LAYOUT_ROW>
+template <bool NT = false, int L = LAYOUT_ROW, int BLK = SAMPLED_BLOCK>
 __device__ __forceinline__ uint64_t cas_lane_sampled(const uint4* __restrict__ q, uint64_t size,
-                                                     LdsStack& stk) {
+                                                     LdsStack<BLK>& stk) {
   uint32_t c0 = (uint32_t)size, c1 = (uint32_t)(size >> 32);
   uint4 A[8], B[8];
   load_pair<NT, L>(q, 0, A);
@@ -154,16 +155,38 @@ __device__ __forceinline__ uint64_t cas_lane_sampled(const uint4* __restrict__ q
 }
 
 // K1: sampled path, uniform 57,344-B contents at a fixed stride (>= 57,344, 16-B aligned).
+// Two grid shapes of the same lane program: 512-lane workgroups (80 KiB of LDS stack, 2 per
+// CU) for batches of >= 2 quanta, and 256-lane workgroups (40 KiB, 4 per CU) below: a batch
+// of one quantum is 128 workgroups of 512 lanes, which the dispatcher puts on 128 CUs at 2
+// waves per SIMD — half the chip idle and twice the latency (measured 2.27 vs 1.15 ms for
+// 65,536 files, profiles/r02_latency_sweep.log) — while 256 workgroups of 256 lanes put one
+// wave on every SIMD.
+template <int B>
+__device__ __forceinline__ void sampled_kernel_body(const uint8_t* __restrict__ content,
+                                                    uint64_t stride,
+                                                    const uint64_t* __restrict__ sizes, uint64_t n,
+                                                    uint64_t* __restrict__ keys) {
+  __shared__ uint32_t stack_lds[SAMPLED_DEPTH][8][B];
+  const uint64_t f = (uint64_t)blockIdx.x * B + threadIdx.x;
+  if (f >= n) return;  // no barrier below: each lane only touches its own stack column
+  LdsStack<B> stk{stack_lds, threadIdx.x};
+  const uint4* q = reinterpret_cast<const uint4*>(content + f * stride);
+  keys[f] = cas_lane_sampled<false, LAYOUT_ROW, B>(q, sizes[f], stk);
+}
+
 extern "C" __global__ void __launch_bounds__(SAMPLED_BLOCK)
 sd_cas_sampled_kernel(const uint8_t* __restrict__ content, uint64_t stride,
                       const uint64_t* __restrict__ sizes, uint64_t n,
                       uint64_t* __restrict__ keys) {
-  __shared__ uint32_t stack_lds[SAMPLED_DEPTH][8][SAMPLED_BLOCK];
-  const uint64_t f = (uint64_t)blockIdx.x * SAMPLED_BLOCK + threadIdx.x;
-  if (f >= n) return;  // no barrier below: each lane only touches its own stack column
-  LdsStack stk{stack_lds, threadIdx.x};
-  const uint4* q = reinterpret_cast<const uint4*>(content + f * stride);
-  keys[f] = cas_lane_sampled(q, sizes[f], stk);
+  sampled_kernel_body<SAMPLED_BLOCK>(content, stride, sizes, n, keys);
+}
+
+constexpr int SAMPLED_BLOCK_NARROW = 256;
+extern "C" __global__ void __launch_bounds__(SAMPLED_BLOCK_NARROW)
+sd_cas_sampled_kernel_256(const uint8_t* __restrict__ content, uint64_t stride,
+                          const uint64_t* __restrict__ sizes, uint64_t n,
+                          uint64_t* __restrict__ keys) {
+  sampled_kernel_body<SAMPLED_BLOCK_NARROW>(content, stride, sizes, n, keys);
 }
 
 // ---- K2: the whole-file (packed) path ------------------------------------------------
@@ -541,10 +564,22 @@ sd_cas_length_keys(const uint32_t* __restrict__ lens, uint64_t n, uint64_t* __re
 int length_key_bits(uint64_t) { return (int)CHUNK_KEY_BITS; }
 
 hipError_t hash_sampled(const uint8_t* content, uint64_t stride, const uint64_t* sizes,
-                        uint64_t n, uint64_t* keys, hipStream_t s) {
+                        uint64_t n, uint64_t* keys, hipStream_t s, uint32_t cus) {
   if (n == 0) return hipSuccess;
   const uint64_t blocks = (n + SAMPLED_BLOCK - 1) / SAMPLED_BLOCK;
-  sd_cas_sampled_kernel<<<(uint32_t)blocks, SAMPLED_BLOCK, 0, s>>>(content, stride, sizes, n, keys);
+  // One file per lane at 4 waves per SIMD: the 512-lane grid fills the chip in rounds of
+  // two quanta (one workgroup per CU per round), the 256-lane grid in rounds of one.  The
+  // wide grid is 1-2 % faster per file (profiles/r01_k1_block_ab.log) but an odd number of
+  // quantum rounds leaves half its last round's SIMDs idle (3 quanta: 4.96 vs ~3.5 ms), so
+  // it runs only when the batch spans an even number of quanta.
+  const uint64_t quanta = cus ? (n + (uint64_t)cus * 256 - 1) / ((uint64_t)cus * 256) : 0;
+  if (cus && (blocks < cus || (quanta & 1))) {
+    const uint64_t nb = (n + SAMPLED_BLOCK_NARROW - 1) / SAMPLED_BLOCK_NARROW;
+    sd_cas_sampled_kernel_256<<<(uint32_t)nb, SAMPLED_BLOCK_NARROW, 0, s>>>(content, stride, sizes,
+                                                                           n, keys);
+  } else {
+    sd_cas_sampled_kernel<<<(uint32_t)blocks, SAMPLED_BLOCK, 0, s>>>(content, stride, sizes, n, keys);
+  }
   return hipGetLastError();
 }
 

@@ -87,16 +87,17 @@ int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
   return SD_CAS_OK;
 }
 
-// Defaults = the measured crossovers on MI355X (profiles/r01_k1l_seg_sweep.log): K1L (four
-// files per wave) wins below ~0.75 of a batch quantum for sampled messages (49,152 files:
-// 1.12 vs 1.16 ms; 65,536: 1.48 vs 1.28) and below ~3.5-4 quanta for ragged whole files
-// (131,072: 3.29 vs 3.46 ms; 262,144: 6.58 vs 6.51), where the lane-per-file K2 waits for
-// the 101-chunk latency of its longest files.
+// Defaults = the measured crossovers on MI355X (profiles/r01_k1l_seg_sweep.log,
+// r02_latency_sweep.log): K1L (four files per wave) wins below ~0.75 of a batch quantum for
+// sampled messages (49,152 files: 1.11 vs 1.15 ms; 65,536: 1.47 vs 1.19) and below ~2
+// quanta for ragged whole files (98,304: 2.47 vs 2.80 ms; 131,072: 3.28 vs 3.24; 163,840:
+// 4.08 vs 3.96 — round 2's K2 fast path moved this from ~3 quanta), where the lane-per-file
+// K2 waits for the 101-chunk latency of its longest files.
 void sd_cas_set_latency_threshold(sd_cas_ctx* c, size_t sampled_files, size_t packed_files) {
   if (!c) return;
   const size_t q = sd_cas_batch_quantum(c);
   c->latency_sampled = sampled_files == SD_CAS_THRESHOLD_DEFAULT ? q * 3 / 4 : sampled_files;
-  c->latency_packed = packed_files == SD_CAS_THRESHOLD_DEFAULT ? q * 3 : packed_files;
+  c->latency_packed = packed_files == SD_CAS_THRESHOLD_DEFAULT ? q * 2 : packed_files;
 }
 
 // Defaults = the measured crossovers between the two K1L shapes (profiles/
@@ -190,9 +191,10 @@ static hipError_t dispatch_sampled(sd_cas_ctx* c, const uint8_t* content, uint64
                          c->chunkpar_seg(n, true), s);
   const size_t q = c->quantum;
   const size_t r = n % q;
-  if (n < q || r == 0 || r >= c->latency_sampled) return hash_sampled(content, stride, sizes, n, keys, s);
+  const uint32_t cus = (uint32_t)(q / 256);
+  if (n < q || r == 0 || r >= c->latency_sampled) return hash_sampled(content, stride, sizes, n, keys, s, cus);
   const size_t full = n - r;
-  hipError_t e = hash_sampled(content, stride, sizes, full, keys, s);
+  hipError_t e = hash_sampled(content, stride, sizes, full, keys, s, cus);
   if (e != hipSuccess) return e;
   return hash_chunkpar(content + full * stride, nullptr, stride, nullptr, SAMPLED_CONTENT_LEN,
                        sizes + full, r, keys + full, c->chunkpar_seg(r, true), s);

@@ -24,8 +24,10 @@ constexpr uint32_t MAX_PACKED_CONTENT_LEN = 104u * 1024u - 8u;
 
 #include <hip/hip_runtime.h>
 namespace sdcas {
+// cus = the device's CU count: batches of fewer 512-lane workgroups than CUs take the
+// 256-lane grid (one wave per SIMD instead of half the CUs at two)
 hipError_t hash_sampled(const uint8_t* content, uint64_t stride, const uint64_t* sizes,
-                        uint64_t n, uint64_t* keys, hipStream_t s);
+                        uint64_t n, uint64_t* keys, hipStream_t s, uint32_t cus);
 hipError_t hash_packed(const uint8_t* arena, const uint64_t* offs, const uint32_t* lens,
                        const uint64_t* sizes, const uint32_t* order, uint64_t n, uint64_t* keys,
                        hipStream_t s);

@@ -325,7 +325,8 @@ int sd_cas_multi_hash_group_sampled_host(sd_cas_multi* m, const void* h_content,
       if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, h2d[2 * i + s], 0);
       if (e == hipSuccess)
         e = hash_sampled((const uint8_t*)slot, stride, (const uint64_t*)(slot + cbytes), cntf,
-                         (uint64_t*)keys[i].p + k * batch, c->stream);
+                         (uint64_t*)keys[i].p + k * batch, c->stream,
+                         (uint32_t)(sd_cas_batch_quantum(c) / 256));
       if (e == hipSuccess) e = hipEventRecord(done[2 * i + s], c->stream);
       if (e != hipSuccess)
         result = mfail(m, SD_CAS_EHIP, std::string("hash shard ") + std::to_string(i) + ": " +

@@ -35,7 +35,9 @@ def main():
     eng = CasEngine(0)
     q = eng.batch_quantum
     ns = [1, 100, 512, 1024, 2048, 4096, 8192, 16384, 32768, 49152, q, q + 4096, q + q // 2,
-          2 * q, 2 * q + 20000, 4 * q]
+          2 * q, 2 * q + 20000, 3 * q, 4 * q, 6 * q]
+    if len(sys.argv) > 1:  # explicit batch sizes, in quanta if suffixed with q
+        ns = [int(float(x[:-1]) * q) if x.endswith("q") else int(x) for x in sys.argv[1:]]
     nmax = max(ns)
     content = torch.empty(nmax * SAMPLED, dtype=torch.uint8, device="cuda")
     sizes = torch.empty(nmax, dtype=torch.int64, device="cuda")

@@ -23,7 +23,7 @@ __global__ void __launch_bounds__(256) k1_variant(const uint8_t* __restrict__ co
   const uint64_t f = (uint64_t)blockIdx.x * sdcas::SAMPLED_BLOCK + threadIdx.x;
   if (f < n) {
     const uint64_t g = (MODE == 0 || MODE == 4) ? f : (MODE == 1 ? (f & 31) : 0);
-    sdcas::LdsStack stk{stack_lds, threadIdx.x};
+    sdcas::LdsStack<> stk{stack_lds, threadIdx.x};
     if (MODE == 5 || MODE == 6) {
       const uint4* q = reinterpret_cast<const uint4*>(content + (f >> 6) * 64 * stride) +
                        (MODE == 5 ? (f & 63) * 8 : (f & 63));
