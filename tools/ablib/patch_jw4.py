@@ -1,0 +1,6 @@
+# small batches: four gather windows
+s=open('sd_hip_cas.cpp').read()
+a="  constexpr size_t GATHER_WINDOW = 2048;"
+assert a in s
+s=s.replace(a,"  const size_t GATHER_WINDOW = n <= 8192 ? std::max<size_t>(32, (n + 3) / 4) : 2048;")
+open('sd_hip_cas.cpp','w').write(s)

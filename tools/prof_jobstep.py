@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""100-file job steps through sd_cas_generate_cas_ids_from_paths (the reference's step
+shape, file_identifier/mod.rs:34): 300 steps over sampled and whole files on tmpfs; with
+the tracing build (tools/ablib/patch_trace_paths.py) stderr carries per-phase times."""
+import os
+import shutil
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
+
+def main():
+    import torch  # noqa: F401
+    from spacedrive_amd import CasEngine
+    eng = CasEngine(0)
+    rng = np.random.default_rng(3)
+    root = "/dev/shm/sdcas_js"
+    os.makedirs(root, exist_ok=True)
+    try:
+        for kind, lo, hi in (("sampled", 200_000, 2_000_000), ("whole", 1_000, 100_000), ("mixed", 1_000, 2_000_000)):
+            paths, sizes = [], []
+            for i in range(100):
+                s = int(np.exp(rng.uniform(np.log(lo), np.log(hi))))
+                p = os.path.join(root, f"{kind}{i:03d}")
+                with open(p, "wb") as fh:
+                    fh.write(rng.integers(0, 256, s, dtype=np.uint8).tobytes())
+                paths.append(p)
+                sizes.append(s)
+            for _ in range(20):
+                eng.generate_cas_keys_from_paths(paths, sizes)
+            ts = []
+            for _ in range(300):
+                t = time.perf_counter()
+                eng.generate_cas_keys_from_paths(paths, sizes)
+                ts.append(time.perf_counter() - t)
+            print(f"{kind}: median {np.median(ts) * 1e3:.3f} ms  p10 {np.percentile(ts, 10) * 1e3:.3f}  p90 {np.percentile(ts, 90) * 1e3:.3f}", flush=True)
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()
