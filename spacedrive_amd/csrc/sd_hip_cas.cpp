@@ -707,26 +707,29 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
         // seeks SeekFrom::End(-8192) (cas.rs:54-55), so it is located after the samples
         // with fstat on the open descriptor (a grown or shrunk file keeps the reference's
         // outcome: a cas_id while every read fits, UnexpectedEof = -EIO otherwise)
-        uint64_t offs[6], lns[6];
+        // the header and sample 0 are contiguous in the file ([0, 8192) and [8192, 18432):
+        // the first sample is read where the header read left off, cas.rs:35-44), so they
+        // are one pread — the outcome of a short file is the same UnexpectedEof either way
+        uint64_t offs[5], lns[5];
         int parts;
         const bool sampled = sizes[i] > MINIMUM_FILE_SIZE;
         if (sampled) {
           const uint64_t jump = (sizes[i] - 2 * HEADER_OR_FOOTER_SIZE) / SAMPLE_COUNT;
-          offs[0] = 0; lns[0] = HEADER_OR_FOOTER_SIZE;
-          for (int k = 0; k < 4; k++) { offs[1 + k] = HEADER_OR_FOOTER_SIZE + k * jump; lns[1 + k] = SAMPLE_SIZE; }
-          offs[5] = 0; lns[5] = HEADER_OR_FOOTER_SIZE;  // offset set below
-          parts = 6;
+          offs[0] = 0; lns[0] = HEADER_OR_FOOTER_SIZE + SAMPLE_SIZE;
+          for (int k = 1; k < 4; k++) { offs[k] = HEADER_OR_FOOTER_SIZE + k * jump; lns[k] = SAMPLE_SIZE; }
+          offs[4] = 0; lns[4] = HEADER_OR_FOOTER_SIZE;  // offset set below
+          parts = 5;
         } else {
           offs[0] = 0; lns[0] = lens[i];
           parts = 1;
         }
         for (int k = 0; k < parts && !status[i] && !redo[i]; k++) {
-          if (sampled && k == 5) {
+          if (sampled && k == 4) {
             struct stat st;
             if (fstat(fd, &st) != 0) { status[i] = -errno; break; }
             // lseek to a negative position: EINVAL (io::ErrorKind::InvalidInput)
             if ((uint64_t)st.st_size < HEADER_OR_FOOTER_SIZE) { status[i] = -EINVAL; break; }
-            offs[5] = (uint64_t)st.st_size - HEADER_OR_FOOTER_SIZE;
+            offs[4] = (uint64_t)st.st_size - HEADER_OR_FOOTER_SIZE;
           }
           size_t got = 0;
           while (got < lns[k]) {
