@@ -415,17 +415,17 @@ __device__ __forceinline__ uint32_t next_slot(uint32_t s) {
 }
 
 // Linear-probing tables: LDS (the normal case) and global memory (overflow).  `fresh`
-// counts keys this thread inserted first.  Returns false if the table has no room.
+// counts keys this thread inserted first.  Returns false if the table has no room.  The
+// LDS insert CASes first (one LDS round trip per probe; at the tables' fill most first
+// probes find the slot empty) — reading the slot before the CAS was 1-2 % slower
+// (profiles/r02_group_ab3.log).
 template <uint32_t TBL>
 __device__ __forceinline__ bool lds_insert(uint64_t* tk, uint32_t* tv, uint32_t& slot, uint64_t k,
                                            uint32_t v, uint64_t empty, uint32_t& fresh) {
   for (uint32_t probe = 0; probe < TBL; ++probe) {
-    uint64_t cur = tk[slot];
-    if (cur == empty) {
-      const uint64_t old = atomicCAS((unsigned long long*)&tk[slot], (unsigned long long)empty,
-                                     (unsigned long long)k);
-      if (old == empty) { ++fresh; cur = k; } else { cur = old; }
-    }
+    uint64_t cur = atomicCAS((unsigned long long*)&tk[slot], (unsigned long long)empty,
+                             (unsigned long long)k);
+    if (cur == empty) { ++fresh; cur = k; }
     if (cur == k) {
       atomicMin(&tv[slot], v);
       return true;
