@@ -12,7 +12,8 @@
 //                           out[i] = val(i)                                  8 B read, 4 B write
 //   K4h-b  sd_part_scatter  keys -> coarse-bucket-contiguous (mixed key, position),
 //                           LDS-staged so stores are coalesced runs; each trip reserves its
-//                           run in a bucket with one atomic per bucket     8 B read, 12 B write
+//                           run inside its totals replica's sub-run of each bucket (one
+//                           atomic per bucket, 1/16 of the blocks per cursor) 8 B read, 12 B write
 //   K4h-c  sd_part_refine   one workgroup per coarse bucket splits it by the next bits
 //                           (only above 1.44M keys)                     20 B read, 12 B write
 //   K5h    sd_bucket_min    one workgroup per fine bucket: LDS hash table of the bucket's
@@ -27,8 +28,8 @@
 // of a bijective mix of the key, so any set of DISTINCT keys spreads evenly (BLAKE3 keys are
 // uniform anyway; test keys such as 0..n-1 are not), while duplicates — however many —
 // share one table slot.  A bucket whose distinct keys overflow the LDS table (never for
-// uniform keys: mean <= 1,536 distinct per bucket vs 3,584 allowed) is redone by the same
-// workgroup in a global-memory table.
+// uniform keys: mean <= 1,536 distinct per bucket vs 3,584 allowed, ~5,100 vs 10,752 in the
+// big tables) is redone by the same workgroup in a global-memory table.
 //
 // The same two kernels give the key-RANGE partition of the multi-GPU exchange (SURVEY §8e:
 // dest = floor(key * G / 2^64)), with the bucket function applied to the raw key.
