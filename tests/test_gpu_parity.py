@@ -559,6 +559,31 @@ def test_sampled_quantum_plus_remainder(eng, oracle):
         del content
 
 
+def test_k1_grids_agree(eng, oracle):
+    """K1's two grid shapes (512-lane workgroups for an even number of quanta, 256-lane
+    otherwise) give the same keys: 3 quanta (narrow grid) vs their first 2 quanta (wide
+    grid) vs the first quantum and a 1.5-quantum batch (narrow K1 + K1L remainder), with
+    oracle parity on 1,500 random files."""
+    q = eng.batch_quantum
+    n = 3 * q
+    content = torch.empty((n, SAMPLED_CONTENT_LEN), dtype=torch.uint8, device="cuda")
+    sizes = torch.empty(n, dtype=torch.int64, device="cuda")
+    eng.synth_sampled(0x6D1, 0, n, content, sizes, SAMPLED_CONTENT_LEN, dup_permille=100)
+    runs = {}
+    for m in (n, 2 * q, q, q + q // 2):
+        k = torch.empty(m, dtype=torch.int64, device="cuda")
+        eng.hash_sampled(content, sizes, k, n=m)
+        runs[m] = host64(k)
+    for m, k in runs.items():
+        assert (k == runs[n][:m]).all(), m
+    rng = np.random.default_rng(90)
+    idx = np.sort(rng.choice(n, 1500, replace=False))
+    sub = content[torch.from_numpy(idx).cuda()].cpu().numpy()
+    want = oracle.fast_cas_keys_strided(sub.reshape(-1), SAMPLED_CONTENT_LEN, SAMPLED_CONTENT_LEN,
+                                        host64(sizes)[idx], 8)
+    assert (runs[n][idx] == want).all()
+
+
 def test_random_cases_1e5(path_eng, oracle):
     """SURVEY §7's minimum-slice bar on every kernel shape: 10^5 random whole-file messages
     (sizes uniform in [0, 102,400]) and 10^5 random sampled files, every cas key vs the
