@@ -46,7 +46,11 @@ sd_radix_upsweep(const uint64_t* __restrict__ keys, uint64_t n, uint32_t shift, 
   hist[(uint64_t)t * ntiles + blockIdx.x] = cnt[t];
 }
 
-// Stable scatter of one tile.  offs = exclusive-scanned hist (same layout).
+// Stable scatter of one tile.  offs = exclusive-scanned hist (same layout).  The tile is
+// first ranked into LDS in digit order (stable: round, then wave, then lane order within a
+// digit), then written out so that consecutive lanes store consecutive slots of one digit's
+// run: coalesced runs of ~16 keys per digit instead of ~1 key per digit per store
+// instruction (PMC: 41.5 B/key written per pass for 12 algorithmic, profiles/r02_pmc_group.txt).
 template <bool HAS_VALS>
 __device__ __forceinline__ void downsweep_body(const uint64_t* __restrict__ keys_in,
                                                const uint32_t* __restrict__ vals_in,
@@ -58,18 +62,51 @@ __device__ __forceinline__ void downsweep_body(const uint64_t* __restrict__ keys
   __shared__ uint32_t run[RADIX];        // per-digit running count within this tile
   __shared__ uint32_t wcnt[4][RADIX];    // per-wave digit counts of the current round
   __shared__ uint32_t gbase[RADIX];      // global offset of this tile's digit d
+  __shared__ uint32_t tstart[RADIX];     // first LDS slot of digit d in this tile
+  __shared__ uint32_t wsum[SORT_THREADS / 64];
+  __shared__ uint64_t skey[TILE];
+  __shared__ uint32_t sval[TILE];
   const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+  const uint64_t idx = (uint64_t)t * ntiles + blockIdx.x;
+  const uint32_t mine = offs[idx];
+  // this tile's count of digit t: the next entry of the digit-major scan minus this one
+  const uint32_t cnt = (idx + 1 < (uint64_t)RADIX * ntiles ? offs[idx + 1] : (uint32_t)n) - mine;
   run[t] = 0;
   wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
-  gbase[t] = offs[(uint64_t)t * ntiles + blockIdx.x];
+  gbase[t] = mine;
+  {  // tstart = exclusive scan of the tile's digit counts (256 threads, one digit each)
+    uint32_t inc = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= (uint32_t)o) inc += y;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (uint32_t i = 0; i < w; ++i) pre += wsum[i];
+    tstart[t] = pre + inc - cnt;
+  }
   __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * TILE;
+  const uint32_t tile_n = (uint32_t)(n - base < (uint64_t)TILE ? n - base : (uint64_t)TILE);
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  // every round's key (and value) is loaded up front: one memory latency per tile, not one
+  // per round (the rounds are separated by barriers)
+  uint64_t kr[SORT_ROUNDS];
+  uint32_t vr[SORT_ROUNDS];
+#pragma unroll
+  for (int r = 0; r < SORT_ROUNDS; ++r) {
+    const uint64_t i = base + (uint64_t)r * SORT_THREADS + t;
+    kr[r] = i < n ? keys_in[i] : 0ull;
+    vr[r] = (HAS_VALS && i < n) ? vals_in[i] : (uint32_t)i;
+  }
+#pragma unroll
   for (int r = 0; r < SORT_ROUNDS; ++r) {
     const uint64_t i = base + (uint64_t)r * SORT_THREADS + t;
     const bool valid = i < n;
-    const uint64_t k = valid ? keys_in[i] : 0ull;
-    const uint32_t v = (HAS_VALS && valid) ? vals_in[i] : (uint32_t)i;
+    const uint64_t k = kr[r];
+    const uint32_t v = vr[r];
     const uint32_t d = digit_of(k, shift, mask);
     // lanes of this wave holding the same digit
     uint64_t peers = __ballot(valid);
@@ -81,20 +118,24 @@ __device__ __forceinline__ void downsweep_body(const uint64_t* __restrict__ keys
     const uint32_t rank_in_wave = __popcll(peers & lt_mask);
     if (valid && rank_in_wave == 0) wcnt[w][d] = (uint32_t)__popcll(peers);
     __syncthreads();
-    uint32_t pos = 0;
     if (valid) {
       uint32_t before = run[d];
       for (uint32_t ww = 0; ww < w; ++ww) before += wcnt[ww][d];
-      pos = gbase[d] + before + rank_in_wave;
+      const uint32_t slot = tstart[d] + before + rank_in_wave;
+      skey[slot] = k;
+      sval[slot] = v;
     }
     __syncthreads();
     run[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
     wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
-    if (valid) {
-      keys_out[pos] = k;
-      vals_out[pos] = v;
-    }
-    __syncthreads();
+  }
+  __syncthreads();
+  for (uint32_t s = t; s < tile_n; s += SORT_THREADS) {
+    const uint64_t k = skey[s];
+    const uint32_t d = digit_of(k, shift, mask);
+    const uint32_t pos = gbase[d] + (s - tstart[d]);
+    keys_out[pos] = k;
+    vals_out[pos] = sval[s];
   }
 }
 
