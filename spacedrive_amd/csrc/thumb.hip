@@ -51,25 +51,35 @@ struct ThumbPrefix {
 extern "C" __global__ void __launch_bounds__(kThreads)
 sd_thumb_paths(const uint64_t* __restrict__ keys, uint64_t n, uint32_t stride,
                const ThumbPrefix prefix, uint32_t plen, uint4* __restrict__ out) {
-  __shared__ uint8_t pre[kMaxPrefix];
-  for (uint32_t i = threadIdx.x; i < plen; i += kThreads) pre[i] = prefix.bytes[i];
+  __shared__ uint4 pre4[kMaxPrefix / 16];  // the prefix as 16-B quads (zero-padded)
+  uint8_t* pre = reinterpret_cast<uint8_t*>(pre4);
+  for (uint32_t i = threadIdx.x; i < kMaxPrefix; i += kThreads) pre[i] = i < plen ? prefix.bytes[i] : 0;
   __syncthreads();
   const uint32_t q_per = stride >> 4;  // 16-B quads per record
   const uint64_t total = n * q_per;
   for (uint64_t g = (uint64_t)blockIdx.x * kThreads + threadIdx.x; g < total;
        g += (uint64_t)gridDim.x * kThreads) {
-    const uint64_t r = g / q_per;
+    // 32-bit index math while the batch has < 2^32 quads (always, in practice)
+    const uint64_t r = total < (1ull << 32) ? (uint32_t)g / q_per : g / q_per;
     const uint32_t o0 = (uint32_t)(g - r * q_per) << 4;
-    const uint64_t key = keys[r];
-    uint32_t w[4];
+    uint4 qd;
+    if (o0 + 16 <= plen) {
+      qd = pre4[o0 >> 4];  // a quad wholly inside the prefix: one LDS read
+    } else if (o0 >= plen + kTail) {
+      qd = make_uint4(0u, 0u, 0u, 0u);  // NUL padding
+    } else {  // the 2-3 quads holding the end of the prefix, shard, cas_id and extension
+      const uint64_t key = keys[r];
+      uint32_t w[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      uint32_t v = 0;
+      for (int k = 0; k < 4; ++k) {
+        uint32_t v = 0;
 #pragma unroll
-      for (int b = 0; b < 4; ++b) v |= record_byte(pre, plen, key, o0 + 4 * k + b) << (8 * b);
-      w[k] = v;
+        for (int b = 0; b < 4; ++b) v |= record_byte(pre, plen, key, o0 + 4 * k + b) << (8 * b);
+        w[k] = v;
+      }
+      qd = make_uint4(w[0], w[1], w[2], w[3]);
     }
-    out[g] = make_uint4(w[0], w[1], w[2], w[3]);
+    out[g] = qd;
   }
 }
 
