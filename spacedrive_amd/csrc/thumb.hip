@@ -30,29 +30,39 @@ __device__ __forceinline__ uint32_t hex_digit(uint64_t key, uint32_t i) {  // i-
   return v < 10 ? '0' + v : 'a' + (v - 10);
 }
 
-// byte o of the record of `key` behind a prefix of P bytes (prefix bytes come from LDS)
-__device__ __forceinline__ uint32_t record_byte(const uint8_t* pre, uint32_t P, uint64_t key,
-                                                uint32_t o) {
-  if (o < P) return pre[o];
-  o -= P;
-  if (o < 3) return hex_digit(key, o);
-  if (o == 3) return '/';
-  if (o < 20) return hex_digit(key, o - 4);
-  if (o < 25) return (uint32_t)(uint8_t)kExt[o - 20];
-  return 0;
-}
-
 }  // namespace
 
 struct ThumbPrefix {
   uint8_t bytes[kMaxPrefix];
 };
 
+// The 16 hex chars of a key as 4 little-endian words (char 4i+j = byte j of word i): each
+// 16-bit chunk spread to one nibble per byte, then SWAR ascii ('0' + n, +39 for a-f).
+__device__ __forceinline__ uint32_t hex_word(uint64_t key, int i) {
+  const uint32_t c = (uint32_t)(key >> (48 - 16 * i)) & 0xFFFFu;
+  const uint32_t v = (c >> 12) | (((c >> 8) & 15u) << 8) | (((c >> 4) & 15u) << 16) | ((c & 15u) << 24);
+  return v + 0x30303030u + (((v + 0x06060606u) >> 4) & 0x01010101u) * 39u;
+}
+
+// word (4 bytes at record offset o, o % 4 == 0) of prefix ‖ tail ‖ zeros, where the tail is
+// shard '/' cas_id ".webp" = 25 bytes, held as 8 words tw[0..7] (tw[7] = 0)
+__device__ __forceinline__ uint32_t tail_word(const uint32_t (&tw)[8], int d) {  // d = o - P >= 0
+  const int a = d >> 2, sh = (d & 3) * 8;
+  uint32_t lo = 0, hi = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {  // select, not a dynamically indexed (scratch) array
+    lo = a == j ? tw[j] : lo;
+    hi = a + 1 == j ? tw[j] : hi;
+  }
+  return sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
+}
+
 extern "C" __global__ void __launch_bounds__(kThreads)
 sd_thumb_paths(const uint64_t* __restrict__ keys, uint64_t n, uint32_t stride,
                const ThumbPrefix prefix, uint32_t plen, uint4* __restrict__ out) {
   __shared__ uint4 pre4[kMaxPrefix / 16];  // the prefix as 16-B quads (zero-padded)
   uint8_t* pre = reinterpret_cast<uint8_t*>(pre4);
+  const uint32_t* prew = reinterpret_cast<const uint32_t*>(pre4);
   for (uint32_t i = threadIdx.x; i < kMaxPrefix; i += kThreads) pre[i] = i < plen ? prefix.bytes[i] : 0;
   __syncthreads();
   const uint32_t q_per = stride >> 4;  // 16-B quads per record
@@ -67,15 +77,29 @@ sd_thumb_paths(const uint64_t* __restrict__ keys, uint64_t n, uint32_t stride,
       qd = pre4[o0 >> 4];  // a quad wholly inside the prefix: one LDS read
     } else if (o0 >= plen + kTail) {
       qd = make_uint4(0u, 0u, 0u, 0u);  // NUL padding
-    } else {  // the 2-3 quads holding the end of the prefix, shard, cas_id and extension
+    } else {  // the 2-3 quads holding the end of the prefix and the 25-byte tail
       const uint64_t key = keys[r];
+      uint32_t tw[8];
+      tw[1] = hex_word(key, 0);
+      tw[2] = hex_word(key, 1);
+      tw[3] = hex_word(key, 2);
+      tw[4] = hex_word(key, 3);
+      tw[0] = (tw[1] & 0x00FFFFFFu) | ((uint32_t)'/' << 24);  // shard + '/'
+      tw[5] = 0x6265772Eu;                                     // ".web"
+      tw[6] = (uint32_t)'p';
+      tw[7] = 0u;
       uint32_t w[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) v |= record_byte(pre, plen, key, o0 + 4 * k + b) << (8 * b);
-        w[k] = v;
+        const int o = (int)o0 + 4 * k, d = o - (int)plen;
+        if (d >= 0) {
+          w[k] = d < (int)kTail ? tail_word(tw, d) : 0u;
+        } else if (d <= -4) {
+          w[k] = prew[o >> 2];
+        } else {  // -3..-1: the prefix's last bytes, then the tail's first
+          const int keep = -d;  // prefix bytes in this word
+          w[k] = (prew[o >> 2] & ((1u << (8 * keep)) - 1u)) | (tw[0] << (8 * keep));
+        }
       }
       qd = make_uint4(w[0], w[1], w[2], w[3]);
     }
