@@ -226,11 +226,14 @@ int sd_cas_exchange_pack_fixed_dev(sd_cas_ctx* ctx, const uint64_t* d_keys, cons
                                    const uint64_t* d_counts, uint32_t G, uint64_t cap,
                                    uint64_t spill, uint64_t file0, uint32_t* d_rows,
                                    uint32_t* d_spill_rows, uint32_t* d_overflow, void* stream);
-/* received rows -> keys + vals; *d_has_sentinel |= 1 if any key equals `sentinel` (this
- * receiver's sentinel: the first key of range rank+1; zero it first). */
+/* received rows -> keys + vals.  `sentinel` = this receiver's sentinel (the first key of
+ * range rank+1); received row j carrying it gets the distinct key sentinel + j (outside the
+ * receiver's range, so the padding spreads over the grouping's buckets instead of forming one
+ * hot key) and *d_sentinel_rows (device u64; zero it first) += the number of such rows: each
+ * is one extra Object of the grouping, to be subtracted from its count. */
 int sd_cas_exchange_split_fixed_dev(sd_cas_ctx* ctx, const uint32_t* d_rows, size_t m,
                                     uint64_t sentinel, uint64_t* d_keys, uint32_t* d_vals,
-                                    uint64_t* d_has_sentinel, void* stream);
+                                    uint64_t* d_sentinel_rows, void* stream);
 /* mirror of pack_fixed: d_rep[d_pos[o_p + t]] = (main or spill block) rep for t < count_p. */
 int sd_cas_exchange_unpack_fixed_dev(sd_cas_ctx* ctx, const uint32_t* d_back,
                                      const uint32_t* d_spill_back, const uint32_t* d_pos,

@@ -94,7 +94,7 @@ extern "C" {
                                           d_overflow: *mut u32, stream: *mut c_void) -> c_int;
     pub fn sd_cas_exchange_split_fixed_dev(ctx: *mut sd_cas_ctx, d_rows: *const u32, m: usize,
                                            sentinel: u64, d_keys: *mut u64, d_vals: *mut u32,
-                                           d_has_sentinel: *mut u64, stream: *mut c_void) -> c_int;
+                                           d_sentinel_rows: *mut u64, stream: *mut c_void) -> c_int;
     pub fn sd_cas_exchange_unpack_fixed_dev(ctx: *mut sd_cas_ctx, d_back: *const u32,
                                             d_spill_back: *const u32, d_pos: *const u32,
                                             d_counts: *const u64, G: u32, cap: u64, spill: u64,

@@ -129,20 +129,44 @@ sd_exch_pack_fixed(const uint64_t* __restrict__ keys, const uint32_t* __restrict
   }
 }
 
-// received rows -> keys/vals, has_sentinel |= any key == sentinel (this receiver's)
-extern "C" __global__ void __launch_bounds__(256)
+// received rows -> keys/vals.  A sentinel row (key == this receiver's sentinel) gets the
+// distinct key sentinel + j: still outside the receiver's range (m < 2^64 - range width),
+// so it never merges with a real key, and the padding of a step (~8% of the rows) no longer
+// forms one hot key whose bucket serialises the grouping (world 8, 1.42 M rows: group_min
+// 0.168 -> 0.074 ms, profiles/r02_exchange_timing.log).  sentinel_rows += their number
+// (each is one extra Object, subtracted by the caller): counted per workgroup in LDS, one
+// device atomic per workgroup that saw any (one per wave put ~1,700 same-address atomics in
+// a row: 0.035 ms for the split alone).
+constexpr int SPLIT_THREADS = 256, SPLIT_ITEMS = 8;
+extern "C" __global__ void __launch_bounds__(SPLIT_THREADS)
 sd_exch_split_fixed(const uint32_t* __restrict__ rows, uint64_t m, uint64_t sentinel,
                     uint64_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                    unsigned long long* __restrict__ has_sentinel) {
-  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool hit = false;
-  if (j < m) {
-    const uint64_t k = (uint64_t)rows[3 * j] | ((uint64_t)rows[3 * j + 1] << 32);
-    keys[j] = k;
-    vals[j] = rows[3 * j + 2];
-    hit = k == sentinel;
+                    unsigned long long* __restrict__ sentinel_rows) {
+  __shared__ uint32_t nsent;
+  if (threadIdx.x == 0) nsent = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * SPLIT_THREADS * SPLIT_ITEMS + threadIdx.x;
+  uint32_t lo[SPLIT_ITEMS], hi[SPLIT_ITEMS], v[SPLIT_ITEMS];
+#pragma unroll
+  for (int i = 0; i < SPLIT_ITEMS; ++i) {
+    const uint64_t j = base + (uint64_t)i * SPLIT_THREADS;
+    if (j < m) { lo[i] = rows[3 * j]; hi[i] = rows[3 * j + 1]; v[i] = rows[3 * j + 2]; }
   }
-  if (__ballot(hit) && (threadIdx.x & 63u) == 0) atomicOr(has_sentinel, 1ull);
+  uint32_t hits = 0;
+#pragma unroll
+  for (int i = 0; i < SPLIT_ITEMS; ++i) {
+    const uint64_t j = base + (uint64_t)i * SPLIT_THREADS;
+    if (j < m) {
+      const uint64_t k = (uint64_t)lo[i] | ((uint64_t)hi[i] << 32);
+      const bool hit = k == sentinel;
+      hits += hit;
+      keys[j] = hit ? sentinel + j : k;
+      vals[j] = v[i];
+    }
+  }
+  if (hits) atomicAdd(&nsent, hits);
+  __syncthreads();
+  if (threadIdx.x == 0 && nsent) atomicAdd(sentinel_rows, (unsigned long long)nsent);
 }
 
 // rep[pos[o_p + t]] = back (main block t < cap, spill block otherwise) for t < counts[p]
@@ -236,10 +260,12 @@ hipError_t exch_pack_fixed(const uint64_t* keys, const uint32_t* pos, const uint
 }
 
 hipError_t exch_split_fixed(const uint32_t* rows, uint64_t m, uint64_t sentinel, uint64_t* keys,
-                            uint32_t* vals, uint64_t* has_sentinel, hipStream_t s) {
+                            uint32_t* vals, uint64_t* sentinel_rows, hipStream_t s) {
   if (m == 0) return hipSuccess;
-  sd_exch_split_fixed<<<(uint32_t)((m + 255) / 256), 256, 0, s>>>(
-      rows, m, sentinel, keys, vals, (unsigned long long*)has_sentinel);
+  constexpr uint64_t per = (uint64_t)SPLIT_THREADS * SPLIT_ITEMS;
+  if ((m + per - 1) / per > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  sd_exch_split_fixed<<<(uint32_t)((m + per - 1) / per), SPLIT_THREADS, 0, s>>>(
+      rows, m, sentinel, keys, vals, (unsigned long long*)sentinel_rows);
   return hipGetLastError();
 }
 

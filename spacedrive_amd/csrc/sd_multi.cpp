@@ -407,11 +407,11 @@ int sd_cas_exchange_pack_fixed_dev(sd_cas_ctx* c, const uint64_t* d_keys, const 
 
 int sd_cas_exchange_split_fixed_dev(sd_cas_ctx* c, const uint32_t* d_rows, size_t m,
                                     uint64_t sentinel, uint64_t* d_keys, uint32_t* d_vals,
-                                    uint64_t* d_has_sentinel, void* stream) {
+                                    uint64_t* d_sentinel_rows, void* stream) {
   if (!c) return SD_CAS_EINVAL;
-  if (m && (!d_rows || !d_keys || !d_vals || !d_has_sentinel))
+  if (m && (!d_rows || !d_keys || !d_vals || !d_sentinel_rows))
     return sd_fail(c, SD_CAS_EINVAL, "exchange_split_fixed: null");
-  HIP_TRY(c, exch_split_fixed(d_rows, m, sentinel, d_keys, d_vals, d_has_sentinel, sd_pick(c, stream)));
+  HIP_TRY(c, exch_split_fixed(d_rows, m, sentinel, d_keys, d_vals, d_sentinel_rows, sd_pick(c, stream)));
   return SD_CAS_OK;
 }
 

@@ -26,7 +26,7 @@ hipError_t exch_pack_fixed(const uint64_t* keys, const uint32_t* pos, const uint
                            uint32_t G, uint64_t cap, uint64_t spill, uint64_t file0, uint32_t* rows,
                            uint32_t* srows, uint32_t* overflow, hipStream_t s);
 hipError_t exch_split_fixed(const uint32_t* rows, uint64_t m, uint64_t sentinel, uint64_t* keys,
-                            uint32_t* vals, uint64_t* has_sentinel, hipStream_t s);
+                            uint32_t* vals, uint64_t* sentinel_rows, hipStream_t s);
 hipError_t exch_unpack_fixed(const uint32_t* back, const uint32_t* sback, const uint32_t* pos,
                              const uint64_t* counts, uint32_t G, uint64_t cap, uint64_t spill,
                              uint64_t* rep, hipStream_t s);

@@ -64,7 +64,8 @@ class ShardOps(Protocol):
         """(rows [parts*cap, 3], spill rows [parts*spill, 3], overflow int32 [1])"""
 
     def split_fixed(self, rows, sentinel: int) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-        """(int64 keys, int32 vals, int64 [1] = 1 if any key == sentinel)"""
+        """(int64 keys, int32 vals, int64 [1] = number of sentinel rows; row j with key ==
+        sentinel gets key sentinel + j)"""
 
     def unpack_fixed(self, back, spill_back, pos, counts, parts: int, cap: int, spill: int) -> torch.Tensor:
         """int64 rep: mirror of pack_fixed"""
@@ -248,9 +249,9 @@ def _sharded_group_fixed(local_keys, file0, ops, group, capacity) -> ShardResult
         rsrows = torch.empty_like(srows)
         dist.all_to_all_single(rsrows, srows, group=group)
         rrows = torch.cat([rrows, rsrows])
-    rkeys, ridx, has_sentinel = ops.split_fixed(rrows, range_start(rank + 1, world))
+    rkeys, ridx, nsent = ops.split_fixed(rrows, range_start(rank + 1, world))
     rep_min, obj = ops.group_min_dev(rkeys, ridx)                             # 3
-    tot = obj - has_sentinel                      # the sentinel rows form one extra key
+    tot = obj - nsent                             # each sentinel row is one extra key
     back = torch.empty(world * cap, dtype=torch.int32, device=dev)
     dist.all_to_all_single(back, rep_min[:world * cap].contiguous(), group=group)   # 4
     sback = torch.empty(world * spill, dtype=torch.int32, device=dev)

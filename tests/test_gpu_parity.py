@@ -889,9 +889,16 @@ def test_fixed_capacity_exchange_kernels(eng, oracle, world):
     objects = 0
     for d in range(world):  # receiver d: block d of every sender, main then spill
         rr = torch.cat([s[2][d] for s in sent] + [s[3][d] for s in sent])
-        rk, rv, hit = ops.split_fixed(rr, range_start(d + 1, world))
+        rk, rv, nsent = ops.split_fixed(rr, range_start(d + 1, world))
+        ku = rr[:, 0].cpu().numpy().view(np.uint32).astype(np.uint64) | (
+            rr[:, 1].cpu().numpy().view(np.uint32).astype(np.uint64) << np.uint64(32))
+        pad = ku == np.uint64(range_start(d + 1, world))
+        assert int(nsent.item()) == int(pad.sum())
+        got = rk.cpu().numpy().view(np.uint64)
+        want = np.where(pad, np.uint64(range_start(d + 1, world)) + np.arange(len(ku), dtype=np.uint64), ku)
+        assert (got == want).all()  # padding spread to distinct keys, real keys untouched
         out, obj = ops.group_min_dev(rk, rv)
-        objects += int(obj.item()) - int(hit.item())
+        objects += int(obj.item()) - int(nsent.item())
         backs.append(out)
     orep, oobj = oracle.group_canonical(keys)
     assert objects == oobj

@@ -90,8 +90,11 @@ class HostOps:
 
     def split_fixed(self, rows, sentinel):
         k, v = self.split(rows)
-        hit = bool((k.numpy().view(np.uint64) == np.uint64(sentinel)).any())
-        return k, v, torch.tensor([int(hit)], dtype=torch.int64)
+        ku = k.numpy().view(np.uint64)
+        hit = ku == np.uint64(sentinel)
+        j = np.arange(len(ku), dtype=np.uint64)
+        ku[hit] = np.uint64(sentinel) + j[hit]  # distinct keys, outside the receiver's range
+        return k, v, torch.tensor([int(hit.sum())], dtype=torch.int64)
 
     def unpack_fixed(self, back, spill_back, pos, counts, parts, cap, spill):
         b, sb, p, c = back.numpy().view(np.uint32), spill_back.numpy().view(np.uint32), pos.numpy(), counts.numpy()
