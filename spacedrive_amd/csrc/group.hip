@@ -60,7 +60,10 @@ __device__ __forceinline__ void downsweep_body(const uint64_t* __restrict__ keys
                                                const uint32_t* __restrict__ offs,
                                                uint32_t ntiles) {
   __shared__ uint32_t run[RADIX];        // per-digit running count within this tile
-  __shared__ uint32_t wcnt[4][RADIX];    // per-wave digit counts of the current round
+  // per-wave digit counts, double-buffered by round parity: a wave that runs ahead into
+  // round r+1 writes the other buffer while thread d may still be folding round r's counts
+  // of digit d into run[d] and zeroing them (one buffer raced there: rare lost counts)
+  __shared__ uint32_t wcnt[2][4][RADIX];
   __shared__ uint32_t gbase[RADIX];      // global offset of this tile's digit d
   __shared__ uint32_t tstart[RADIX];     // first LDS slot of digit d in this tile
   __shared__ uint32_t wsum[SORT_THREADS / 64];
@@ -72,7 +75,8 @@ __device__ __forceinline__ void downsweep_body(const uint64_t* __restrict__ keys
   // this tile's count of digit t: the next entry of the digit-major scan minus this one
   const uint32_t cnt = (idx + 1 < (uint64_t)RADIX * ntiles ? offs[idx + 1] : (uint32_t)n) - mine;
   run[t] = 0;
-  wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
+#pragma unroll
+  for (int b = 0; b < 8; ++b) wcnt[b >> 2][b & 3][t] = 0;
   gbase[t] = mine;
   {  // tstart = exclusive scan of the tile's digit counts (256 threads, one digit each)
     uint32_t inc = cnt;
@@ -116,18 +120,21 @@ __device__ __forceinline__ void downsweep_body(const uint64_t* __restrict__ keys
       peers &= ((d >> b) & 1u) ? bal : ~bal;
     }
     const uint32_t rank_in_wave = __popcll(peers & lt_mask);
-    if (valid && rank_in_wave == 0) wcnt[w][d] = (uint32_t)__popcll(peers);
+    uint32_t (&wc)[4][RADIX] = wcnt[r & 1];
+    if (valid && rank_in_wave == 0) wc[w][d] = (uint32_t)__popcll(peers);
     __syncthreads();
     if (valid) {
       uint32_t before = run[d];
-      for (uint32_t ww = 0; ww < w; ++ww) before += wcnt[ww][d];
+      for (uint32_t ww = 0; ww < w; ++ww) before += wc[ww][d];
       const uint32_t slot = tstart[d] + before + rank_in_wave;
       skey[slot] = k;
       sval[slot] = v;
     }
     __syncthreads();
-    run[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
-    wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
+    // round r+1 writes the other buffer; round r+2 (this buffer again) is behind round
+    // r+1's barriers, which this thread reaches only after the lines below
+    run[t] += wc[0][t] + wc[1][t] + wc[2][t] + wc[3][t];
+    wc[0][t] = 0; wc[1][t] = 0; wc[2][t] = 0; wc[3][t] = 0;
   }
   __syncthreads();
   for (uint32_t s = t; s < tile_n; s += SORT_THREADS) {
