@@ -509,7 +509,10 @@ __device__ __forceinline__ void bucket_min(const uint64_t* __restrict__ pkeys,
   __shared__ uint64_t tk[TBL];
   __shared__ uint32_t tv[TBL];
   __shared__ uint32_t distinct;
-  __shared__ int overflow;
+  // overflow flag of trip t lives in ovf[t & 1] and is read after trip t+1's barrier: a
+  // single flag could be raised by a fast wave's trip-(t+1) insert while a slower wave was
+  // still reading it for trip t+1, splitting the waves over different barriers
+  __shared__ int ovf[2];
   const uint32_t b = blockIdx.x;
   const uint64_t s = starts[b];
   const uint64_t e = b + 1 < nb ? starts[b + 1] : n;
@@ -517,10 +520,11 @@ __device__ __forceinline__ void bucket_min(const uint64_t* __restrict__ pkeys,
   // every stored key of this bucket has top bits == b, so a key from bucket b^1 is never stored
   const uint64_t empty = (uint64_t)(b ^ 1u) << (64 - bits);
   for (uint32_t i = threadIdx.x; i < TBL; i += THREADS) { tk[i] = empty; tv[i] = 0xFFFFFFFFu; }
-  if (threadIdx.x == 0) { distinct = 0; overflow = 0; }
+  if (threadIdx.x == 0) { distinct = 0; ovf[0] = 0; ovf[1] = 0; }
   uint64_t k[ITEMS];
   uint32_t p[ITEMS], v[ITEMS], sl[ITEMS];
-  for (uint64_t base = s; base < e; base += TILE) {
+  uint32_t trip = 0;
+  for (uint64_t base = s; base < e; base += TILE, ++trip) {
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
       const uint64_t i = base + (uint64_t)j * THREADS + threadIdx.x;
@@ -529,8 +533,8 @@ __device__ __forceinline__ void bucket_min(const uint64_t* __restrict__ pkeys,
     }
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) v[j] = (vals && k[j] != empty) ? vals[p[j]] : p[j];
-    __syncthreads();  // table initialised (first trip) / overflow flag visible
-    if (overflow) break;
+    __syncthreads();  // table initialised (first trip) / the previous trip's flag visible
+    if (ovf[(trip + 1) & 1]) break;  // raised by trip - 1 (ovf[1] = 0 on the first trip)
     uint32_t fresh = 0;
     bool ok = true;
     if (e - s <= TILE) {
@@ -546,10 +550,10 @@ __device__ __forceinline__ void bucket_min(const uint64_t* __restrict__ pkeys,
         if (k[j] != empty) ok &= lds_insert<TBL, true>(tk, tv, sl[j], k[j], v[j], empty, fresh);
       }
     }
-    if (fresh && atomicAdd(&distinct, fresh) + fresh > FILL) overflow = 1;
-    if (!ok) overflow = 1;
+    if ((fresh && atomicAdd(&distinct, fresh) + fresh > FILL) || !ok) ovf[trip & 1] = 1;
   }
   __syncthreads();
+  const bool overflow = ovf[0] | ovf[1];
   if (!overflow) {
     if (e - s <= TILE) {  // the one trip's keys and their slots are still in registers
 #pragma unroll
