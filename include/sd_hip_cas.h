@@ -318,6 +318,23 @@ int sd_cas_checksum_dev(sd_cas_ctx* ctx, const void* d_data, uint64_t len, uint8
  * BLAKE3 subtree per segment on the GPU; out_hex = 64 lowercase hex + NUL.
  * Returns SD_CAS_EIO with *err_no set on an I/O error. */
 int sd_cas_file_checksum(sd_cas_ctx* ctx, const char* path, char out_hex[65], int* err_no);
+/* The validator job over many files (validator_job.rs:107-172 runs one file_checksum per
+ * step): n device buffers hashed by one launch chain — buffer i = d_arena + d_offs[i]
+ * (16-B aligned), d_lens[i] bytes (<= 64 GiB), readable to the 16-B round-up; every buffer
+ * ends within arena_bytes of d_arena (sizes the workspace: one 32-B CV per 1 MiB subtree).
+ * d_out[32 i .. 32 i + 32) = the digest of buffer i (device).  n <= 2^24.  Blocking;
+ * SD_CAS_EINVAL when a length breaks those bounds. */
+int sd_cas_checksums_dev(sd_cas_ctx* ctx, const void* d_arena, uint64_t arena_bytes,
+                         const uint64_t* d_offs, const uint64_t* d_lens, size_t n, uint8_t* d_out,
+                         void* stream);
+/* file_checksum over n paths: each file is read to EOF (the first short read, hash.rs:15-21)
+ * by the gather pool into pinned windows that are hashed with the batch chain above while the
+ * next window is read; a file larger than half a window, or one that grew past its slot,
+ * streams through sd_cas_file_checksum.  out_hex[65 i ..] = 64 hex + NUL ("" on error);
+ * status[i] = 0 or -errno (open/stat/read failure: validator_job.rs:149-151 fails that
+ * step with FileIOError).  Returns SD_CAS_OK unless the batch itself failed.  Blocking. */
+int sd_cas_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char* out_hex,
+                          int32_t* status);
 
 /* ---- multi-device, single process -------------------------------------
  * One context per shard; shard i lives on devices[i] (a device may host several shards).

@@ -122,6 +122,11 @@ extern "C" {
                                stream: *mut c_void) -> c_int;
     pub fn sd_cas_file_checksum(ctx: *mut sd_cas_ctx, path: *const c_char, out_hex: *mut c_char,
                                 err_no: *mut c_int) -> c_int;
+    pub fn sd_cas_checksums_dev(ctx: *mut sd_cas_ctx, d_arena: *const c_void, arena_bytes: u64,
+                                d_offs: *const u64, d_lens: *const u64, n: usize, d_out: *mut u8,
+                                stream: *mut c_void) -> c_int;
+    pub fn sd_cas_file_checksums(ctx: *mut sd_cas_ctx, paths: *const *const c_char, n: usize,
+                                 out_hex: *mut c_char, status: *mut i32) -> c_int;
     pub fn sd_cas_multi_create(devices: *const c_int, ndev: c_int, out: *mut *mut sd_cas_multi) -> c_int;
     pub fn sd_cas_multi_destroy(m: *mut sd_cas_multi);
     pub fn sd_cas_multi_count(m: *const sd_cas_multi) -> c_int;
@@ -317,6 +322,34 @@ impl HipCas {
             return Err(self.err(rc));
         }
         Ok(unsafe { CStr::from_ptr(out.as_ptr()) }.to_string_lossy().into_owned())
+    }
+
+    /// The validator job's checksums over many files in one call (`sd_cas_file_checksums`):
+    /// one `io::Result` per path, as `file_checksum` would return it.
+    pub fn file_checksums(&mut self, paths: &[&Path]) -> io::Result<Vec<io::Result<String>>> {
+        let cs: Vec<CString> = paths
+            .iter()
+            .map(|p| CString::new(p.as_os_str().as_encoded_bytes()).expect("NUL in path"))
+            .collect();
+        let ptrs: Vec<*const c_char> = cs.iter().map(|c| c.as_ptr()).collect();
+        let n = paths.len();
+        let mut out = vec![0 as c_char; 65 * n.max(1)];
+        let mut status = vec![0i32; n];
+        let rc = unsafe {
+            sd_cas_file_checksums(self.ctx, ptrs.as_ptr(), n, out.as_mut_ptr(), status.as_mut_ptr())
+        };
+        if rc != 0 {
+            return Err(self.err(rc));
+        }
+        Ok((0..n)
+            .map(|i| {
+                if status[i] != 0 {
+                    Err(io::Error::from_raw_os_error(-status[i]))
+                } else {
+                    Ok(unsafe { CStr::from_ptr(out.as_ptr().add(65 * i)) }.to_string_lossy().into_owned())
+                }
+            })
+            .collect())
     }
 
     /// Canonical Object grouping of device-resident keys (see `sd_cas_group_dev`); returns

@@ -64,6 +64,8 @@ SIGNATURES = [
     ("sd_cas_sort_pairs_dev", _i, [_vp, _vp, _vp, _sz, _vp, _vp, _i, _i, _vp]),
     ("sd_cas_checksum_dev", _i, [_vp, _vp, _u64, _vp, _vp]),
     ("sd_cas_file_checksum", _i, [_vp, _cp, _cp, ctypes.POINTER(_i)]),
+    ("sd_cas_checksums_dev", _i, [_vp, _vp, _u64, _vp, _vp, _sz, _vp, _vp]),
+    ("sd_cas_file_checksums", _i, [_vp, _vp, _sz, _vp, _vp]),
     ("sd_cas_multi_create", _i, [_vp, _i, ctypes.POINTER(_vp)]),
     ("sd_cas_multi_destroy", None, [_vp]),
     ("sd_cas_multi_count", _i, [_vp]),

@@ -211,6 +211,22 @@ class CasEngine:
         self._check(rc, "file_checksum")
         return out.value.decode()
 
+    def file_checksums(self, paths: Sequence[str]) -> tuple[list[Optional[str]], np.ndarray]:
+        """The validator job over many files (validator_job.rs:107-172, one file_checksum
+        per step, hash.rs:11-25) in one call: returns (64-hex digest or None per path, errno
+        array — 0, or the errno of the failed open/stat/read)."""
+        n = len(paths)
+        enc = [os.fsencode(p) for p in paths]
+        parr = (ctypes.c_char_p * max(n, 1))(*enc)
+        out = ctypes.create_string_buffer(65 * max(n, 1))
+        status = np.zeros(n, dtype=np.int32)
+        if n:
+            self._check(self.L.sd_cas_file_checksums(self.h, ctypes.cast(parr, ctypes.c_void_p), n,
+                                                     out, _np_ptr(status)), "file_checksums")
+        raw = out.raw
+        digests = [None if status[i] else raw[65 * i:65 * i + 64].decode() for i in range(n)]
+        return digests, -status
+
     # ---- device-resident (torch tensors as HBM buffers) ----------------------------------
     def hash_sampled(self, content, sizes, keys, stride: Optional[int] = None,
                      n: Optional[int] = None, stream: Optional[int] = None) -> None:
@@ -349,6 +365,16 @@ class CasEngine:
         self._check(self.L.sd_cas_checksum_dev(self.h, _ptr(data), int(length), out, _stream(stream)),
                     "checksum")
         return out.raw.hex()
+
+    def checksums_dev(self, arena, offs, lens, out, arena_bytes: Optional[int] = None,
+                      stream: Optional[int] = None) -> None:
+        """Digests of many device buffers in one launch chain (sd_cas_checksums_dev): buffer
+        i = arena[offs[i] : offs[i] + lens[i]] (int64 tensors, 16-B aligned offsets), out
+        uint8 [n, 32]."""
+        n = int(offs.numel())
+        ab = int(arena.numel() * arena.element_size()) if arena_bytes is None else int(arena_bytes)
+        self._check(self.L.sd_cas_checksums_dev(self.h, _ptr(arena), ab, _ptr(offs), _ptr(lens), n,
+                                                _ptr(out), _stream(stream)), "checksums_dev")
 
     def synth_sampled(self, seed: int, file0: int, n: int, content, sizes, stride: int,
                       dup_permille: int = 0, stream: Optional[int] = None) -> None:

@@ -18,6 +18,9 @@
 
 #include "blake3_device.hpp"
 #include "sd_checksum.h"
+#include "sd_group.h"
+
+#include <algorithm>
 
 namespace sdcas {
 
@@ -143,15 +146,16 @@ __device__ __forceinline__ void lds_reduce(uint32_t (*cvs)[8], uint32_t count, b
   }
 }
 
-// One workgroup = chunks [g*GC, g*GC+GC) of the buffer (global chunk index chunk0 + ...).
-// out[g] = subtree CV; when nchunks_total == 1 the single chunk is the root (digest).
+// Chunks [g*GC, g*GC+GC) of the buffer (global chunk index chunk0 + ...) -> their subtree
+// CV in out8[0..8); when the buffer has one group and root_if_single_group, the ROOT digest
+// (a single chunk is then the root itself).  Called by the whole workgroup; leaves cvs free.
 template <int LC>
-__device__ __forceinline__ void chunk_groups(const uint8_t* __restrict__ data, uint64_t len,
-                                             uint64_t chunk0, uint32_t* __restrict__ out,
-                                             int root_if_single_group, uint32_t (*cvs)[8]) {
+__device__ __forceinline__ void group_subtree(const uint8_t* __restrict__ data, uint64_t len,
+                                              uint64_t chunk0, uint64_t g, uint32_t* __restrict__ out8,
+                                              int root_if_single_group, uint32_t (*cvs)[8]) {
   constexpr uint32_t GC = GROUP * LC;
   const uint64_t nchunks = len == 0 ? 1 : (len + 1023) >> 10;
-  const uint64_t first = (uint64_t)blockIdx.x * GC;
+  const uint64_t first = g * GC;
   const uint32_t count = (uint32_t)min((uint64_t)GC, nchunks - first);
   const uint32_t t = threadIdx.x;
   const bool whole_tree = root_if_single_group && nchunks <= (uint64_t)GC;
@@ -174,7 +178,17 @@ __device__ __forceinline__ void chunk_groups(const uint8_t* __restrict__ data, u
   }
   __syncthreads();
   lds_reduce<(LC + 1) / 2>(cvs, count, whole_tree);
-  if (t < 8) out[(uint64_t)blockIdx.x * 8 + t] = cvs[0][t];
+  if (t < 8) out8[t] = cvs[0][t];
+  __syncthreads();  // cvs[0] read before the caller's next group overwrites it
+}
+
+// One workgroup per group of the buffer: out[8 g ..] = subtree CV of group g.
+template <int LC>
+__device__ __forceinline__ void chunk_groups(const uint8_t* __restrict__ data, uint64_t len,
+                                             uint64_t chunk0, uint32_t* __restrict__ out,
+                                             int root_if_single_group, uint32_t (*cvs)[8]) {
+  group_subtree<LC>(data, len, chunk0, blockIdx.x, out + (uint64_t)blockIdx.x * 8,
+                    root_if_single_group, cvs);
 }
 
 extern "C" __global__ void __launch_bounds__(GROUP)
@@ -199,6 +213,143 @@ sd_b3_reduce_cvs(const uint32_t* __restrict__ in, uint64_t cnt, uint32_t* __rest
   __syncthreads();
   lds_reduce<1>(cvs, count, root_if_single_group && cnt <= (uint64_t)GROUP);
   if (t < 8) out[(uint64_t)blockIdx.x * 8 + t] = cvs[0][t];
+}
+
+// ---- many buffers per launch chain (the validator job over a location) -------------------
+// validator_job.rs:107-172 runs one file_checksum (hash.rs:11-25) per job step; here a
+// batch of n buffers is hashed by ONE chain of launches: every buffer is cut into the
+// same 1 MiB subtree groups (GROUP_CHUNKS chunks) as K3, the groups of all buffers form
+// one work list (gstart = exclusive scan of the per-buffer group counts), and
+//   sd_b3_batch_groups: a persistent grid walks the work list — group i of buffer f
+//     (binary search in gstart) -> its subtree CV in cvs[i], or f's ROOT digest directly
+//     when f has a single group;
+//   sd_b3_batch_reduce: a persistent grid walks the buffers with >= 2 groups: aligned
+//     blocks of 256 group CVs pair-and-promote to one CV each in LDS (a buffer of up to
+//     65,536 groups = 64 GiB has <= 256 of them), then those to the ROOT digest — the same
+//     level-wise tree as K3's reduce_to_one.
+constexpr uint32_t BATCH_MAX_GROUPS = GROUP * GROUP;  // 64 GiB per buffer
+
+__device__ __forceinline__ uint32_t groups_of(uint64_t len) {
+  const uint64_t nchunks = len == 0 ? 1 : (len + 1023) >> 10;
+  return (uint32_t)((nchunks + GROUP_CHUNKS - 1) / GROUP_CHUNKS);
+}
+
+extern "C" __global__ void __launch_bounds__(256)
+sd_b3_batch_count(const uint64_t* __restrict__ lens, uint64_t n, uint32_t* __restrict__ groups,
+                  uint32_t* __restrict__ bad) {
+  const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= n) return;
+  const uint64_t len = lens[f];
+  const uint32_t g = len > (uint64_t)BATCH_MAX_GROUPS * GROUP_CHUNKS * 1024 ? 1u : groups_of(len);
+  if (len > (uint64_t)BATCH_MAX_GROUPS * GROUP_CHUNKS * 1024) atomicOr(bad, 1u);
+  groups[f] = g;
+}
+
+// the buffer owning work item `item`: the last f with gstart[f] <= item
+__device__ __forceinline__ uint64_t owner_of(const uint32_t* gstart, uint64_t n, uint64_t item) {
+  uint64_t lo = 0, hi = n;  // gstart[lo] <= item < gstart[hi] (gstart[n] = total)
+  while (hi - lo > 1) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (gstart[mid] <= item) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+extern "C" __global__ void __launch_bounds__(GROUP)
+sd_b3_batch_groups(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
+                   const uint64_t* __restrict__ lens, const uint32_t* __restrict__ gstart,
+                   const uint32_t* __restrict__ groups, uint64_t n, uint64_t items_cap,
+                   uint32_t* __restrict__ cvs_out, uint32_t* __restrict__ digests,
+                   uint32_t* __restrict__ bad) {
+  __shared__ uint32_t cvs[GROUP * K3_LANE_CHUNKS][8];
+  __shared__ uint64_t owner;
+  const uint64_t total = (uint64_t)gstart[n - 1] + groups[n - 1];
+  if (total > items_cap) {  // lengths beyond arena_bytes: the CV list would overflow
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(bad, 2u);
+    return;
+  }
+  for (uint64_t item = blockIdx.x; item < total; item += gridDim.x) {
+    if (threadIdx.x == 0) {
+      // skip empty-range owners: buffers own >= 1 group, so the search is exact
+      owner = owner_of(gstart, n, item);
+    }
+    __syncthreads();
+    const uint64_t f = owner;
+    __syncthreads();  // owner read by every wave before thread 0 rewrites it
+    const uint64_t g = item - gstart[f];
+    const bool single = groups[f] == 1;
+    uint32_t* out8 = single ? digests + 8 * f : cvs_out + 8 * item;
+    group_subtree<K3_LANE_CHUNKS>(arena + offs[f], lens[f], 0, g, out8, single ? 1 : 0, cvs);
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(GROUP)
+sd_b3_batch_reduce(const uint32_t* __restrict__ gstart, const uint32_t* __restrict__ groups,
+                   uint64_t n, uint64_t items_cap, const uint32_t* __restrict__ cvs_in,
+                   uint32_t* __restrict__ digests) {
+  __shared__ uint32_t work[GROUP][8];
+  __shared__ uint32_t top[GROUP][8];
+  const uint32_t t = threadIdx.x;
+  if ((uint64_t)gstart[n - 1] + groups[n - 1] > items_cap) return;
+  for (uint64_t f = blockIdx.x; f < n; f += gridDim.x) {
+    const uint32_t cnt = groups[f];
+    if (cnt < 2) continue;  // uniform across the workgroup
+    const uint32_t* in = cvs_in + 8 * (uint64_t)gstart[f];
+    if (cnt <= GROUP) {
+      if (t < cnt) {
+#pragma unroll
+        for (int w = 0; w < 8; ++w) work[t][w] = in[8 * (uint64_t)t + w];
+      }
+      __syncthreads();
+      lds_reduce<1>(work, cnt, true);
+      if (t < 8) digests[8 * f + t] = work[0][t];
+      __syncthreads();
+      continue;
+    }
+    const uint32_t blocks = (cnt + GROUP - 1) / GROUP;  // <= GROUP (BATCH_MAX_GROUPS)
+    for (uint32_t b = 0; b < blocks; ++b) {
+      const uint32_t m = min((uint32_t)GROUP, cnt - b * GROUP);
+      if (t < m) {
+#pragma unroll
+        for (int w = 0; w < 8; ++w) work[t][w] = in[8 * ((uint64_t)b * GROUP + t) + w];
+      }
+      __syncthreads();
+      lds_reduce<1>(work, m, false);
+      if (t < 8) top[b][t] = work[0][t];
+      __syncthreads();
+    }
+    lds_reduce<1>(top, blocks, true);
+    if (t < 8) digests[8 * f + t] = top[0][t];
+    __syncthreads();
+  }
+}
+
+size_t checksum_batch_workspace_bytes(uint64_t n, uint64_t arena_bytes) {
+  // groups | gstart (+1) | scan partials | cvs: <= n + arena_bytes / 1 MiB subtree CVs
+  const uint64_t items = n + arena_bytes / (GROUP_CHUNKS * 1024) + 1;
+  return 2 * ((n + 1) * 4 + 255) / 256 * 256 + ((n / 4096 + 2) * 4 + 255) / 256 * 256 + items * 32 + 256;
+}
+
+hipError_t checksum_batch_device(const uint8_t* arena, uint64_t arena_bytes, const uint64_t* offs,
+                                 const uint64_t* lens, uint64_t n, uint32_t* d_digests,
+                                 uint32_t* d_bad, void* ws, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (n > (1ull << 24)) return hipErrorInvalidValue;  // the u32 scan: <= 4096^2 buffers
+  char* p = (char*)ws;
+  uint32_t* groups = (uint32_t*)p; p += ((n + 1) * 4 + 255) / 256 * 256;
+  uint32_t* gstart = (uint32_t*)p; p += ((n + 1) * 4 + 255) / 256 * 256;
+  uint32_t* partial = (uint32_t*)p; p += ((n / 4096 + 2) * 4 + 255) / 256 * 256;
+  uint32_t* cvs = (uint32_t*)p;
+  sd_b3_batch_count<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(lens, n, groups, d_bad);
+  hipError_t e = exclusive_scan_u32(groups, gstart, n, partial, s);
+  if (e != hipSuccess) return e;
+  const uint64_t items = n + arena_bytes / (GROUP_CHUNKS * 1024) + 1;
+  const uint32_t ga = (uint32_t)std::min<uint64_t>(items, 256 * 8);
+  sd_b3_batch_groups<<<ga, GROUP, 0, s>>>(arena, offs, lens, gstart, groups, n, items, cvs,
+                                          d_digests, d_bad);
+  const uint32_t gr = (uint32_t)std::min<uint64_t>(n, 256 * 4);
+  sd_b3_batch_reduce<<<gr, GROUP, 0, s>>>(gstart, groups, n, items, cvs, d_digests);
+  return hipGetLastError();
 }
 
 size_t checksum_workspace_bytes(uint64_t len) {

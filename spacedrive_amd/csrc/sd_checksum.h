@@ -19,4 +19,13 @@ hipError_t checksum_device(const uint8_t* data, uint64_t len, uint64_t chunk0, b
 hipError_t reduce_cvs_device(const uint32_t* d_cvs, uint64_t cnt, uint32_t* d_out8, void* ws,
                              hipStream_t s);
 
+// Many buffers in one launch chain: buffer i = arena[offs[i], offs[i] + lens[i]) (16-B
+// aligned, readable to the 16-B round-up), d_digests[8 i ..] = its 32-byte digest.
+// arena_bytes bounds every buffer's end (sizes the CV list); a buffer over 64 GiB sets *d_bad.
+// n <= 2^24.  ws: checksum_batch_workspace_bytes(n, arena_bytes).
+size_t checksum_batch_workspace_bytes(uint64_t n, uint64_t arena_bytes);
+hipError_t checksum_batch_device(const uint8_t* arena, uint64_t arena_bytes, const uint64_t* offs,
+                                 const uint64_t* lens, uint64_t n, uint32_t* d_digests,
+                                 uint32_t* d_bad, void* ws, hipStream_t s);
+
 }  // namespace sdcas

@@ -1083,6 +1083,199 @@ int sd_cas_file_checksum(sd_cas_ctx* c, const char* path, char out_hex[65], int*
   return SD_CAS_OK;
 }
 
+// ---- the validator job over many files -----------------------------------------------
+
+int sd_cas_checksums_dev(sd_cas_ctx* c, const void* d_arena, uint64_t arena_bytes,
+                         const uint64_t* d_offs, const uint64_t* d_lens, size_t n, uint8_t* d_out,
+                         void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (n == 0) return SD_CAS_OK;
+  if (!d_arena || !d_offs || !d_lens || !d_out || ((uintptr_t)d_arena & 15) ||
+      ((uintptr_t)d_out & 3) || n > (1u << 24))
+    return fail(c, SD_CAS_EINVAL, "checksums: bad arguments");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  int rc = ensure(c, c->ws, checksum_batch_workspace_bytes(n, arena_bytes));
+  if (rc) return rc;
+  uint32_t* d_bad = (uint32_t*)(c->d_scalar + 6);
+  uint32_t bad = 0;
+  HIP_TRY(c, sd_ws_acquire(c, s));
+  HIP_TRY(c, hipMemsetAsync(d_bad, 0, 4, s));
+  HIP_TRY(c, checksum_batch_device((const uint8_t*)d_arena, arena_bytes, d_offs, d_lens, n,
+                                   (uint32_t*)d_out, d_bad, c->ws.p, s));
+  HIP_TRY(c, hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, sd_ws_release(c, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  if (bad)
+    return fail(c, SD_CAS_EINVAL, "checksums: %s",
+                (bad & 1) ? "a buffer is longer than 64 GiB" : "buffers extend past arena_bytes");
+  return SD_CAS_OK;
+}
+
+// file_checksum over many paths.  Windows of up to CK_WIN bytes / CK_WIN_FILES files in
+// index order, double-buffered: the pool reads window w (one slot of up128(st_size + 1) per
+// file: the spare byte shows EOF, so a file that grew since stat fills its slot and is
+// redone by the streaming path) into one pinned slot while the GPU copies and hashes window
+// w-1 from the other.  Pinned slot layout: offs | lens | digests | data.
+int sd_cas_file_checksums(sd_cas_ctx* c, const char* const* paths, size_t n, char* out_hex,
+                          int32_t* status) {
+  if (!c) return SD_CAS_EINVAL;
+  if (n == 0) return SD_CAS_OK;
+  if (!paths || !out_hex || !status) return fail(c, SD_CAS_EINVAL, "file_checksums: null argument");
+  HIP_TRY(c, hipSetDevice(c->device));
+  constexpr uint64_t CK_WIN = 128ull << 20;  // data bytes per window
+  constexpr uint64_t CK_BIG = CK_WIN / 2;    // larger files stream on their own (64 MiB segments)
+  constexpr size_t CK_WIN_FILES = 32768;
+  constexpr size_t HDR = CK_WIN_FILES * (8 + 8 + 32);
+  constexpr size_t SLOT = HDR + CK_WIN + 256;
+  enum : uint8_t { K_BATCH = 0, K_STREAM = 1, K_ERROR = 2 };
+  std::vector<uint64_t> fsize(n, 0);
+  std::vector<uint8_t> kind(n, K_BATCH);
+  for (size_t i = 0; i < n; i++) { status[i] = 0; out_hex[65 * i] = 0; }
+  {  // stat pass
+    std::atomic<size_t> next{0};
+    c->pool.run(std::max(1u, std::min(16u, (unsigned)((n + 63) / 64))), [&]() {
+      for (size_t i; (i = next.fetch_add(1)) < n;) {
+        struct stat st;
+        if (stat(paths[i], &st) != 0) { status[i] = -errno; kind[i] = K_ERROR; continue; }
+        fsize[i] = (uint64_t)st.st_size;
+        if (fsize[i] > CK_BIG) kind[i] = K_STREAM;
+      }
+    });
+  }
+  // windows: [w0, w1) file ranges in index order
+  std::vector<size_t> wstart{0};
+  {
+    uint64_t bytes = 0;
+    size_t files = 0;
+    for (size_t i = 0; i < n; i++) {
+      if (kind[i] != K_BATCH) continue;
+      const uint64_t need = up128(fsize[i] + 1);
+      if (files && (bytes + need > CK_WIN || files == CK_WIN_FILES)) {
+        wstart.push_back(i);
+        bytes = 0;
+        files = 0;
+      }
+      bytes += need;
+      files++;
+    }
+    wstart.push_back(n);
+  }
+  const size_t nw = wstart.size() - 1;
+  int rc = ensure_pinned(c, 2 * SLOT);
+  if (rc) return rc;
+  if ((rc = ensure(c, c->staging, 2 * SLOT))) return rc;
+  if ((rc = ensure(c, c->ws, checksum_batch_workspace_bytes(CK_WIN_FILES, CK_WIN)))) return rc;
+  hipStream_t s = c->stream;
+  hipEvent_t done[2] = {nullptr, nullptr};
+  for (int b = 0; b < 2; b++)
+    if (hipEventCreateWithFlags(&done[b], hipEventDisableTiming) != hipSuccess) {
+      if (done[0]) (void)hipEventDestroy(done[0]);
+      return fail(c, SD_CAS_EHIP, "file_checksums: event create");
+    }
+  std::vector<size_t> members[2];  // file index of each batch entry of the window in a slot
+  static const char* hx = "0123456789abcdef";
+  auto emit = [&](int b) {  // the window in slot b is complete: digests -> hex
+    const uint8_t* dg = (const uint8_t*)c->pinned + (size_t)b * SLOT + CK_WIN_FILES * 16;
+    for (size_t k = 0; k < members[b].size(); k++) {
+      char* o = out_hex + 65 * members[b][k];
+      for (int j = 0; j < 32; j++) { o[2 * j] = hx[dg[32 * k + j] >> 4]; o[2 * j + 1] = hx[dg[32 * k + j] & 15]; }
+      o[64] = 0;
+    }
+    members[b].clear();
+  };
+  bool pending[2] = {false, false};
+  HIP_TRY(c, sd_ws_acquire(c, s));
+  uint32_t* d_bad = (uint32_t*)(c->d_scalar + 6);
+  HIP_TRY(c, hipMemsetAsync(d_bad, 0, 4, s));
+  for (size_t w = 0; w < nw && rc == SD_CAS_OK; w++) {
+    const int b = (int)(w & 1);
+    if (pending[b]) {  // slot b's previous window: copied, hashed and its digests back
+      if (hipEventSynchronize(done[b]) != hipSuccess) { rc = fail(c, SD_CAS_EHIP, "file_checksums: sync"); break; }
+      emit(b);
+      pending[b] = false;
+    }
+    char* pin = (char*)c->pinned + (size_t)b * SLOT;
+    uint64_t* h_offs = (uint64_t*)pin;
+    uint64_t* h_lens = h_offs + CK_WIN_FILES;
+    char* data = pin + HDR;
+    std::vector<size_t>& mem = members[b];
+    std::vector<uint64_t> cap;
+    uint64_t o = 0;
+    for (size_t i = wstart[w]; i < wstart[w + 1]; i++) {
+      if (kind[i] != K_BATCH) continue;
+      h_offs[mem.size()] = o;
+      cap.push_back(up128(fsize[i] + 1));
+      o += cap.back();
+      mem.push_back(i);
+    }
+    const size_t m = mem.size();
+    if (m == 0) continue;
+    std::atomic<size_t> next{0};
+    c->pool.run(std::max(1u, std::min(16u, (unsigned)((m + 3) / 4))), [&]() {
+      for (size_t k; (k = next.fetch_add(1)) < m;) {
+        const size_t i = mem[k];
+        int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
+        if (fd < 0) { status[i] = -errno; kind[i] = K_ERROR; h_lens[k] = 0; continue; }
+        uint64_t got = 0;
+        while (got < cap[k]) {
+          ssize_t r = pread(fd, data + h_offs[k] + got, cap[k] - got, (off_t)got);
+          if (r < 0 && errno == EINTR) continue;
+          if (r < 0) { status[i] = -errno; kind[i] = K_ERROR; break; }
+          if (r == 0) break;  // EOF: hash.rs stops at the first short read
+          got += (uint64_t)r;
+        }
+        close(fd);
+        if (got == cap[k]) kind[i] = K_STREAM;  // grew past its slot: stream it afterwards
+        h_lens[k] = kind[i] == K_BATCH ? got : 0;
+      }
+    });
+    // entries that failed or grew are hashed as empty buffers and ignored
+    hipError_t e = hipMemcpyAsync((char*)c->staging.p + (size_t)b * SLOT, pin, CK_WIN_FILES * 16,
+                                  hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync((char*)c->staging.p + (size_t)b * SLOT + HDR, data, o, hipMemcpyHostToDevice, s);
+    char* dbase = (char*)c->staging.p + (size_t)b * SLOT;
+    if (e == hipSuccess)
+      e = checksum_batch_device((const uint8_t*)(dbase + HDR), o, (const uint64_t*)dbase,
+                                (const uint64_t*)dbase + CK_WIN_FILES, m,
+                                (uint32_t*)(dbase + CK_WIN_FILES * 16), d_bad, c->ws.p, s);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(pin + CK_WIN_FILES * 16, dbase + CK_WIN_FILES * 16, m * 32,
+                         hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipEventRecord(done[b], s);
+    if (e != hipSuccess) { rc = fail(c, SD_CAS_EHIP, "file_checksums window: %s", hipGetErrorString(e)); break; }
+    pending[b] = true;
+  }
+  uint32_t bad = 0;
+  if (rc == SD_CAS_OK) {
+    hipError_t e = hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) rc = fail(c, SD_CAS_EHIP, "file_checksums: %s", hipGetErrorString(e));
+    else if (bad) rc = fail(c, SD_CAS_EHIP, "file_checksums: batch work list overflow");
+  }
+  (void)sd_ws_release(c, s);
+  (void)hipStreamSynchronize(s);
+  for (int b = 0; b < 2; b++) {
+    if (rc == SD_CAS_OK && pending[b]) emit(b);
+    (void)hipEventDestroy(done[b]);
+  }
+  if (rc) return rc;
+  // big files and files that grew: the streaming path, one at a time (after the windows:
+  // it reuses the pinned and device staging)
+  for (size_t i = 0; i < n; i++) {
+    if (kind[i] != K_STREAM) continue;
+    char* o = out_hex + 65 * i;
+    int err_no = 0;
+    const int r = sd_cas_file_checksum(c, paths[i], o, &err_no);
+    if (r == SD_CAS_EIO) { status[i] = -(err_no ? err_no : EIO); o[0] = 0; continue; }
+    if (r) return r;
+  }
+  for (size_t i = 0; i < n; i++)
+    if (status[i]) out_hex[65 * i] = 0;
+  return SD_CAS_OK;
+}
+
 // ---- synthetic inputs ----------------------------------------------------------------
 
 int sd_cas_synth_sampled_dev(sd_cas_ctx* c, uint64_t seed, uint64_t file0, size_t n,

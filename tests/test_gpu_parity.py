@@ -509,6 +509,63 @@ def test_file_checksum_reads_to_eof(eng, oracle):
     assert eng.file_checksum(p) == oracle.file_checksum(p) == oracle.blake3(open(p, "rb").read()).hex()
 
 
+def test_checksums_batch_dev_vs_oracle(eng, oracle):
+    """The validator over many buffers in one launch chain (sd_cas_checksums_dev): ragged
+    lengths around every chunk / 1 MiB-subtree boundary, a 300 MiB buffer (> 256 subtree CVs:
+    the two-level in-LDS reduce), buffers in shuffled arena order, vs the oracle per buffer."""
+    rng = np.random.default_rng(9)
+    lens = (CHECKSUM_LENS[:-1] + [(1 << 20) - 1, 1 << 20, (1 << 20) + 1, (256 << 20) + 4097,
+                                  (300 << 20) + 5, 5 * (1 << 20) + 17]
+            + [int(x) for x in rng.integers(0, 3 << 20, 300)])
+    order = rng.permutation(len(lens))
+    offs = np.zeros(len(lens), dtype=np.uint64)
+    o = 0
+    for i in order:  # arena order != index order
+        offs[i] = o
+        o += (lens[i] + 15) // 16 * 16 + 16 * int(rng.integers(0, 3))
+    arena_bytes = o + 16
+    arena = torch.empty(arena_bytes, dtype=torch.uint8, device="cuda")
+    seed = 91
+    eng.synth_stream(seed, 1, 0, arena_bytes // 8 * 8, arena)
+    host = arena.cpu().numpy()
+    out = torch.zeros((len(lens), 32), dtype=torch.uint8, device="cuda")
+    eng.checksums_dev(arena, dev64(offs), dev64(np.array(lens, dtype=np.uint64)), out)
+    got = out.cpu().numpy()
+    for i, L in enumerate(lens):
+        want = oracle.blake3(host[int(offs[i]):int(offs[i]) + L].tobytes())
+        assert got[i].tobytes() == want, (i, L)
+    # lengths past arena_bytes are refused, not hashed out of bounds
+    with pytest.raises(Exception):
+        eng.checksums_dev(arena, dev64(offs), dev64(np.array(lens, dtype=np.uint64)), out,
+                          arena_bytes=1 << 20)
+
+
+def test_file_checksums_many_paths(eng, oracle, tmp_path):
+    """The validator job over a directory (sd_cas_file_checksums): small and empty files,
+    files straddling the window and the streaming threshold, a missing path, a procfs file
+    with st_size 0 (read to EOF), vs the oracle's file_checksum per path."""
+    rng = np.random.default_rng(10)
+    sizes = ([0, 1, 1023, 1024, 1025, (1 << 20) + 3, (64 << 20) + 1, (70 << 20) + 5]
+             + [int(x) for x in rng.integers(0, 2 << 20, 120)] + [int(x) for x in rng.integers(20 << 20, 40 << 20, 8)])
+    paths = []
+    for i, L in enumerate(sizes):
+        p = tmp_path / f"c{i}"
+        p.write_bytes(rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+        paths.append(str(p))
+    paths.insert(5, str(tmp_path / "missing"))
+    proc = "/proc/sys/kernel/ostype"
+    if os.path.exists(proc):
+        paths.append(proc)
+    digests, errs = eng.file_checksums(paths)
+    for p, d, e in zip(paths, digests, errs):
+        if p.endswith("missing"):
+            assert d is None and e == 2
+            continue
+        assert e == 0 and d == oracle.file_checksum(p), p
+    d0, e0 = eng.file_checksums([])
+    assert d0 == [] and len(e0) == 0
+
+
 def test_synth_matches_oracle_generator(eng, oracle):
     n, seed = 64, 12345
     content = torch.empty((n, SAMPLED_CONTENT_LEN), dtype=torch.uint8, device="cuda")

@@ -1,0 +1,125 @@
+#!/usr/bin/env python3
+"""The validator job over many files (sd_cas_checksums_dev / sd_cas_file_checksums).
+
+Device batches (resident, synthetic): one launch chain per batch, HIP events on the
+engine's stream; every digest of a sample checked against the oracle.  Library shapes:
+  photos  4,096 buffers of U(1, 8) MiB      (~18 GB)
+  docs    262,144 buffers of U(1, 128) KiB  (~17 GB)
+  small   1,048,576 buffers of U(0, 16) KiB (~8.6 GB)
+  one     one 16 GiB buffer (the K3 single-buffer chain's shape, for comparison)
+Paths (--paths N): N files of U(0.25, 4) MiB on /dev/shm through sd_cas_file_checksums vs
+the oracle's file_checksum on 1 thread (hash.rs is single-threaded) and file-parallel on
+the host cores.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+SHAPES = {"photos": (4096, 1 << 20, 8 << 20), "docs": (262144, 1 << 10, 128 << 10),
+          "small": (1 << 20, 0, 16 << 10), "one": (1, 16 << 30, 16 << 30)}
+
+
+def device_batch(eng, orc, name, iters):
+    import numpy as np
+    import torch
+    n, lo, hi = SHAPES[name]
+    rng = np.random.default_rng(5)
+    lens = rng.integers(lo, hi + 1, n, dtype=np.uint64) if hi > lo else np.full(n, lo, dtype=np.uint64)
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum((lens[:-1] + 127) // 128 * 128)
+    total = int(offs[-1] + lens[-1])
+    ab = (total + 127) // 128 * 128 + 128
+    arena = torch.empty(ab, dtype=torch.uint8, device="cuda")
+    eng.synth_stream(77, 0, 0, ab // 8 * 8, arena)
+    d_offs = torch.from_numpy(offs.view(np.int64)).cuda()
+    d_lens = torch.from_numpy(lens.view(np.int64)).cuda()
+    out = torch.zeros((n, 32), dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream()
+    eng.checksums_dev(arena, d_offs, d_lens, out, stream=s.cuda_stream)
+    ts = []
+    for _ in range(iters):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        eng.checksums_dev(arena, d_offs, d_lens, out, stream=s.cuda_stream)
+        b.record(s)
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    ms = float(np.median(ts))
+    got = out.cpu().numpy()
+    idx = sorted(set(rng.integers(0, n, min(n, 64)).tolist()) | {0, n - 1})
+    ok = True
+    for i in idx:
+        o, L = int(offs[i]), int(lens[i])
+        if L > (1 << 30):  # the single 16 GiB buffer: the oracle's tree-parallel hash
+            want = orc.blake3_mt(arena[o:o + L].cpu().numpy(), 16)
+        else:
+            want = orc.blake3(arena[o:o + L].cpu().numpy().tobytes())
+        ok &= got[i].tobytes() == want
+    comps = int((lens // 64).sum() + (lens // 1024).sum())
+    del arena, out
+    torch.cuda.empty_cache()
+    return {"shape": name, "buffers": n, "bytes": int(lens.sum()), "ms": ms,
+            "ms_all": ts, "gb_per_s": float(lens.sum()) / (ms / 1e3) / 1e9,
+            "buffers_per_s": n / (ms / 1e3),
+            "valu_slot_frac": comps * 1014 / 64 / (ms / 1e3) / (1024 * 2.4e9 / 2),
+            "parity_sample": len(idx), "parity": bool(ok)}
+
+
+def paths_run(eng, orc, n, root):
+    import numpy as np
+    rng = np.random.default_rng(6)
+    os.makedirs(root, exist_ok=True)
+    sizes = rng.integers(1 << 18, 4 << 20, n)
+    paths = []
+    for i, L in enumerate(sizes):
+        p = os.path.join(root, f"v{i}")
+        with open(p, "wb") as fh:
+            fh.write(orc.fill_content_range(88, i, 0, int(L) // 8 * 8).tobytes())
+        paths.append(p)
+    total = int(sum(int(L) // 8 * 8 for L in sizes))
+    eng.file_checksums(paths[:8])
+    t = time.perf_counter()
+    got, errs = eng.file_checksums(paths)
+    gpu_s = time.perf_counter() - t
+    # CPU: hash.rs is one thread per file; the job is one file per step
+    m1 = min(n, 64)
+    t = time.perf_counter()
+    one = [orc.file_checksum(p) for p in paths[:m1]]
+    cpu1_s = (time.perf_counter() - t) * n / m1
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    t = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        allc = list(ex.map(orc.file_checksum, paths))
+    cpun_s = time.perf_counter() - t
+    parity = got == allc and got[:m1] == one and not any(errs)
+    for p in paths:
+        os.unlink(p)
+    return {"files": n, "bytes": total, "gpu_s": gpu_s, "gpu_gb_per_s": total / gpu_s / 1e9,
+            "gpu_files_per_s": n / gpu_s, "cpu_1thread_gb_per_s": total / cpu1_s / 1e9,
+            "cpu_threads": threads, "cpu_all_gb_per_s": total / cpun_s / 1e9,
+            "parity": bool(parity)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", action="append", default=None)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--paths", type=int, default=0)
+    ap.add_argument("--root", default="/dev/shm/sdcas_validator")
+    a = ap.parse_args()
+    from spacedrive_amd import CasEngine
+    from oracle.pyoracle import Oracle
+    eng, orc = CasEngine(0), Oracle()
+    for name in a.shape or ["photos", "docs", "small", "one"]:
+        print(json.dumps(device_batch(eng, orc, name, a.iters)), flush=True)
+    if a.paths:
+        print(json.dumps(paths_run(eng, orc, a.paths, a.root)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
