@@ -217,69 +217,169 @@ sd_b3_reduce_cvs(const uint32_t* __restrict__ in, uint64_t cnt, uint32_t* __rest
 
 // ---- many buffers per launch chain (the validator job over a location) -------------------
 // validator_job.rs:107-172 runs one file_checksum (hash.rs:11-25) per job step; here a
-// batch of n buffers is hashed by ONE chain of launches: every buffer is cut into the
-// same 1 MiB subtree groups (GROUP_CHUNKS chunks) as K3, the groups of all buffers form
-// one work list (gstart = exclusive scan of the per-buffer group counts), and
-//   sd_b3_batch_groups: a persistent grid walks the work list — group i of buffer f
-//     (binary search in gstart) -> its subtree CV in cvs[i], or f's ROOT digest directly
-//     when f has a single group;
-//   sd_b3_batch_reduce: a persistent grid walks the buffers with >= 2 groups: aligned
-//     blocks of 256 group CVs pair-and-promote to one CV each in LDS (a buffer of up to
-//     65,536 groups = 64 GiB has <= 256 of them), then those to the ROOT digest — the same
-//     level-wise tree as K3's reduce_to_one.
+// batch of n buffers is hashed by ONE chain of launches, split by size:
+//   small buffers (<= SMALL_CHUNKS KiB, documents): ONE WAVE per buffer — lane c hashes
+//     chunk c, the wave pair-and-promotes its chunk CVs in its own LDS slice (no workgroup
+//     barrier), 4 buffers per workgroup in flight;
+//   larger buffers: cut into the same 1 MiB subtree groups (GROUP_CHUNKS chunks) as K3;
+//     their groups form one work list (gstart = exclusive scan of the per-buffer group
+//     counts, owner[item] = the buffer of work item `item`) that a large grid strides over:
+//       sd_b3_batch_groups: item -> its subtree CV, or the buffer's ROOT digest directly
+//         when the buffer has a single group;
+//       sd_b3_batch_reduce: the buffers with >= 2 groups: aligned blocks of 256 group CVs
+//         pair-and-promote to one CV each in LDS (a buffer of up to 65,536 groups = 64 GiB
+//         has <= 256 of them), then those to the ROOT digest — the level-wise tree of K3's
+//         reduce_to_one.
 constexpr uint32_t BATCH_MAX_GROUPS = GROUP * GROUP;  // 64 GiB per buffer
+constexpr uint32_t SMALL_CHUNKS = 64;                 // a wave's lanes
+constexpr uint64_t BATCH_MAX_LEN = (uint64_t)BATCH_MAX_GROUPS * GROUP_CHUNKS * 1024;
 
-__device__ __forceinline__ uint32_t groups_of(uint64_t len) {
-  const uint64_t nchunks = len == 0 ? 1 : (len + 1023) >> 10;
-  return (uint32_t)((nchunks + GROUP_CHUNKS - 1) / GROUP_CHUNKS);
-}
+__device__ __forceinline__ uint64_t chunks_of(uint64_t len) { return len == 0 ? 1 : (len + 1023) >> 10; }
 
+// per-buffer group counts for the big-buffer work list (0 for small buffers)
 extern "C" __global__ void __launch_bounds__(256)
 sd_b3_batch_count(const uint64_t* __restrict__ lens, uint64_t n, uint32_t* __restrict__ groups,
                   uint32_t* __restrict__ bad) {
   const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= n) return;
   const uint64_t len = lens[f];
-  const uint32_t g = len > (uint64_t)BATCH_MAX_GROUPS * GROUP_CHUNKS * 1024 ? 1u : groups_of(len);
-  if (len > (uint64_t)BATCH_MAX_GROUPS * GROUP_CHUNKS * 1024) atomicOr(bad, 1u);
-  groups[f] = g;
+  const uint64_t nch = chunks_of(len);
+  if (len > BATCH_MAX_LEN) atomicOr(bad, 1u);
+  groups[f] = nch <= SMALL_CHUNKS || len > BATCH_MAX_LEN
+                  ? 0u : (uint32_t)((nch + GROUP_CHUNKS - 1) / GROUP_CHUNKS);
 }
 
-// the buffer owning work item `item`: the last f with gstart[f] <= item
-__device__ __forceinline__ uint64_t owner_of(const uint32_t* gstart, uint64_t n, uint64_t item) {
-  uint64_t lo = 0, hi = n;  // gstart[lo] <= item < gstart[hi] (gstart[n] = total)
-  while (hi - lo > 1) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if (gstart[mid] <= item) lo = mid; else hi = mid;
+// owner[item] = the last f with gstart[f] <= item (every listed buffer owns >= 1 item)
+extern "C" __global__ void __launch_bounds__(256)
+sd_b3_batch_owner(const uint32_t* __restrict__ gstart, const uint32_t* __restrict__ groups,
+                  uint64_t n, uint64_t items_cap, uint32_t* __restrict__ owner) {
+  const uint64_t total = (uint64_t)gstart[n - 1] + groups[n - 1];
+  const uint64_t lim = total < items_cap ? total : items_cap;
+  for (uint64_t item = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; item < lim;
+       item += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t lo = 0, hi = n;  // gstart[lo] <= item < gstart[hi] (gstart[n] = total)
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (gstart[mid] <= item) lo = mid; else hi = mid;
+    }
+    owner[item] = (uint32_t)lo;
   }
-  return lo;
 }
 
-extern "C" __global__ void __launch_bounds__(GROUP)
+// wave-synchronous LDS phases of the small-buffer path (one wave per buffer: no workgroup
+// barrier, only ordering of this wave's own LDS accesses)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// One buffer per SEG-lane segment (SEG = 16: buffers of <= 16 chunks, 4 per wave; SEG = 64:
+// 17..64 chunks, one per wave): lane l of the segment hashes chunk l, and the segment
+// pair-and-promotes its chunk CVs in its own LDS slice, log2(SEG) fixed levels run by the
+// whole wave in step (segments whose tree is done idle through the rest).
+template <uint32_t SEG>
+__device__ __forceinline__ void batch_small_body(const uint8_t* __restrict__ arena,
+                                                 const uint64_t* __restrict__ offs,
+                                                 const uint64_t* __restrict__ lens, uint64_t n,
+                                                 uint32_t* __restrict__ digests,
+                                                 uint32_t (*cvs)[8]) {
+  constexpr uint32_t PER_WAVE = 64 / SEG;
+  constexpr uint32_t LOW = SEG == 64 ? 16 : 0;  // this class: LOW < chunks <= SEG
+  const uint32_t lane = threadIdx.x & 63u, seg = lane / SEG, sl = lane % SEG;
+  uint32_t (*mine)[8] = cvs + (threadIdx.x >> 6) * 64 + seg * SEG;  // the segment's slice
+  const uint64_t slots = (uint64_t)gridDim.x * (blockDim.x / 64) * PER_WAVE;
+  const uint64_t first = ((uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * PER_WAVE + seg;
+  for (uint64_t base = first - seg; base < n; base += slots) {  // wave-uniform trip count
+    const uint64_t f = base + seg;
+    const uint64_t len = f < n ? lens[f] : 0;
+    const uint64_t nch = chunks_of(len);
+    const bool mine_class = f < n && nch > LOW && nch <= SEG;
+    const uint32_t count = mine_class ? (uint32_t)nch : 0u;
+    if (sl < count) {
+      const uint64_t off = (uint64_t)sl << 10;
+      const uint32_t clen = (uint32_t)min((uint64_t)1024, len - min(len, off));
+      uint32_t cv[8];
+      // the generic chunk loop for every lane (a full-chunk fast path would diverge from
+      // the buffer's partial last chunk inside the wave)
+      chunk_cv(reinterpret_cast<const uint4*>(arena + offs[f] + off), clen, sl, count == 1, cv);
+      if (count == 1) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) digests[8 * f + k] = cv[k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) mine[sl][k] = cv[k];
+      }
+    }
+    wave_sync();
+    uint32_t c = count;
+#pragma unroll 1
+    for (uint32_t lvl = 1; lvl < SEG; lvl <<= 1) {
+      const uint32_t pairs = c >> 1;
+      const bool odd = c & 1u;
+      const bool work = c > 1 && (sl < pairs || (odd && sl == pairs));
+      uint32_t out[8];
+      if (c > 1 && sl < pairs) {
+        uint32_t l[8], r[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { l[k] = mine[2 * sl][k]; r[k] = mine[2 * sl + 1][k]; }
+        parent(out, l, r, c == 2 ? (uint32_t)ROOT : 0u);
+      } else if (work) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) out[k] = mine[c - 1][k];
+      }
+      wave_sync();
+      if (work) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) mine[sl][k] = out[k];
+      }
+      wave_sync();
+      if (c > 1) c = pairs + (odd ? 1u : 0u);
+    }
+    if (count > 1 && sl < 8) digests[8 * f + sl] = mine[0][sl];
+    wave_sync();  // mine[0] read before the next buffer's chunk CVs overwrite it
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(256)
+sd_b3_batch_small16(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
+                    const uint64_t* __restrict__ lens, uint64_t n, uint32_t* __restrict__ digests) {
+  __shared__ uint32_t cvs[4 * 64][8];
+  batch_small_body<16>(arena, offs, lens, n, digests, cvs);
+}
+
+extern "C" __global__ void __launch_bounds__(256)
+sd_b3_batch_small64(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
+                    const uint64_t* __restrict__ lens, uint64_t n, uint32_t* __restrict__ digests) {
+  __shared__ uint32_t cvs[4 * 64][8];
+  batch_small_body<64>(arena, offs, lens, n, digests, cvs);
+}
+
+// A large grid (up to 65,536 workgroups: far more than are resident) strides over the work
+// list, so the hardware dispatcher balances it at workgroup granularity like K3's one
+// workgroup per group; an atomic work cursor over a resident-sized grid ran 14 % slower on
+// one 16 GiB buffer (2.41 vs 2.8 TB/s).  4 waves per SIMD like sd_b3_chunk_groups.
+extern "C" __global__ void __launch_bounds__(GROUP) __attribute__((amdgpu_waves_per_eu(4)))
 sd_b3_batch_groups(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                    const uint64_t* __restrict__ lens, const uint32_t* __restrict__ gstart,
-                   const uint32_t* __restrict__ groups, uint64_t n, uint64_t items_cap,
-                   uint32_t* __restrict__ cvs_out, uint32_t* __restrict__ digests,
-                   uint32_t* __restrict__ bad) {
+                   const uint32_t* __restrict__ groups, const uint32_t* __restrict__ owner,
+                   uint64_t n, uint64_t items_cap, uint32_t* __restrict__ cvs_out,
+                   uint32_t* __restrict__ digests, uint32_t* __restrict__ bad) {
   __shared__ uint32_t cvs[GROUP * K3_LANE_CHUNKS][8];
-  __shared__ uint64_t owner;
   const uint64_t total = (uint64_t)gstart[n - 1] + groups[n - 1];
   if (total > items_cap) {  // lengths beyond arena_bytes: the CV list would overflow
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(bad, 2u);
     return;
   }
+  // the item's state is workgroup-uniform: readfirstlane keeps it in SGPRs
+  auto uni = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
+  auto uni64 = [&](uint64_t x) { return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x); };
   for (uint64_t item = blockIdx.x; item < total; item += gridDim.x) {
-    if (threadIdx.x == 0) {
-      // skip empty-range owners: buffers own >= 1 group, so the search is exact
-      owner = owner_of(gstart, n, item);
-    }
-    __syncthreads();
-    const uint64_t f = owner;
-    __syncthreads();  // owner read by every wave before thread 0 rewrites it
-    const uint64_t g = item - gstart[f];
-    const bool single = groups[f] == 1;
-    uint32_t* out8 = single ? digests + 8 * f : cvs_out + 8 * item;
-    group_subtree<K3_LANE_CHUNKS>(arena + offs[f], lens[f], 0, g, out8, single ? 1 : 0, cvs);
+    const uint32_t f = uni(owner[item]);
+    const uint64_t g = item - uni(gstart[f]);
+    const bool single = uni(groups[f]) == 1;
+    uint32_t* out8 = single ? digests + 8 * (uint64_t)f : cvs_out + 8 * item;
+    group_subtree<K3_LANE_CHUNKS>(arena + uni64(offs[f]), uni64(lens[f]), 0, g, out8,
+                                  single ? 1 : 0, cvs);
   }
 }
 
@@ -324,10 +424,18 @@ sd_b3_batch_reduce(const uint32_t* __restrict__ gstart, const uint32_t* __restri
   }
 }
 
+static inline size_t al256c(size_t x) { return (x + 255) / 256 * 256; }
+
+// work items of the big-buffer list: <= n + arena_bytes / 1 MiB (disjoint buffers)
+static inline uint64_t batch_items_cap(uint64_t n, uint64_t arena_bytes) {
+  return n + arena_bytes / (GROUP_CHUNKS * 1024) + 1;
+}
+
 size_t checksum_batch_workspace_bytes(uint64_t n, uint64_t arena_bytes) {
-  // groups | gstart (+1) | scan partials | cvs: <= n + arena_bytes / 1 MiB subtree CVs
-  const uint64_t items = n + arena_bytes / (GROUP_CHUNKS * 1024) + 1;
-  return 2 * ((n + 1) * 4 + 255) / 256 * 256 + ((n / 4096 + 2) * 4 + 255) / 256 * 256 + items * 32 + 256;
+  // groups | gstart | scan partials | owner | cvs
+  const uint64_t items = batch_items_cap(n, arena_bytes);
+  return 2 * al256c((n + 1) * 4) + al256c((n / 4096 + 2) * 4) + al256c(items * 4) +
+         items * 32 + 256;
 }
 
 hipError_t checksum_batch_device(const uint8_t* arena, uint64_t arena_bytes, const uint64_t* offs,
@@ -335,20 +443,31 @@ hipError_t checksum_batch_device(const uint8_t* arena, uint64_t arena_bytes, con
                                  uint32_t* d_bad, void* ws, hipStream_t s) {
   if (n == 0) return hipSuccess;
   if (n > (1ull << 24)) return hipErrorInvalidValue;  // the u32 scan: <= 4096^2 buffers
+  const uint64_t items = batch_items_cap(n, arena_bytes);
   char* p = (char*)ws;
-  uint32_t* groups = (uint32_t*)p; p += ((n + 1) * 4 + 255) / 256 * 256;
-  uint32_t* gstart = (uint32_t*)p; p += ((n + 1) * 4 + 255) / 256 * 256;
-  uint32_t* partial = (uint32_t*)p; p += ((n / 4096 + 2) * 4 + 255) / 256 * 256;
+  uint32_t* groups = (uint32_t*)p; p += al256c((n + 1) * 4);
+  uint32_t* gstart = (uint32_t*)p; p += al256c((n + 1) * 4);
+  uint32_t* partial = (uint32_t*)p; p += al256c((n / 4096 + 2) * 4);
+  uint32_t* owner = (uint32_t*)p; p += al256c(items * 4);
   uint32_t* cvs = (uint32_t*)p;
-  sd_b3_batch_count<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(lens, n, groups, d_bad);
+  const uint32_t nb = (uint32_t)((n + 255) / 256);
+  sd_b3_batch_count<<<nb, 256, 0, s>>>(lens, n, groups, d_bad);
   hipError_t e = exclusive_scan_u32(groups, gstart, n, partial, s);
   if (e != hipSuccess) return e;
-  const uint64_t items = n + arena_bytes / (GROUP_CHUNKS * 1024) + 1;
-  const uint32_t ga = (uint32_t)std::min<uint64_t>(items, 256 * 8);
-  sd_b3_batch_groups<<<ga, GROUP, 0, s>>>(arena, offs, lens, gstart, groups, n, items, cvs,
-                                          d_digests, d_bad);
-  const uint32_t gr = (uint32_t)std::min<uint64_t>(n, 256 * 4);
-  sd_b3_batch_reduce<<<gr, GROUP, 0, s>>>(gstart, groups, n, items, cvs, d_digests);
+  sd_b3_batch_owner<<<(uint32_t)std::min<uint64_t>((items + 255) / 256, 2048), 256, 0, s>>>(
+      gstart, groups, n, items, owner);
+  // small buffers: <= 16 chunks four per wave, 17..64 chunks one per wave (up to 8
+  // workgroups of 4 waves per CU)
+  sd_b3_batch_small16<<<(uint32_t)std::min<uint64_t>((n + 15) / 16, 256 * 8), 256, 0, s>>>(
+      arena, offs, lens, n, d_digests);
+  sd_b3_batch_small64<<<(uint32_t)std::min<uint64_t>((n + 3) / 4, 256 * 8), 256, 0, s>>>(
+      arena, offs, lens, n, d_digests);
+  // big buffers: a grid of up to 65,536 workgroups strides over the item list (those past
+  // the list's end exit at once)
+  sd_b3_batch_groups<<<(uint32_t)std::min<uint64_t>(items, 65536), GROUP, 0, s>>>(
+      arena, offs, lens, gstart, groups, owner, n, items, cvs, d_digests, d_bad);
+  sd_b3_batch_reduce<<<(uint32_t)std::min<uint64_t>(n, 256 * 4), GROUP, 0, s>>>(
+      gstart, groups, n, items, cvs, d_digests);
   return hipGetLastError();
 }
 

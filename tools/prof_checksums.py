@@ -61,13 +61,26 @@ def device_batch(eng, orc, name, iters):
             want = orc.blake3(arena[o:o + L].cpu().numpy().tobytes())
         ok &= got[i].tobytes() == want
     comps = int((lens // 64).sum() + (lens // 1024).sum())
+    k3 = None
+    if n == 1:  # the single-buffer K3 chain on the same bytes, for comparison
+        L = int(lens[0])
+        t3 = []
+        for _ in range(iters):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s)
+            d3 = eng.checksum_dev(arena, L, stream=s.cuda_stream)
+            b.record(s)
+            b.synchronize()
+            t3.append(a.elapsed_time(b))
+        k3 = {"ms": float(np.median(t3)), "gb_per_s": L / (float(np.median(t3)) / 1e3) / 1e9,
+              "same_digest": d3 == got[0].tobytes().hex()}
     del arena, out
     torch.cuda.empty_cache()
     return {"shape": name, "buffers": n, "bytes": int(lens.sum()), "ms": ms,
             "ms_all": ts, "gb_per_s": float(lens.sum()) / (ms / 1e3) / 1e9,
             "buffers_per_s": n / (ms / 1e3),
             "valu_slot_frac": comps * 1014 / 64 / (ms / 1e3) / (1024 * 2.4e9 / 2),
-            "parity_sample": len(idx), "parity": bool(ok)}
+            "parity_sample": len(idx), "parity": bool(ok), "k3_same_bytes": k3}
 
 
 def paths_run(eng, orc, n, root):
