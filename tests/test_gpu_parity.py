@@ -566,6 +566,30 @@ def test_file_checksums_many_paths(eng, oracle, tmp_path):
     assert d0 == [] and len(e0) == 0
 
 
+def test_file_checksums_many_small_files(eng, oracle, tmp_path):
+    """More files than one gather window holds (32,768): 40,000 files of 0-2 KiB, split over
+    windows by file count, every digest vs the oracle."""
+    d = "/dev/shm" if os.path.isdir("/dev/shm") else str(tmp_path)
+    root = os.path.join(d, f"sdcas_many_{os.getpid()}")
+    os.makedirs(root)
+    rng = np.random.default_rng(12)
+    paths = []
+    try:
+        for i, L in enumerate(rng.integers(0, 2049, 40_000)):
+            p = os.path.join(root, f"{i}")
+            with open(p, "wb") as fh:
+                fh.write(rng.integers(0, 256, int(L), dtype=np.uint8).tobytes())
+            paths.append(p)
+        digests, errs = eng.file_checksums(paths)
+        assert not errs.any()
+        bad = [p for p, g in zip(paths, digests) if g != oracle.file_checksum(p)]
+        assert not bad, bad[:3]
+    finally:
+        for p in paths:
+            os.unlink(p)
+        os.rmdir(root)
+
+
 def test_synth_matches_oracle_generator(eng, oracle):
     n, seed = 64, 12345
     content = torch.empty((n, SAMPLED_CONTENT_LEN), dtype=torch.uint8, device="cuda")

@@ -3,7 +3,7 @@
 # sharing the one GPU of a gpurun box over gloo: correctness of the code path, not scaling.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-OUT=$R/gpurun_out/reh2
+OUT=$R/gpurun_out/${1:-reh2}
 mkdir -p $OUT
 cd $R
 export SD_BENCH_ONE_DEVICE=1
