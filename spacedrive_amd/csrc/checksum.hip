@@ -226,9 +226,10 @@ sd_b3_reduce_cvs(const uint32_t* __restrict__ in, uint64_t cnt, uint32_t* __rest
 //     counts, owner[item] = the buffer of work item `item`) that a large grid strides over:
 //       sd_b3_batch_groups: item -> its subtree CV, or the buffer's ROOT digest directly
 //         when the buffer has a single group;
-//       sd_b3_batch_reduce: the buffers with >= 2 groups: aligned blocks of 256 group CVs
-//         pair-and-promote to one CV each in LDS (a buffer of up to 65,536 groups = 64 GiB
-//         has <= 256 of them), then those to the ROOT digest — the level-wise tree of K3's
+//       sd_b3_batch_blocks + sd_b3_batch_reduce: the buffers with >= 2 groups: aligned
+//         blocks of 256 group CVs pair-and-promote to one CV each in LDS, one workgroup per
+//         block (a buffer of up to 65,536 groups = 64 GiB has <= 256 blocks), then one
+//         workgroup per buffer takes those to the ROOT digest — the level-wise tree of K3's
 //         reduce_to_one.
 constexpr uint32_t BATCH_MAX_GROUPS = GROUP * GROUP;  // 64 GiB per buffer
 constexpr uint32_t SMALL_CHUNKS = 64;                 // a wave's lanes
@@ -383,43 +384,66 @@ sd_b3_batch_groups(const uint8_t* __restrict__ arena, const uint64_t* __restrict
   }
 }
 
+// First reduce level of buffers with > 256 groups, spread over workgroups: workgroup k
+// takes the item window [256 k, 256 k + 256) and reduces every 256-CV block of such a
+// buffer that STARTS in it (block j of buffer f starts at item gstart[f] + 256 j), writing
+// the block's CV over the block's first slot (a 16 GiB buffer: 64 blocks on 64 workgroups
+// instead of one workgroup walking all 16,384 CVs, 0.38 ms).
+extern "C" __global__ void __launch_bounds__(GROUP)
+sd_b3_batch_blocks(const uint32_t* __restrict__ gstart, const uint32_t* __restrict__ groups,
+                   const uint32_t* __restrict__ owner, uint64_t n, uint64_t items_cap,
+                   uint32_t* __restrict__ cvs) {
+  __shared__ uint32_t work[GROUP][8];
+  const uint32_t t = threadIdx.x;
+  const uint64_t total = (uint64_t)gstart[n - 1] + groups[n - 1];
+  if (total > items_cap) return;
+  const uint64_t w0 = (uint64_t)blockIdx.x * GROUP;
+  if (w0 >= total) return;
+  const uint64_t w1 = w0 + GROUP < total ? w0 + GROUP : total;
+  const uint32_t f1 = owner[w1 - 1];
+  for (uint32_t f = owner[w0]; f <= f1; ++f) {  // buffers with items in the window
+    const uint32_t cnt = groups[f];
+    if (cnt <= GROUP) continue;
+    const uint64_t base = gstart[f];
+    for (uint64_t j = w0 > base ? (w0 - base + GROUP - 1) / GROUP : 0;
+         base + GROUP * j < w1 && GROUP * j < cnt; ++j) {
+      const uint32_t m = (uint32_t)min((uint64_t)GROUP, cnt - GROUP * j);
+      uint32_t* blk = cvs + 8 * (base + GROUP * j);
+      if (t < m) {
+#pragma unroll
+        for (int w = 0; w < 8; ++w) work[t][w] = blk[8 * t + w];
+      }
+      __syncthreads();
+      lds_reduce<1>(work, m, false);
+      if (t < 8) blk[t] = work[0][t];
+      __syncthreads();
+    }
+  }
+}
+
+// Per buffer with >= 2 groups: <= 256 group CVs (or, above 256 groups, the block CVs that
+// sd_b3_batch_blocks left at stride 256) pair-and-promote to the ROOT digest in LDS.
 extern "C" __global__ void __launch_bounds__(GROUP)
 sd_b3_batch_reduce(const uint32_t* __restrict__ gstart, const uint32_t* __restrict__ groups,
                    uint64_t n, uint64_t items_cap, const uint32_t* __restrict__ cvs_in,
                    uint32_t* __restrict__ digests) {
   __shared__ uint32_t work[GROUP][8];
-  __shared__ uint32_t top[GROUP][8];
   const uint32_t t = threadIdx.x;
   if ((uint64_t)gstart[n - 1] + groups[n - 1] > items_cap) return;
   for (uint64_t f = blockIdx.x; f < n; f += gridDim.x) {
     const uint32_t cnt = groups[f];
     if (cnt < 2) continue;  // uniform across the workgroup
     const uint32_t* in = cvs_in + 8 * (uint64_t)gstart[f];
-    if (cnt <= GROUP) {
-      if (t < cnt) {
+    // above 256 groups the level-1 block CVs sit at stride 256 (<= 256 of them: 64 GiB)
+    const uint32_t stride = cnt <= GROUP ? 1u : GROUP;
+    const uint32_t m = cnt <= GROUP ? cnt : (cnt + GROUP - 1) / GROUP;
+    if (t < m) {
 #pragma unroll
-        for (int w = 0; w < 8; ++w) work[t][w] = in[8 * (uint64_t)t + w];
-      }
-      __syncthreads();
-      lds_reduce<1>(work, cnt, true);
-      if (t < 8) digests[8 * f + t] = work[0][t];
-      __syncthreads();
-      continue;
+      for (int w = 0; w < 8; ++w) work[t][w] = in[8 * (uint64_t)t * stride + w];
     }
-    const uint32_t blocks = (cnt + GROUP - 1) / GROUP;  // <= GROUP (BATCH_MAX_GROUPS)
-    for (uint32_t b = 0; b < blocks; ++b) {
-      const uint32_t m = min((uint32_t)GROUP, cnt - b * GROUP);
-      if (t < m) {
-#pragma unroll
-        for (int w = 0; w < 8; ++w) work[t][w] = in[8 * ((uint64_t)b * GROUP + t) + w];
-      }
-      __syncthreads();
-      lds_reduce<1>(work, m, false);
-      if (t < 8) top[b][t] = work[0][t];
-      __syncthreads();
-    }
-    lds_reduce<1>(top, blocks, true);
-    if (t < 8) digests[8 * f + t] = top[0][t];
+    __syncthreads();
+    lds_reduce<1>(work, m, true);
+    if (t < 8) digests[8 * f + t] = work[0][t];
     __syncthreads();
   }
 }
@@ -466,6 +490,8 @@ hipError_t checksum_batch_device(const uint8_t* arena, uint64_t arena_bytes, con
   // the list's end exit at once)
   sd_b3_batch_groups<<<(uint32_t)std::min<uint64_t>(items, 65536), GROUP, 0, s>>>(
       arena, offs, lens, gstart, groups, owner, n, items, cvs, d_digests, d_bad);
+  sd_b3_batch_blocks<<<(uint32_t)((items + GROUP - 1) / GROUP), GROUP, 0, s>>>(
+      gstart, groups, owner, n, items, cvs);
   sd_b3_batch_reduce<<<(uint32_t)std::min<uint64_t>(n, 256 * 4), GROUP, 0, s>>>(
       gstart, groups, n, items, cvs, d_digests);
   return hipGetLastError();

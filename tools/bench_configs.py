@@ -283,9 +283,30 @@ def config5(eng, orc, gib: float, file_mb: int):
     for f in range(nf):
         digs.append(eng.checksum_dev(buf[f * fl:], fl))
     dtf = time.perf_counter() - t
-    ok = all(d == orc.stream_blake3_mt(5, 100 + f, fl, THREADS).hex() for f, d in enumerate(digs))
+    wants = [orc.stream_blake3_mt(5, 100 + f, fl, THREADS).hex() for f in range(nf)]
+    ok = digs == wants
     emit({"config": "5-files", "files": nf, "file_bytes": fl, "bytes": nf * fl, "seconds": dtf,
           "gb_per_s": nf * fl / dtf / 1e9, "hbm_frac": nf * fl / dtf / 8e12, "parity_full": ok})
+    # (b') the same 16 files in ONE launch chain (sd_cas_checksums_dev, K3b: the validator
+    # job's batch form), HIP events on the stream
+    import numpy as np
+    offs = torch.tensor([f * fl for f in range(nf)], dtype=torch.int64, device="cuda")
+    lens = torch.full((nf,), fl, dtype=torch.int64, device="cuda")
+    out = torch.zeros((nf, 32), dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream()
+    eng.checksums_dev(buf, offs, lens, out, stream=s.cuda_stream)
+    tb = []
+    for _ in range(3):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        eng.checksums_dev(buf, offs, lens, out, stream=s.cuda_stream)
+        b.record(s)
+        b.synchronize()
+        tb.append(a.elapsed_time(b) / 1e3)
+    dtb = float(np.median(tb))
+    okb = [bytes(r).hex() for r in out.cpu().numpy()] == wants
+    emit({"config": "5-files-batch", "files": nf, "bytes": nf * fl, "seconds": dtb,
+          "gb_per_s": nf * fl / dtb / 1e9, "hbm_frac": nf * fl / dtb / 8e12, "parity_full": okb})
     del buf
     torch.cuda.empty_cache()
     # (c) streamed file_checksum through pinned staging (tmpfs file)
