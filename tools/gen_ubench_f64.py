@@ -10,6 +10,7 @@ AD = "v_add_u32 v{d}, v{d}, v90"
 DA = "v_add_f64 v[{d}:{d1}], v[{d}:{d1}], v[92:93]"
 DF = "v_fma_f64 v[{d}:{d1}], v[{d}:{d1}], v[94:95], v[92:93]"
 FA = "v_add_f32 v{d}, v{d}, v90"
+PK = "v_pack_b32_f16 v{d}, v{d}, v{d} op_sel:[1,0,0]"  # = rotr16 if it moves bits unchanged
 seqs = {
     "DA": [DA] * 12,
     "A": [A] * 12,
@@ -23,6 +24,11 @@ seqs = {
     "G f64": [DA, DA, X, A, DA, X, A, DA, DA, X, A, DA, X, A],
     # G with only c+d on FP64
     "G half": [D3, X, A, DA, X, A, D3, X, A, DA, X, A],
+    "PK": [PK] * 12,
+    "A PK": [A, PK] * 6,
+    "X PK": [X, PK] * 6,
+    # G with its rotate-by-16 as v_pack_b32_f16 (op_sel: high half first)
+    "G pk16": [D3, X, PK, AD, X, A, D3, X, A, AD, X, A],
 }
 NCH = 12
 out, names = [], []
