@@ -112,13 +112,21 @@ __device__ void part_totals_body(const uint64_t* __restrict__ keys, uint64_t n, 
   __syncthreads();
   const uint64_t lo = (uint64_t)blockIdx.x * per_block;
   const uint64_t hi = lo + per_block < n ? lo + per_block : n;
-  for (uint64_t base = lo; base < hi; base += PART_TILE) {
-    uint64_t k[ITEMS];
+  // the next trip's keys are loaded before this trip's counting atomics
+  uint64_t kn[ITEMS];
+  auto load = [&](uint64_t base) {
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
       const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
-      k[j] = i < hi ? keys[i] : 0;
+      kn[j] = i < hi ? keys[i] : 0;
     }
+  };
+  if (lo < hi) load(lo);
+  for (uint64_t base = lo; base < hi; base += PART_TILE) {
+    uint64_t k[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) k[j] = kn[j];
+    if (base + PART_TILE < hi) load(base + PART_TILE);
     if (prefill) {
 #pragma unroll
       for (int j = 0; j < ITEMS; ++j) {
@@ -285,9 +293,13 @@ __device__ void part_scatter_body(const uint64_t* __restrict__ keys, uint64_t n,
     __syncthreads();
     auto bfn = [nb](uint64_t x) { return bucket_of(x, nb); };
     for (uint64_t base = lo; base < hi; base += PART_TILE) {
-      if (base != lo) load_trip(base);
+      uint64_t kc[ITEMS];
+      uint32_t qc[ITEMS];
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) { kc[j] = k[j]; qc[j] = q[j]; }
+      if (base + PART_TILE < hi) load_trip(base + PART_TILE);  // in flight during this trip
       const uint64_t left = hi - base;
-      staged_trip<true>(k, q, left < PART_TILE ? (uint32_t)left : PART_TILE, nb, bfn, gcur, tcnt,
+      staged_trip<true>(kc, qc, left < PART_TILE ? (uint32_t)left : PART_TILE, nb, bfn, gcur, tcnt,
                         tstart, skey, spos, rbase, myfill, out_keys, out_pos);
     }
     return;
@@ -361,19 +373,31 @@ sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict_
   const uint64_t e = c + 1 < nb1 ? starts1[c + 1] : n;
   if (threadIdx.x < nb2) cnt[threadIdx.x] = 0;
   __syncthreads();
-  for (uint64_t base = s; base < e; base += PART_TILE) {
-    uint64_t k[ITEMS];
+  // one workgroup per coarse bucket (~1 per CU): each trip's loads are issued a trip ahead,
+  // so the ~12 trips of a 12.5M-key refine do not each wait out an HBM round trip
+  uint64_t kn[ITEMS];
+  uint32_t qn[ITEMS];
+  auto load = [&](uint64_t base, bool with_pos) {
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
       const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
-      k[j] = i < e ? in_keys[i] : 0;
+      kn[j] = i < e ? in_keys[i] : 0;
+      if (with_pos) qn[j] = i < e ? in_pos[i] : 0;
     }
+  };
+  if (s < e) load(s, false);
+  for (uint64_t base = s; base < e; base += PART_TILE) {
+    uint64_t k[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) k[j] = kn[j];
+    if (base + PART_TILE < e) load(base + PART_TILE, false);
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
       const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
       if (i < e) atomicAdd(&cnt[(uint32_t)((k[j] << b1) >> (64 - b2))], 1u);
     }
   }
+  if (s < e) load(s, true);  // the scatter pass's first trip, in flight during the plan
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t run = (uint32_t)s;
@@ -391,11 +415,8 @@ sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict_
     uint64_t k[ITEMS];
     uint32_t q[ITEMS];
 #pragma unroll
-    for (int j = 0; j < ITEMS; ++j) {
-      const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
-      k[j] = i < e ? in_keys[i] : 0;
-      q[j] = i < e ? in_pos[i] : 0;
-    }
+    for (int j = 0; j < ITEMS; ++j) { k[j] = kn[j]; q[j] = qn[j]; }
+    if (base + PART_TILE < e) load(base + PART_TILE, true);
     const uint64_t left = e - base;
     staged_trip<false>(k, q, left < PART_TILE ? (uint32_t)left : PART_TILE, nb2, bfn, gcur, tcnt,
                        tstart, skey, spos, nullptr, nullptr, out_keys, out_pos);
@@ -496,7 +517,7 @@ __device__ __forceinline__ uint64_t g_find(const uint64_t* tk, uint64_t cap, uin
 // ms), slower for the 4,096-slot ones (12.5M keys: 0.369 -> 0.398 ms; A/B in
 // profiles/r02_group_ab.log), so only sd_bucket_min_big keeps it.
 template <uint32_t TBL, int THREADS, bool KEEP_SLOT>
-__device__ __forceinline__ void bucket_min(const uint64_t* __restrict__ pkeys,
+__device__ __forceinline__ void bucket_min(uint32_t bucket, const uint64_t* __restrict__ pkeys,
                                            const uint32_t* __restrict__ ppos,
                                            const uint32_t* __restrict__ vals,
                                            const uint32_t* __restrict__ starts, uint32_t nb,
@@ -513,7 +534,7 @@ __device__ __forceinline__ void bucket_min(const uint64_t* __restrict__ pkeys,
   // single flag could be raised by a fast wave's trip-(t+1) insert while a slower wave was
   // still reading it for trip t+1, splitting the waves over different barriers
   __shared__ int ovf[2];
-  const uint32_t b = blockIdx.x;
+  const uint32_t b = bucket;
   const uint64_t s = starts[b];
   const uint64_t e = b + 1 < nb ? starts[b + 1] : n;
   if (s == e) return;  // uniform for the whole workgroup
@@ -616,7 +637,8 @@ sd_bucket_min(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ p
               uint32_t bits, uint64_t n, uint32_t* __restrict__ out,
               unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
               uint32_t* __restrict__ gvals) {
-  bucket_min<TABLE, MIN_THREADS, false>(pkeys, ppos, vals, starts, nb, bits, n, out, objects, gkeys, gvals);
+  bucket_min<TABLE, MIN_THREADS, false>(blockIdx.x, pkeys, ppos, vals, starts, nb, bits, n, out,
+                                        objects, gkeys, gvals);
 }
 
 // Small batches (<= BIG_MAX_KEYS): the 2^8 coarse buckets of the first partition level
@@ -630,8 +652,8 @@ sd_bucket_min_big(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict
                   uint32_t nb, uint32_t bits, uint64_t n, uint32_t* __restrict__ out,
                   unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
                   uint32_t* __restrict__ gvals) {
-  bucket_min<BIG_TABLE, BIG_THREADS, true>(pkeys, ppos, vals, starts, nb, bits, n, out, objects, gkeys,
-                                     gvals);
+  bucket_min<BIG_TABLE, BIG_THREADS, true>(blockIdx.x, pkeys, ppos, vals, starts, nb, bits, n, out,
+                                           objects, gkeys, gvals);
 }
 
 }  // namespace sdcas
@@ -765,6 +787,9 @@ hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n
     sd_bucket_min_big<<<g.nb(), BIG_THREADS, 0, s>>>(fk, fp, vals, fstarts, g.nb(), g.b1, n, out,
                                                      (unsigned long long*)d_objects, gkeys, gvals);
   else
+    // one workgroup per fine bucket: a persistent grid walking the buckets (with or without
+    // the next bucket's first trip prefetched) was 2-10 % slower
+    // (profiles/r02b_bucket_min_persist_ab.log)
     sd_bucket_min<<<g.nb(), MIN_THREADS, 0, s>>>(fk, fp, vals, fstarts, g.nb(), g.b1 + g.b2, n, out,
                                                  (unsigned long long*)d_objects, gkeys, gvals);
   return hipGetLastError();
