@@ -1198,9 +1198,12 @@ int sd_cas_file_checksums(sd_cas_ctx* c, const char* const* paths, size_t n, cha
     members[b].clear();
   };
   bool pending[2] = {false, false};
-  HIP_TRY(c, sd_ws_acquire(c, s));
   uint32_t* d_bad = (uint32_t*)(c->d_scalar + 6);
-  HIP_TRY(c, hipMemsetAsync(d_bad, 0, 4, s));
+  {
+    hipError_t e = sd_ws_acquire(c, s);
+    if (e == hipSuccess) e = hipMemsetAsync(d_bad, 0, 4, s);
+    if (e != hipSuccess) rc = fail(c, SD_CAS_EHIP, "file_checksums: %s", hipGetErrorString(e));
+  }
   for (size_t w = 0; w < nw && rc == SD_CAS_OK; w++) {
     const int b = (int)(w & 1);
     if (pending[b]) {  // slot b's previous window: copied, hashed and its digests back
