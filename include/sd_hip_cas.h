@@ -323,7 +323,7 @@ int sd_cas_file_checksum(sd_cas_ctx* ctx, const char* path, char out_hex[65], in
  * (16-B aligned), d_lens[i] bytes (<= 64 GiB), readable to the 16-B round-up; every buffer
  * ends within arena_bytes of d_arena (sizes the workspace: one 32-B CV per 1 MiB subtree).
  * d_out[32 i .. 32 i + 32) = the digest of buffer i (device).  n <= 2^24.  Blocking;
- * SD_CAS_EINVAL when a length breaks those bounds. */
+ * SD_CAS_EINVAL when a buffer breaks those bounds (it is then not read). */
 int sd_cas_checksums_dev(sd_cas_ctx* ctx, const void* d_arena, uint64_t arena_bytes,
                          const uint64_t* d_offs, const uint64_t* d_lens, size_t n, uint8_t* d_out,
                          void* stream);

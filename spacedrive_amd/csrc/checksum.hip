@@ -237,17 +237,24 @@ constexpr uint64_t BATCH_MAX_LEN = (uint64_t)BATCH_MAX_GROUPS * GROUP_CHUNKS * 1
 
 __device__ __forceinline__ uint64_t chunks_of(uint64_t len) { return len == 0 ? 1 : (len + 1023) >> 10; }
 
-// per-buffer group counts for the big-buffer work list (0 for small buffers)
+// A buffer is hashed only if it is 16-B aligned and ends within the arena (a bad offset or
+// length is reported, not read out of bounds).
+__device__ __forceinline__ bool buffer_ok(uint64_t off, uint64_t len, uint64_t arena_bytes) {
+  return (off & 15) == 0 && len <= arena_bytes && off <= arena_bytes - len && len <= BATCH_MAX_LEN;
+}
+
+// per-buffer group counts for the big-buffer work list (0 for small and for rejected
+// buffers); *bad |= 1 for a buffer over 64 GiB, 4 for one outside the arena or misaligned
 extern "C" __global__ void __launch_bounds__(256)
-sd_b3_batch_count(const uint64_t* __restrict__ lens, uint64_t n, uint32_t* __restrict__ groups,
-                  uint32_t* __restrict__ bad) {
+sd_b3_batch_count(const uint64_t* __restrict__ offs, const uint64_t* __restrict__ lens, uint64_t n,
+                  uint64_t arena_bytes, uint32_t* __restrict__ groups, uint32_t* __restrict__ bad) {
   const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= n) return;
   const uint64_t len = lens[f];
   const uint64_t nch = chunks_of(len);
-  if (len > BATCH_MAX_LEN) atomicOr(bad, 1u);
-  groups[f] = nch <= SMALL_CHUNKS || len > BATCH_MAX_LEN
-                  ? 0u : (uint32_t)((nch + GROUP_CHUNKS - 1) / GROUP_CHUNKS);
+  const bool ok = buffer_ok(offs[f], len, arena_bytes);
+  if (!ok) atomicOr(bad, len > BATCH_MAX_LEN ? 1u : 4u);
+  groups[f] = nch <= SMALL_CHUNKS || !ok ? 0u : (uint32_t)((nch + GROUP_CHUNKS - 1) / GROUP_CHUNKS);
 }
 
 // owner[item] = the last f with gstart[f] <= item (every listed buffer owns >= 1 item)
@@ -280,6 +287,7 @@ __device__ __forceinline__ void wave_sync() {
 // whole wave in step (segments whose tree is done idle through the rest).
 template <uint32_t SEG>
 __device__ __forceinline__ void batch_small_body(const uint8_t* __restrict__ arena,
+                                                 uint64_t arena_bytes,
                                                  const uint64_t* __restrict__ offs,
                                                  const uint64_t* __restrict__ lens, uint64_t n,
                                                  uint32_t* __restrict__ digests,
@@ -294,7 +302,7 @@ __device__ __forceinline__ void batch_small_body(const uint8_t* __restrict__ are
     const uint64_t f = base + seg;
     const uint64_t len = f < n ? lens[f] : 0;
     const uint64_t nch = chunks_of(len);
-    const bool mine_class = f < n && nch > LOW && nch <= SEG;
+    const bool mine_class = f < n && nch > LOW && nch <= SEG && buffer_ok(offs[f], len, arena_bytes);
     const uint32_t count = mine_class ? (uint32_t)nch : 0u;
     if (sl < count) {
       const uint64_t off = (uint64_t)sl << 10;
@@ -342,17 +350,19 @@ __device__ __forceinline__ void batch_small_body(const uint8_t* __restrict__ are
 }
 
 extern "C" __global__ void __launch_bounds__(256)
-sd_b3_batch_small16(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
-                    const uint64_t* __restrict__ lens, uint64_t n, uint32_t* __restrict__ digests) {
+sd_b3_batch_small16(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                    const uint64_t* __restrict__ offs, const uint64_t* __restrict__ lens, uint64_t n,
+                    uint32_t* __restrict__ digests) {
   __shared__ uint32_t cvs[4 * 64][8];
-  batch_small_body<16>(arena, offs, lens, n, digests, cvs);
+  batch_small_body<16>(arena, arena_bytes, offs, lens, n, digests, cvs);
 }
 
 extern "C" __global__ void __launch_bounds__(256)
-sd_b3_batch_small64(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
-                    const uint64_t* __restrict__ lens, uint64_t n, uint32_t* __restrict__ digests) {
+sd_b3_batch_small64(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                    const uint64_t* __restrict__ offs, const uint64_t* __restrict__ lens, uint64_t n,
+                    uint32_t* __restrict__ digests) {
   __shared__ uint32_t cvs[4 * 64][8];
-  batch_small_body<64>(arena, offs, lens, n, digests, cvs);
+  batch_small_body<64>(arena, arena_bytes, offs, lens, n, digests, cvs);
 }
 
 // A large grid (up to 65,536 workgroups: far more than are resident) strides over the work
@@ -475,7 +485,7 @@ hipError_t checksum_batch_device(const uint8_t* arena, uint64_t arena_bytes, con
   uint32_t* owner = (uint32_t*)p; p += al256c(items * 4);
   uint32_t* cvs = (uint32_t*)p;
   const uint32_t nb = (uint32_t)((n + 255) / 256);
-  sd_b3_batch_count<<<nb, 256, 0, s>>>(lens, n, groups, d_bad);
+  sd_b3_batch_count<<<nb, 256, 0, s>>>(offs, lens, n, arena_bytes, groups, d_bad);
   hipError_t e = exclusive_scan_u32(groups, gstart, n, partial, s);
   if (e != hipSuccess) return e;
   sd_b3_batch_owner<<<(uint32_t)std::min<uint64_t>((items + 255) / 256, 2048), 256, 0, s>>>(
@@ -483,9 +493,9 @@ hipError_t checksum_batch_device(const uint8_t* arena, uint64_t arena_bytes, con
   // small buffers: <= 16 chunks four per wave, 17..64 chunks one per wave (up to 8
   // workgroups of 4 waves per CU)
   sd_b3_batch_small16<<<(uint32_t)std::min<uint64_t>((n + 15) / 16, 256 * 8), 256, 0, s>>>(
-      arena, offs, lens, n, d_digests);
+      arena, arena_bytes, offs, lens, n, d_digests);
   sd_b3_batch_small64<<<(uint32_t)std::min<uint64_t>((n + 3) / 4, 256 * 8), 256, 0, s>>>(
-      arena, offs, lens, n, d_digests);
+      arena, arena_bytes, offs, lens, n, d_digests);
   // big buffers: a grid of up to 65,536 workgroups strides over the item list (those past
   // the list's end exit at once)
   sd_b3_batch_groups<<<(uint32_t)std::min<uint64_t>(items, 65536), GROUP, 0, s>>>(

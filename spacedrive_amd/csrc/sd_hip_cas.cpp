@@ -1121,7 +1121,9 @@ int sd_cas_checksums_dev(sd_cas_ctx* c, const void* d_arena, uint64_t arena_byte
   HIP_TRY(c, hipStreamSynchronize(s));
   if (bad)
     return fail(c, SD_CAS_EINVAL, "checksums: %s",
-                (bad & 1) ? "a buffer is longer than 64 GiB" : "buffers extend past arena_bytes");
+                (bad & 1) ? "a buffer is longer than 64 GiB"
+                          : (bad & 4) ? "a buffer is misaligned or extends past arena_bytes"
+                                      : "the buffers' subtrees exceed arena_bytes' bound (overlapping buffers?)");
   return SD_CAS_OK;
 }
 

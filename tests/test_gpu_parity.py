@@ -534,10 +534,17 @@ def test_checksums_batch_dev_vs_oracle(eng, oracle):
     for i, L in enumerate(lens):
         want = oracle.blake3(host[int(offs[i]):int(offs[i]) + L].tobytes())
         assert got[i].tobytes() == want, (i, L)
-    # lengths past arena_bytes are refused, not hashed out of bounds
+    # buffers past arena_bytes or misaligned are refused, not read out of bounds
     with pytest.raises(Exception):
         eng.checksums_dev(arena, dev64(offs), dev64(np.array(lens, dtype=np.uint64)), out,
                           arena_bytes=1 << 20)
+    bad_offs = offs.copy()
+    bad_offs[3] += 8
+    with pytest.raises(Exception):
+        eng.checksums_dev(arena, dev64(bad_offs), dev64(np.array(lens, dtype=np.uint64)), out)
+    # a valid call on the same context still works afterwards
+    eng.checksums_dev(arena, dev64(offs), dev64(np.array(lens, dtype=np.uint64)), out)
+    assert (out.cpu().numpy() == got).all()
 
 
 def test_file_checksums_many_paths(eng, oracle, tmp_path):
