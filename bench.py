@@ -242,6 +242,22 @@ def main() -> None:
             gts.append(a.elapsed_time(b))
         group_ms = float(np.median(gts))
 
+    # the N > 1 exchange alone (partition + fixed-capacity all-to-all + grouping of the
+    # received keys + mirror all-to-all), serially after the timed region, max over ranks
+    exchange_ms = None
+    if sharded:
+        xs = []
+        for _ in range(3):
+            dist.barrier()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            sharded_group(last_keys, file0, ops, capacity=capacity)
+            torch.cuda.synchronize()
+            xs.append(time.perf_counter() - t1)
+        xt = torch.tensor([float(np.median(xs)) * 1e3], dtype=torch.float64, device=dev)
+        dist.all_reduce(xt, op=dist.ReduceOp.MAX)
+        exchange_ms = float(xt.item())
+
     # sustained: the same pipelined steps back to back (DVFS-settled; long enough for an
     # outside utilisation sampler to see the GPU busy), after the headline timed region
     sustained = None
@@ -314,7 +330,11 @@ def main() -> None:
                 "objects": objects,
                 "exchange": None if not sharded else {
                     "capacity_per_peer": capacity[0], "spill_per_peer": capacity[1],
-                    "host_syncs_per_step": 0, "timed_steps_overflowed": n_overflow},
+                    "host_syncs_per_step": 0, "timed_steps_overflowed": n_overflow,
+                    "serial_ms": exchange_ms,
+                    "serial_ms_note": "one step's exchange + grouping alone (max over ranks, "
+                                      "after the timed region); inside the steps it overlaps "
+                                      "the next K1 on a side stream"},
             },
             "roofline": {
                 # achieved = files x 953 compressions x 792 spec int32 ops /
