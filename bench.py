@@ -230,8 +230,12 @@ def main() -> None:
         objects = res.objects
     # the grouping alone (after the timed region: inside the steps it overlaps the next K1
     # on a side stream and shares the CUs with it, so its own speed is measured serially)
-    group_ms = None
+    group_ms = group_ms_sync = None
     if not sharded:
+        # (a) each call synchronised: includes the host's enqueue latency of its 4-5 launches
+        # (the GPU idles ~4 us between the first two: profiles/r02b_group_chain_trace.txt);
+        # (b) 10 calls back to back: the GPU time per grouping as the pipelined steps see it,
+        # where the chain is enqueued ahead behind the hashing
         gts = []
         for _ in range(5):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -240,7 +244,17 @@ def main() -> None:
             b.record(main)
             b.synchronize()
             gts.append(a.elapsed_time(b))
-        group_ms = float(np.median(gts))
+        group_ms_sync = float(np.median(gts))
+        gb = []
+        for _ in range(3):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(main)
+            for _ in range(10):
+                eng.group(last_keys, rep, want_objects=False)
+            b.record(main)
+            b.synchronize()
+            gb.append(a.elapsed_time(b) / 10)
+        group_ms = float(np.median(gb))
 
     # the N > 1 exchange alone (partition + fixed-capacity all-to-all + grouping of the
     # received keys + mirror all-to-all), serially after the timed region, max over ranks
@@ -374,8 +388,9 @@ def main() -> None:
             "e2e": e2e,
             "group": None if group_ms is None else {
                 # Object grouping of one step's keys alone (K4h partition + K5h LDS hash
-                # min), HIP events around it on the stream it runs on, after the timed region
-                "ms": group_ms, "keys": F,
+                # min), HIP events on the stream it runs on, after the timed region: `ms` per
+                # call over 10 back-to-back calls, `ms_each_synced` one call at a time
+                "ms": group_ms, "ms_each_synced": group_ms_sync, "keys": F,
                 "algorithmic_bytes_per_key": group_bytes_per_key(F),
                 "achieved_gb_s": F * group_bytes_per_key(F) / (group_ms / 1e3) / 1e9,
                 "hbm_frac": F * group_bytes_per_key(F) / (group_ms / 1e3) / 1e9 / HBM_PEAK_GBS,

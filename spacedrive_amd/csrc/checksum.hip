@@ -458,6 +458,18 @@ sd_b3_batch_reduce(const uint32_t* __restrict__ gstart, const uint32_t* __restri
   }
 }
 
+// one buffer at offset 0 (sd_cas_checksum_dev): its offs/lens words and the flag, in one
+// tiny kernel rather than three runtime fills
+extern "C" __global__ void sd_b3_single_setup(uint64_t* __restrict__ ol, uint64_t len,
+                                              uint32_t* __restrict__ bad) {
+  if (threadIdx.x == 0) { ol[0] = 0; ol[1] = len; *bad = 0; }
+}
+
+hipError_t checksum_single_setup(uint64_t* d_ol, uint64_t len, uint32_t* d_bad, hipStream_t s) {
+  sd_b3_single_setup<<<1, 64, 0, s>>>(d_ol, len, d_bad);
+  return hipGetLastError();
+}
+
 static inline size_t al256c(size_t x) { return (x + 255) / 256 * 256; }
 
 // work items of the big-buffer list: <= n + arena_bytes / 1 MiB (disjoint buffers)

@@ -24,6 +24,8 @@ hipError_t reduce_cvs_device(const uint32_t* d_cvs, uint64_t cnt, uint32_t* d_ou
 // arena_bytes bounds every buffer's end (sizes the CV list); a buffer over 64 GiB sets *d_bad.
 // n <= 2^24.  ws: checksum_batch_workspace_bytes(n, arena_bytes).
 size_t checksum_batch_workspace_bytes(uint64_t n, uint64_t arena_bytes);
+// d_ol[0] = 0, d_ol[1] = len, *d_bad = 0 (the one-buffer batch of sd_cas_checksum_dev)
+hipError_t checksum_single_setup(uint64_t* d_ol, uint64_t len, uint32_t* d_bad, hipStream_t s);
 hipError_t checksum_batch_device(const uint8_t* arena, uint64_t arena_bytes, const uint64_t* offs,
                                  const uint64_t* lens, uint64_t n, uint32_t* d_digests,
                                  uint32_t* d_bad, void* ws, hipStream_t s);

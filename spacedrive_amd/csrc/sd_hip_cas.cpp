@@ -931,9 +931,7 @@ int sd_cas_checksum_dev(sd_cas_ctx* c, const void* d_data, uint64_t len, uint8_t
   HIP_TRY(c, sd_ws_acquire(c, s));
   if (batch) {
     uint64_t* d_ol = c->d_scalar + 4;
-    HIP_TRY(c, hipMemsetAsync(d_ol, 0, 16, s));
-    HIP_TRY(c, hipMemsetD32Async((hipDeviceptr_t)(d_ol + 1), (int)(uint32_t)len, 1, s));
-    HIP_TRY(c, hipMemsetD32Async((hipDeviceptr_t)((uint32_t*)(d_ol + 1) + 1), (int)(uint32_t)(len >> 32), 1, s));
+    HIP_TRY(c, checksum_single_setup(d_ol, len, (uint32_t*)(c->d_scalar + 6), s));
     HIP_TRY(c, checksum_batch_device((const uint8_t*)d_data, len, d_ol, d_ol + 1, 1, d_out,
                                      (uint32_t*)(c->d_scalar + 6), c->ws.p, s));
   } else {
