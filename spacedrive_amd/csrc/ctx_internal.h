@@ -87,6 +87,9 @@ struct sd_cas_ctx {
   void* pinned = nullptr;
   size_t pinned_bytes = 0;
   uint64_t* d_scalar = nullptr;  // 8 x u64 scratch for counters
+  // the hash grouping's bucket totals: zero between calls (each call's last kernel re-zeroes
+  // them), so the chain has no zeroing launch; ordered across streams like ws
+  uint32_t* gtotals = nullptr;
   // ws and d_scalar are shared by every device call of the context, whatever stream the
   // caller passes: the last enqueued use is recorded here and a use on another stream
   // waits for it first (sd_ws_acquire / sd_ws_release)

@@ -517,7 +517,9 @@ __device__ __forceinline__ uint64_t g_find(const uint64_t* tk, uint64_t cap, uin
 // ms), slower for the 4,096-slot ones (12.5M keys: 0.369 -> 0.398 ms; A/B in
 // profiles/r02_group_ab.log), so only sd_bucket_min_big keeps it.
 template <uint32_t TBL, int THREADS, bool KEEP_SLOT>
-__device__ __forceinline__ void bucket_min(uint32_t bucket, const uint64_t* __restrict__ pkeys,
+__device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict__ rezero,
+                                           uint32_t rezero_words,
+                                           const uint64_t* __restrict__ pkeys,
                                            const uint32_t* __restrict__ ppos,
                                            const uint32_t* __restrict__ vals,
                                            const uint32_t* __restrict__ starts, uint32_t nb,
@@ -535,6 +537,10 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, const uint64_t* __re
   // still reading it for trip t+1, splitting the waves over different barriers
   __shared__ int ovf[2];
   const uint32_t b = bucket;
+  // the chain's bucket totals were last read by the scatter: zero them for the next call
+  // (the persistent buffer's invariant, see hash_group_min)
+  if (bucket == 0)
+    for (uint32_t i = threadIdx.x; i < rezero_words; i += THREADS) rezero[i] = 0;
   const uint64_t s = starts[b];
   const uint64_t e = b + 1 < nb ? starts[b + 1] : n;
   if (s == e) return;  // uniform for the whole workgroup
@@ -636,9 +642,9 @@ sd_bucket_min(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ p
               const uint32_t* __restrict__ vals, const uint32_t* __restrict__ starts, uint32_t nb,
               uint32_t bits, uint64_t n, uint32_t* __restrict__ out,
               unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
-              uint32_t* __restrict__ gvals) {
-  bucket_min<TABLE, MIN_THREADS, false>(blockIdx.x, pkeys, ppos, vals, starts, nb, bits, n, out,
-                                        objects, gkeys, gvals);
+              uint32_t* __restrict__ gvals, uint32_t* __restrict__ rezero, uint32_t rezero_words) {
+  bucket_min<TABLE, MIN_THREADS, false>(blockIdx.x, rezero, rezero_words, pkeys, ppos, vals, starts,
+                                        nb, bits, n, out, objects, gkeys, gvals);
 }
 
 // Small batches (<= BIG_MAX_KEYS): the 2^8 coarse buckets of the first partition level
@@ -651,9 +657,10 @@ sd_bucket_min_big(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict
                   const uint32_t* __restrict__ vals, const uint32_t* __restrict__ starts,
                   uint32_t nb, uint32_t bits, uint64_t n, uint32_t* __restrict__ out,
                   unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
-                  uint32_t* __restrict__ gvals) {
-  bucket_min<BIG_TABLE, BIG_THREADS, true>(blockIdx.x, pkeys, ppos, vals, starts, nb, bits, n, out,
-                                           objects, gkeys, gvals);
+                  uint32_t* __restrict__ gvals, uint32_t* __restrict__ rezero,
+                  uint32_t rezero_words) {
+  bucket_min<BIG_TABLE, BIG_THREADS, true>(blockIdx.x, rezero, rezero_words, pkeys, ppos, vals,
+                                           starts, nb, bits, n, out, objects, gkeys, gvals);
 }
 
 }  // namespace sdcas
@@ -715,12 +722,12 @@ bool hash_group_supported(uint64_t n) {
 
 static uint32_t totals_repl(uint32_t nb) { return nb <= STAGED_MAX_NB ? TOTALS_REPL : 1; }
 
-// workspace: k1 | p1 | k2 | p2 | totals (repl copies) | fill (repl copies) | starts1 | starts |
-// overflow tables
+// workspace: k1 | p1 | k2 | p2 | fill (repl copies) | starts1 | starts | overflow tables (the
+// bucket totals live in a persistent buffer of the caller, GROUP_TOTALS_WORDS)
 size_t hash_group_workspace_bytes(uint64_t n, uint64_t target) {
   const GroupPlan g = group_plan(n, target);
   const size_t nb1 = g.l1.nb;
-  return 2 * (al256(n * 8) + al256(n * 4)) + 2 * al256(totals_repl(nb1) * nb1 * 4) +
+  return 2 * (al256(n * 8) + al256(n * 4)) + al256(totals_repl(nb1) * nb1 * 4) +
          al256(nb1 * 4) + al256((size_t)g.nb() * 4) + al256(2 * n * 8) + al256(2 * n * 4);
 }
 
@@ -737,15 +744,17 @@ sd_zero_words(uint32_t* __restrict__ p, uint32_t n) {
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) p[i] = 0;
 }
 
-// totals (zeroed here) -> bucket-contiguous (out_keys, out_pos); starts_out / counts_out
+// totals (zeroed here unless the caller guarantees them zero) -> bucket-contiguous
+// (out_keys, out_pos); starts_out / counts_out
 static hipError_t run_partition(const uint64_t* keys, uint64_t n, const PartPlan& p, int mode,
                                 uint64_t* out_keys, uint32_t* out_pos, uint32_t* totals,
-                                uint32_t* fill, uint32_t* starts_out, uint64_t* counts_out,
-                                unsigned long long* objects, hipStream_t s,
+                                bool totals_zero, uint32_t* fill, uint32_t* starts_out,
+                                uint64_t* counts_out, unsigned long long* objects, hipStream_t s,
                                 const uint32_t* vals = nullptr, uint32_t* prefill = nullptr) {
   const uint32_t repl = totals_repl(p.nb);
   const uint32_t words = repl * p.nb;
-  sd_zero_words<<<(words + 255) / 256 < 64 ? (words + 255) / 256 : 64, 256, 0, s>>>(totals, words);
+  if (!totals_zero)
+    sd_zero_words<<<(words + 255) / 256 < 64 ? (words + 255) / 256 : 64, 256, 0, s>>>(totals, words);
   const size_t lds = (size_t)p.nb * 4, slds = scatter_lds_bytes(p.nb);
   if (mode == 0) {
     sd_part_totals_mix<<<p.nblk, PART_THREADS, lds, s>>>(keys, n, p.nb, p.per_block, totals, repl,
@@ -761,8 +770,13 @@ static hipError_t run_partition(const uint64_t* keys, uint64_t n, const PartPlan
   return hipGetLastError();
 }
 
+// `totals` = the caller's persistent GROUP_TOTALS_WORDS buffer, zero on entry and left zero
+// by the chain's last kernel (the bucket tables zero it once the scatter has read it): the
+// chain needs no zeroing launch of its own (one dependent launch fewer: 1.31M keys ~0.052 ->
+// ~0.048 ms back to back)
 hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n, uint32_t* out,
-                          uint64_t* d_objects, void* ws, hipStream_t s, uint64_t target) {
+                          uint64_t* d_objects, void* ws, uint32_t* totals, hipStream_t s,
+                          uint64_t target) {
   if (n == 0) return hipMemsetAsync(d_objects, 0, 8, s);
   if (!hash_group_supported(n)) return hipErrorInvalidValue;
   const GroupPlan g = group_plan(n, target);
@@ -772,13 +786,13 @@ hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n
   uint32_t* p1 = (uint32_t*)q; q += al256(n * 4);
   uint64_t* k2 = (uint64_t*)q; q += al256(n * 8);
   uint32_t* p2 = (uint32_t*)q; q += al256(n * 4);
-  uint32_t* totals = (uint32_t*)q; q += al256(totals_repl(nb1) * nb1 * 4);
   uint32_t* fill = (uint32_t*)q; q += al256(totals_repl(nb1) * nb1 * 4);
   uint32_t* starts1 = (uint32_t*)q; q += al256(nb1 * 4);
   uint32_t* starts = (uint32_t*)q; q += al256((size_t)g.nb() * 4);
   uint64_t* gkeys = (uint64_t*)q; q += al256(2 * n * 8);
   uint32_t* gvals = (uint32_t*)q;
-  hipError_t e = run_partition(keys, n, g.l1, 0, k1, p1, totals, fill, starts1, nullptr,
+  const uint32_t twords = totals_repl((uint32_t)nb1) * (uint32_t)nb1;  // <= GROUP_TOTALS_WORDS
+  hipError_t e = run_partition(keys, n, g.l1, 0, k1, p1, totals, true, fill, starts1, nullptr,
                                (unsigned long long*)d_objects, s, vals, out);
   if (e != hipSuccess) return e;
   const uint64_t* fk = k1;
@@ -793,14 +807,18 @@ hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n
   }
   if (g.big)
     sd_bucket_min_big<<<g.nb(), BIG_THREADS, 0, s>>>(fk, fp, vals, fstarts, g.nb(), g.b1, n, out,
-                                                     (unsigned long long*)d_objects, gkeys, gvals);
+                                                     (unsigned long long*)d_objects, gkeys, gvals,
+                                                     totals, twords);
   else
     // one workgroup per fine bucket: a persistent grid walking the buckets (with or without
     // the next bucket's first trip prefetched) was 2-10 % slower
     // (profiles/r02b_bucket_min_persist_ab.log)
     sd_bucket_min<<<g.nb(), MIN_THREADS, 0, s>>>(fk, fp, vals, fstarts, g.nb(), g.b1 + g.b2, n, out,
-                                                 (unsigned long long*)d_objects, gkeys, gvals);
-  return hipGetLastError();
+                                                 (unsigned long long*)d_objects, gkeys, gvals,
+                                                 totals, twords);
+  e = hipGetLastError();
+  if (e != hipSuccess) (void)hipMemsetAsync(totals, 0, GROUP_TOTALS_WORDS * 4, s);  // restore
+  return e;
 }
 
 hipError_t partition_range(const uint64_t* keys, uint64_t n, uint32_t parts, uint64_t* out_keys,
@@ -810,7 +828,8 @@ hipError_t partition_range(const uint64_t* keys, uint64_t n, uint32_t parts, uin
   const PartPlan p = part_plan(n, parts);
   uint32_t* totals = (uint32_t*)ws;
   uint32_t* fill = (uint32_t*)((char*)ws + al256((size_t)totals_repl(parts) * parts * 4));
-  return run_partition(keys, n, p, 1, out_keys, out_pos, totals, fill, nullptr, d_counts, nullptr, s);
+  return run_partition(keys, n, p, 1, out_keys, out_pos, totals, false, fill, nullptr, d_counts,
+                       nullptr, s);
 }
 
 }  // namespace sdcas

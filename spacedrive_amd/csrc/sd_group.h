@@ -43,9 +43,13 @@ bool hash_group_supported(uint64_t n);
 size_t hash_group_workspace_bytes(uint64_t n, uint64_t target = 0);
 size_t partition_workspace_bytes(uint64_t n, uint32_t parts);
 // out[i] = min{ val(j) : keys[j] == keys[i] } with val(j) = vals ? vals[j] : j;
-// *d_objects = #distinct keys (written on the device).  n < 2^32.
+// *d_objects = #distinct keys (written on the device).  n < 2^32.  `totals`: a persistent
+// device buffer of GROUP_TOTALS_WORDS u32, all zero before the first call (every call leaves
+// it zero again); calls using it must be stream-ordered.
+constexpr uint32_t GROUP_TOTALS_WORDS = 16 * 1024;
 hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n, uint32_t* out,
-                          uint64_t* d_objects, void* ws, hipStream_t stream, uint64_t target = 0);
+                          uint64_t* d_objects, void* ws, uint32_t* totals, hipStream_t stream,
+                          uint64_t target = 0);
 // Key-range partition: part(k) = floor(k * parts / 2^64); out_keys/out_pos hold the keys and
 // their input positions part-contiguous (order inside a part unspecified), d_counts[p] the
 // part sizes.  ws: partition_workspace_bytes(n, parts).

@@ -75,7 +75,9 @@ int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
       hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->h2d_done, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ws_ev, hipEventDisableTiming) != hipSuccess ||
-      hipMalloc((void**)&c->d_scalar, 64) != hipSuccess) {
+      hipMalloc((void**)&c->d_scalar, 64) != hipSuccess ||
+      hipMalloc((void**)&c->gtotals, GROUP_TOTALS_WORDS * 4) != hipSuccess ||
+      hipMemset(c->gtotals, 0, GROUP_TOTALS_WORDS * 4) != hipSuccess) {
     sd_cas_ctx_destroy(c);
     g_ctx_create_err = "stream/event/scratch creation failed on device " + std::to_string(device);
     return SD_CAS_EHIP;
@@ -123,6 +125,7 @@ void sd_cas_ctx_destroy(sd_cas_ctx* c) {
   if (c->cvbuf.p) (void)hipFree(c->cvbuf.p);
   if (c->io.p) (void)hipFree(c->io.p);
   if (c->d_scalar) (void)hipFree(c->d_scalar);
+  if (c->gtotals) (void)hipFree(c->gtotals);
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->h2d_done) (void)hipEventDestroy(c->h2d_done);
   if (c->ws_ev) (void)hipEventDestroy(c->ws_ev);
@@ -283,7 +286,8 @@ int sd_cas_group_dev(sd_cas_ctx* c, const uint64_t* d_keys, size_t n, uint32_t* 
     int rc = ensure(c, c->ws, hash_group_workspace_bytes(n, c->group_target));
     if (rc) return rc;
     HIP_TRY(c, sd_ws_acquire(c, s));
-    HIP_TRY(c, hash_group_min(d_keys, nullptr, n, d_rep, c->d_scalar, c->ws.p, s, c->group_target));
+    HIP_TRY(c, hash_group_min(d_keys, nullptr, n, d_rep, c->d_scalar, c->ws.p, c->gtotals, s,
+                              c->group_target));
   } else {  // beyond the hash grouping's range: LSD radix sort + run heads (K4 + K5)
     int rc = ensure(c, c->ws, group_workspace_bytes(n));
     if (rc) return rc;
@@ -310,7 +314,8 @@ int sd_cas_group_min_dev(sd_cas_ctx* c, const uint64_t* d_keys, const uint32_t* 
     int rc = ensure(c, c->ws, hash_group_workspace_bytes(n, c->group_target));
     if (rc) return rc;
     HIP_TRY(c, sd_ws_acquire(c, s));
-    HIP_TRY(c, hash_group_min(d_keys, d_vals, n, d_out, c->d_scalar, c->ws.p, s, c->group_target));
+    HIP_TRY(c, hash_group_min(d_keys, d_vals, n, d_out, c->d_scalar, c->ws.p, c->gtotals, s,
+                              c->group_target));
   } else {  // beyond the hash grouping's range: stable LSD sort of (key, val) + run minima
     int rc = ensure(c, c->ws, group_min_sorted_workspace_bytes(n));
     if (rc) return rc;

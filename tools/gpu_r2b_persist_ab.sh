@@ -1,5 +1,6 @@
 #!/bin/bash
 # A/B of sd_bucket_min's grid: one workgroup per bucket (0) vs k workgroups per CU walking them.
+# (the SD_GROUP_PERSIST knob and sd_bucket_min_pf were removed after this A/B: profiles/r02b_bucket_min_persist_ab.log)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/${1:-r2b_pab}
