@@ -794,7 +794,10 @@ hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n
   const uint32_t twords = totals_repl((uint32_t)nb1) * (uint32_t)nb1;  // <= GROUP_TOTALS_WORDS
   hipError_t e = run_partition(keys, n, g.l1, 0, k1, p1, totals, true, fill, starts1, nullptr,
                                (unsigned long long*)d_objects, s, vals, out);
-  if (e != hipSuccess) return e;
+  if (e != hipSuccess) {
+    (void)hipMemsetAsync(totals, 0, GROUP_TOTALS_WORDS * 4, s);  // restore the invariant
+    return e;
+  }
   const uint64_t* fk = k1;
   const uint32_t* fp = p1;
   const uint32_t* fstarts = starts1;
