@@ -816,6 +816,8 @@ hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n
     // one workgroup per fine bucket: a persistent grid walking the buckets (with or without
     // the next bucket's first trip prefetched) was 2-10 % slower
     // (profiles/r02b_bucket_min_persist_ab.log)
+    // (2,048-slot tables in 256-lane workgroups, twice the buckets: 1.28x slower,
+    // profiles/r02b_group_small_tables_ab.log)
     sd_bucket_min<<<g.nb(), MIN_THREADS, 0, s>>>(fk, fp, vals, fstarts, g.nb(), g.b1 + g.b2, n, out,
                                                  (unsigned long long*)d_objects, gkeys, gvals,
                                                  totals, twords);
