@@ -808,6 +808,8 @@ hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n
     fp = p2;
     fstarts = starts;
   }
+  // (above 1.44M keys, refining into these big tables instead — 4,096 buckets of ~3,050 at
+  // 12.5M — was 1.13x slower: profiles/r02b_group_big_tables_ab.log)
   if (g.big)
     sd_bucket_min_big<<<g.nb(), BIG_THREADS, 0, s>>>(fk, fp, vals, fstarts, g.nb(), g.b1, n, out,
                                                      (unsigned long long*)d_objects, gkeys, gvals,
