@@ -230,7 +230,7 @@ def main() -> None:
         objects = res.objects
     # the grouping alone (after the timed region: inside the steps it overlaps the next K1
     # on a side stream and shares the CUs with it, so its own speed is measured serially)
-    group_ms = group_ms_sync = None
+    group_ms = group_ms_sync = group12_ms = group12_objects = None
     if not sharded:
         # (a) each call synchronised: includes the host's enqueue latency of its 4-5 launches
         # (the GPU idles ~4 us between the first two: profiles/r02b_group_chain_trace.txt);
@@ -255,6 +255,28 @@ def main() -> None:
             b.synchronize()
             gb.append(a.elapsed_time(b) / 10)
         group_ms = float(np.median(gb))
+        # the same grouping at one rank's share of config 4 (12.5 M keys, 30 % duplicates,
+        # two partition levels: 76 B/key), random keys generated on the device
+        g = torch.Generator(device=dev)
+        g.manual_seed(args.seed)
+        nk, nd = 12_500_000, 3_750_000
+        base = torch.randint(-2 ** 63, 2 ** 63 - 1, (nk - nd,), dtype=torch.int64, device=dev, generator=g)
+        big = torch.cat([base, base[torch.randint(0, nk - nd, (nd,), device=dev, generator=g)]])
+        big = big[torch.randperm(nk, device=dev, generator=g)]
+        rep_big = torch.empty(nk, dtype=torch.int32, device=dev)
+        eng.group(big, rep_big, want_objects=False)
+        gb = []
+        for _ in range(3):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(main)
+            for _ in range(5):
+                eng.group(big, rep_big, want_objects=False)
+            b.record(main)
+            b.synchronize()
+            gb.append(a.elapsed_time(b) / 5)
+        group12_ms = float(np.median(gb))
+        group12_objects = eng.group(big, rep_big)
+        del big, base, rep_big
 
     # the N > 1 exchange alone (partition + fixed-capacity all-to-all + grouping of the
     # received keys + mirror all-to-all), serially after the timed region, max over ranks
@@ -394,6 +416,12 @@ def main() -> None:
                 "algorithmic_bytes_per_key": group_bytes_per_key(F),
                 "achieved_gb_s": F * group_bytes_per_key(F) / (group_ms / 1e3) / 1e9,
                 "hbm_frac": F * group_bytes_per_key(F) / (group_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                "rank_share_config4": {
+                    "keys": 12_500_000, "dup_keys": 3_750_000, "objects": group12_objects,
+                    "objects_expected": 12_500_000 - 3_750_000,
+                    "ms": group12_ms, "algorithmic_bytes_per_key": group_bytes_per_key(12_500_000),
+                    "hbm_frac": 12_500_000 * group_bytes_per_key(12_500_000) / (group12_ms / 1e3)
+                                / 1e9 / HBM_PEAK_GBS},
             },
             "cpu_baseline": cpu,
         }
