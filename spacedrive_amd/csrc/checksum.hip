@@ -233,6 +233,7 @@ sd_b3_reduce_cvs(const uint32_t* __restrict__ in, uint64_t cnt, uint32_t* __rest
 //         reduce_to_one.
 constexpr uint32_t BATCH_MAX_GROUPS = GROUP * GROUP;  // 64 GiB per buffer
 constexpr uint32_t SMALL_CHUNKS = 64;                 // a wave's lanes
+constexpr uint32_t MID_CHUNKS = 256;                  // a wave's lanes x 4 chunks
 constexpr uint64_t BATCH_MAX_LEN = (uint64_t)BATCH_MAX_GROUPS * GROUP_CHUNKS * 1024;
 
 __device__ __forceinline__ uint64_t chunks_of(uint64_t len) { return len == 0 ? 1 : (len + 1023) >> 10; }
@@ -254,7 +255,7 @@ sd_b3_batch_count(const uint64_t* __restrict__ offs, const uint64_t* __restrict_
   const uint64_t nch = chunks_of(len);
   const bool ok = buffer_ok(offs[f], len, arena_bytes);
   if (!ok) atomicOr(bad, len > BATCH_MAX_LEN ? 1u : 4u);
-  groups[f] = nch <= SMALL_CHUNKS || !ok ? 0u : (uint32_t)((nch + GROUP_CHUNKS - 1) / GROUP_CHUNKS);
+  groups[f] = nch <= MID_CHUNKS || !ok ? 0u : (uint32_t)((nch + GROUP_CHUNKS - 1) / GROUP_CHUNKS);
 }
 
 // owner[item] = the last f with gstart[f] <= item (every listed buffer owns >= 1 item)
@@ -363,6 +364,88 @@ sd_b3_batch_small64(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                     uint32_t* __restrict__ digests) {
   __shared__ uint32_t cvs[4 * 64][8];
   batch_small_body<64>(arena, arena_bytes, offs, lens, n, digests, cvs);
+}
+
+// Buffers of 65..256 chunks (64-256 KiB): ONE WAVE per buffer with CPL = 2 or 4 consecutive
+// chunks per lane (lane l: chunks [l CPL, (l+1) CPL), an aligned subtree merged in registers),
+// then the lanes' subtree CVs pair-and-promote in the wave's LDS slice — level-wise over
+// aligned power-of-two groups, i.e. BLAKE3's left-balanced tree.  In a 1 MiB group
+// workgroup (the path above 256 chunks) such a buffer kept 25-100 of 256 lanes busy.
+extern "C" __global__ void __launch_bounds__(256)
+sd_b3_batch_mid(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                const uint64_t* __restrict__ offs, const uint64_t* __restrict__ lens, uint64_t n,
+                uint32_t* __restrict__ digests) {
+  __shared__ uint32_t wcv[4 * 64][8];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  uint32_t (*mine)[8] = wcv + w * 64;
+  const uint64_t waves = (uint64_t)gridDim.x * 4;
+  for (uint64_t f = (uint64_t)blockIdx.x * 4 + w; f < n; f += waves) {
+    const uint64_t len = lens[f];
+    const uint64_t nch = chunks_of(len);
+    if (nch <= SMALL_CHUNKS || nch > MID_CHUNKS || !buffer_ok(offs[f], len, arena_bytes)) continue;
+    const uint32_t cpl = nch <= 128 ? 2u : 4u;               // wave-uniform
+    const uint32_t count = (uint32_t)((nch + cpl - 1) / cpl);  // lanes holding a subtree
+    const uint8_t* data = arena + offs[f];
+    if (lane < count) {
+      uint32_t cv[8], acc[8], pend[8];
+      uint32_t have = 0;  // subtrees pending: pend (2 chunks) for cpl 4
+      for (uint32_t k = 0; k < cpl; ++k) {
+        const uint64_t c = (uint64_t)lane * cpl + k;
+        if (c >= nch) break;
+        const uint64_t off = c << 10;
+        const uint32_t clen = (uint32_t)min((uint64_t)1024, len - off);
+        chunk_cv(reinterpret_cast<const uint4*>(data + off), clen, c, false, cv);
+        if ((k & 1u) == 0) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc[q] = cv[q];
+        } else {
+          parent(acc, acc, cv, 0u);  // chunks 2j, 2j+1 -> their parent
+          if (k == 3) {
+            parent(acc, pend, acc, 0u);  // (0,1), (2,3) -> the lane's 4-chunk subtree
+            have = 0;
+          } else if (cpl == 4) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) pend[q] = acc[q];
+            have = 1;
+          }
+        }
+      }
+      // a partial last group (the buffer's end): pend (chunks 0,1) + acc (chunk 2) -> parent
+      const uint32_t got = (uint32_t)min((uint64_t)cpl, nch - (uint64_t)lane * cpl);
+      if (cpl == 4 && got == 3) parent(acc, pend, acc, 0u);
+      else if (cpl == 4 && got == 2 && have) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] = pend[q];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) mine[lane][q] = acc[q];
+    }
+    wave_sync();
+#pragma unroll 1
+    for (uint32_t c = count; c > 1;) {
+      const uint32_t pairs = c >> 1;
+      const bool odd = c & 1u;
+      uint32_t out[8];
+      if (lane < pairs) {
+        uint32_t l[8], r[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) { l[q] = mine[2 * lane][q]; r[q] = mine[2 * lane + 1][q]; }
+        parent(out, l, r, c == 2 ? (uint32_t)ROOT : 0u);
+      } else if (odd && lane == pairs) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) out[q] = mine[c - 1][q];
+      }
+      wave_sync();
+      if (lane < pairs || (odd && lane == pairs)) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) mine[lane][q] = out[q];
+      }
+      wave_sync();
+      c = pairs + (odd ? 1u : 0u);
+    }
+    if (lane < 8) digests[8 * f + lane] = mine[0][lane];
+    wave_sync();
+  }
 }
 
 // A large grid (up to 65,536 workgroups: far more than are resident) strides over the work
@@ -507,6 +590,8 @@ hipError_t checksum_batch_device(const uint8_t* arena, uint64_t arena_bytes, con
   sd_b3_batch_small16<<<(uint32_t)std::min<uint64_t>((n + 15) / 16, 256 * 8), 256, 0, s>>>(
       arena, arena_bytes, offs, lens, n, d_digests);
   sd_b3_batch_small64<<<(uint32_t)std::min<uint64_t>((n + 3) / 4, 256 * 8), 256, 0, s>>>(
+      arena, arena_bytes, offs, lens, n, d_digests);
+  sd_b3_batch_mid<<<(uint32_t)std::min<uint64_t>((n + 3) / 4, 256 * 8), 256, 0, s>>>(
       arena, arena_bytes, offs, lens, n, d_digests);
   // big buffers: a grid of up to 65,536 workgroups strides over the item list (those past
   // the list's end exit at once)
