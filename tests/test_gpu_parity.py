@@ -547,6 +547,25 @@ def test_checksums_batch_dev_vs_oracle(eng, oracle):
     assert (out.cpu().numpy() == got).all()
 
 
+def test_checksums_batch_over_64k_items(eng, oracle):
+    """Two 40 GiB buffers in one batch chain: 81,920 subtree work items, more than the
+    65,536-workgroup grid, so the groups kernel strides; 160 reduce blocks per buffer; byte
+    offsets past 2^32 — vs the oracle's tree-parallel hash of the same generated streams."""
+    L = 40 << 30
+    arena = torch.empty(2 * L + 64, dtype=torch.uint8, device="cuda")
+    for f in range(2):
+        eng.synth_stream(57, 10 + f, 0, L, arena[f * L:])
+    offs = torch.tensor([0, L], dtype=torch.int64, device="cuda")
+    lens = torch.tensor([L, L - 4096 - 5], dtype=torch.int64, device="cuda")
+    out = torch.zeros((2, 32), dtype=torch.uint8, device="cuda")
+    eng.checksums_dev(arena, offs, lens, out)
+    got = [bytes(r).hex() for r in out.cpu().numpy()]
+    assert got[0] == oracle.stream_blake3_mt(57, 10, L, ORC_THREADS).hex()
+    assert got[1] == oracle.stream_blake3_mt(57, 11, L - 4096 - 5, ORC_THREADS).hex()
+    del arena
+    torch.cuda.empty_cache()
+
+
 def test_file_checksums_many_paths(eng, oracle, tmp_path):
     """The validator job over a directory (sd_cas_file_checksums): small and empty files,
     files straddling the window and the streaming threshold, a missing path, a procfs file
