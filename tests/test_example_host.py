@@ -87,3 +87,41 @@ def test_example_job_vs_oracle_and_replay(exe, oracle, tmp_path):
         assert (x["step"] if x["step"] is not None else 0xFFFFFFFF) == step[i], i
         assert (x["object"] if x["object"] is not None else 0xFFFFFFFF) == obj[i], i
     assert [(s["total_created"], s["total_linked"]) for s in steps] == [tuple(c) for c in counts]
+
+
+VEXE = os.path.join(ROOT, "examples", "sd_validate")
+
+
+def test_validate_example_refuses_without_gpu(exe, tmp_path):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present: the GPU test covers the example")
+    (tmp_path / "a").write_bytes(b"x")
+    r = subprocess.run([VEXE, str(tmp_path)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 1 and "sd_cas_ctx_create: -5" in r.stderr
+
+
+@pytest.mark.gpu
+def test_validate_example_vs_oracle(exe, oracle, tmp_path):
+    """examples/sd_validate.c: the validator job over a directory from a compiled host —
+    one sd_cas_file_checksums call; every integrity_checksum equals the oracle's
+    file_checksum (hash.rs:11-25), an unreadable file reports errno 13."""
+    rng = np.random.default_rng(22)
+    d = tmp_path / "lib"
+    (d / "sub").mkdir(parents=True)
+    for i in range(120):
+        p = d / ("sub" if i % 4 == 0 else ".") / f"v{i:03d}"
+        L = 0 if i % 37 == 5 else int(rng.integers(1, 3_000_000 if i % 10 else 70_000_000))
+        p.write_bytes(rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+    bad = d / "v050"
+    os.chmod(bad, 0)
+    r = subprocess.run([VEXE, str(d)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    rows = [json.loads(x) for x in r.stdout.splitlines()]
+    assert [x["path"] for x in rows] == sorted(str(p) for p in d.rglob("*") if p.is_file())
+    for x in rows:
+        assert x["size"] == os.path.getsize(x["path"])
+        if not os.access(x["path"], os.R_OK):
+            assert x["integrity_checksum"] is None and x["errno"] == 13
+        else:
+            assert x["errno"] == 0 and x["integrity_checksum"] == oracle.file_checksum(x["path"]), x["path"]
