@@ -579,9 +579,12 @@ def test_file_checksums_many_paths(eng, oracle, tmp_path):
         p.write_bytes(rng.integers(0, 256, L, dtype=np.uint8).tobytes())
         paths.append(str(p))
     paths.insert(5, str(tmp_path / "missing"))
-    proc = "/proc/sys/kernel/ostype"
-    if os.path.exists(proc):
-        paths.append(proc)
+    # st_size 0 with content: /proc/sys/kernel/ostype fits its 128-B slot; /proc/filesystems
+    # (a few hundred static bytes) overflows it, which sends the file through the streaming
+    # redo path
+    for proc in ("/proc/sys/kernel/ostype", "/proc/filesystems"):
+        if os.path.exists(proc) and os.stat(proc).st_size == 0:
+            paths.append(proc)
     digests, errs = eng.file_checksums(paths)
     for p, d, e in zip(paths, digests, errs):
         if p.endswith("missing"):
