@@ -5,7 +5,9 @@ check, every iteration,
   * sd_cas_group_dev (hash grouping; every 4th iteration the forced LSD path) against the
     canonical rep from numpy's stable sort (rep[i] = smallest index with the same key),
   * sd_cas_group_min_dev with random u32 values against numpy,
-  * sd_cas_sort_pairs_dev against numpy's stable argsort.
+  * sd_cas_sort_pairs_dev against numpy's stable argsort,
+  * (--validator) sd_cas_checksums_dev over a random batch of ragged buffers of every size
+    class against the oracle's BLAKE3.
 Key patterns: uniform 64-bit, few distinct keys (hot keys), small integers (not uniform
 after any mix), bucket-sorted runs.  Prints one JSON line per iteration and a summary.
 """
@@ -59,11 +61,15 @@ def main():
     ap.add_argument("--seconds", type=float, default=180)
     ap.add_argument("--max-n", type=int, default=4_000_000)
     ap.add_argument("--seed", type=int, default=2026)
+    ap.add_argument("--validator", action="store_true",
+                    help="also stress sd_cas_checksums_dev: random batches of ragged buffers vs the oracle")
     a = ap.parse_args()
     import numpy as np
     import torch
     from spacedrive_amd import CasEngine
+    from oracle.pyoracle import Oracle
     eng = CasEngine(0)
+    orc = Oracle() if a.validator else None
     rng = np.random.default_rng(a.seed)
     t_end = time.time() + a.seconds
     it = fails = 0
@@ -93,7 +99,30 @@ def main():
         eng.sort_pairs(dk, None, ko, vo)
         order = np.argsort(keys, kind="stable")
         res["sort"] = bool((vo.cpu().numpy() == order).all())
-        ok = res["group"] and res["group_min"] and res["sort"]
+        if orc is not None:
+            # a batch of ragged buffers across every size class (<=16, 17-64, 65-256 and
+            # > 256 chunks), shuffled arena order
+            nb = int(rng.integers(1, 400))
+            cls = rng.integers(0, 4, nb)
+            hi = np.array([16 << 10, 64 << 10, 256 << 10, 3 << 20])[cls]
+            lens = (rng.random(nb) * hi).astype(np.uint64)
+            offs = np.zeros(nb, dtype=np.uint64)
+            o = 0
+            for i in rng.permutation(nb):
+                offs[i] = o
+                o += (int(lens[i]) + 15) // 16 * 16 + 16 * int(rng.integers(0, 3))
+            ab = (o + 16) // 8 * 8 + 8
+            arena = torch.empty(ab, dtype=torch.uint8, device="cuda")
+            eng.synth_stream(a.seed, it, 0, ab, arena)
+            host = arena.cpu().numpy()
+            out = torch.zeros((nb, 32), dtype=torch.uint8, device="cuda")
+            eng.checksums_dev(arena, torch.from_numpy(offs.view(np.int64)).cuda(),
+                              torch.from_numpy(lens.view(np.int64)).cuda(), out)
+            got = out.cpu().numpy()
+            res["checksums"] = all(got[i].tobytes() == orc.blake3(host[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes())
+                                   for i in range(nb))
+            res["buffers"] = nb
+        ok = res["group"] and res["group_min"] and res["sort"] and res.get("checksums", True)
         fails += 0 if ok else 1
         res["ok"] = ok
         print(json.dumps(res), flush=True)
