@@ -79,8 +79,7 @@ __device__ __forceinline__ void chunk_cv(const uint4* __restrict__ q, uint32_t c
   const uint32_t nblk = clen == 0 ? 1u : (clen + 63u) >> 6;
   set_iv(cv);
   const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-  uint4 a0, a1, a2, a3;
-  (void)z;
+  uint4 a0 = z, a1 = z, a2 = z, a3 = z;  // an empty input reads nothing (its round-up is 0 B)
   auto load = [&](uint32_t b) {
     const uint32_t o = b << 6;
     a0 = q[(o < clen) ? 4 * b : 0u];
@@ -88,7 +87,7 @@ __device__ __forceinline__ void chunk_cv(const uint4* __restrict__ q, uint32_t c
     a2 = q[(o + 32u < clen) ? 4 * b + 2 : 0u];
     a3 = q[(o + 48u < clen) ? 4 * b + 3 : 0u];
   };
-  load(0);
+  if (clen) load(0);
   for (uint32_t b = 0; b < nblk; ++b) {
     uint32_t m[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
                       a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
@@ -374,7 +373,7 @@ sd_b3_batch_small64(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
 extern "C" __global__ void __launch_bounds__(256)
 sd_b3_batch_mid(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                 const uint64_t* __restrict__ offs, const uint64_t* __restrict__ lens, uint64_t n,
-                uint32_t* __restrict__ digests) {
+                uint32_t low, uint32_t* __restrict__ digests) {
   __shared__ uint32_t wcv[4 * 64][8];
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   uint32_t (*mine)[8] = wcv + w * 64;
@@ -382,7 +381,8 @@ sd_b3_batch_mid(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
   for (uint64_t f = (uint64_t)blockIdx.x * 4 + w; f < n; f += waves) {
     const uint64_t len = lens[f];
     const uint64_t nch = chunks_of(len);
-    if (nch <= SMALL_CHUNKS || nch > MID_CHUNKS || !buffer_ok(offs[f], len, arena_bytes)) continue;
+    // this class: low < nch <= MID_CHUNKS (low = SMALL_CHUNKS, or LANE_CHUNKS with the lane path)
+    if (nch <= low || nch > MID_CHUNKS || !buffer_ok(offs[f], len, arena_bytes)) continue;
     const uint32_t cpl = nch <= 128 ? 2u : 4u;               // wave-uniform
     const uint32_t count = (uint32_t)((nch + cpl - 1) / cpl);  // lanes holding a subtree
     const uint8_t* data = arena + offs[f];
@@ -446,6 +446,201 @@ sd_b3_batch_mid(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
     if (lane < 8) digests[8 * f + lane] = mine[0][lane];
     wave_sync();
   }
+}
+
+// ---- ONE BUFFER PER LANE (batches of many small buffers) -------------------------------
+// A batch of >= LANE_MIN_BUFFERS buffers has enough of them to fill the chip one per lane,
+// K2's shape: every lane walks its own buffer (128-B line loads, one line ahead), full
+// chunks on a fixed 16-block schedule, only the last chunk generic, the CV stack's bottom
+// entry in VGPRs and the rest in an LDS column per lane.  Buffers are visited by
+// descending chunk count (one stable radix pass, sd_b3_lane_keys), so a wave's lanes share
+// their trip counts and same-count buffers keep their arena order.  The segment kernels
+// above spend lanes on the pair-and-promote levels and on buffers shorter than their
+// segment; they stay for smaller batches, where one buffer per lane would leave the chip
+// idle and the per-buffer latency is ~nch x 17 compressions instead of ~16 + log2(nch).
+#ifndef LANE_MAX_CHUNKS
+#define LANE_MAX_CHUNKS 128
+#endif
+#ifndef LANE_MIN_BUFFERS
+#define LANE_MIN_BUFFERS 65536
+#endif
+constexpr uint32_t LANE_CHUNKS = LANE_MAX_CHUNKS;
+static_assert(LANE_CHUNKS >= SMALL_CHUNKS && LANE_CHUNKS <= MID_CHUNKS &&
+                  (LANE_CHUNKS & (LANE_CHUNKS - 1)) == 0,
+              "the lane class replaces the segment kernels' classes");
+constexpr int ilog2c(uint32_t x) { return x <= 1 ? 0 : 1 + ilog2c(x >> 1); }
+// popcount(c) <= log2(LANE_CHUNKS) pending subtrees after c < LANE_CHUNKS chunks; the
+// bottom one in VGPRs: 6 x 32 B x 256 lanes = 48 KiB per workgroup for 128 chunks.
+// Occupancy is capped at 2 waves per SIMD by LANE_LDS_PAD bytes of dynamic LDS at launch
+// (80 KiB per workgroup, 2 per CU): every lane streams its own buffer, and fewer concurrent
+// streams run faster (profiles/r02b_lane_ab*: 4 waves/SIMD (64-chunk class) < 3 < 2 > 1;
+// docs 1.82 / 2.50 / 2.71 / 2.63 TB/s; a 512-lane workgroup (2 waves, 1 per CU) 2.61).
+constexpr int LANE_LDS_DEPTH = ilog2c(LANE_CHUNKS) - 1;
+constexpr int LANE_BLOCK = 256;
+constexpr size_t LANE_LDS_PAD = (80u << 10) - sizeof(uint32_t) * LANE_LDS_DEPTH * 8 * LANE_BLOCK;
+constexpr int LANE_KEY_BITS = ilog2c(LANE_CHUNKS) + 1;  // keys 0..LANE_CHUNKS
+
+struct LaneStack {
+  uint32_t (*s)[8][LANE_BLOCK];
+  uint32_t t;
+  uint32_t sp = 0;
+  uint32_t bottom[8];
+  __device__ __forceinline__ void push(const uint32_t (&cv)[8]) {
+    if (sp == 0) {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) bottom[w] = cv[w];
+    } else {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) s[sp - 1][w][t] = cv[w];
+    }
+    ++sp;
+  }
+  __device__ __forceinline__ void pop(uint32_t (&out)[8]) {
+    --sp;
+    if (sp == 0) {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) out[w] = bottom[w];
+    } else {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) out[w] = s[sp - 1][w][t];
+    }
+  }
+};
+
+// line P of the buffer (quads 8P..8P+7); all 8 quads are in bounds
+__device__ __forceinline__ void lane_line(const uint4* __restrict__ q, uint32_t P, uint4 (&buf)[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) buf[i] = q[8u * P + i];
+}
+// the same with quads at or past the 16-B round-up of len re-pointed at quad 0 (len > 0);
+// their bytes only reach the final block, which is masked
+__device__ __forceinline__ void lane_line_clamped(const uint4* __restrict__ q, uint32_t P,
+                                                  uint32_t len, uint4 (&buf)[8]) {
+  const uint32_t b0 = P << 7;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) buf[i] = q[(b0 + 16u * i < len) ? 8u * P + i : 0u];
+}
+__device__ __forceinline__ void lane_compress_line(uint32_t (&cv)[8], const uint4 (&A)[8],
+                                                   uint32_t ctr, uint32_t f0, uint32_t f1) {
+  {
+    const uint32_t m[16] = {A[0].x, A[0].y, A[0].z, A[0].w, A[1].x, A[1].y, A[1].z, A[1].w,
+                            A[2].x, A[2].y, A[2].z, A[2].w, A[3].x, A[3].y, A[3].z, A[3].w};
+    compress(cv, m, ctr, 0u, BLOCK_LEN, f0);
+  }
+  {
+    const uint32_t m[16] = {A[4].x, A[4].y, A[4].z, A[4].w, A[5].x, A[5].y, A[5].z, A[5].w,
+                            A[6].x, A[6].y, A[6].z, A[6].w, A[7].x, A[7].y, A[7].z, A[7].w};
+    compress(cv, m, ctr, 0u, BLOCK_LEN, f1);
+  }
+}
+
+// CV of full chunk c (not the buffer's last): A holds line 8c on entry and line 8(c+1)
+// (clamped: the next chunk may be the partial last one) on exit; the lines ping-pong
+// between A and B with no register moves.
+__device__ __forceinline__ void lane_full_chunk(const uint4* __restrict__ q, uint32_t len, uint32_t c,
+                                                uint32_t (&cv)[8], uint4 (&A)[8], uint4 (&B)[8]) {
+  set_iv(cv);
+#pragma unroll 1
+  for (uint32_t pp = 0; pp < 3; ++pp) {
+    const uint32_t P = 8u * c + 2u * pp;
+    lane_line(q, P + 1, B);
+    lane_compress_line(cv, A, c, pp == 0 ? (uint32_t)CHUNK_START : 0u, 0u);
+    lane_line(q, P + 2, A);
+    lane_compress_line(cv, B, c, 0u, 0u);
+  }
+  lane_line(q, 8u * c + 7u, B);
+  lane_compress_line(cv, A, c, 0u, 0u);
+  lane_line_clamped(q, 8u * c + 8u, len, A);
+  lane_compress_line(cv, B, c, 0u, CHUNK_END);
+}
+
+// BLAKE3 digest of buffer q[0, len), len <= LANE_CHUNKS KiB, into cv
+__device__ __forceinline__ void lane_digest(const uint4* __restrict__ q, uint32_t len, LaneStack& stk,
+                                            uint32_t (&cv)[8]) {
+  const uint32_t nch = len == 0 ? 1u : (len + 1023u) >> 10;
+  uint4 A[8], B[8];
+  if (len) {
+    lane_line_clamped(q, 0, len, A);
+  } else {  // an empty buffer reads nothing (its round-up is 0 bytes)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) A[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  for (uint32_t c = 0; c + 1 < nch; ++c) {
+    lane_full_chunk(q, len, c, cv, A, B);
+    for (uint32_t total = c + 1; (total & 1u) == 0u; total >>= 1) {
+      uint32_t left[8];
+      stk.pop(left);
+      parent(cv, left, cv, 0u);
+    }
+    stk.push(cv);
+  }
+  // the last chunk: per-block length, tail mask, CHUNK_END and (single chunk) ROOT
+  const uint32_t c = nch - 1;
+  const uint32_t clen = len - (c << 10);
+  const uint32_t cblocks = clen == 0 ? 1u : (clen + 63u) >> 6;
+  set_iv(cv);
+  for (uint32_t b = 0; b < cblocks; b += 2) {
+    if (b + 2 < cblocks) lane_line_clamped(q, 8u * c + (b >> 1) + 1u, len, B);
+#pragma unroll
+    for (uint32_t h = 0; h < 2; ++h) {
+      if (h == 1 && b + 1 >= cblocks) break;
+      uint32_t m[16];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint4 v = A[4 * h + i];
+        m[4 * i] = v.x; m[4 * i + 1] = v.y; m[4 * i + 2] = v.z; m[4 * i + 3] = v.w;
+      }
+      const uint32_t bo = (b + h) << 6;
+      const uint32_t blen = clen - bo < 64u ? clen - bo : 64u;  // clen > bo, or both 0
+      if (blen < 64u) {
+#pragma unroll
+        for (int w = 0; w < 16; ++w) {
+          const int vb = (int)blen - 4 * w;
+          m[w] &= vb >= 4 ? 0xFFFFFFFFu : (vb <= 0 ? 0u : ((1u << (8 * vb)) - 1u));
+        }
+      }
+      const bool end = b + h + 1 == cblocks;
+      const uint32_t f = (b + h == 0 ? (uint32_t)CHUNK_START : 0u) | (end ? (uint32_t)CHUNK_END : 0u) |
+                         (end && nch == 1 ? (uint32_t)ROOT : 0u);
+      compress(cv, m, c, 0u, blen, f);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) A[i] = B[i];
+  }
+  while (stk.sp > 0) {
+    uint32_t left[8];
+    stk.pop(left);
+    parent(cv, left, cv, stk.sp == 0 ? (uint32_t)ROOT : 0u);
+  }
+}
+
+// visiting key: descending chunk count for the lane class, LANE_CHUNKS (last) for the rest
+extern "C" __global__ void __launch_bounds__(256)
+sd_b3_lane_keys(const uint64_t* __restrict__ offs, const uint64_t* __restrict__ lens, uint64_t n,
+                uint64_t arena_bytes, uint64_t* __restrict__ keys) {
+  const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= n) return;
+  const uint64_t len = lens[f];
+  const uint64_t nch = chunks_of(len);
+  const bool mine = nch <= LANE_CHUNKS && buffer_ok(offs[f], len, arena_bytes);
+  keys[f] = mine ? LANE_CHUNKS - nch : LANE_CHUNKS;
+}
+
+extern "C" __global__ void __launch_bounds__(LANE_BLOCK)
+sd_b3_batch_lane(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                 const uint64_t* __restrict__ offs, const uint64_t* __restrict__ lens,
+                 const uint32_t* __restrict__ order, uint64_t n, uint32_t* __restrict__ digests) {
+  __shared__ uint32_t stack_lds[LANE_LDS_DEPTH][8][LANE_BLOCK];
+  const uint64_t t = (uint64_t)blockIdx.x * LANE_BLOCK + threadIdx.x;
+  if (t >= n) return;
+  const uint32_t f = order[t];
+  const uint64_t len = lens[f];
+  if (chunks_of(len) > LANE_CHUNKS || !buffer_ok(offs[f], len, arena_bytes)) return;
+  LaneStack stk{stack_lds, threadIdx.x};
+  uint32_t cv[8];
+  lane_digest(reinterpret_cast<const uint4*>(arena + offs[f]), (uint32_t)len, stk, cv);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) digests[8ull * f + k] = cv[k];
 }
 
 // A large grid (up to 65,536 workgroups: far more than are resident) strides over the work
@@ -560,11 +755,15 @@ static inline uint64_t batch_items_cap(uint64_t n, uint64_t arena_bytes) {
   return n + arena_bytes / (GROUP_CHUNKS * 1024) + 1;
 }
 
+static inline bool lane_path(uint64_t n) { return n >= LANE_MIN_BUFFERS; }
+
 size_t checksum_batch_workspace_bytes(uint64_t n, uint64_t arena_bytes) {
-  // groups | gstart | scan partials | owner | cvs
+  // groups | gstart | scan partials | owner | cvs [| lane keys | sorted keys | order | sort ws]
   const uint64_t items = batch_items_cap(n, arena_bytes);
-  return 2 * al256c((n + 1) * 4) + al256c((n / 4096 + 2) * 4) + al256c(items * 4) +
-         items * 32 + 256;
+  size_t b = 2 * al256c((n + 1) * 4) + al256c((n / 4096 + 2) * 4) + al256c(items * 4) +
+             al256c(items * 32);
+  if (lane_path(n)) b += 2 * al256c(n * 8) + al256c(n * 4) + sort_workspace_bytes(n);
+  return b + 256;
 }
 
 hipError_t checksum_batch_device(const uint8_t* arena, uint64_t arena_bytes, const uint64_t* offs,
@@ -578,21 +777,34 @@ hipError_t checksum_batch_device(const uint8_t* arena, uint64_t arena_bytes, con
   uint32_t* gstart = (uint32_t*)p; p += al256c((n + 1) * 4);
   uint32_t* partial = (uint32_t*)p; p += al256c((n / 4096 + 2) * 4);
   uint32_t* owner = (uint32_t*)p; p += al256c(items * 4);
-  uint32_t* cvs = (uint32_t*)p;
+  uint32_t* cvs = (uint32_t*)p; p += al256c(items * 32);
   const uint32_t nb = (uint32_t)((n + 255) / 256);
   sd_b3_batch_count<<<nb, 256, 0, s>>>(offs, lens, n, arena_bytes, groups, d_bad);
   hipError_t e = exclusive_scan_u32(groups, gstart, n, partial, s);
   if (e != hipSuccess) return e;
   sd_b3_batch_owner<<<(uint32_t)std::min<uint64_t>((items + 255) / 256, 2048), 256, 0, s>>>(
       gstart, groups, n, items, owner);
-  // small buffers: <= 16 chunks four per wave, 17..64 chunks one per wave (up to 8
-  // workgroups of 4 waves per CU)
-  sd_b3_batch_small16<<<(uint32_t)std::min<uint64_t>((n + 15) / 16, 256 * 8), 256, 0, s>>>(
-      arena, arena_bytes, offs, lens, n, d_digests);
-  sd_b3_batch_small64<<<(uint32_t)std::min<uint64_t>((n + 3) / 4, 256 * 8), 256, 0, s>>>(
-      arena, arena_bytes, offs, lens, n, d_digests);
+  const bool lane = lane_path(n);
+  if (lane) {
+    // buffers of <= LANE_CHUNKS chunks one per lane, by descending chunk count
+    uint64_t* lkeys = (uint64_t*)p; p += al256c(n * 8);
+    uint64_t* skeys = (uint64_t*)p; p += al256c(n * 8);
+    uint32_t* order = (uint32_t*)p; p += al256c(n * 4);
+    sd_b3_lane_keys<<<nb, 256, 0, s>>>(offs, lens, n, arena_bytes, lkeys);
+    e = radix_sort_pairs(lkeys, nullptr, skeys, order, n, 0, LANE_KEY_BITS, p, s);
+    if (e != hipSuccess) return e;
+    sd_b3_batch_lane<<<(uint32_t)((n + LANE_BLOCK - 1) / LANE_BLOCK), LANE_BLOCK, LANE_LDS_PAD, s>>>(
+        arena, arena_bytes, offs, lens, order, n, d_digests);
+  } else {
+    // small buffers: <= 16 chunks four per wave, 17..64 chunks one per wave (up to 8
+    // workgroups of 4 waves per CU)
+    sd_b3_batch_small16<<<(uint32_t)std::min<uint64_t>((n + 15) / 16, 256 * 8), 256, 0, s>>>(
+        arena, arena_bytes, offs, lens, n, d_digests);
+    sd_b3_batch_small64<<<(uint32_t)std::min<uint64_t>((n + 3) / 4, 256 * 8), 256, 0, s>>>(
+        arena, arena_bytes, offs, lens, n, d_digests);
+  }
   sd_b3_batch_mid<<<(uint32_t)std::min<uint64_t>((n + 3) / 4, 256 * 8), 256, 0, s>>>(
-      arena, arena_bytes, offs, lens, n, d_digests);
+      arena, arena_bytes, offs, lens, n, lane ? LANE_CHUNKS : SMALL_CHUNKS, d_digests);
   // big buffers: a grid of up to 65,536 workgroups strides over the item list (those past
   // the list's end exit at once)
   sd_b3_batch_groups<<<(uint32_t)std::min<uint64_t>(items, 65536), GROUP, 0, s>>>(

@@ -547,6 +547,43 @@ def test_checksums_batch_dev_vs_oracle(eng, oracle):
     assert (out.cpu().numpy() == got).all()
 
 
+def test_checksums_batch_lane_path(eng, oracle):
+    """A batch of 140,000 buffers (>= LANE_MIN_BUFFERS: buffers of <= 128 chunks one per lane,
+    sorted by chunk count): lengths at every chunk / block / quad boundary of the lane class
+    (0, 1, 15, 16, 63, 64, 1023-1025, 64 and 128 KiB +-1), 128 KiB + 1 and larger buffers in
+    the same batch (the mid and subtree kernels), an arena whose last buffer ends exactly at
+    arena_bytes, shuffled arena order — every digest vs the oracle."""
+    rng = np.random.default_rng(12)
+    edge = [0, 1, 15, 16, 17, 63, 64, 65, 127, 128, 1023, 1024, 1025, 2047, 2048, 2049,
+            (63 << 10) + 1, (64 << 10) - 1, 64 << 10, (64 << 10) + 1, (127 << 10) + 1,
+            (128 << 10) - 1, 128 << 10, (128 << 10) + 1, (200 << 10) + 3, (3 << 20) + 11]
+    n = 140_000
+    lens = rng.integers(0, 128 << 10, n).astype(np.int64)
+    lens[rng.integers(0, n, 5000)] = rng.integers(0, 1100, 5000)  # one-chunk buffers
+    lens[: len(edge)] = edge
+    lens[rng.integers(len(edge), n, 40)] = rng.integers(129 << 10, 2 << 20, 40)
+    order = rng.permutation(n)
+    offs = np.zeros(n, dtype=np.uint64)
+    o = 0
+    for i in order:
+        offs[i] = o
+        o += (int(lens[i]) + 15) // 16 * 16
+    last = int(order[-1])
+    arena_bytes = int(offs[last]) + int(lens[last])  # the last buffer ends at arena_bytes
+    arena = torch.empty(o + 16, dtype=torch.uint8, device="cuda")
+    eng.synth_stream(33, 2, 0, (o + 16) // 8 * 8, arena)
+    host = arena.cpu().numpy()
+    out = torch.zeros((n, 32), dtype=torch.uint8, device="cuda")
+    eng.checksums_dev(arena, dev64(offs), dev64(lens.astype(np.uint64)), out,
+                      arena_bytes=arena_bytes)
+    got = out.cpu().numpy()
+    bad = [i for i in range(n)
+           if got[i].tobytes() != oracle.blake3(host[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes())]
+    assert not bad, (len(bad), [(i, int(lens[i])) for i in bad[:8]])
+    del arena
+    torch.cuda.empty_cache()
+
+
 def test_checksums_batch_over_64k_items(eng, oracle):
     """Two 40 GiB buffers in one batch chain: 81,920 subtree work items, more than the
     65,536-workgroup grid, so the groups kernel strides; 160 reduce blocks per buffer; byte

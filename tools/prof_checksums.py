@@ -7,6 +7,8 @@ engine's stream; every digest of a sample checked against the oracle.  Library s
   docs    262,144 buffers of U(1, 128) KiB  (~17 GB)
   small   1,048,576 buffers of U(0, 16) KiB (~8.6 GB)
   one     one 16 GiB buffer (the K3 single-buffer chain's shape, for comparison)
+  small16k .. small256k  16,384 .. 262,144 buffers of U(0, 16) KiB (batch-size sweep)
+  docs64  262,144 buffers of U(1, 64) KiB
 Paths (--paths N): N files of U(0.25, 4) MiB on /dev/shm through sd_cas_file_checksums vs
 the oracle's file_checksum on 1 thread (hash.rs is single-threaded) and file-parallel on
 the host cores.
@@ -21,7 +23,11 @@ from concurrent.futures import ThreadPoolExecutor
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 SHAPES = {"photos": (4096, 1 << 20, 8 << 20), "docs": (262144, 1 << 10, 128 << 10),
-          "small": (1 << 20, 0, 16 << 10), "one": (1, 16 << 30, 16 << 30)}
+          "small": (1 << 20, 0, 16 << 10), "one": (1, 16 << 30, 16 << 30),
+          # batch-size sweep of the small shape (the lane-per-buffer path's crossover)
+          "small16k": (16384, 0, 16 << 10), "small32k": (32768, 0, 16 << 10),
+          "small64k": (65536, 0, 16 << 10), "small128k": (131072, 0, 16 << 10),
+          "small256k": (262144, 0, 16 << 10), "docs64": (262144, 1 << 10, 64 << 10)}
 
 
 def device_batch(eng, orc, name, iters):

@@ -7,7 +7,8 @@ check, every iteration,
   * sd_cas_group_min_dev with random u32 values against numpy,
   * sd_cas_sort_pairs_dev against numpy's stable argsort,
   * (--validator) sd_cas_checksums_dev over a random batch of ragged buffers of every size
-    class against the oracle's BLAKE3.
+    class against the oracle's BLAKE3; every 8th iteration a batch of 65,536-80,000 buffers
+    (the lane-per-buffer path, mostly <= 128 KiB).
 Key patterns: uniform 64-bit, few distinct keys (hot keys), small integers (not uniform
 after any mix), bucket-sorted runs.  Prints one JSON line per iteration and a summary.
 """
@@ -102,15 +103,16 @@ def main():
         if orc is not None:
             # a batch of ragged buffers across every size class (<=16, 17-64, 65-256 and
             # > 256 chunks), shuffled arena order
-            nb = int(rng.integers(1, 400))
-            cls = rng.integers(0, 4, nb)
-            hi = np.array([16 << 10, 64 << 10, 256 << 10, 3 << 20])[cls]
+            big = it % 8 == 7
+            nb = int(rng.integers(65536, 80000)) if big else int(rng.integers(1, 400))
+            cls = rng.choice(4, nb, p=[0.45, 0.3, 0.249, 0.001]) if big else rng.integers(0, 4, nb)
+            hi = np.array([16 << 10, 64 << 10, 128 << 10 if big else 256 << 10, 3 << 20])[cls]
             lens = (rng.random(nb) * hi).astype(np.uint64)
             offs = np.zeros(nb, dtype=np.uint64)
             o = 0
             for i in rng.permutation(nb):
                 offs[i] = o
-                o += (int(lens[i]) + 15) // 16 * 16 + 16 * int(rng.integers(0, 3))
+                o += (int(lens[i]) + 15) // 16 * 16 + (0 if big else 16 * int(rng.integers(0, 3)))
             ab = (o + 16) // 8 * 8 + 8
             arena = torch.empty(ab, dtype=torch.uint8, device="cuda")
             eng.synth_stream(a.seed, it, 0, ab, arena)
