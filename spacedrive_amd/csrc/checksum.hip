@@ -237,6 +237,54 @@ constexpr uint64_t BATCH_MAX_LEN = (uint64_t)BATCH_MAX_GROUPS * GROUP_CHUNKS * 1
 
 __device__ __forceinline__ uint64_t chunks_of(uint64_t len) { return len == 0 ? 1 : (len + 1023) >> 10; }
 
+// ---- the lane-per-buffer class (sd_b3_batch_lane below) --------------------------------
+#ifndef LANE_MAX_CHUNKS
+#define LANE_MAX_CHUNKS 128
+#endif
+#ifndef LANE_MIN_BUFFERS
+#define LANE_MIN_BUFFERS 65536
+#endif
+constexpr uint32_t LANE_CHUNKS = LANE_MAX_CHUNKS;
+static_assert(LANE_CHUNKS >= SMALL_CHUNKS && LANE_CHUNKS <= MID_CHUNKS &&
+                  (LANE_CHUNKS & (LANE_CHUNKS - 1)) == 0,
+              "the lane class replaces the segment kernels' classes");
+// The lane kernel takes the lane-class buffers of at most `cut` chunks; the segment / mid
+// kernels the rest.  A lane of c chunks runs c x 17 compressions back to back, so a few
+// long buffers in a batch of short ones would make a tail far longer than the whole
+// batch's share of the chip: cut = min(LANE_CHUNKS, LANE_TAIL x the class's total chunks /
+// LANE_SLOTS) keeps the longest lane within LANE_TAIL x the time the class needs at full
+// occupancy (LANE_SLOTS lanes: 256 CUs x 4 SIMDs x 2 waves x 64).  Measured
+// (profiles/r02b_lane_ab_pass4/): 65,536 buffers, 8 % of them 96-128 KiB: no cut 2.86 ms,
+// segment kernels only 1.07, cut 0.87; LANE_TAIL 1 and 2 split uniform batches between two
+// serial kernels (65,536 x U(0, 16) KiB: 0.70-0.77 vs 0.54 ms), 4 does not.
+#ifndef LANE_TAIL
+#define LANE_TAIL 4
+#endif
+constexpr uint64_t LANE_SLOTS = 256ull * 4 * 2 * 64;
+// With the lane path the batch is visited in one stable order by descending chunk count
+// (sd_b3_lane_keys + one radix sort): positions [0, info[1]) hold the 65..256-chunk
+// buffers, then info[2] of 17..64 chunks, then info[3] of <= 16, then the rest (over
+// MID_CHUNKS, or refused); info[0] = the lane class's chunk count.  Each segment / mid kernel
+// walks its own range of positions and stops at the first buffer the lane kernel takes.
+struct LaneInfo {
+  const uint32_t* order;  // nullptr: no lane path, positions = buffer indices
+  const uint32_t* info;
+};
+__device__ __forceinline__ uint32_t lane_cut(const uint32_t* __restrict__ info) {
+  if (!info) return 0u;
+  const uint64_t c = (uint64_t)LANE_TAIL * info[0] / LANE_SLOTS;
+  return (uint32_t)(c < LANE_CHUNKS ? c : LANE_CHUNKS);
+}
+// positions [lo, hi) of the class ending at SEG chunks (16, 64 or MID_CHUNKS)
+template <uint32_t SEG>
+__device__ __forceinline__ void lane_range(const uint32_t* __restrict__ info, uint64_t n,
+                                           uint64_t& lo, uint64_t& hi) {
+  if (!info) { lo = 0; hi = n; return; }
+  const uint64_t m = info[1], s64 = info[2], s16 = info[3];
+  lo = SEG == MID_CHUNKS ? 0 : SEG == SMALL_CHUNKS ? m : m + s64;
+  hi = SEG == MID_CHUNKS ? m : SEG == SMALL_CHUNKS ? m + s64 : m + s64 + s16;
+}
+
 // A buffer is hashed only if it is 16-B aligned and ends within the arena (a bad offset or
 // length is reported, not read out of bounds).
 __device__ __forceinline__ bool buffer_ok(uint64_t off, uint64_t len, uint64_t arena_bytes) {
@@ -247,8 +295,10 @@ __device__ __forceinline__ bool buffer_ok(uint64_t off, uint64_t len, uint64_t a
 // buffers); *bad |= 1 for a buffer over 64 GiB, 4 for one outside the arena or misaligned
 extern "C" __global__ void __launch_bounds__(256)
 sd_b3_batch_count(const uint64_t* __restrict__ offs, const uint64_t* __restrict__ lens, uint64_t n,
-                  uint64_t arena_bytes, uint32_t* __restrict__ groups, uint32_t* __restrict__ bad) {
+                  uint64_t arena_bytes, uint32_t* __restrict__ groups, uint32_t* __restrict__ bad,
+                  uint32_t* __restrict__ lane_info) {
   const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f < 4 && lane_info) lane_info[f] = 0u;  // sd_b3_lane_keys accumulates them next
   if (f >= n) return;
   const uint64_t len = lens[f];
   const uint64_t nch = chunks_of(len);
@@ -291,18 +341,24 @@ __device__ __forceinline__ void batch_small_body(const uint8_t* __restrict__ are
                                                  const uint64_t* __restrict__ offs,
                                                  const uint64_t* __restrict__ lens, uint64_t n,
                                                  uint32_t* __restrict__ digests,
-                                                 uint32_t (*cvs)[8]) {
+                                                 uint32_t (*cvs)[8], LaneInfo li) {
   constexpr uint32_t PER_WAVE = 64 / SEG;
+  const uint32_t cut = lane_cut(li.info);
+  uint64_t lo, hi;
+  lane_range<SEG>(li.info, n, lo, hi);
   constexpr uint32_t LOW = SEG == 64 ? 16 : 0;  // this class: LOW < chunks <= SEG
   const uint32_t lane = threadIdx.x & 63u, seg = lane / SEG, sl = lane % SEG;
   uint32_t (*mine)[8] = cvs + (threadIdx.x >> 6) * 64 + seg * SEG;  // the segment's slice
   const uint64_t slots = (uint64_t)gridDim.x * (blockDim.x / 64) * PER_WAVE;
   const uint64_t first = ((uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * PER_WAVE + seg;
-  for (uint64_t base = first - seg; base < n; base += slots) {  // wave-uniform trip count
-    const uint64_t f = base + seg;
+  for (uint64_t base = lo + first - seg; base < hi; base += slots) {  // wave-uniform trips
+    if (li.order && chunks_of(lens[li.order[base]]) <= cut) break;  // the wave's longest: the
+                                                                      // rest go one per lane
+    const uint64_t t = base + seg;
+    const uint64_t f = t < hi ? (li.order ? li.order[t] : t) : n;
     const uint64_t len = f < n ? lens[f] : 0;
     const uint64_t nch = chunks_of(len);
-    const bool mine_class = f < n && nch > LOW && nch <= SEG && buffer_ok(offs[f], len, arena_bytes);
+    const bool mine_class = f < n && nch > LOW && nch > cut && nch <= SEG && buffer_ok(offs[f], len, arena_bytes);
     const uint32_t count = mine_class ? (uint32_t)nch : 0u;
     if (sl < count) {
       const uint64_t off = (uint64_t)sl << 10;
@@ -352,17 +408,19 @@ __device__ __forceinline__ void batch_small_body(const uint8_t* __restrict__ are
 extern "C" __global__ void __launch_bounds__(256)
 sd_b3_batch_small16(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                     const uint64_t* __restrict__ offs, const uint64_t* __restrict__ lens, uint64_t n,
+                    const uint32_t* __restrict__ order, const uint32_t* __restrict__ lane_info,
                     uint32_t* __restrict__ digests) {
   __shared__ uint32_t cvs[4 * 64][8];
-  batch_small_body<16>(arena, arena_bytes, offs, lens, n, digests, cvs);
+  batch_small_body<16>(arena, arena_bytes, offs, lens, n, digests, cvs, LaneInfo{order, lane_info});
 }
 
 extern "C" __global__ void __launch_bounds__(256)
 sd_b3_batch_small64(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                     const uint64_t* __restrict__ offs, const uint64_t* __restrict__ lens, uint64_t n,
+                    const uint32_t* __restrict__ order, const uint32_t* __restrict__ lane_info,
                     uint32_t* __restrict__ digests) {
   __shared__ uint32_t cvs[4 * 64][8];
-  batch_small_body<64>(arena, arena_bytes, offs, lens, n, digests, cvs);
+  batch_small_body<64>(arena, arena_bytes, offs, lens, n, digests, cvs, LaneInfo{order, lane_info});
 }
 
 // Buffers of 65..256 chunks (64-256 KiB): ONE WAVE per buffer with CPL = 2 or 4 consecutive
@@ -373,16 +431,22 @@ sd_b3_batch_small64(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
 extern "C" __global__ void __launch_bounds__(256)
 sd_b3_batch_mid(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                 const uint64_t* __restrict__ offs, const uint64_t* __restrict__ lens, uint64_t n,
-                uint32_t low, uint32_t* __restrict__ digests) {
+                const uint32_t* __restrict__ order, const uint32_t* __restrict__ lane_info,
+                uint32_t* __restrict__ digests) {
   __shared__ uint32_t wcv[4 * 64][8];
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   uint32_t (*mine)[8] = wcv + w * 64;
   const uint64_t waves = (uint64_t)gridDim.x * 4;
-  for (uint64_t f = (uint64_t)blockIdx.x * 4 + w; f < n; f += waves) {
+  const uint32_t cut = lane_cut(lane_info);
+  uint64_t lo, hi;
+  lane_range<MID_CHUNKS>(lane_info, n, lo, hi);
+  for (uint64_t t = lo + (uint64_t)blockIdx.x * 4 + w; t < hi; t += waves) {
+    const uint64_t f = order ? order[t] : t;
     const uint64_t len = lens[f];
     const uint64_t nch = chunks_of(len);
-    // this class: low < nch <= MID_CHUNKS (low = SMALL_CHUNKS, or LANE_CHUNKS with the lane path)
-    if (nch <= low || nch > MID_CHUNKS || !buffer_ok(offs[f], len, arena_bytes)) continue;
+    if (order && nch <= cut) break;  // sorted: every later buffer goes one per lane
+    // this class: SMALL_CHUNKS < nch <= MID_CHUNKS, less those the lane kernel takes
+    if (nch <= SMALL_CHUNKS || nch <= cut || nch > MID_CHUNKS || !buffer_ok(offs[f], len, arena_bytes)) continue;
     const uint32_t cpl = nch <= 128 ? 2u : 4u;               // wave-uniform
     const uint32_t count = (uint32_t)((nch + cpl - 1) / cpl);  // lanes holding a subtree
     const uint8_t* data = arena + offs[f];
@@ -449,7 +513,8 @@ sd_b3_batch_mid(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
 }
 
 // ---- ONE BUFFER PER LANE (batches of many small buffers) -------------------------------
-// A batch of >= LANE_MIN_BUFFERS buffers has enough of them to fill the chip one per lane,
+// A batch of >= LANE_MIN_BUFFERS buffers has enough of them to fill the chip one per lane
+// (those of <= lane_cut() chunks: a few long buffers stay on the kernels above),
 // K2's shape: every lane walks its own buffer (128-B line loads, one line ahead), full
 // chunks on a fixed 16-block schedule, only the last chunk generic, the CV stack's bottom
 // entry in VGPRs and the rest in an LDS column per lane.  Buffers are visited by
@@ -458,16 +523,6 @@ sd_b3_batch_mid(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
 // above spend lanes on the pair-and-promote levels and on buffers shorter than their
 // segment; they stay for smaller batches, where one buffer per lane would leave the chip
 // idle and the per-buffer latency is ~nch x 17 compressions instead of ~16 + log2(nch).
-#ifndef LANE_MAX_CHUNKS
-#define LANE_MAX_CHUNKS 128
-#endif
-#ifndef LANE_MIN_BUFFERS
-#define LANE_MIN_BUFFERS 65536
-#endif
-constexpr uint32_t LANE_CHUNKS = LANE_MAX_CHUNKS;
-static_assert(LANE_CHUNKS >= SMALL_CHUNKS && LANE_CHUNKS <= MID_CHUNKS &&
-                  (LANE_CHUNKS & (LANE_CHUNKS - 1)) == 0,
-              "the lane class replaces the segment kernels' classes");
 constexpr int ilog2c(uint32_t x) { return x <= 1 ? 0 : 1 + ilog2c(x >> 1); }
 // popcount(c) <= log2(LANE_CHUNKS) pending subtrees after c < LANE_CHUNKS chunks; the
 // bottom one in VGPRs: 6 x 32 B x 256 lanes = 48 KiB per workgroup for 128 chunks.
@@ -478,7 +533,7 @@ constexpr int ilog2c(uint32_t x) { return x <= 1 ? 0 : 1 + ilog2c(x >> 1); }
 constexpr int LANE_LDS_DEPTH = ilog2c(LANE_CHUNKS) - 1;
 constexpr int LANE_BLOCK = 256;
 constexpr size_t LANE_LDS_PAD = (80u << 10) - sizeof(uint32_t) * LANE_LDS_DEPTH * 8 * LANE_BLOCK;
-constexpr int LANE_KEY_BITS = ilog2c(LANE_CHUNKS) + 1;  // keys 0..LANE_CHUNKS
+constexpr int LANE_KEY_BITS = ilog2c(MID_CHUNKS) + 1;  // keys 0..MID_CHUNKS: two radix passes
 
 struct LaneStack {
   uint32_t (*s)[8][LANE_BLOCK];
@@ -614,28 +669,56 @@ __device__ __forceinline__ void lane_digest(const uint4* __restrict__ q, uint32_
   }
 }
 
-// visiting key: descending chunk count for the lane class, LANE_CHUNKS (last) for the rest
+// visiting key: descending chunk count up to MID_CHUNKS, MID_CHUNKS (last) for the rest;
+// info[0] += the lane class's chunks, info[1..3] += the 65..256 / 17..64 / <= 16 chunk
+// class sizes (wave sums, one atomic each per wave)
 extern "C" __global__ void __launch_bounds__(256)
 sd_b3_lane_keys(const uint64_t* __restrict__ offs, const uint64_t* __restrict__ lens, uint64_t n,
-                uint64_t arena_bytes, uint64_t* __restrict__ keys) {
-  const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= n) return;
-  const uint64_t len = lens[f];
-  const uint64_t nch = chunks_of(len);
-  const bool mine = nch <= LANE_CHUNKS && buffer_ok(offs[f], len, arena_bytes);
-  keys[f] = mine ? LANE_CHUNKS - nch : LANE_CHUNKS;
+                uint64_t arena_bytes, uint64_t* __restrict__ keys, uint32_t* __restrict__ info) {
+  __shared__ uint32_t part[4][4];
+  uint32_t v[4] = {0u, 0u, 0u, 0u};  // <= 2^24 buffers x 128 chunks: fits u32
+  for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < n;
+       f += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t len = lens[f];
+    const uint64_t nch = chunks_of(len);
+    const bool ok = nch <= MID_CHUNKS && buffer_ok(offs[f], len, arena_bytes);
+    keys[f] = ok ? MID_CHUNKS - nch : MID_CHUNKS;
+    v[0] += ok && nch <= LANE_CHUNKS ? (uint32_t)nch : 0u;
+    v[1] += ok && nch > SMALL_CHUNKS;
+    v[2] += ok && nch > 16 && nch <= SMALL_CHUNKS;
+    v[3] += ok && nch <= 16;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v[k] += __shfl_xor(v[k], d, 64);
+  }
+  const uint32_t w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63u) == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) part[w][k] = v[k];
+  }
+  __syncthreads();
+  // one atomic per counter per workgroup over a <= 1,024-workgroup grid (one per wave on
+  // the same four words took 0.37 ms for 1 M buffers)
+  if (threadIdx.x < 4) {
+    const uint32_t k = threadIdx.x;
+    const uint32_t sum = part[0][k] + part[1][k] + part[2][k] + part[3][k];
+    if (sum) atomicAdd(info + k, sum);
+  }
 }
 
 extern "C" __global__ void __launch_bounds__(LANE_BLOCK)
 sd_b3_batch_lane(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                  const uint64_t* __restrict__ offs, const uint64_t* __restrict__ lens,
-                 const uint32_t* __restrict__ order, uint64_t n, uint32_t* __restrict__ digests) {
+                 const uint32_t* __restrict__ order, uint64_t n, const uint32_t* __restrict__ lane_info,
+                 uint32_t* __restrict__ digests) {
   __shared__ uint32_t stack_lds[LANE_LDS_DEPTH][8][LANE_BLOCK];
   const uint64_t t = (uint64_t)blockIdx.x * LANE_BLOCK + threadIdx.x;
   if (t >= n) return;
   const uint32_t f = order[t];
   const uint64_t len = lens[f];
-  if (chunks_of(len) > LANE_CHUNKS || !buffer_ok(offs[f], len, arena_bytes)) return;
+  if (chunks_of(len) > lane_cut(lane_info) || !buffer_ok(offs[f], len, arena_bytes)) return;
   LaneStack stk{stack_lds, threadIdx.x};
   uint32_t cv[8];
   lane_digest(reinterpret_cast<const uint4*>(arena + offs[f]), (uint32_t)len, stk, cv);
@@ -716,23 +799,36 @@ sd_b3_batch_reduce(const uint32_t* __restrict__ gstart, const uint32_t* __restri
                    uint64_t n, uint64_t items_cap, const uint32_t* __restrict__ cvs_in,
                    uint32_t* __restrict__ digests) {
   __shared__ uint32_t work[GROUP][8];
+  __shared__ uint32_t list[GROUP];
+  __shared__ uint32_t listed;
   const uint32_t t = threadIdx.x;
   if ((uint64_t)gstart[n - 1] + groups[n - 1] > items_cap) return;
-  for (uint64_t f = blockIdx.x; f < n; f += gridDim.x) {
-    const uint32_t cnt = groups[f];
-    if (cnt < 2) continue;  // uniform across the workgroup
-    const uint32_t* in = cvs_in + 8 * (uint64_t)gstart[f];
-    // above 256 groups the level-1 block CVs sit at stride 256 (<= 256 of them: 64 GiB)
-    const uint32_t stride = cnt <= GROUP ? 1u : GROUP;
-    const uint32_t m = cnt <= GROUP ? cnt : (cnt + GROUP - 1) / GROUP;
-    if (t < m) {
+  // the workgroup scans 256 buffers at a time in parallel and lists those with >= 2 groups
+  // (one buffer per workgroup iteration cost a dependent load per buffer: 0.4 ms for a
+  // batch of 1 M small buffers, none of them multi-group)
+  for (uint64_t base = (uint64_t)blockIdx.x * GROUP; base < n; base += (uint64_t)gridDim.x * GROUP) {
+    if (t == 0) listed = 0;
+    __syncthreads();
+    if (base + t < n && groups[base + t] >= 2) list[atomicAdd(&listed, 1u)] = t;
+    __syncthreads();
+    const uint32_t k = listed;
+    for (uint32_t i = 0; i < k; ++i) {
+      const uint64_t f = base + list[i];
+      const uint32_t cnt = groups[f];
+      const uint32_t* in = cvs_in + 8 * (uint64_t)gstart[f];
+      // above 256 groups the level-1 block CVs sit at stride 256 (<= 256 of them: 64 GiB)
+      const uint32_t stride = cnt <= GROUP ? 1u : GROUP;
+      const uint32_t m = cnt <= GROUP ? cnt : (cnt + GROUP - 1) / GROUP;
+      if (t < m) {
 #pragma unroll
-      for (int w = 0; w < 8; ++w) work[t][w] = in[8 * (uint64_t)t * stride + w];
+        for (int w = 0; w < 8; ++w) work[t][w] = in[8 * (uint64_t)t * stride + w];
+      }
+      __syncthreads();
+      lds_reduce<1>(work, m, true);
+      if (t < 8) digests[8 * f + t] = work[0][t];
+      __syncthreads();
     }
-    __syncthreads();
-    lds_reduce<1>(work, m, true);
-    if (t < 8) digests[8 * f + t] = work[0][t];
-    __syncthreads();
+    __syncthreads();  // `listed` and `list` read by every wave before the next trip resets them
   }
 }
 
@@ -758,11 +854,12 @@ static inline uint64_t batch_items_cap(uint64_t n, uint64_t arena_bytes) {
 static inline bool lane_path(uint64_t n) { return n >= LANE_MIN_BUFFERS; }
 
 size_t checksum_batch_workspace_bytes(uint64_t n, uint64_t arena_bytes) {
-  // groups | gstart | scan partials | owner | cvs [| lane keys | sorted keys | order | sort ws]
+  // groups | gstart | scan partials | owner | cvs
+  //   [| lane class total | lane keys | sorted keys | order | sort ws]
   const uint64_t items = batch_items_cap(n, arena_bytes);
   size_t b = 2 * al256c((n + 1) * 4) + al256c((n / 4096 + 2) * 4) + al256c(items * 4) +
              al256c(items * 32);
-  if (lane_path(n)) b += 2 * al256c(n * 8) + al256c(n * 4) + sort_workspace_bytes(n);
+  if (lane_path(n)) b += 256 + 2 * al256c(n * 8) + al256c(n * 4) + sort_workspace_bytes(n);
   return b + 256;
 }
 
@@ -778,33 +875,36 @@ hipError_t checksum_batch_device(const uint8_t* arena, uint64_t arena_bytes, con
   uint32_t* partial = (uint32_t*)p; p += al256c((n / 4096 + 2) * 4);
   uint32_t* owner = (uint32_t*)p; p += al256c(items * 4);
   uint32_t* cvs = (uint32_t*)p; p += al256c(items * 32);
+  const bool lane = lane_path(n);
+  uint32_t* lane_info = nullptr;  // LaneInfo counters (zeroed by the count kernel)
+  uint32_t* order = nullptr;
+  if (lane) { lane_info = (uint32_t*)p; p += 256; }
   const uint32_t nb = (uint32_t)((n + 255) / 256);
-  sd_b3_batch_count<<<nb, 256, 0, s>>>(offs, lens, n, arena_bytes, groups, d_bad);
+  sd_b3_batch_count<<<nb, 256, 0, s>>>(offs, lens, n, arena_bytes, groups, d_bad, lane_info);
   hipError_t e = exclusive_scan_u32(groups, gstart, n, partial, s);
   if (e != hipSuccess) return e;
   sd_b3_batch_owner<<<(uint32_t)std::min<uint64_t>((items + 255) / 256, 2048), 256, 0, s>>>(
       gstart, groups, n, items, owner);
-  const bool lane = lane_path(n);
   if (lane) {
-    // buffers of <= LANE_CHUNKS chunks one per lane, by descending chunk count
+    // buffers of <= lane_cut() chunks one per lane, by descending chunk count
     uint64_t* lkeys = (uint64_t*)p; p += al256c(n * 8);
     uint64_t* skeys = (uint64_t*)p; p += al256c(n * 8);
-    uint32_t* order = (uint32_t*)p; p += al256c(n * 4);
-    sd_b3_lane_keys<<<nb, 256, 0, s>>>(offs, lens, n, arena_bytes, lkeys);
+    order = (uint32_t*)p; p += al256c(n * 4);
+    sd_b3_lane_keys<<<std::min<uint32_t>(nb, 1024), 256, 0, s>>>(offs, lens, n, arena_bytes, lkeys,
+                                                               lane_info);
     e = radix_sort_pairs(lkeys, nullptr, skeys, order, n, 0, LANE_KEY_BITS, p, s);
     if (e != hipSuccess) return e;
     sd_b3_batch_lane<<<(uint32_t)((n + LANE_BLOCK - 1) / LANE_BLOCK), LANE_BLOCK, LANE_LDS_PAD, s>>>(
-        arena, arena_bytes, offs, lens, order, n, d_digests);
-  } else {
-    // small buffers: <= 16 chunks four per wave, 17..64 chunks one per wave (up to 8
-    // workgroups of 4 waves per CU)
-    sd_b3_batch_small16<<<(uint32_t)std::min<uint64_t>((n + 15) / 16, 256 * 8), 256, 0, s>>>(
-        arena, arena_bytes, offs, lens, n, d_digests);
-    sd_b3_batch_small64<<<(uint32_t)std::min<uint64_t>((n + 3) / 4, 256 * 8), 256, 0, s>>>(
-        arena, arena_bytes, offs, lens, n, d_digests);
+        arena, arena_bytes, offs, lens, order, n, lane_info, d_digests);
   }
+  // small buffers (those the lane kernel does not take): <= 16 chunks four per wave, 17..64
+  // chunks one per wave (up to 8 workgroups of 4 waves per CU); then 65..256 chunks
+  sd_b3_batch_small16<<<(uint32_t)std::min<uint64_t>((n + 15) / 16, 256 * 8), 256, 0, s>>>(
+      arena, arena_bytes, offs, lens, n, order, lane_info, d_digests);
+  sd_b3_batch_small64<<<(uint32_t)std::min<uint64_t>((n + 3) / 4, 256 * 8), 256, 0, s>>>(
+      arena, arena_bytes, offs, lens, n, order, lane_info, d_digests);
   sd_b3_batch_mid<<<(uint32_t)std::min<uint64_t>((n + 3) / 4, 256 * 8), 256, 0, s>>>(
-      arena, arena_bytes, offs, lens, n, lane ? LANE_CHUNKS : SMALL_CHUNKS, d_digests);
+      arena, arena_bytes, offs, lens, n, order, lane_info, d_digests);
   // big buffers: a grid of up to 65,536 workgroups strides over the item list (those past
   // the list's end exit at once)
   sd_b3_batch_groups<<<(uint32_t)std::min<uint64_t>(items, 65536), GROUP, 0, s>>>(

@@ -547,19 +547,30 @@ def test_checksums_batch_dev_vs_oracle(eng, oracle):
     assert (out.cpu().numpy() == got).all()
 
 
-def test_checksums_batch_lane_path(eng, oracle):
+@pytest.mark.parametrize("shape", ["uniform", "skewed"])
+def test_checksums_batch_lane_path(eng, oracle, shape):
     """A batch of 140,000 buffers (>= LANE_MIN_BUFFERS: buffers of <= 128 chunks one per lane,
     sorted by chunk count): lengths at every chunk / block / quad boundary of the lane class
     (0, 1, 15, 16, 63, 64, 1023-1025, 64 and 128 KiB +-1), 128 KiB + 1 and larger buffers in
     the same batch (the mid and subtree kernels), an arena whose last buffer ends exactly at
-    arena_bytes, shuffled arena order — every digest vs the oracle."""
-    rng = np.random.default_rng(12)
+    arena_bytes, shuffled arena order — every digest vs the oracle.  "uniform": lengths
+    U(0, 128 KiB), every lane-class buffer goes one per lane; "skewed": ~96 % U(0, 1 KiB),
+    1.5 % U(64, 128 KiB) and 3,500 of U(1, 64) KiB, so the tail cut (~13 chunks) leaves
+    14..16-chunk buffers to sd_b3_batch_small16, 17..64 to small64 and 65..128 to mid, each
+    walking its range of the sorted order, in the same chain."""
+    rng = np.random.default_rng(12 if shape == "uniform" else 13)
     edge = [0, 1, 15, 16, 17, 63, 64, 65, 127, 128, 1023, 1024, 1025, 2047, 2048, 2049,
             (63 << 10) + 1, (64 << 10) - 1, 64 << 10, (64 << 10) + 1, (127 << 10) + 1,
             (128 << 10) - 1, 128 << 10, (128 << 10) + 1, (200 << 10) + 3, (3 << 20) + 11]
     n = 140_000
-    lens = rng.integers(0, 128 << 10, n).astype(np.int64)
-    lens[rng.integers(0, n, 5000)] = rng.integers(0, 1100, 5000)  # one-chunk buffers
+    if shape == "uniform":
+        lens = rng.integers(0, 128 << 10, n).astype(np.int64)
+        lens[rng.integers(0, n, 5000)] = rng.integers(0, 1100, 5000)  # one-chunk buffers
+    else:
+        lens = rng.integers(0, 1 << 10, n).astype(np.int64)
+        long_ = rng.random(n) < 0.015
+        lens[long_] = rng.integers(64 << 10, 128 << 10, int(long_.sum()))
+        lens[rng.integers(0, n, 3500)] = rng.integers(1 << 10, 64 << 10, 3500)  # 2-64 chunks
     lens[: len(edge)] = edge
     lens[rng.integers(len(edge), n, 40)] = rng.integers(129 << 10, 2 << 20, 40)
     order = rng.permutation(n)

@@ -3,7 +3,8 @@
 # in-tree library (lane path from 65,536 buffers, <= 128 chunks, 3 waves/SIMD) against
 # variants without it, at 2 waves/SIMD, and for <= 64 chunks (tools/ablib/patch_*.py).
 # (Passes: 1 = in-tree <= 64 chunks from 131,072 buffers vs nolane / lane128 / lanemin16k;
-# 2 = the defaults above; 3 = VARIANTS='intree laneocc2 laneocc1 lane512' on the big shapes.
+# 2 = the defaults above; 3 = VARIANTS='intree laneocc2 laneocc1 lane512' on the big shapes;
+# 4 = the tail cut: VARIANTS='intree nolane lanenocut lanetail1' with the skewed shapes.
 # (First pass: in-tree = <= 64 chunks from 131,072 buffers vs nolane / lane128 / lanemin16k.)
 set -o pipefail
 R=$GRAFT_REPO_ROOT

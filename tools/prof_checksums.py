@@ -9,6 +9,7 @@ engine's stream; every digest of a sample checked against the oracle.  Library s
   one     one 16 GiB buffer (the K3 single-buffer chain's shape, for comparison)
   small16k .. small256k  16,384 .. 262,144 buffers of U(0, 16) KiB (batch-size sweep)
   docs64  262,144 buffers of U(1, 64) KiB
+  skew64k / skew1m  mostly U(0, 4) KiB with 8 % U(96, 128) KiB / 3 % U(64, 128) KiB
 Paths (--paths N): N files of U(0.25, 4) MiB on /dev/shm through sd_cas_file_checksums vs
 the oracle's file_checksum on 1 thread (hash.rs is single-threaded) and file-parallel on
 the host cores.
@@ -27,15 +28,25 @@ SHAPES = {"photos": (4096, 1 << 20, 8 << 20), "docs": (262144, 1 << 10, 128 << 1
           # batch-size sweep of the small shape (the lane-per-buffer path's crossover)
           "small16k": (16384, 0, 16 << 10), "small32k": (32768, 0, 16 << 10),
           "small64k": (65536, 0, 16 << 10), "small128k": (131072, 0, 16 << 10),
-          "small256k": (262144, 0, 16 << 10), "docs64": (262144, 1 << 10, 64 << 10)}
+          "small256k": (262144, 0, 16 << 10), "docs64": (262144, 1 << 10, 64 << 10),
+          # skewed libraries: mostly tiny files and a few long ones (n, [(fraction, lo, hi)])
+          "skew64k": (65536, [(0.92, 0, 4 << 10), (0.08, 96 << 10, 128 << 10)]),
+          "skew1m": (1 << 20, [(0.97, 0, 4 << 10), (0.03, 64 << 10, 128 << 10)])}
 
 
 def device_batch(eng, orc, name, iters):
     import numpy as np
     import torch
-    n, lo, hi = SHAPES[name]
+    spec = SHAPES[name]
+    n = spec[0]
     rng = np.random.default_rng(5)
-    lens = rng.integers(lo, hi + 1, n, dtype=np.uint64) if hi > lo else np.full(n, lo, dtype=np.uint64)
+    if isinstance(spec[1], list):  # a mixture, shuffled
+        parts = [rng.integers(lo, hi + 1, int(round(fr * n)), dtype=np.uint64) for fr, lo, hi in spec[1]]
+        lens = np.concatenate(parts)[:n]
+        lens = np.concatenate([lens, np.zeros(n - len(lens), dtype=np.uint64)])[rng.permutation(n)]
+    else:
+        lo, hi = spec[1], spec[2]
+        lens = rng.integers(lo, hi + 1, n, dtype=np.uint64) if hi > lo else np.full(n, lo, dtype=np.uint64)
     offs = np.zeros(n, dtype=np.uint64)
     offs[1:] = np.cumsum((lens[:-1] + 127) // 128 * 128)
     total = int(offs[-1] + lens[-1])
