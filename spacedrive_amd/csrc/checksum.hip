@@ -803,13 +803,15 @@ sd_b3_batch_reduce(const uint32_t* __restrict__ gstart, const uint32_t* __restri
   __shared__ uint32_t listed;
   const uint32_t t = threadIdx.x;
   if ((uint64_t)gstart[n - 1] + groups[n - 1] > items_cap) return;
-  // the workgroup scans 256 buffers at a time in parallel and lists those with >= 2 groups
-  // (one buffer per workgroup iteration cost a dependent load per buffer: 0.4 ms for a
-  // batch of 1 M small buffers, none of them multi-group)
-  for (uint64_t base = (uint64_t)blockIdx.x * GROUP; base < n; base += (uint64_t)gridDim.x * GROUP) {
+  // the workgroup scans a window of up to 256 buffers in parallel and lists those with >= 2
+  // groups (one buffer per workgroup iteration cost a dependent load per buffer: 0.4 ms for
+  // a batch of 1 M small buffers, none of them multi-group); windows of n / grid buffers
+  // below that, so a few thousand big buffers still spread over the whole grid
+  const uint64_t win = min((uint64_t)GROUP, (n + gridDim.x - 1) / gridDim.x);
+  for (uint64_t base = (uint64_t)blockIdx.x * win; base < n; base += (uint64_t)gridDim.x * win) {
     if (t == 0) listed = 0;
     __syncthreads();
-    if (base + t < n && groups[base + t] >= 2) list[atomicAdd(&listed, 1u)] = t;
+    if (t < win && base + t < n && groups[base + t] >= 2) list[atomicAdd(&listed, 1u)] = t;
     __syncthreads();
     const uint32_t k = listed;
     for (uint32_t i = 0; i < k; ++i) {

@@ -10,7 +10,7 @@ cd $R
 for round in 1 2; do
   for v in intree lanev1; do
     if [ $v = intree ]; then L=""; else L=$R/tools/ablib/$v.so; fi
-    SD_HIP_CAS_LIB=$L timeout -k 10 200 python3 -u tools/prof_checksums.py --shape small --shape small256k --shape docs --shape skew1m --iters 5 > $OUT/$v.$round.log 2>&1 || { echo FAIL $v; tail -20 $OUT/$v.$round.log; exit 1; }
+    SD_HIP_CAS_LIB=$L timeout -k 10 200 python3 -u tools/prof_checksums.py ${SH:---shape small --shape small256k --shape docs --shape skew1m --iters 5} > $OUT/$v.$round.log 2>&1 || { echo FAIL $v; tail -20 $OUT/$v.$round.log; exit 1; }
     echo "== $v round $round"; grep "^{" $OUT/$v.$round.log | cut -c1-90
   done
 done
