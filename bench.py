@@ -93,6 +93,12 @@ def main() -> None:
     ap.add_argument("--inline-group", action="store_true",
                     help="issue the grouping from the main thread (A/B of the worker thread)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    rehearsal = bool(os.environ.get("SD_BENCH_ONE_DEVICE"))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N`: launch the N ranks ourselves, before any GPU call here
+        sys.exit(spawn_ranks(args.gpus, rehearsal))
 
     import numpy as np
     import torch
@@ -101,11 +107,15 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    rehearsal = bool(os.environ.get("SD_BENCH_ONE_DEVICE"))
+    if world != args.gpus:
+        fail(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     if rehearsal:
         # rehearsal of the N > 1 code path with every rank on one GPU (RCCL refuses two
         # ranks on one device, so the exchange goes through gloo): not a measurement
         local = 0
+    elif torch.cuda.device_count() < world:
+        fail(f"bench: {world} ranks need {world} visible GPUs, found {torch.cuda.device_count()} "
+             "(SD_BENCH_ONE_DEVICE=1 rehearses the N > 1 path on one GPU)")
     torch.cuda.set_device(local)
     sharded = world > 1 or args.exchange
     if world == 1 and args.exchange:
@@ -118,9 +128,12 @@ def main() -> None:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if dist.get_world_size() != args.gpus:
+            fail(f"bench: the process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
 
     from spacedrive_amd import CasEngine
-    from spacedrive_amd.shard import HipShardOps, fixed_capacity, sharded_group
+    from spacedrive_amd.shard import (HipShardOps, exchange_bytes_per_step, fixed_capacity,
+                                      sharded_group)
 
     eng = CasEngine(local)
     F = args.files_per_gpu
@@ -213,12 +226,15 @@ def main() -> None:
     res = results[-1] if results else None
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    km = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
+    # every rank's K1 mean (slot r = rank r; a summed vector, so gloo rehearsals work too)
+    km = torch.zeros(world, dtype=torch.float64, device=dev)
+    km[rank] = kern_ms
     if sharded:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(km, op=dist.ReduceOp.MAX)
+        dist.all_reduce(km)
     dt = float(t.item())
-    kern_ms = float(km.item())
+    k1_ms_ranks = km.cpu().tolist()
+    kern_ms = max(k1_ms_ranks)
 
     # objects (for the record) — outside the timed region
     if not sharded:
@@ -281,18 +297,31 @@ def main() -> None:
     # the N > 1 exchange alone (partition + fixed-capacity all-to-all + grouping of the
     # received keys + mirror all-to-all), serially after the timed region, max over ranks
     exchange_ms = None
+    exchange_phases = None
     if sharded:
-        xs = []
+        xs, phases = [], []
         for _ in range(3):
             dist.barrier()
             torch.cuda.synchronize()
+            marks = [("start", torch.cuda.Event(enable_timing=True))]
+            marks[0][1].record()
+
+            def mark(name: str) -> None:
+                e = torch.cuda.Event(enable_timing=True)
+                e.record()
+                marks.append((name, e))
             t1 = time.perf_counter()
-            sharded_group(last_keys, file0, ops, capacity=capacity)
+            sharded_group(last_keys, file0, ops, capacity=capacity, mark=mark)
             torch.cuda.synchronize()
             xs.append(time.perf_counter() - t1)
+            phases.append([marks[j - 1][1].elapsed_time(marks[j][1]) for j in range(1, len(marks))])
+        names = [m[0] for m in marks[1:]]
+        ph = torch.tensor(np.median(np.array(phases), axis=0), dtype=torch.float64, device=dev)
         xt = torch.tensor([float(np.median(xs)) * 1e3], dtype=torch.float64, device=dev)
         dist.all_reduce(xt, op=dist.ReduceOp.MAX)
+        dist.all_reduce(ph, op=dist.ReduceOp.MAX)
         exchange_ms = float(xt.item())
+        exchange_phases = dict(zip(names, ph.cpu().tolist()))
 
     # sustained: the same pipelined steps back to back (DVFS-settled; long enough for an
     # outside utilisation sampler to see the GPU busy), after the headline timed region
@@ -339,13 +368,14 @@ def main() -> None:
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(content, sizes, last_keys, args.cpu_seconds)
 
+    n_gpus = dist.get_world_size() if sharded else 1
     if rank == 0:
         line = {
             "metric": "cas_ids/sec + hashed GB/s (whole node), 10M files at 1/2/4/8 MI355X",
             "value": value,
             "unit": "cas_ids/s",
             "hashed_gb_per_s": gbs,
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
@@ -365,11 +395,18 @@ def main() -> None:
                              else "hash then group, serial"),
                 "objects": objects,
                 "exchange": None if not sharded else {
+                    "backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                    "rehearsal_one_device": rehearsal,
                     "capacity_per_peer": capacity[0], "spill_per_peer": capacity[1],
+                    "bytes_sent_per_rank_per_step": exchange_bytes_per_step(world, capacity),
+                    "bytes_sent_per_step_all_ranks": world * exchange_bytes_per_step(world, capacity),
                     "host_syncs_per_step": 0, "timed_steps_overflowed": n_overflow,
                     "serial_ms": exchange_ms,
+                    "serial_ms_phases": exchange_phases,
                     "serial_ms_note": "one step's exchange + grouping alone (max over ranks, "
-                                      "after the timed region); inside the steps it overlaps "
+                                      "after the timed region; phases = HIP events on the "
+                                      "issuing stream between the phase boundaries, median of "
+                                      "3, max over ranks); inside the steps it overlaps "
                                       "the next K1 on a side stream"},
             },
             "roofline": {
@@ -388,6 +425,8 @@ def main() -> None:
                 "frac": valu / VALU_PEAK_TOPS,
                 "traffic": traffic,
                 "kernel_ms": kern_ms,
+                "kernel_ms_ranks": {"min": min(k1_ms_ranks), "max": max(k1_ms_ranks),
+                                    "per_rank": k1_ms_ranks},
                 "work_per_file": {"message_bytes": MSG_BYTES, "compressions": COMPRESSIONS,
                                   "spec_ops_per_compression": SPEC_OPS,
                                   "issue_slots_per_wave_compression": SLOTS},
@@ -430,6 +469,36 @@ def main() -> None:
         worker.shutdown()
     if sharded:
         dist.destroy_process_group()
+
+
+def fail(msg: str) -> None:
+    print(msg, file=sys.stderr, flush=True)
+    sys.exit(2)
+
+
+def spawn_ranks(n: int, rehearsal: bool) -> int:
+    """Run this bench as n ranks (one process per GPU) under torch.distributed.run, the way
+    the driver launches it, and return the launcher's exit status.  The parent makes no GPU
+    call and does not exec: it counts devices (no HIP initialisation on this image),
+    starts the launcher as a child, lets rank 0's one JSON line through to its own stdout
+    and exits with the child's code."""
+    import socket
+    import subprocess
+    import torch
+    have = torch.cuda.device_count()
+    if have < n and not rehearsal:
+        print(f"bench: --gpus {n} needs {n} visible GPUs, found {have} "
+              "(SD_BENCH_ONE_DEVICE=1 rehearses the N > 1 path on one GPU)",
+              file=sys.stderr, flush=True)
+        return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.run(cmd).returncode
 
 
 def e2e_leg(eng, content, sizes, keys, args, world, rank, dev, dist):

@@ -170,7 +170,10 @@ def fixed_capacity(n_per_rank: int, parts: int) -> tuple[int, int]:
 
 @dataclass
 class ShardResult:
-    rep: torch.Tensor        # int64 global idx of the file owning each local file's Object
+    """One grouping's result.  ``rep`` and ``objects`` resolve first: with the fixed-capacity
+    form an overflowed part leaves garbage in the raw representatives until the exact redo,
+    so neither is readable before :meth:`resolve` has run (it runs on first access)."""
+    _rep: torch.Tensor       # int64 global idx of the file owning each local file's Object
     objects_dev: torch.Tensor  # int64 [1]: Objects over all ranks (= distinct keys), device
     sent: Optional[int] = None  # keys this rank sent to other ranks (exact form only)
     overflow: Optional[torch.Tensor] = None  # int32 [1] (fixed form): a part exceeded cap+spill
@@ -183,10 +186,16 @@ class ShardResult:
         if self.overflow is not None:
             if int(self.overflow.item()):
                 exact = self._redo()
-                self.rep, self.objects_dev, self.sent = exact.rep, exact.objects_dev, exact.sent
+                self._rep, self.objects_dev, self.sent = exact._rep, exact.objects_dev, exact.sent
             self.overflow = None
             self._redo = None
         return self
+
+    @property
+    def rep(self) -> torch.Tensor:
+        """rep(f) = min global idx of f's key (resolves the overflow flag first: collective)."""
+        self.resolve()
+        return self._rep
 
     @property
     def objects(self) -> int:
@@ -195,15 +204,25 @@ class ShardResult:
 
 
 def sharded_group(local_keys: torch.Tensor, file0: int, ops: ShardOps, group=None,
-                  capacity: Optional[tuple[int, int]] = None) -> ShardResult:
+                  capacity: Optional[tuple[int, int]] = None, mark=None) -> ShardResult:
     """Canonical grouping across all ranks: rep(f) = min{ g : key(g) == key(f) }.
     capacity = (cap, spill) selects the sync-free fixed-capacity exchange (every rank must
-    pass the same values, e.g. fixed_capacity(max files per rank, world)); None = exact."""
+    pass the same values, e.g. fixed_capacity(max files per rank, world)); None = exact.
+    mark(name), if given, is called after each phase of the fixed form (partition, pack,
+    all_to_all, group, all_to_all_back, unpack, all_reduce) on the issuing thread — the
+    bench records a stream event there to split the exchange's time."""
     if file0 + local_keys.numel() > (1 << 32):
         raise ValueError("sharded_group: global file idx must fit in u32")
     if capacity is None:
         return _sharded_group_exact(local_keys, file0, ops, group)
-    return _sharded_group_fixed(local_keys, file0, ops, group, capacity)
+    return _sharded_group_fixed(local_keys, file0, ops, group, capacity, mark)
+
+
+def exchange_bytes_per_step(world: int, capacity: tuple[int, int]) -> int:
+    """Bytes one rank sends to OTHER ranks per fixed-capacity step: (cap + spill) 12-byte
+    rows and the mirror 4-byte reps to each of the world - 1 peers (its own block stays)."""
+    cap, spill = capacity
+    return (world - 1) * (cap + spill) * (12 + 4)
 
 
 def _sharded_group_exact(local_keys, file0, ops, group) -> ShardResult:
@@ -231,34 +250,42 @@ def _sharded_group_exact(local_keys, file0, ops, group) -> ShardResult:
     rep = ops.unpack(back, ppos)
     tot = torch.tensor([objects], dtype=torch.int64, device=dev)
     dist.all_reduce(tot, group=group)
-    return ShardResult(rep=rep, objects_dev=tot, sent=n - int(sc[rank]))
+    return ShardResult(_rep=rep, objects_dev=tot, sent=n - int(sc[rank]))
 
 
-def _sharded_group_fixed(local_keys, file0, ops, group, capacity) -> ShardResult:
+def _sharded_group_fixed(local_keys, file0, ops, group, capacity, mark=None) -> ShardResult:
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     if world == 1:  # one range: no slot can hold a key outside it, nothing to exchange
         return _sharded_group_exact(local_keys, file0, ops, group)
     cap, spill = capacity
     dev = local_keys.device
+    mark = mark or (lambda name: None)
     pkeys, ppos, counts = ops.partition(local_keys, world)                    # 1
+    mark("partition")
     rows, srows, overflow = ops.pack_fixed(pkeys, ppos, counts, world, cap, spill, file0)
+    mark("pack")
     rrows = torch.empty_like(rows)
     dist.all_to_all_single(rrows, rows, group=group)                          # 2: equal splits
     if spill:
         rsrows = torch.empty_like(srows)
         dist.all_to_all_single(rsrows, srows, group=group)
         rrows = torch.cat([rrows, rsrows])
+    mark("all_to_all")
     rkeys, ridx, nsent = ops.split_fixed(rrows, range_start(rank + 1, world))
     rep_min, obj = ops.group_min_dev(rkeys, ridx)                             # 3
     tot = obj - nsent                             # each sentinel row is one extra key
+    mark("group")
     back = torch.empty(world * cap, dtype=torch.int32, device=dev)
     dist.all_to_all_single(back, rep_min[:world * cap].contiguous(), group=group)   # 4
     sback = torch.empty(world * spill, dtype=torch.int32, device=dev)
     if spill:
         dist.all_to_all_single(sback, rep_min[world * cap:].contiguous(), group=group)
+    mark("all_to_all_back")
     rep = ops.unpack_fixed(back, sback, ppos, counts, world, cap, spill)
+    mark("unpack")
     dist.all_reduce(tot, group=group)
     dist.all_reduce(overflow, op=dist.ReduceOp.MAX, group=group)
-    return ShardResult(rep=rep, objects_dev=tot, overflow=overflow,
+    mark("all_reduce")
+    return ShardResult(_rep=rep, objects_dev=tot, overflow=overflow,
                        _redo=lambda: _sharded_group_exact(local_keys, file0, ops, group))
