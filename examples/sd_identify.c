@@ -104,13 +104,17 @@ int main(int argc, char** argv) {
   uint64_t* keys = calloc(m ? m : 1, 8);
   int32_t* status = calloc(m ? m : 1, 4);
   uint8_t* state = calloc(m ? m : 1, 1);
-  if (m && (rc = sd_cas_generate_cas_ids_from_paths(ctx, hp, hs, m, keys, status)) != SD_CAS_OK) {
+  /* FileMetadata::new per row (mod.rs:55-95) behind the ABI: sizes NULL = the library takes
+   * fs::metadata itself (the walk's sizes are the indexer's, only used for the orphan filter) */
+  if (m && (rc = sd_cas_generate_cas_ids_from_paths(ctx, hp, NULL, m, keys, status)) != SD_CAS_OK) {
     fprintf(stderr, "generate_cas_ids_from_paths: %d (%s)\n", rc, sd_cas_last_error(ctx));
     return 1;
   }
-  /* a row whose length is 0 by now gets no cas_id (mod.rs:78-86): the gather reports the
-   * file as it is, so a failed read is an ERROR row (dropped from its step, mod.rs:125-141) */
-  for (size_t j = 0; j < m; j++) state[j] = status[j] ? SD_CAS_ROW_ERROR : SD_CAS_ROW_HASHED;
+  /* a row whose length is 0 by now has no cas_id (mod.rs:78-86); a failed metadata/read is
+   * an ERROR row (dropped from its step, mod.rs:125-141) */
+  for (size_t j = 0; j < m; j++)
+    state[j] = status[j] == SD_CAS_STATUS_NO_CAS ? SD_CAS_ROW_NO_CAS
+               : status[j] ? SD_CAS_ROW_ERROR : SD_CAS_ROW_HASHED;
   const size_t max_steps = sd_cas_identifier_max_steps(m, chunk);
   uint32_t* step = calloc(m ? m : 1, 4);
   uint32_t* object = calloc(m ? m : 1, 4);
@@ -146,7 +150,7 @@ int main(int argc, char** argv) {
     } else {
       printf(", \"cas_id\": null");
     }
-    printf(", \"errno\": %d", status[j] ? -status[j] : 0);
+    printf(", \"errno\": %d", status[j] < 0 ? -status[j] : 0);
     if (step[j] == SD_CAS_NO_STEP) printf(", \"step\": null");
     else printf(", \"step\": %u", step[j]);
     if (object[j] == SD_CAS_NO_OBJECT) printf(", \"object\": null");

@@ -112,13 +112,22 @@ int sd_cas_free_pinned(sd_cas_ctx* ctx, void* p);
 int sd_cas_generate_cas_ids(sd_cas_ctx* ctx, const uint8_t* const* bufs, const uint64_t* buf_lens,
                             const uint64_t* sizes, size_t n, uint64_t* out_keys);
 
-/* Same, gathering each file from its path with pread at the cas.rs:27-58 offsets.
- * status[i] = 0, or -errno for a file that failed to open/read (a short read of a sampled
- * file is -EIO == tokio's UnexpectedEof); such files get out_keys[i] = 0 and are to be
- * dropped from the step like mod.rs:125-141 does.  A whole file (size <= 100 KiB) is
- * hashed as it is on disk even when its length no longer matches `size` (cas.rs:29 reads
- * the file, not `size` bytes; one longer than the whole-file limit goes through the
- * validator tree).  Returns SD_CAS_OK unless the batch itself failed. */
+/* The cas part of FileMetadata::new (file_identifier/mod.rs:55-95) over a batch of paths,
+ * gathering each file with pread at the cas.rs:27-58 offsets.  sizes[i] = the file's
+ * fs::metadata().len() (mod.rs:63,78-79) as the caller just read it, or sizes == NULL: the
+ * library takes that metadata itself (stat, following symlinks, like fs::metadata).
+ * status[i] / out_keys[i]:
+ *   0                    cas key of generate_cas_id(path, size) (cas.rs:23-62);
+ *   SD_CAS_STATUS_NO_CAS metadata length 0: no cas_id (mod.rs:78-86), nothing read, key 0;
+ *   -errno               metadata, open or read failed (a short read of a sampled file is
+ *                        -EIO == tokio's UnexpectedEof), -EISDIR for a directory (the
+ *                        reference asserts, mod.rs:67-70); key 0 — the row is dropped from
+ *                        its step like mod.rs:125-141 does.
+ * A whole file (0 < size <= 100 KiB) is hashed as it is on disk even when its length no
+ * longer matches `size` (cas.rs:29 reads the file, not `size` bytes; one longer than the
+ * whole-file limit goes through the validator tree).  Returns SD_CAS_OK unless the batch
+ * itself failed. */
+#define SD_CAS_STATUS_NO_CAS 1
 int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* ctx, const char* const* paths,
                                        const uint64_t* sizes, size_t n, uint64_t* out_keys,
                                        int32_t* status);
@@ -314,8 +323,14 @@ int sd_cas_sort_pairs_dev(sd_cas_ctx* ctx, const uint64_t* d_keys_in, const uint
  * of len).  Blocking. */
 int sd_cas_checksum_dev(sd_cas_ctx* ctx, const void* d_data, uint64_t len, uint8_t out[32],
                         void* stream);
-/* file_checksum(path): streams the file through pinned staging in 64 MiB segments, one
- * BLAKE3 subtree per segment on the GPU; out_hex = 64 lowercase hex + NUL.
+/* file_checksum(path): the bytes hash.rs:15-21 hashes — its loop issues 1 MiB read()s and
+ * stops after the FIRST read shorter than 1 MiB, which is EOF on a local regular file but
+ * not on a procfs seq_file (about one page per read), a FIFO or a FUSE/network mount.
+ * Regular files are read in parallel (pread pieces) and streamed through pinned staging in
+ * 64 MiB segments, one BLAKE3 subtree per segment on the GPU; a regular file whose reads
+ * come back short before its end (or that ends before st_size), and every non-regular
+ * file, is read as hash.rs reads it: sequential 1 MiB read()s from the start up to and
+ * including the first short one.  out_hex = 64 lowercase hex + NUL.
  * Returns SD_CAS_EIO with *err_no set on an I/O error. */
 int sd_cas_file_checksum(sd_cas_ctx* ctx, const char* path, char out_hex[65], int* err_no);
 /* The validator job over many files (validator_job.rs:107-172 runs one file_checksum per
@@ -327,10 +342,12 @@ int sd_cas_file_checksum(sd_cas_ctx* ctx, const char* path, char out_hex[65], in
 int sd_cas_checksums_dev(sd_cas_ctx* ctx, const void* d_arena, uint64_t arena_bytes,
                          const uint64_t* d_offs, const uint64_t* d_lens, size_t n, uint8_t* d_out,
                          void* stream);
-/* file_checksum over n paths: each file is read to EOF (the first short read, hash.rs:15-21)
- * by the gather pool into pinned windows that are hashed with the batch chain above while the
- * next window is read; a file larger than half a window, or one that grew past its slot,
- * streams through sd_cas_file_checksum.  out_hex[65 i ..] = 64 hex + NUL ("" on error);
+/* file_checksum over n paths, each with sd_cas_file_checksum's result: regular files are
+ * read by the gather pool into pinned windows that are hashed with the batch chain above while
+ * the next window is read; a file larger than half a window, one that grew past its slot, a
+ * non-regular file, and one whose reads came back short before its end or that ended before
+ * st_size (hash.rs:15-21 would stop at its first short read) go through
+ * sd_cas_file_checksum.  out_hex[65 i ..] = 64 hex + NUL ("" on error);
  * status[i] = 0 or -errno (open/stat/read failure: validator_job.rs:149-151 fails that
  * step with FileIOError).  Returns SD_CAS_OK unless the batch itself failed.  Blocking. */
 int sd_cas_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char* out_hex,

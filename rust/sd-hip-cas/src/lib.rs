@@ -33,7 +33,10 @@ pub const SD_CAS_LINK_LINKED: u8 = 1;
 pub const SD_CAS_LINK_DROPPED: u8 = 2;
 pub const SD_CAS_LINK_NOT_REACHED: u8 = 3;
 pub const SD_CAS_NO_OBJECT: u32 = 0xFFFF_FFFF;
+pub const SD_CAS_NO_STEP: u32 = 0xFFFF_FFFF;
 pub const SD_CAS_CHUNK_SIZE: u32 = 100;
+/// status of a row whose fs::metadata length is 0: no cas_id (file_identifier/mod.rs:78-86)
+pub const SD_CAS_STATUS_NO_CAS: i32 = 1;
 
 extern "C" {
     pub fn sd_cas_abi_version() -> c_int;
@@ -245,19 +248,36 @@ impl HipCas {
         Ok(keys.into_iter().map(CasId).collect())
     }
 
-    /// Gather (cas.rs:27-58 offsets) + hash; per-file io errors like FileMetadata::new.
+    /// The cas part of `FileMetadata::new` (file_identifier/mod.rs:55-95) over a batch:
+    /// gather (cas.rs:27-58 offsets) + hash.  `size` = the `fs::metadata().len()` just read.
+    /// Per file: `Ok(Some(cas_id))`, `Ok(None)` for length 0 (no cas_id, mod.rs:78-86), or the
+    /// io error (a directory is `EISDIR`; the reference asserts, mod.rs:67-70).
     pub fn generate_cas_ids_from_paths(&mut self, files: &[(&Path, u64)])
-        -> io::Result<Vec<Result<CasId, io::Error>>> {
-        let cpaths: Vec<CString> = files
+        -> io::Result<Vec<Result<Option<CasId>, io::Error>>> {
+        let paths: Vec<&Path> = files.iter().map(|(p, _)| *p).collect();
+        let sizes: Vec<u64> = files.iter().map(|(_, s)| *s).collect();
+        self.cas_ids_from_paths(&paths, Some(&sizes))
+    }
+
+    /// Same with the metadata taken by the library (stat, following symlinks like
+    /// `fs::metadata`, mod.rs:63): `FileMetadata::new`'s cas_id for each path.
+    pub fn file_metadata_cas_ids(&mut self, paths: &[&Path])
+        -> io::Result<Vec<Result<Option<CasId>, io::Error>>> {
+        self.cas_ids_from_paths(paths, None)
+    }
+
+    fn cas_ids_from_paths(&mut self, paths: &[&Path], sizes: Option<&[u64]>)
+        -> io::Result<Vec<Result<Option<CasId>, io::Error>>> {
+        let cpaths: Vec<CString> = paths
             .iter()
-            .map(|(p, _)| CString::new(p.as_os_str().as_encoded_bytes()).expect("NUL in path"))
+            .map(|p| CString::new(p.as_os_str().as_encoded_bytes()).expect("NUL in path"))
             .collect();
         let ptrs: Vec<*const c_char> = cpaths.iter().map(|c| c.as_ptr()).collect();
-        let sizes: Vec<u64> = files.iter().map(|(_, s)| *s).collect();
-        let mut keys = vec![0u64; files.len()];
-        let mut status = vec![0i32; files.len()];
+        let mut keys = vec![0u64; paths.len()];
+        let mut status = vec![0i32; paths.len()];
         let rc = unsafe {
-            sd_cas_generate_cas_ids_from_paths(self.ctx, ptrs.as_ptr(), sizes.as_ptr(), files.len(),
+            sd_cas_generate_cas_ids_from_paths(self.ctx, ptrs.as_ptr(),
+                                               sizes.map_or(ptr::null(), |s| s.as_ptr()), paths.len(),
                                                keys.as_mut_ptr(), status.as_mut_ptr())
         };
         if rc != 0 {
@@ -266,7 +286,11 @@ impl HipCas {
         Ok(keys
             .into_iter()
             .zip(status)
-            .map(|(k, s)| if s == 0 { Ok(CasId(k)) } else { Err(io::Error::from_raw_os_error(-s)) })
+            .map(|(k, s)| match s {
+                0 => Ok(Some(CasId(k))),
+                SD_CAS_STATUS_NO_CAS => Ok(None),
+                e => Err(io::Error::from_raw_os_error(-e)),
+            })
             .collect())
     }
 
@@ -304,6 +328,22 @@ impl HipCas {
                 SD_CAS_LINK_CREATED => out[step[i] as usize].creates.push(i),
                 SD_CAS_LINK_LINKED => out[step[i] as usize].links.push((i, object[i] as usize)),
                 _ => {}
+            }
+        }
+        // A NoCas row that ends a chunk stays orphan (cas_id NULL), so the next step's
+        // `id >= cursor` query returns it again and it gets an Object in BOTH steps
+        // (mod.rs:277-283, 401-405); `step` holds its last step only.  The row missing from
+        // step k's creates is the first row of step k+1 (the cursor row): the smallest row
+        // whose last step is after k — processed rows' steps are non-decreasing in row order.
+        let mut first = 0usize;
+        for k in 0..out.len() {
+            if out[k].total_created as usize > out[k].creates.len() {
+                while first < n && (step[first] == SD_CAS_NO_STEP || step[first] as usize <= k) {
+                    first += 1;
+                }
+                if first < n {
+                    out[k].creates.push(first);
+                }
             }
         }
         Ok(out)

@@ -153,20 +153,24 @@ class CasEngine:
     def generate_cas_ids(self, items: Sequence[tuple[bytes, int]]) -> list[str]:
         return [key_to_cas_id(k) for k in self.generate_cas_keys(items)]
 
-    def generate_cas_keys_from_paths(self, paths: Sequence[str], sizes: Sequence[int]):
-        """Gather (pread at the cas.rs:27-58 offsets) + hash. Returns (keys, errno array)."""
+    def generate_cas_keys_from_paths(self, paths: Sequence[str], sizes: Optional[Sequence[int]] = None):
+        """The cas part of FileMetadata::new (file_identifier/mod.rs:55-95) over a batch:
+        gather (pread at the cas.rs:27-58 offsets) + hash.  sizes = fs::metadata lengths, or
+        None to let the library take the metadata (stat).  Returns (keys, status): status 0 =
+        hashed, STATUS_NO_CAS = length 0 (no cas_id, key 0), -errno = error (EISDIR for a
+        directory)."""
         n = len(paths)
         enc = [os.fsencode(p) for p in paths]
         parr = (ctypes.c_char_p * n)(*enc)
-        sz = np.array([int(s) for s in sizes], dtype=np.uint64)
+        sz = None if sizes is None else np.array([int(s) for s in sizes], dtype=np.uint64)
         keys = np.zeros(n, dtype=np.uint64)
         status = np.zeros(n, dtype=np.int32)
         if n:
             rc = self.L.sd_cas_generate_cas_ids_from_paths(
-                self.h, ctypes.cast(parr, ctypes.c_void_p), _np_ptr(sz), n, _np_ptr(keys),
-                _np_ptr(status))
+                self.h, ctypes.cast(parr, ctypes.c_void_p), None if sz is None else _np_ptr(sz), n,
+                _np_ptr(keys), _np_ptr(status))
             self._check(rc, "generate_cas_ids_from_paths")
-        return keys, -status
+        return keys, status
 
     def alloc_pinned(self, nbytes: int) -> np.ndarray:
         """Page-locked host buffer (uint8 numpy view); free with free_pinned."""
@@ -422,10 +426,15 @@ def engine(device: int = 0) -> CasEngine:
 # ---- reference-shaped free functions -----------------------------------------------------
 def generate_cas_id(path: str, size: int) -> str:
     """``generate_cas_id(path, size)`` (cas.rs:23): a one-file batch on the GPU.
-    Raises OSError like the reference's io::Error."""
-    keys, errs = engine().generate_cas_keys_from_paths([path], [size])
-    if errs[0]:
-        raise OSError(int(errs[0]), os.strerror(int(errs[0])), path)
+    Raises OSError like the reference's io::Error.  (size 0 is what FileMetadata::new never
+    passes — the batch ABI answers it with no cas_id — so the one-file drop-in hashes
+    le64(0) || the file as cas.rs:29 would.)"""
+    if size == 0:
+        with open(path, "rb") as fh:
+            return engine().generate_cas_ids([(fh.read(), 0)])[0]
+    keys, status = engine().generate_cas_keys_from_paths([path], [size])
+    if status[0] < 0:
+        raise OSError(int(-status[0]), os.strerror(int(-status[0])), path)
     return key_to_cas_id(keys[0])
 
 
@@ -447,6 +456,7 @@ class FileMetadata:
 
 
 ROW_HASHED, ROW_NO_CAS, ROW_ERROR = 0, 1, 2                          # SD_CAS_ROW_*
+STATUS_NO_CAS = 1                                                    # SD_CAS_STATUS_NO_CAS
 LINK_CREATED, LINK_LINKED, LINK_DROPPED, LINK_NOT_REACHED = 0, 1, 2, 3  # SD_CAS_LINK_*
 
 
@@ -487,27 +497,24 @@ def identifier_job_step(paths: Sequence[str], chunk: int = CHUNK_SIZE,
     eng = eng or engine()
     res = StepResult()
     n = len(paths)
-    sizes = []
-    for i, p in enumerate(paths):
-        try:
-            sizes.append(os.stat(p).st_size)  # fs::metadata (mod.rs:63)
-        except OSError as e:
-            res.errors[i] = e.errno
-            sizes.append(-1)
-    live = [i for i in range(n) if sizes[i] > 0]
-    keys, errs = eng.generate_cas_keys_from_paths([paths[i] for i in live], [sizes[i] for i in live])
-    all_keys = np.zeros(n, dtype=np.uint64)
-    state = np.full(n, ROW_NO_CAS, dtype=np.uint8)
-    for j, i in enumerate(live):
-        if errs[j]:
-            res.errors[i] = int(errs[j])
-        else:
-            all_keys[i] = keys[j]
-            state[i] = ROW_HASHED
-    for i in res.errors:
-        state[i] = ROW_ERROR
     if n == 0:
         return res
+    # FileMetadata::new per row, behind the ABI: fs::metadata (mod.rs:63), a directory or an
+    # error drops the row, length 0 -> no cas_id (mod.rs:78-86), else generate_cas_id
+    all_keys, status = eng.generate_cas_keys_from_paths(paths, None)
+    sizes = []
+    for p in paths:
+        try:
+            sizes.append(os.stat(p).st_size)  # FileMetadata.size, for the record
+        except OSError:
+            sizes.append(-1)
+    state = np.full(n, ROW_HASHED, dtype=np.uint8)
+    for i in range(n):
+        if status[i] == STATUS_NO_CAS:
+            state[i] = ROW_NO_CAS
+        elif status[i] < 0:
+            res.errors[i] = int(-status[i])
+            state[i] = ROW_ERROR
     step, obj, act, counts = eng.identifier_links_host(all_keys, state, chunk)
     res.steps = [StepBatch(k, total_created=int(c), total_linked=int(ln))
                  for k, (c, ln) in enumerate(counts)]
@@ -526,6 +533,16 @@ def identifier_job_step(paths: Sequence[str], chunk: int = CHUNK_SIZE,
             b.creates.append(i)
         else:
             b.links.append((i, int(obj[i])))
+    # a NO_CAS row ending a chunk stays orphan and is queried again by the next step: it
+    # gets an Object in each step (mod.rs:277-283, 401-405), `step` names its last one — the
+    # row missing from step k's creates is step k+1's first (cursor) row
+    first = 0
+    for k, b in enumerate(res.steps):
+        if b.total_created > len(b.creates):
+            while first < n and (int(step[first]) == 0xFFFFFFFF or int(step[first]) <= k):
+                first += 1
+            if first < n:
+                b.creates.append(first)
     res.total_created = int(counts[:, 0].sum()) if len(counts) else 0
     res.total_linked = int(counts[:, 1].sum()) if len(counts) else 0
     return res

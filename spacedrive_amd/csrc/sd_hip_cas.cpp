@@ -651,30 +651,57 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
                                        int32_t* status) {
   if (!c) return SD_CAS_EINVAL;
   if (n == 0) return SD_CAS_OK;
-  if (!paths || !sizes || !out_keys || !status || n >= (1ull << 32))
+  if (!paths || !out_keys || !status || n >= (1ull << 32))
     return fail(c, SD_CAS_EINVAL, "generate_cas_ids_from_paths: null argument");
   HIP_TRY(c, hipSetDevice(c->device));
-  // Content length per file: sampled 57,344; whole file = its actual length (cas.rs:29
-  // reads the file, not `size` bytes).  The plan assumes the actual length is `size` (the
-  // metadata the caller just read, mod.rs:63,78-79); the gather checks it with fstat on
-  // the open descriptor — no separate stat pass and path walk — and a whole file whose
-  // length changed is re-read and hashed after the windows (`redo`).
-  std::vector<uint64_t> lens(n, 0);
-  std::vector<uint8_t> redo(n, 0);
   for (size_t i = 0; i < n; i++) {
     status[i] = 0;
     out_keys[i] = 0;
-    lens[i] = sizes[i] > MINIMUM_FILE_SIZE ? SAMPLED_CONTENT_LEN : sizes[i];
   }
+  // FileMetadata::new (file_identifier/mod.rs:63-86): the metadata — given by the caller, or
+  // taken here with stat (fs::metadata follows symlinks) — decides the row: an error drops
+  // it (-errno), a directory is refused (-EISDIR; the reference asserts, :67-70), length 0
+  // means no cas_id (SD_CAS_STATUS_NO_CAS, nothing is read: :78-86), anything else is
+  // generate_cas_id(path, len).
+  std::vector<uint64_t> msize;
+  if (!sizes) {
+    msize.assign(n, 0);
+    std::atomic<size_t> next{0};
+    c->pool.run(std::max(1u, std::min(16u, (unsigned)((n + 63) / 64))), [&]() {
+      for (size_t i; (i = next.fetch_add(1)) < n;) {
+        struct stat st;
+        if (stat(paths[i], &st) != 0) { status[i] = -errno; continue; }
+        if (S_ISDIR(st.st_mode)) { status[i] = -EISDIR; continue; }
+        msize[i] = (uint64_t)st.st_size;
+      }
+    });
+    sizes = msize.data();
+  }
+  for (size_t i = 0; i < n; i++)
+    if (status[i] == 0 && sizes[i] == 0) status[i] = SD_CAS_STATUS_NO_CAS;
+  // Content length per file: sampled 57,344; whole file = its actual length (cas.rs:29
+  // reads the file, not `size` bytes).  The plan assumes the actual length is `size` (the
+  // metadata just read, mod.rs:63,78-79); the gather checks it with fstat on the open
+  // descriptor — no second path walk — and a whole file whose length changed is re-read and
+  // hashed after the windows (`redo`).  Rows already decided (error, no cas) plan as empty
+  // whole files and are never read.
+  std::vector<uint64_t> lens(n, 0);
+  std::vector<uint8_t> redo(n, 0);
+  for (size_t i = 0; i < n; i++)
+    lens[i] = status[i] ? 0 : sizes[i] > MINIMUM_FILE_SIZE ? SAMPLED_CONTENT_LEN : sizes[i];
   // Windows of GATHER_WINDOW files, double-buffered: the pool gathers window w into one
   // pinned slot while the GPU copies and hashes window w-1 from the other.
   constexpr size_t GATHER_WINDOW = 2048;
   const size_t nw = (n + GATHER_WINDOW - 1) / GATHER_WINDOW;
   std::vector<Plan> plans(nw);
   size_t slot = 0;
+  // decided rows plan as empty whole files (their metadata size may be anything)
+  std::vector<uint64_t> psize(sizes, sizes + n);
+  for (size_t i = 0; i < n; i++)
+    if (status[i]) psize[i] = 0;
   for (size_t w = 0; w < nw; w++) {
     const size_t f0 = w * GATHER_WINDOW, m = std::min(GATHER_WINDOW, n - f0);
-    int rc = plan_batch(c, lens.data() + f0, sizes + f0, m, plans[w]);
+    int rc = plan_batch(c, lens.data() + f0, psize.data() + f0, m, plans[w]);
     if (rc) return rc;
     slot = std::max(slot, up256(staged_pinned_bytes(plans[w], m)));
   }
@@ -702,10 +729,15 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
                            : pin + pl.sampled_bytes + pl.poff[t - ns];
         int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
         if (fd < 0) { status[i] = -errno; continue; }
-        if (sizes[i] <= MINIMUM_FILE_SIZE) {
+        {
           struct stat st;
           if (fstat(fd, &st) != 0) { status[i] = -errno; close(fd); continue; }
-          if ((uint64_t)st.st_size != lens[i]) { redo[i] = 1; close(fd); continue; }
+          if (S_ISDIR(st.st_mode)) { status[i] = -EISDIR; close(fd); continue; }
+          if (sizes[i] <= MINIMUM_FILE_SIZE && (uint64_t)st.st_size != lens[i]) {
+            redo[i] = 1;
+            close(fd);
+            continue;
+          }
         }
         // cas.rs:35-58 offsets: header at 0, sample k at 8192 + k*jump (both from `size`,
         // the metadata length), footer at the file's ACTUAL end - 8192: the reference
@@ -765,7 +797,7 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
     if (w >= 2 && (rc = finish(w - 2))) break;  // slot b free again
     gather(w, pin0 + b * slot);
     const size_t f0 = w * GATHER_WINDOW, m = std::min(GATHER_WINDOW, n - f0);
-    rc = enqueue_staged(c, plans[w], sizes + f0, m, pin0 + b * slot, dev0 + b * slot, done[b]);
+    rc = enqueue_staged(c, plans[w], psize.data() + f0, m, pin0 + b * slot, dev0 + b * slot, done[b]);
   }
   for (size_t w = nw >= 2 ? nw - 2 : 0; w < nw && rc == 0; w++) rc = finish(w);
   if (rc) (void)hipStreamSynchronize(c->stream);
@@ -948,14 +980,22 @@ int sd_cas_checksum_dev(sd_cas_ctx* c, const void* d_data, uint64_t len, uint8_t
   return SD_CAS_OK;
 }
 
-// file_checksum(path) (validation/hash.rs:11-25): the reference reads 1 MiB blocks into one
-// hasher until the first read shorter than 1 MiB — i.e. to EOF on a regular file, whatever
-// the file's length was when it was opened.  Here the file streams through two pinned
-// segment buffers of up to 64 MiB (a segment = one complete 65,536-chunk subtree, hashed
-// on the GPU while the next segment is read by the pool) until a segment comes back short;
-// st_size only sizes the buffers (a file that outgrows its first buffer is re-read with
-// full-size segments).  The segment CVs are merged on the GPU (pair-and-promote, ROOT on
-// the last parent); a file of one segment is hashed with ROOT inside the segment.
+// file_checksum(path) (validation/hash.rs:11-25): the reference issues one read() of
+// BLOCK_LEN = 1 MiB per iteration into one hasher and stops at the FIRST read that returns
+// fewer bytes — the end of a regular file on a local filesystem, but after the first short
+// read on anything that returns short reads before its end (procfs seq_files give about one
+// page per read, FIFOs and FUSE/network mounts whatever is ready).
+// Two read modes, one result:
+//   * parallel (regular files): the file streams through two pinned segment buffers of up
+//     to 64 MiB (a segment = one complete 65,536-chunk subtree, hashed on the GPU while the
+//     pool reads the next one with pread pieces) until a segment comes back short; st_size
+//     only sizes the buffers (a file that outgrows its first buffer is re-read with full-size
+//     segments).  A regular file whose reads show it is not read like a local file — a short
+//     pread followed by more data, or an end before st_size — is redone sequentially;
+//   * sequential (everything else, and those redos): hash.rs's loop literally, 1 MiB read()s
+//     from the start, stopping after the first short one, into the same segment pipeline.
+// The segment CVs are merged on the GPU (pair-and-promote, ROOT on the last parent); a file
+// of one segment is hashed with ROOT inside the segment.
 static int cv_capacity(sd_cas_ctx* c, DevBuf& cvb, size_t need_cvs, hipStream_t s) {
   if (need_cvs * 32 <= cvb.bytes) return SD_CAS_OK;
   DevBuf nb;
@@ -991,8 +1031,12 @@ int sd_cas_file_checksum(sd_cas_ctx* c, const char* path, char out_hex[65], int*
   }
   const uint64_t SEG = 64ull << 20;  // 65,536 chunks: a complete left subtree
   constexpr uint64_t PIECE = 4ull << 20;  // pool read unit (one reader tops out near 5-10 GB/s)
-  // segment capacity: the whole file plus room to see EOF, capped at one subtree
-  uint64_t cap = std::min<uint64_t>(SEG, (((uint64_t)st.st_size + 1 + 4095) / 4096) * 4096);
+  constexpr uint64_t BLOCK_LEN = 1ull << 20;  // hash.rs:9
+  static_assert((64ull << 20) % BLOCK_LEN == 0, "a segment holds whole hash.rs reads");
+  bool seq = !S_ISREG(st.st_mode);
+  // segment capacity: the whole file plus room to see EOF, capped at one subtree (the
+  // sequential mode reads whole 1 MiB blocks: full segments)
+  uint64_t cap = seq ? SEG : std::min<uint64_t>(SEG, (((uint64_t)st.st_size + 1 + 4095) / 4096) * 4096);
   hipStream_t s = c->stream;
   int rc = SD_CAS_OK;
   hipEvent_t done[2] = {nullptr, nullptr};
@@ -1002,23 +1046,33 @@ int sd_cas_file_checksum(sd_cas_ctx* c, const char* path, char out_hex[65], int*
       for (int k = 0; k < i; k++) (void)hipEventDestroy(done[k]);
       return fail(c, SD_CAS_EHIP, "file_checksum: event create");
     }
-  // read segment `sgi` into pinned buffer b: returns its length (< cap at EOF), or -errno
-  auto read_seg = [&](uint64_t sgi, char* dst) -> int64_t {
+  bool irregular = false;  // parallel mode saw reads that a local regular file never gives
+  bool seq_stopped = false;  // sequential mode: the first short read has happened
+  // parallel: read segment `sgi` into dst with pread pieces; its length (< cap at EOF) or -errno
+  auto read_seg_par = [&](uint64_t sgi, char* dst) -> int64_t {
     const uint64_t off = sgi * cap;
     const uint64_t npieces = (cap + PIECE - 1) / PIECE;
-    std::atomic<uint64_t> next{0}, eof{cap};
+    std::atomic<uint64_t> next{0}, eof{cap}, data_end{0};
     std::atomic<int> rd_err{0};
+    std::atomic<bool> short_then_more{false};
     c->pool.run((unsigned)std::min<uint64_t>(8, npieces), [&]() {
       for (uint64_t p; (p = next.fetch_add(1)) < npieces && !rd_err.load();) {
         const uint64_t p0 = p * PIECE, pn = std::min(PIECE, cap - p0);
         if (p0 >= eof.load()) break;
         uint64_t got = 0;
+        bool was_short = false;
         while (got < pn) {
           ssize_t r = pread(fd, dst + p0 + got, pn - got, (off_t)(off + p0 + got));
           if (r < 0 && errno == EINTR) continue;
           if (r < 0) { rd_err.store(errno); break; }
-          if (r == 0) break;  // EOF: the first short read ends the file (hash.rs:18-20)
+          if (r == 0) break;
+          if (was_short) short_then_more.store(true);  // data after a short read
+          if ((uint64_t)r < pn - got) was_short = true;
           got += (uint64_t)r;
+        }
+        if (got) {
+          uint64_t cur = data_end.load();
+          while (p0 + got > cur && !data_end.compare_exchange_weak(cur, p0 + got)) {}
         }
         if (got < pn) {  // eof = min(eof, p0 + got)
           uint64_t cur = eof.load();
@@ -1027,17 +1081,38 @@ int sd_cas_file_checksum(sd_cas_ctx* c, const char* path, char out_hex[65], int*
       }
     });
     if (int e = rd_err.load()) return -(int64_t)e;
+    // bytes past the first end (a short piece whose successor still had data)
+    if (short_then_more.load() || data_end.load() > eof.load()) irregular = true;
     return (int64_t)eof.load();
   };
+  // sequential: hash.rs:15-21 — 1 MiB read()s in order, stop after the first short one
+  auto read_seg_seq = [&](char* dst) -> int64_t {
+    if (seq_stopped) return 0;
+    uint64_t got = 0;
+    while (got < cap) {
+      ssize_t r = read(fd, dst + got, BLOCK_LEN);
+      if (r < 0 && errno == EINTR) continue;
+      if (r < 0) return -(int64_t)errno;
+      got += (uint64_t)r;
+      if ((uint64_t)r != BLOCK_LEN) { seq_stopped = true; break; }
+    }
+    return (int64_t)got;
+  };
+  auto read_seg = [&](uint64_t sgi, char* dst) -> int64_t {
+    return seq ? read_seg_seq(dst) : read_seg_par(sgi, dst);
+  };
   uint8_t digest[32];
-  for (int attempt = 0; attempt < 2; attempt++) {
+  for (int attempt = 0; attempt < 3; attempt++) {
     const size_t sb = up256(cap + 16);
     if ((rc = ensure_pinned(c, 2 * sb)) || (rc = ensure(c, c->staging, 2 * sb))) break;
     if ((rc = ensure(c, c->ws, std::max(checksum_workspace_bytes(cap), checksum_workspace_bytes(1 << 20)))))
       break;
     char* pin[2] = {(char*)c->pinned, (char*)c->pinned + sb};
     char* dev[2] = {(char*)c->staging.p, (char*)c->staging.p + sb};
-    HIP_TRY(c, sd_ws_acquire(c, s));
+    if (hipError_t e = sd_ws_acquire(c, s); e != hipSuccess) {
+      rc = fail(c, SD_CAS_EHIP, "file_checksum: %s", hipGetErrorString(e));
+      break;
+    }
     // segment k is dispatched once it is known whether it is the only one (k == 0 waits for
     // segment 1's read); ROOT sits inside it only then
     auto dispatch = [&](uint64_t sgi, uint64_t len, bool only) -> int {
@@ -1052,41 +1127,72 @@ int sd_cas_file_checksum(sd_cas_ctx* c, const char* path, char out_hex[65], int*
       if (e != hipSuccess) return fail(c, SD_CAS_EHIP, "checksum segment: %s", hipGetErrorString(e));
       return SD_CAS_OK;
     };
+    auto io_fail = [&](int64_t neg) {
+      if (err_no) *err_no = (int)-neg;
+      return fail(c, SD_CAS_EIO, "read(%s): %s", path, strerror((int)-neg));
+    };
+    enum { DONE, GROW, GO_SEQ } next = DONE;
+    uint64_t nseg = 1, total = 0;
     int64_t len0 = read_seg(0, pin[0]);
-    if (len0 < 0) { if (err_no) *err_no = (int)-len0; rc = fail(c, SD_CAS_EIO, "read(%s): %s", path, strerror((int)-len0)); break; }
-    if ((uint64_t)len0 == cap && cap < SEG) { cap = SEG; continue; }  // grew past the buffer
-    uint64_t nseg = 1;
-    if ((uint64_t)len0 < cap) {
+    if (len0 < 0) {
+      rc = io_fail(len0);
+    } else if (irregular) {
+      next = GO_SEQ;
+    } else if ((uint64_t)len0 == cap && cap < SEG) {
+      next = GROW;  // grew past the buffer
+    } else if ((uint64_t)len0 < cap) {
+      total = (uint64_t)len0;
       rc = dispatch(0, (uint64_t)len0, true);
     } else {  // a full first segment: more may follow
-      uint64_t prev_len = (uint64_t)len0;
+      total = (uint64_t)len0;
       for (uint64_t sgi = 1;; sgi++) {
         const int b = (int)(sgi & 1);
         if (sgi >= 2 && hipEventSynchronize(done[b]) != hipSuccess) { rc = fail(c, SD_CAS_EHIP, "checksum: segment sync"); break; }
         const int64_t ln = read_seg(sgi, pin[b]);
-        if (ln < 0) { if (err_no) *err_no = (int)-ln; rc = fail(c, SD_CAS_EIO, "read(%s): %s", path, strerror((int)-ln)); break; }
+        if (ln < 0) { rc = io_fail(ln); break; }
+        if (irregular) { next = GO_SEQ; break; }
+        total += (uint64_t)ln;
         if (sgi == 1) {  // segment 0 is the only one iff nothing follows it
-          if ((rc = dispatch(0, prev_len, ln == 0))) break;
+          if ((rc = dispatch(0, (uint64_t)len0, ln == 0))) break;
         }
         if (ln == 0) { nseg = sgi; break; }
         if ((rc = dispatch(sgi, (uint64_t)ln, false))) break;
         if ((uint64_t)ln < cap) { nseg = sgi + 1; break; }
       }
     }
-    if (rc == SD_CAS_OK) {
+    // a regular file that ended before its st_size (it shrank, or a read came back short at
+    // a piece boundary): redo it the way hash.rs reads
+    if (rc == SD_CAS_OK && next == DONE && !seq && total < (uint64_t)st.st_size) next = GO_SEQ;
+    if (rc == SD_CAS_OK && next == DONE) {
       uint32_t* d_out = (uint32_t*)c->d_scalar;
       hipError_t e = hipSuccess;
       // reduce_cvs_device ping-pongs ceil(nseg / 256) CVs per level through ws
       const size_t red_ws = 2 * up256((nseg + 255) / 256 * 32) + 512;
-      if (nseg > 1 && (rc = ensure(c, c->ws, red_ws))) break;
-      if (nseg == 1) e = hipMemcpyAsync(d_out, c->cvbuf.p, 32, hipMemcpyDeviceToDevice, s);
-      else e = reduce_cvs_device((uint32_t*)c->cvbuf.p, nseg, d_out, c->ws.p, s);
-      if (e == hipSuccess) e = hipMemcpyAsync(digest, d_out, 32, hipMemcpyDeviceToHost, s);
-      if (e == hipSuccess) e = hipStreamSynchronize(s);
-      if (e != hipSuccess) rc = fail(c, SD_CAS_EHIP, "checksum reduce: %s", hipGetErrorString(e));
+      if (nseg > 1) rc = ensure(c, c->ws, red_ws);
+      if (rc == SD_CAS_OK) {
+        if (nseg == 1) e = hipMemcpyAsync(d_out, c->cvbuf.p, 32, hipMemcpyDeviceToDevice, s);
+        else e = reduce_cvs_device((uint32_t*)c->cvbuf.p, nseg, d_out, c->ws.p, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(digest, d_out, 32, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = fail(c, SD_CAS_EHIP, "checksum reduce: %s", hipGetErrorString(e));
+      }
     }
+    (void)hipStreamSynchronize(s);  // no segment copy may still read the pinned buffers
     (void)sd_ws_release(c, s);
-    break;
+    if (rc != SD_CAS_OK || next == DONE) break;
+    if (next == GROW) {
+      cap = SEG;
+    } else {  // GO_SEQ: from the start, hash.rs's reads
+      seq = true;
+      cap = SEG;
+      irregular = false;
+      if (lseek(fd, 0, SEEK_SET) != 0) {
+        if (err_no) *err_no = errno;
+        rc = fail(c, SD_CAS_EIO, "lseek(%s): %s", path, strerror(errno));
+        break;
+      }
+    }
+    if (attempt == 2) rc = fail(c, SD_CAS_EIO, "file_checksum(%s): no stable read", path);
   }
   close(fd);
   (void)hipStreamSynchronize(s);
@@ -1157,7 +1263,8 @@ int sd_cas_file_checksums(sd_cas_ctx* c, const char* const* paths, size_t n, cha
         struct stat st;
         if (stat(paths[i], &st) != 0) { status[i] = -errno; kind[i] = K_ERROR; continue; }
         fsize[i] = (uint64_t)st.st_size;
-        if (fsize[i] > CK_BIG) kind[i] = K_STREAM;
+        // not a regular file (FIFO, device, ...): hash.rs's sequential reads, streamed
+        if (fsize[i] > CK_BIG || !S_ISREG(st.st_mode)) kind[i] = K_STREAM;
       }
     });
   }
@@ -1239,15 +1346,21 @@ int sd_cas_file_checksums(sd_cas_ctx* c, const char* const* paths, size_t n, cha
         int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
         if (fd < 0) { status[i] = -errno; kind[i] = K_ERROR; h_lens[k] = 0; continue; }
         uint64_t got = 0;
+        bool was_short = false, irregular = false;
         while (got < cap[k]) {
           ssize_t r = pread(fd, data + h_offs[k] + got, cap[k] - got, (off_t)got);
           if (r < 0 && errno == EINTR) continue;
           if (r < 0) { status[i] = -errno; kind[i] = K_ERROR; break; }
-          if (r == 0) break;  // EOF: hash.rs stops at the first short read
+          if (r == 0) break;  // EOF
+          if (was_short) irregular = true;  // data after a short read: not a local file
+          if ((uint64_t)r < cap[k] - got) was_short = true;
           got += (uint64_t)r;
         }
         close(fd);
-        if (got == cap[k]) kind[i] = K_STREAM;  // grew past its slot: stream it afterwards
+        // grew past its slot, or read unlike a local regular file (a short read before the
+        // end, or an end before st_size): sd_cas_file_checksum afterwards, which reads such
+        // a file exactly as hash.rs:15-21 does (1 MiB reads, stop at the first short one)
+        if (kind[i] == K_BATCH && (got == cap[k] || irregular || got < fsize[i])) kind[i] = K_STREAM;
         h_lens[k] = kind[i] == K_BATCH ? got : 0;
       }
     });

@@ -95,7 +95,7 @@ LINK_CREATED, LINK_LINKED, LINK_DROPPED, LINK_NOT_REACHED = 0, 1, 2, 3
 NO_STEP = NO_OBJECT = 0xFFFFFFFF
 
 
-def replay_identifier_job(keys, states, chunk: int = 100):
+def replay_identifier_job(keys, states, chunk: int = 100, with_creates: bool = False):
     """Literal replay of one file-identifier job over a fresh library, DB state included:
     file_identifier_job.rs:86-178 (init: orphan count, ceil(n/chunk) steps, cursor = first
     orphan id), :180-236 (execute_step: get_orphan_file_paths = orphan rows with id >=
@@ -105,7 +105,9 @@ def replay_identifier_job(keys, states, chunk: int = 100):
     ascending row) and mod.rs:401-405 (the next cursor = the chunk's last row).
     Rows: file_path ids 0..n-1, all orphan at init (object_id and cas_id NULL).
     Returns (step[], object[], action[], [(created, linked)] per step) where object[i] is
-    the row that created the Object row i is connected to."""
+    the row that created the Object row i is connected to; with_creates: also the rows that
+    created an Object in each step (a re-queried empty row appears in every step it was
+    processed in)."""
     n = len(keys)
     cas_col = [None] * n         # file_path.cas_id
     obj_col = [None] * n         # file_path.object_id
@@ -115,6 +117,7 @@ def replay_identifier_job(keys, states, chunk: int = 100):
     processed_ok = [False] * n   # last processing of the row succeeded
     processed = [False] * n
     counts = []
+    step_creates = []
     cursor = 0
     for k in range(-(-n // chunk) if chunk else 0):
         rows = []
@@ -144,6 +147,7 @@ def replay_identifier_job(keys, states, chunk: int = 100):
                 obj_col[r] = existing[c][0]
                 linked += 1
         created = 0
+        step_creates.append([])
         for r in sorted(meta):                       # :246-347 one new Object per remaining row
             c = meta[r]
             if c is None or c not in existing:
@@ -153,6 +157,7 @@ def replay_identifier_job(keys, states, chunk: int = 100):
                 if c is not None:
                     cas_objects.setdefault(c, []).append(oid)
                 created += 1
+                step_creates[-1].append(r)
         counts.append((created, linked))
         cursor = rows[-1]                            # mod.rs:401-405
     obj = [NO_OBJECT] * n
@@ -165,6 +170,8 @@ def replay_identifier_job(keys, states, chunk: int = 100):
             continue
         obj[r] = creator[obj_col[r]]
         act[r] = LINK_CREATED if obj[r] == r else LINK_LINKED
+    if with_creates:
+        return step, obj, act, counts, step_creates
     return step, obj, act, counts
 
 

@@ -150,8 +150,8 @@ def test_generate_from_paths_and_errors(eng, oracle, tmp_path):
     for i in list(range(7)) + [9, 10, 11]:
         assert errs[i] == 0, i
         assert f"{keys[i]:016x}" == oracle.generate_cas_id(paths[i], sizes[i]), i
-    assert errs[7] == 2  # ENOENT
-    assert errs[8] == 5  # EIO (UnexpectedEof)
+    assert errs[7] == -2  # ENOENT
+    assert errs[8] == -5  # EIO (UnexpectedEof)
     # the single-file drop-in raises like io::Error
     assert sd.generate_cas_id(paths[5], sizes[5]) == oracle.generate_cas_id(paths[5], sizes[5])
     with pytest.raises(OSError):
@@ -173,7 +173,7 @@ def test_from_paths_stale_sampled_footer(eng, oracle, tmp_path):
         except UnexpectedEof:
             want = None
         if want is None:
-            assert e == 5 and k == 0, (path, size)
+            assert e == -5 and k == 0, (path, size)
         else:
             assert e == 0 and f"{k:016x}" == want == oracle.generate_cas_id(path, size), (path, size)
 
@@ -192,12 +192,73 @@ def test_from_paths_windowed_pipeline(eng, oracle, tmp_path):
     keys, errs = eng.generate_cas_keys_from_paths(paths, sizes)
     for i in range(n):
         if i % 997 == 13:
-            assert errs[i] == 2 and keys[i] == 0, i
+            assert errs[i] == -2 and keys[i] == 0, i
         else:
             assert errs[i] == 0, i
     check = [i for i in range(n) if i % 997 != 13][::7]
     bad = [i for i in check if f"{keys[i]:016x}" != oracle.generate_cas_id(paths[i], sizes[i])]
     assert not bad, bad[:5]
+
+
+def test_from_paths_file_metadata_rules(eng, oracle, tmp_path):
+    """FileMetadata::new's rules behind the ABI (file_identifier/mod.rs:55-95): with the
+    metadata taken by the library (sizes NULL) a file emptied after it was indexed gets no
+    cas_id (SD_CAS_STATUS_NO_CAS, key 0), a directory is refused with EISDIR (the reference
+    asserts, :67-70), a missing path is ENOENT, a symlink is followed (fs::metadata); with
+    caller sizes a 0 is NO_CAS without any read.  The rows then go through the link emission
+    vs the literal job replay, the NO_CAS row at a chunk end included."""
+    import errno
+
+    import spacedrive_amd as sd
+    from oracle.pyoracle import py_generate_cas_id_file
+    rng = np.random.default_rng(31)
+    paths, indexed = [], []
+    for i in range(14):
+        p = tmp_path / f"m{i:02d}"
+        size = [700, 102400, 102401, 333_333][i % 4]
+        p.write_bytes(rng.integers(0, 256, size, dtype=np.uint8).tobytes())
+        paths.append(str(p))
+        indexed.append(size)
+    # row 5 (the last row of the second chunk of 3): emptied after indexing
+    with open(paths[5], "wb"):
+        pass
+    os.symlink(paths[2], str(tmp_path / "link"))
+    paths[8] = str(tmp_path / "link")
+    os.mkdir(str(tmp_path / "adir"))
+    paths[10] = str(tmp_path / "adir")
+    paths[12] = str(tmp_path / "gone")
+    keys, status = eng.generate_cas_keys_from_paths(paths, None)
+    states, want_keys = [], []
+    for i, p in enumerate(paths):
+        if i == 5:
+            assert status[i] == sd.cas.STATUS_NO_CAS and keys[i] == 0
+            states.append(1); want_keys.append(0)
+        elif i == 10:
+            assert status[i] == -errno.EISDIR and keys[i] == 0
+            states.append(2); want_keys.append(0)
+        elif i == 12:
+            assert status[i] == -errno.ENOENT and keys[i] == 0
+            states.append(2); want_keys.append(0)
+        else:
+            size = os.stat(p).st_size
+            want = py_generate_cas_id_file(p, size)
+            assert status[i] == 0 and f"{keys[i]:016x}" == want == oracle.generate_cas_id(p, size), i
+            states.append(0); want_keys.append(int(want, 16))
+    # caller-given metadata: a length of 0 is NO_CAS (not read), a directory still EISDIR
+    k2, s2 = eng.generate_cas_keys_from_paths([paths[5], paths[10], paths[0]], [0, 4096, 700])
+    assert list(s2) == [sd.cas.STATUS_NO_CAS, -errno.EISDIR, 0] and k2[0] == 0 and k2[2] == keys[0]
+    # the job over these rows: decisions and per-step batches vs the literal replay
+    for chunk in (3, 100):
+        res = sd.identifier_job_step(paths, chunk=chunk, eng=eng)
+        step, obj, act, counts, creates = replay_identifier_job(want_keys, states, chunk, with_creates=True)
+        assert res.errors == {10: errno.EISDIR, 12: errno.ENOENT}
+        assert [(b.total_created, b.total_linked) for b in res.steps] == counts
+        assert [b.creates for b in res.steps] == creates
+        assert {i: o for i, (o, a) in enumerate(zip(obj, act)) if a in (0, 1)} == res.object_of
+        assert res.metadata[5].cas_id is None
+    assert 5 in res.steps[0].creates  # chunk 100: one step
+    res3 = sd.identifier_job_step(paths, chunk=3, eng=eng)
+    assert 5 in res3.steps[1].creates and 5 in res3.steps[2].creates  # re-queried NO_CAS row
 
 
 def test_sort_pairs_vs_numpy(eng):
@@ -507,6 +568,78 @@ def test_file_checksum_reads_to_eof(eng, oracle):
     if not os.path.exists(p) or os.stat(p).st_size != 0:
         pytest.skip("no procfs file with st_size 0")
     assert eng.file_checksum(p) == oracle.file_checksum(p) == oracle.blake3(open(p, "rb").read()).hex()
+
+
+def _short_read_files():
+    """procfs seq_files whose first 1 MiB read() returns less than the whole file (about one
+    page): hash.rs:15-21 stops there.  Returns [(path, first read, rest)]."""
+    out = []
+    for p in ("/proc/self/mountinfo", "/proc/kallsyms", "/proc/self/mounts"):
+        try:
+            fd = os.open(p, os.O_RDONLY)
+        except OSError:
+            continue
+        try:
+            first = os.read(fd, 1 << 20)
+            rest = os.read(fd, 1 << 20)
+        finally:
+            os.close(fd)
+        if 0 < len(first) < (1 << 20) and rest:
+            out.append((p, first, rest))
+    return out
+
+
+def test_file_checksum_short_reads(eng, oracle):
+    """hash.rs:15-21 issues 1 MiB reads and stops after the FIRST short one.  A procfs
+    seq_file returns about one page per read, so the reference hashes only that page — and
+    so must both entry points (sd_cas_file_checksum and the batched sd_cas_file_checksums'
+    redo path), vs the oracle's literal read loop on the same file."""
+    files = _short_read_files()
+    if not files:
+        pytest.skip("no procfs seq_file longer than one read")
+    for p, first, rest in files[:2]:
+        want = oracle.file_checksum(p)
+        assert want == oracle.blake3(first).hex(), p  # the literal loop hashed one read
+        assert want != oracle.blake3(first + rest).hex()
+        assert eng.file_checksum(p) == want, p
+        digests, errs = eng.file_checksums([p, "/proc/sys/kernel/ostype", p])
+        assert list(errs) == [0, 0, 0]
+        assert digests[0] == digests[2] == want, p
+
+
+def test_file_checksum_fifo(eng, oracle, tmp_path):
+    """A FIFO is not a regular file: its reads return what the writer has written so far.
+    The writer puts 4,000 bytes (< PIPE_BUF: one atomic write), waits, then writes more; the
+    first 1 MiB read returns the 4,000 bytes and hash.rs:15-21 stops there — both entry
+    points must hash exactly those bytes."""
+    import threading
+    import time
+    rng = np.random.default_rng(32)
+    a = rng.integers(0, 256, 4000, dtype=np.uint8).tobytes()
+    b = rng.integers(0, 256, 70_000, dtype=np.uint8).tobytes()
+    want = oracle.blake3(a).hex()
+    for entry in ("one", "batch"):
+        fifo = str(tmp_path / f"fifo_{entry}")
+        os.mkfifo(fifo)
+
+        def writer():
+            try:
+                with open(fifo, "wb", buffering=0) as fh:
+                    fh.write(a)
+                    time.sleep(0.5)
+                    fh.write(b)
+            except BrokenPipeError:
+                pass  # the reader stopped after its first short read
+        t = threading.Thread(target=writer, daemon=True)
+        t.start()
+        if entry == "one":
+            got = eng.file_checksum(fifo)
+        else:
+            digests, errs = eng.file_checksums([fifo])
+            assert errs[0] == 0
+            got = digests[0]
+        t.join(5)
+        assert got == want, entry
 
 
 def test_checksums_batch_dev_vs_oracle(eng, oracle):
@@ -914,13 +1047,17 @@ def test_identifier_job_step(eng, oracle, tmp_path):
             continue
         want = None if states[i] else f"{keys[i]:016x}"
         assert res.metadata[i].cas_id == want
-    step, obj, act, counts = replay_identifier_job(keys, states, 100)
+    step, obj, act, counts, creates = replay_identifier_job(keys, states, 100, with_creates=True)
     assert {i: o for i, (o, a) in enumerate(zip(obj, act)) if a in (0, 1)} == res.object_of
     assert [(b.total_created, b.total_linked) for b in res.steps] == counts
     assert (res.total_created, res.total_linked) == tuple(map(sum, zip(*counts)))
-    assert 99 in [r for b in res.steps for r in b.creates] or step[99] == 1  # re-queried row
+    # every step's create batch, including the empty row 198 that ends step 1's chunk and is
+    # created again by step 2 (creates.len() == total_created per step)
+    assert [b.creates for b in res.steps] == creates
+    assert 198 in res.steps[1].creates and 198 in res.steps[2].creates
     for b in res.steps:
-        assert all(step[r] == b.step and act[r] == 0 for r in b.creates)
+        assert len(b.creates) == b.total_created
+        assert all(act[r] == 0 for r in b.creates)
         assert all(step[r] == b.step and obj[r] == o and act[r] == 1 for r, o in b.links)
 
 
