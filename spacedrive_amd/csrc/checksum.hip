@@ -18,6 +18,7 @@
 
 #include "blake3_device.hpp"
 #include "sd_checksum.h"
+#include "sd_debug.h"
 #include "sd_group.h"
 
 #include <algorithm>
@@ -309,10 +310,11 @@ sd_b3_batch_count(const uint64_t* __restrict__ offs, const uint64_t* __restrict_
 
 // owner[item] = the last f with gstart[f] <= item (every listed buffer owns >= 1 item)
 extern "C" __global__ void __launch_bounds__(256)
-sd_b3_batch_owner(const uint32_t* __restrict__ gstart, const uint32_t* __restrict__ groups,
+sd_b3_batch_owner(const uint32_t* __restrict__ gstart, const unsigned long long* __restrict__ gtotal,
                   uint64_t n, uint64_t items_cap, uint32_t* __restrict__ owner) {
-  const uint64_t total = (uint64_t)gstart[n - 1] + groups[n - 1];
-  const uint64_t lim = total < items_cap ? total : items_cap;
+  const uint64_t total = *gtotal;
+  if (total > items_cap) return;  // overlapping buffers: the list does not fit (reported below)
+  const uint64_t lim = total;
   for (uint64_t item = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; item < lim;
        item += (uint64_t)gridDim.x * blockDim.x) {
     uint64_t lo = 0, hi = n;  // gstart[lo] <= item < gstart[hi] (gstart[n] = total)
@@ -320,6 +322,10 @@ sd_b3_batch_owner(const uint32_t* __restrict__ gstart, const uint32_t* __restric
       const uint64_t mid = (lo + hi) >> 1;
       if (gstart[mid] <= item) lo = mid; else hi = mid;
     }
+    // the search needs a monotone gstart: item inside its owner's range
+    SD_DBG_CHECK(gstart[lo] <= item && (lo + 1 == n || item < gstart[lo + 1]),
+                 "batch owner: item %llu -> buffer %llu [%u, %u)", (unsigned long long)item,
+                 (unsigned long long)lo, gstart[lo], lo + 1 < n ? gstart[lo + 1] : (uint32_t)total);
     owner[item] = (uint32_t)lo;
   }
 }
@@ -734,10 +740,13 @@ extern "C" __global__ void __launch_bounds__(GROUP) __attribute__((amdgpu_waves_
 sd_b3_batch_groups(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                    const uint64_t* __restrict__ lens, const uint32_t* __restrict__ gstart,
                    const uint32_t* __restrict__ groups, const uint32_t* __restrict__ owner,
+                   const unsigned long long* __restrict__ gtotal,
                    uint64_t n, uint64_t items_cap, uint32_t* __restrict__ cvs_out,
                    uint32_t* __restrict__ digests, uint32_t* __restrict__ bad) {
   __shared__ uint32_t cvs[GROUP * K3_LANE_CHUNKS][8];
-  const uint64_t total = (uint64_t)gstart[n - 1] + groups[n - 1];
+  // the true (u64) total: overlapping buffers can sum past 2^32 groups, where the u32
+  // gstart scan wraps and a wrapped total would pass this check
+  const uint64_t total = *gtotal;
   if (total > items_cap) {  // lengths beyond arena_bytes: the CV list would overflow
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(bad, 2u);
     return;
@@ -762,11 +771,11 @@ sd_b3_batch_groups(const uint8_t* __restrict__ arena, const uint64_t* __restrict
 // instead of one workgroup walking all 16,384 CVs, 0.38 ms).
 extern "C" __global__ void __launch_bounds__(GROUP)
 sd_b3_batch_blocks(const uint32_t* __restrict__ gstart, const uint32_t* __restrict__ groups,
-                   const uint32_t* __restrict__ owner, uint64_t n, uint64_t items_cap,
-                   uint32_t* __restrict__ cvs) {
+                   const uint32_t* __restrict__ owner, const unsigned long long* __restrict__ gtotal,
+                   uint64_t n, uint64_t items_cap, uint32_t* __restrict__ cvs) {
   __shared__ uint32_t work[GROUP][8];
   const uint32_t t = threadIdx.x;
-  const uint64_t total = (uint64_t)gstart[n - 1] + groups[n - 1];
+  const uint64_t total = *gtotal;
   if (total > items_cap) return;
   const uint64_t w0 = (uint64_t)blockIdx.x * GROUP;
   if (w0 >= total) return;
@@ -796,13 +805,13 @@ sd_b3_batch_blocks(const uint32_t* __restrict__ gstart, const uint32_t* __restri
 // sd_b3_batch_blocks left at stride 256) pair-and-promote to the ROOT digest in LDS.
 extern "C" __global__ void __launch_bounds__(GROUP)
 sd_b3_batch_reduce(const uint32_t* __restrict__ gstart, const uint32_t* __restrict__ groups,
-                   uint64_t n, uint64_t items_cap, const uint32_t* __restrict__ cvs_in,
-                   uint32_t* __restrict__ digests) {
+                   const unsigned long long* __restrict__ gtotal, uint64_t n, uint64_t items_cap,
+                   const uint32_t* __restrict__ cvs_in, uint32_t* __restrict__ digests) {
   __shared__ uint32_t work[GROUP][8];
   __shared__ uint32_t list[GROUP];
   __shared__ uint32_t listed;
   const uint32_t t = threadIdx.x;
-  if ((uint64_t)gstart[n - 1] + groups[n - 1] > items_cap) return;
+  if (*gtotal > items_cap) return;
   // the workgroup scans a window of up to 256 buffers in parallel and lists those with >= 2
   // groups (one buffer per workgroup iteration cost a dependent load per buffer: 0.4 ms for
   // a batch of 1 M small buffers, none of them multi-group); windows of n / grid buffers
@@ -814,6 +823,8 @@ sd_b3_batch_reduce(const uint32_t* __restrict__ gstart, const uint32_t* __restri
     if (t < win && base + t < n && groups[base + t] >= 2) list[atomicAdd(&listed, 1u)] = t;
     __syncthreads();
     const uint32_t k = listed;
+    SD_DBG_CHECK(t != 0 || k <= win, "batch reduce: %u buffers listed in a window of %llu", k,
+                 (unsigned long long)win);
     for (uint32_t i = 0; i < k; ++i) {
       const uint64_t f = base + list[i];
       const uint32_t cnt = groups[f];
@@ -848,6 +859,8 @@ hipError_t checksum_single_setup(uint64_t* d_ol, uint64_t len, uint32_t* d_bad, 
 
 static inline size_t al256c(size_t x) { return (x + 255) / 256 * 256; }
 
+SD_DBG_ACCESSOR(sd_dbg_violations_checksum)
+
 // work items of the big-buffer list: <= n + arena_bytes / 1 MiB (disjoint buffers)
 static inline uint64_t batch_items_cap(uint64_t n, uint64_t arena_bytes) {
   return n + arena_bytes / (GROUP_CHUNKS * 1024) + 1;
@@ -856,10 +869,10 @@ static inline uint64_t batch_items_cap(uint64_t n, uint64_t arena_bytes) {
 static inline bool lane_path(uint64_t n) { return n >= LANE_MIN_BUFFERS; }
 
 size_t checksum_batch_workspace_bytes(uint64_t n, uint64_t arena_bytes) {
-  // groups | gstart | scan partials | owner | cvs
+  // groups | gstart | scan partials | group total (u64) | owner | cvs
   //   [| lane class total | lane keys | sorted keys | order | sort ws]
   const uint64_t items = batch_items_cap(n, arena_bytes);
-  size_t b = 2 * al256c((n + 1) * 4) + al256c((n / 4096 + 2) * 4) + al256c(items * 4) +
+  size_t b = 2 * al256c((n + 1) * 4) + al256c((n / 4096 + 2) * 4) + 256 + al256c(items * 4) +
              al256c(items * 32);
   if (lane_path(n)) b += 256 + 2 * al256c(n * 8) + al256c(n * 4) + sort_workspace_bytes(n);
   return b + 256;
@@ -871,10 +884,13 @@ hipError_t checksum_batch_device(const uint8_t* arena, uint64_t arena_bytes, con
   if (n == 0) return hipSuccess;
   if (n > (1ull << 24)) return hipErrorInvalidValue;  // the u32 scan: <= 4096^2 buffers
   const uint64_t items = batch_items_cap(n, arena_bytes);
+  // item indices (owner, gstart) are u32: an arena past 4 PiB is refused
+  if (items > 0xFFFFFFFFull) return hipErrorInvalidValue;
   char* p = (char*)ws;
   uint32_t* groups = (uint32_t*)p; p += al256c((n + 1) * 4);
   uint32_t* gstart = (uint32_t*)p; p += al256c((n + 1) * 4);
   uint32_t* partial = (uint32_t*)p; p += al256c((n / 4096 + 2) * 4);
+  unsigned long long* gtotal = (unsigned long long*)p; p += 256;
   uint32_t* owner = (uint32_t*)p; p += al256c(items * 4);
   uint32_t* cvs = (uint32_t*)p; p += al256c(items * 32);
   const bool lane = lane_path(n);
@@ -883,10 +899,10 @@ hipError_t checksum_batch_device(const uint8_t* arena, uint64_t arena_bytes, con
   if (lane) { lane_info = (uint32_t*)p; p += 256; }
   const uint32_t nb = (uint32_t)((n + 255) / 256);
   sd_b3_batch_count<<<nb, 256, 0, s>>>(offs, lens, n, arena_bytes, groups, d_bad, lane_info);
-  hipError_t e = exclusive_scan_u32(groups, gstart, n, partial, s);
+  hipError_t e = exclusive_scan_u32(groups, gstart, n, partial, s, gtotal);
   if (e != hipSuccess) return e;
   sd_b3_batch_owner<<<(uint32_t)std::min<uint64_t>((items + 255) / 256, 2048), 256, 0, s>>>(
-      gstart, groups, n, items, owner);
+      gstart, gtotal, n, items, owner);
   if (lane) {
     // buffers of <= lane_cut() chunks one per lane, by descending chunk count
     uint64_t* lkeys = (uint64_t*)p; p += al256c(n * 8);
@@ -910,11 +926,11 @@ hipError_t checksum_batch_device(const uint8_t* arena, uint64_t arena_bytes, con
   // big buffers: a grid of up to 65,536 workgroups strides over the item list (those past
   // the list's end exit at once)
   sd_b3_batch_groups<<<(uint32_t)std::min<uint64_t>(items, 65536), GROUP, 0, s>>>(
-      arena, offs, lens, gstart, groups, owner, n, items, cvs, d_digests, d_bad);
+      arena, offs, lens, gstart, groups, owner, gtotal, n, items, cvs, d_digests, d_bad);
   sd_b3_batch_blocks<<<(uint32_t)((items + GROUP - 1) / GROUP), GROUP, 0, s>>>(
-      gstart, groups, owner, n, items, cvs);
+      gstart, groups, owner, gtotal, n, items, cvs);
   sd_b3_batch_reduce<<<(uint32_t)std::min<uint64_t>(n, 256 * 4), GROUP, 0, s>>>(
-      gstart, groups, n, items, cvs, d_digests);
+      gstart, groups, gtotal, n, items, cvs, d_digests);
   return hipGetLastError();
 }
 

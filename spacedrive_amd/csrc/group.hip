@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "sd_debug.h"
 #include "sd_group.h"
 
 namespace sdcas {
@@ -137,6 +138,10 @@ __device__ __forceinline__ void downsweep_body(const uint64_t* __restrict__ keys
     wc[0][t] = 0; wc[1][t] = 0; wc[2][t] = 0; wc[3][t] = 0;
   }
   __syncthreads();
+  // conservation: the per-wave digit counts of every round add up to the tile's count of
+  // digit t from the upsweep (the round-2 race lost exactly such a count)
+  SD_DBG_CHECK(run[t] == cnt, "downsweep tile %u digit %u: ranked %u, counted %u", blockIdx.x, t,
+               run[t], cnt);
   for (uint32_t s = t; s < tile_n; s += SORT_THREADS) {
     const uint64_t k = skey[s];
     const uint32_t d = digit_of(k, shift, mask);
@@ -356,6 +361,22 @@ sd_group_emit(const uint64_t* __restrict__ skeys, const uint32_t* __restrict__ s
   }
 }
 
+// *total = sum of v[0..m) in u64 (one workgroup; m <= SCAN_TILE tile sums, or one tile):
+// callers of a u32 scan whose sum may pass 2^32 check the true total with it
+extern "C" __global__ void __launch_bounds__(SCAN_THREADS)
+sd_sum_u32_block(const uint32_t* __restrict__ v, uint64_t m, unsigned long long* __restrict__ total) {
+  __shared__ unsigned long long red[SCAN_THREADS];
+  unsigned long long acc = 0;
+  for (uint64_t i = threadIdx.x; i < m; i += SCAN_THREADS) acc += v[i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int h = SCAN_THREADS / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total = red[0];
+}
+
 // chunk-of-`chunk` reference emulation (mod.rs:202-311):
 // rep_c[i] = i if canonical rep is in i's own chunk, else canonical rep.
 extern "C" __global__ void __launch_bounds__(256)
@@ -397,6 +418,8 @@ sd_gather_vals(const uint32_t* __restrict__ vals, const uint32_t* __restrict__ r
 // ---- host launchers ----------------------------------------------------------------
 namespace sdcas {
 
+SD_DBG_ACCESSOR(sd_dbg_violations_group)
+
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 static inline uint32_t tiles_of(uint64_t n, uint64_t tile) { return (uint32_t)((n + tile - 1) / tile); }
 
@@ -414,14 +437,17 @@ size_t group_workspace_bytes(uint64_t n) {
 }
 
 hipError_t exclusive_scan_u32(const uint32_t* in, uint32_t* out, uint64_t m, uint32_t* partial,
-                              hipStream_t s) {
+                              hipStream_t s, unsigned long long* total) {
   const uint32_t nt = tiles_of(m, SCAN_TILE);
   if (nt <= 1) {
+    if (total) sd_sum_u32_block<<<1, SCAN_THREADS, 0, s>>>(in, m, total);
     sd_scan_tiles<<<1, SCAN_THREADS, 0, s>>>(in, m, out, nullptr);
     return hipGetLastError();
   }
   if (nt > (uint32_t)SCAN_TILE) return hipErrorInvalidValue;
   sd_scan_reduce<<<nt, SCAN_THREADS, 0, s>>>(in, m, partial);
+  // the tile sums before their (u32) scan: the true total, even when the scan wraps
+  if (total) sd_sum_u32_block<<<1, SCAN_THREADS, 0, s>>>(partial, nt, total);
   sd_scan_tiles<<<1, SCAN_THREADS, 0, s>>>(partial, nt, partial, nullptr);
   sd_scan_tiles<<<nt, SCAN_THREADS, 0, s>>>(in, m, out, partial);
   return hipGetLastError();

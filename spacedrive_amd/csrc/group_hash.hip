@@ -37,6 +37,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "sd_debug.h"
 #include "sd_group.h"
 
 namespace sdcas {
@@ -141,6 +142,20 @@ __device__ void part_totals_body(const uint64_t* __restrict__ keys, uint64_t n, 
     }
   }
   __syncthreads();
+#if SD_DBG
+  {  // conservation: the block's bucket counts add up to its slice
+    __shared__ unsigned int dbg_sum;
+    if (threadIdx.x == 0) dbg_sum = 0;
+    __syncthreads();
+    unsigned int part = 0;
+    for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS) part += cnt[b];
+    atomicAdd(&dbg_sum, part);
+    __syncthreads();
+    const uint64_t want = hi > lo ? hi - lo : 0;
+    SD_DBG_CHECK(threadIdx.x != 0 || dbg_sum == want, "part_totals block %u counted %u of %llu keys",
+                 blockIdx.x, dbg_sum, (unsigned long long)want);
+  }
+#endif
   uint32_t* mine = totals + (uint64_t)(blockIdx.x % repl) * nb;
   for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS)
     if (cnt[b]) atomicAdd(&mine[b], cnt[b]);
@@ -197,6 +212,10 @@ __device__ __forceinline__ void staged_trip(const uint64_t (&k)[ITEMS], const ui
       if (tcnt[b]) gcur[b] = bstart[b] + atomicAdd(&fill[b], tcnt[b]);
   }
   lds_exclusive_scan(tcnt, tstart, nb);  // (its barriers also publish gcur)
+  // conservation: the trip's per-bucket counts add up to the trip
+  SD_DBG_CHECK(threadIdx.x != 0 || tstart[nb - 1] + tcnt[nb - 1] == trip_n,
+               "staged trip (block %u) counted %u of %u keys", blockIdx.x,
+               tstart[nb - 1] + tcnt[nb - 1], trip_n);
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const uint32_t t = (uint32_t)j * PART_THREADS + threadIdx.x;
@@ -399,6 +418,9 @@ sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict_
   }
   if (s < e) load(s, true);  // the scatter pass's first trip, in flight during the plan
   __syncthreads();
+#if SD_DBG
+  __shared__ uint32_t dbg_end[MAX_FINE];  // where each fine bucket's cursor must end
+#endif
   if (threadIdx.x == 0) {
     uint32_t run = (uint32_t)s;
     for (uint32_t j = 0; j < nb2; ++j) {
@@ -406,7 +428,12 @@ sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict_
       gcur[j] = run;
       starts[(uint64_t)c * nb2 + j] = run;
       run += x;
+#if SD_DBG
+      dbg_end[j] = run;
+#endif
     }
+    SD_DBG_CHECK(run == (uint32_t)e, "refine bucket %u: fine counts add to %u, segment ends at %llu",
+                 c, run, (unsigned long long)e);
   }
   if (threadIdx.x < nb2) tcnt[threadIdx.x] = 0;
   __syncthreads();
@@ -421,6 +448,11 @@ sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict_
     staged_trip<false>(k, q, left < PART_TILE ? (uint32_t)left : PART_TILE, nb2, bfn, gcur, tcnt,
                        tstart, skey, spos, nullptr, nullptr, out_keys, out_pos);
   }
+  // conservation: every fine bucket's cursor advanced by exactly its count (rows written ==
+  // rows counted); staged_trip's last barrier published gcur
+  SD_DBG_CHECK(threadIdx.x >= nb2 || gcur[threadIdx.x] == dbg_end[threadIdx.x],
+               "refine bucket %u.%u: cursor %u, expected %u", c, threadIdx.x, gcur[threadIdx.x],
+               dbg_end[threadIdx.x]);
 }
 
 // Home slot of a (mixed, uniform) key in a TBL-slot table — its low bits for a power of two,
@@ -548,6 +580,10 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
   const uint64_t empty = (uint64_t)(b ^ 1u) << (64 - bits);
   for (uint32_t i = threadIdx.x; i < TBL; i += THREADS) { tk[i] = empty; tv[i] = 0xFFFFFFFFu; }
   if (threadIdx.x == 0) { distinct = 0; ovf[0] = 0; ovf[1] = 0; }
+#if SD_DBG
+  __shared__ unsigned int dbg_seen;  // keys inserted: must be the bucket's e - s
+  if (threadIdx.x == 0) dbg_seen = 0;
+#endif
   uint64_t k[ITEMS];
   uint32_t p[ITEMS], v[ITEMS], sl[ITEMS];
   uint32_t trip = 0;
@@ -578,9 +614,18 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
       }
     }
     if ((fresh && atomicAdd(&distinct, fresh) + fresh > FILL) || !ok) ovf[trip & 1] = 1;
+#if SD_DBG
+    unsigned int seen = 0;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) seen += k[j] != empty;
+    if (seen) atomicAdd(&dbg_seen, seen);
+#endif
   }
   __syncthreads();
   const bool overflow = ovf[0] | ovf[1];
+  SD_DBG_CHECK(threadIdx.x != 0 || overflow || (dbg_seen == e - s && distinct <= e - s),
+               "bucket %u: inserted %u of %llu keys, %u distinct", b, dbg_seen,
+               (unsigned long long)(e - s), distinct);
   if (!overflow) {
     if (e - s <= TILE) {  // the one trip's keys and their slots are still in registers
 #pragma unroll
@@ -744,6 +789,18 @@ sd_zero_words(uint32_t* __restrict__ p, uint32_t n) {
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) p[i] = 0;
 }
 
+#if SD_DBG
+// conservation of the coarse scatter: every (totals replica, bucket) sub-run was reserved
+// exactly as far as it was counted (rows reserved == rows counted == rows written)
+extern "C" __global__ void __launch_bounds__(256)
+sd_dbg_fill_check(const uint32_t* __restrict__ totals, const uint32_t* __restrict__ fill, uint32_t n) {
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+    SD_DBG_CHECK(fill[i] == totals[i], "scatter sub-run %u: reserved %u, counted %u", i, fill[i],
+                 totals[i]);
+}
+SD_DBG_ACCESSOR(sd_dbg_violations_group_hash)
+#endif
+
 // totals (zeroed here unless the caller guarantees them zero) -> bucket-contiguous
 // (out_keys, out_pos); starts_out / counts_out
 static hipError_t run_partition(const uint64_t* keys, uint64_t n, const PartPlan& p, int mode,
@@ -767,6 +824,9 @@ static hipError_t run_partition(const uint64_t* keys, uint64_t n, const PartPlan
     sd_part_scatter_range<<<p.nblk, PART_THREADS, slds, s>>>(keys, n, p.nb, p.per_block, totals,
                                                              repl, fill, out_keys, out_pos, counts_out);
   }
+#if SD_DBG
+  sd_dbg_fill_check<<<(words + 255) / 256, 256, 0, s>>>(totals, fill, words);
+#endif
   return hipGetLastError();
 }
 

@@ -33,8 +33,9 @@ hipError_t group_sorted(const uint64_t* skeys, const uint32_t* svals, uint64_t n
                         uint64_t* d_objects, void* ws, hipStream_t stream);
 
 // Device-wide exclusive scan of m <= 4096^2 u32 (partial: >= m/4096 + 1 u32 of scratch).
+// total (optional, device): the sum of in[] in u64 — exact even where the u32 scan wraps.
 hipError_t exclusive_scan_u32(const uint32_t* in, uint32_t* out, uint64_t m, uint32_t* partial,
-                              hipStream_t stream);
+                              hipStream_t stream, unsigned long long* total = nullptr);
 
 // ---- group_hash.hip: grouping without a full sort -------------------------------------
 bool hash_group_supported(uint64_t n);

@@ -32,6 +32,21 @@
 
 using namespace sdcas;
 
+#include "sd_debug.h"
+#if SD_DBG
+namespace sdcas {
+uint32_t sd_dbg_violations_group_hash();
+uint32_t sd_dbg_violations_group();
+uint32_t sd_dbg_violations_checksum();
+}  // namespace sdcas
+// debug library only (libsd_hip_cas_debug.so, not in the ABI header): invariant violations
+// counted by the device checks of sd_debug.h since the library was loaded
+extern "C" uint64_t sd_cas_debug_violations(void) {
+  return (uint64_t)sd_dbg_violations_group_hash() + sd_dbg_violations_group() +
+         sd_dbg_violations_checksum();
+}
+#endif
+
 #include "ctx_internal.h"
 
 // short local names for the shared helpers

@@ -728,6 +728,33 @@ def test_checksums_batch_lane_path(eng, oracle, shape):
     torch.cuda.empty_cache()
 
 
+def test_checksums_batch_overlapping_buffers_refused(eng, oracle):
+    """The ABI does not forbid overlapping buffers, but their subtree work list can exceed
+    the workspace sized from arena_bytes: such a batch is refused with EINVAL, never read
+    out of bounds — including 4,194,305 buffers of (0, 1 GiB) in a 1 GiB arena, whose 2^32 +
+    1,024 subtree groups wrap the u32 group scan to 1,024 (the wrapped total used
+    to pass the check).  A valid call on the same context works afterwards."""
+    G = 1 << 30
+    arena = torch.empty(G + 64, dtype=torch.uint8, device="cuda")
+    eng.synth_stream(58, 1, 0, 1 << 20, arena)
+    for n, L in [(64, 64 << 20), (4_194_305, G)]:
+        offs = torch.zeros(n, dtype=torch.int64, device="cuda")
+        lens = torch.full((n,), L, dtype=torch.int64, device="cuda")
+        out = torch.zeros((n, 32), dtype=torch.uint8, device="cuda")
+        with pytest.raises(Exception, match="exceed"):
+            eng.checksums_dev(arena, offs, lens, out, arena_bytes=G)
+        del offs, lens, out
+    offs = torch.tensor([0, 1 << 20], dtype=torch.int64, device="cuda")
+    lens = torch.tensor([1 << 20, (3 << 20) + 5], dtype=torch.int64, device="cuda")
+    out = torch.zeros((2, 32), dtype=torch.uint8, device="cuda")
+    eng.checksums_dev(arena, offs, lens, out, arena_bytes=G)
+    host = arena[:(4 << 20) + 5].cpu().numpy()
+    assert bytes(out[0].cpu().numpy()) == oracle.blake3(host[:1 << 20].tobytes())
+    assert bytes(out[1].cpu().numpy()) == oracle.blake3(host[1 << 20:(4 << 20) + 5].tobytes())
+    del arena
+    torch.cuda.empty_cache()
+
+
 def test_checksums_batch_over_64k_items(eng, oracle):
     """Two 40 GiB buffers in one batch chain: 81,920 subtree work items, more than the
     65,536-workgroup grid, so the groups kernel strides; 160 reduce blocks per buffer; byte
