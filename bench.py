@@ -57,6 +57,17 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 # read 12 / write 12 = 76 B/key (the minima of duplicates are the only other stores)
 def group_bytes_per_key(n: int) -> int:
     return 44 if n <= 256 * 5632 else 76
+FUSED_MAX_FILES = 256 * 5632  # the fused chain's single-level regions (sd_cas_hash_group_sampled_dev)
+
+
+def eng_region_capacity(n: int) -> int:
+    """Rows per coarse-bucket region of the fused chain (group_hash.hip region_capacity)."""
+    mean = n / 256
+    var = mean * (1 - 1 / 256)
+    sd = 1
+    while sd * sd < var:
+        sd += 1
+    return int(mean) + 1 + 8 * sd + 64
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # 256 CUs x 4 SIMD32 x 32 lanes x 2.4 GHz = 78.6
 # measured ceiling of K1's own instruction stream (compute-only loop at 2.38 GHz, no loads):
 # profiles/r01_ubench_k1_clock.log
@@ -92,6 +103,9 @@ def main() -> None:
                          "measures the exchange path's cost on one GPU")
     ap.add_argument("--inline-group", action="store_true",
                     help="issue the grouping from the main thread (A/B of the worker thread)")
+    ap.add_argument("--unfused", action="store_true",
+                    help="N=1: K1 + the standalone grouping chain on the side stream (the round-2 "
+                         "pipeline) instead of K1G (K1 partitioning its own keys) + bucket tables")
     args = ap.parse_args()
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -146,6 +160,13 @@ def main() -> None:
     NBUF = 3
     keys = [torch.empty(F, dtype=torch.int64, device=dev) for _ in range(NBUF)]
     rep = torch.empty(F, dtype=torch.int32, device=dev)
+    # N=1: the fused chain — K1G partitions its own keys into fixed-capacity coarse-bucket
+    # regions (two sets, alternating), the bucket tables of step i run on the side stream
+    # while step i+1 hashes; each step's rep in its own buffer
+    fused = (not sharded and not args.unfused and F % eng.batch_quantum == 0
+             and F <= FUSED_MAX_FILES)
+    reps = [torch.empty(F, dtype=torch.int32, device=dev) for _ in range(NBUF)] if fused else None
+    ovf = torch.zeros(1, dtype=torch.int32, device=dev)
     eng.synth_sampled(args.seed, file0, F, content, sizes, 57344, dup_permille=args.dup_permille)
     torch.cuda.synchronize()
     ops = HipShardOps(eng)
@@ -172,7 +193,9 @@ def main() -> None:
         b = i % NBUF
         with torch.cuda.stream(side):
             side.wait_event(hashed[b])
-            if not sharded:
+            if fused:
+                eng.group_regions(F, reps[b], stream=side.cuda_stream, want_objects=False)
+            elif not sharded:
                 eng.group(keys[b], rep, want_objects=False)  # K4h + K5h, async
             else:
                 r = sharded_group(keys[b], file0, ops, capacity=capacity)
@@ -183,11 +206,13 @@ def main() -> None:
 
     def launch_group(i: int):
         b = i % NBUF
-        pending[b] = worker.submit(group, i) if worker is not None else group(i)
+        # the fused chain's tables must be enqueued before the next batch's hash_regions
+        # (they group the context's LAST batch): from the main thread; no host sync in them
+        pending[b] = worker.submit(group, i) if worker is not None and not fused else group(i)
 
     def wait_group(b: int):
         if pending[b] is not None:
-            if worker is not None:
+            if worker is not None and not fused:
                 pending[b].result()
             main.wait_event(grouped[b])
             pending[b] = None
@@ -198,7 +223,10 @@ def main() -> None:
             wait_group(b)                       # keys[b] free again
             if timed:
                 ev[i][0].record(main)
-            eng.hash_sampled(content, sizes, keys[b])      # K1 on the main stream
+            if fused:  # K1G on the main stream
+                eng.hash_regions_sampled(content, sizes, keys[b], reps[b], ovf)
+            else:
+                eng.hash_sampled(content, sizes, keys[b])      # K1 on the main stream
             if timed:
                 ev[i][1].record(main)
             hashed[b].record(main)
@@ -215,6 +243,8 @@ def main() -> None:
     torch.cuda.synchronize()
     results.clear()
     overflows.clear()
+    ovf.zero_()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     run(args.steps, True)
     torch.cuda.synchronize()
@@ -237,9 +267,36 @@ def main() -> None:
     kern_ms = max(k1_ms_ranks)
 
     # objects (for the record) — outside the timed region
+    fused_rec = None
     if not sharded:
         objects = eng.group(last_keys, rep)
-    else:
+    if fused:
+        # every timed step's regions must have held their keys (else the step's rep would
+        # need the standalone regroup); the last step's rep == the standalone grouping's
+        timed_overflow = int(ovf.item())
+        last_rep = reps[(args.steps - 1) % NBUF]
+        rep_parity = bool(torch.equal(last_rep, rep))
+        # the bucket tables alone, serially after K1G (inside the steps they share the CUs
+        # with the next K1G on the side stream): HIP events on the stream they run on
+        tabs = []
+        for _ in range(3):
+            a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            eng.hash_regions_sampled(content, sizes, last_keys, last_rep, ovf)
+            a_.record(main)
+            eng.group_regions(F, last_rep, want_objects=False)
+            b_.record(main)
+            b_.synchronize()
+            tabs.append(a_.elapsed_time(b_))
+        fobj = eng.hash_group_sampled(content, sizes, last_keys, last_rep, ovf)
+        fused_rec = {"tables_ms": float(np.median(tabs)), "tables_ms_all": tabs,
+                     "objects": fobj, "parity_vs_standalone": rep_parity and fobj == objects,
+                     "timed_steps_overflowed": timed_overflow,
+                     "region_capacity": eng_region_capacity(F),
+                     "note": "K1G (sd_cas_sampled_group_kernel: K1 + the coarse-bucket partition "
+                             "of its own keys into fixed-capacity regions) + ONE bucket-table "
+                             "launch (sd_bucket_min_regions); tables_ms = that launch alone, "
+                             "after K1G, HIP events on its stream"}
+    if sharded:
         # every timed step's fixed-capacity exchange must have fit (else it would have been
         # redone exactly outside the timed region, and the step time would not stand)
         n_overflow = sum(int(f.item()) for f in overflows)
@@ -357,7 +414,8 @@ def main() -> None:
     # HBM bytes per launch from PMC (TCC_MISS_sum x 128-B lines, committed summary of the
     # separate rocprofv3 --pmc pass on the same kernel), scaled to this launch's files
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_sampled_kernel.json")
+    pmc = os.path.join(ROOT, "profiles", "pmc_sampled_group_kernel.json" if fused
+                       else "pmc_sampled_kernel.json")
     if os.path.exists(pmc):
         with open(pmc) as fh:
             per_file = json.load(fh).get("hbm_bytes_per_file")
@@ -390,9 +448,13 @@ def main() -> None:
                 "files_per_gpu": F,
                 "dup_permille": args.dup_permille,
                 "parallelism": f"shard-by-file x{world}" + (" + RCCL key-range all-to-all" if sharded else ""),
-                "pipeline": ("grouping of step i on a side stream (issued from a worker thread) "
-                             "overlaps hashing of steps i+1 and i+2" if args.overlap
+                "pipeline": (("K1G (K1 + partition of its keys into fixed-capacity bucket "
+                              "regions) on the main stream; step i's bucket tables on a side "
+                              "stream overlap step i+1's K1G" if fused else
+                              "grouping of step i on a side stream (issued from a worker thread) "
+                              "overlaps hashing of steps i+1 and i+2") if args.overlap
                              else "hash then group, serial"),
+                "grouping": "fused" if fused else ("exchange" if sharded else "standalone chain"),
                 "objects": objects,
                 "exchange": None if not sharded else {
                     "backend": dist.get_backend(), "world_size": dist.get_world_size(),
@@ -414,7 +476,7 @@ def main() -> None:
                 # K1 time, vs the guide's int32 VALU peak (78.6 T lane-ops/s).  BLAKE3 is
                 # integer ARX with no contraction (no MFMA path) and K1 moves ~0.4 of HBM
                 # peak, so VALU is the binding roof.
-                "kernel": "sd_cas_sampled_kernel",
+                "kernel": "sd_cas_sampled_group_kernel" if fused else "sd_cas_sampled_kernel",
                 "bound": "valu",
                 "bound_note": ("BLAKE3 is 32-bit integer ARX with no contraction: no MFMA path, and "
                                "HBM runs at ~0.4 of peak (see 'hbm'); the binding roof is VALU "
@@ -448,6 +510,7 @@ def main() -> None:
             "sustained": sustained,
             "e2e": e2e,
             "group": None if group_ms is None else {
+                "fused": fused_rec,
                 # Object grouping of one step's keys alone (K4h partition + K5h LDS hash
                 # min), HIP events on the stream it runs on, after the timed region: `ms` per
                 # call over 10 back-to-back calls, `ms_each_synced` one call at a time

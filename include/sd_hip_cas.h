@@ -200,6 +200,34 @@ int sd_cas_hash_packed_dev(sd_cas_ctx* ctx, const void* d_arena, const uint64_t*
  * out_objects != NULL.  n < 2^32. */
 int sd_cas_group_dev(sd_cas_ctx* ctx, const uint64_t* d_keys, size_t n, uint32_t* d_rep,
                      uint64_t* out_objects, void* stream);
+/* Hash + group in one chain (a sampled batch of the file identifier: generate_cas_id for
+ * every file, then the grouping of mod.rs:98-350): d_keys as sd_cas_hash_sampled_dev, d_rep
+ * as sd_cas_group_dev.  K1 partitions its own keys in its epilogue — each (mixed key, file)
+ * row goes to a fixed-capacity region of its coarse bucket — so the grouping after it is one
+ * bucket-table launch (no key read-back, totals, prefill or scatter pass).  Async unless
+ * out_objects != NULL.  d_overflow (u32, device; zero it first) is set when a region filled
+ * (more than mean + 8 sigma + 64 keys in one coarse bucket: heavily duplicated content) —
+ * d_rep is then not complete and the caller regroups with sd_cas_group_dev(d_keys); with
+ * out_objects != NULL the call blocks and does that itself.  Batches the fused chain does not
+ * take (n not a multiple of sd_cas_batch_quantum, n > 1,441,792, or a non-AUTO/HASH group
+ * method) run the two calls in sequence, d_overflow untouched.  The Object count of an async
+ * call: sd_cas_copy_objects_dev. */
+int sd_cas_hash_group_sampled_dev(sd_cas_ctx* ctx, const void* d_content, uint64_t stride,
+                                  const uint64_t* d_sizes, size_t n, uint64_t* d_keys,
+                                  uint32_t* d_rep, uint32_t* d_overflow, uint64_t* out_objects,
+                                  void* stream);
+/* The same chain in its two halves, for callers that pipeline batches: hash_regions = K1 +
+ * the partition into one of the context's two region sets (n a multiple of the quantum, <=
+ * 1,441,792, default group method: else SD_CAS_EINVAL), async; group_regions = the bucket
+ * tables over the regions of the LAST hash_regions batch (same n), on any stream ordered
+ * after it (an event), async unless out_objects != NULL.  The sets alternate, so batch i's
+ * tables may run on a side stream while batch i+1 hashes; a set is refilled only after its
+ * previous tables finished (the library orders that itself).  d_overflow as above. */
+int sd_cas_hash_regions_sampled_dev(sd_cas_ctx* ctx, const void* d_content, uint64_t stride,
+                                    const uint64_t* d_sizes, size_t n, uint64_t* d_keys,
+                                    uint32_t* d_rep, uint32_t* d_overflow, void* stream);
+int sd_cas_group_regions_dev(sd_cas_ctx* ctx, size_t n, uint32_t* d_rep, uint64_t* out_objects,
+                             void* stream);
 /* Generalised grouping (the receive side of the multi-GPU exchange):
  * d_out[i] = min{ vals[j] : key[j] == key[i] } (vals NULL = identity, i.e. sd_cas_group_dev);
  * *out_objects = distinct keys (blocks when non-NULL).  n < 2^32 (above

@@ -80,6 +80,16 @@ extern "C" {
                                   stream: *mut c_void) -> c_int;
     pub fn sd_cas_group_dev(ctx: *mut sd_cas_ctx, d_keys: *const u64, n: usize, d_rep: *mut u32,
                             out_objects: *mut u64, stream: *mut c_void) -> c_int;
+    pub fn sd_cas_hash_group_sampled_dev(ctx: *mut sd_cas_ctx, d_content: *const c_void, stride: u64,
+                                         d_sizes: *const u64, n: usize, d_keys: *mut u64,
+                                         d_rep: *mut u32, d_overflow: *mut u32,
+                                         out_objects: *mut u64, stream: *mut c_void) -> c_int;
+    pub fn sd_cas_hash_regions_sampled_dev(ctx: *mut sd_cas_ctx, d_content: *const c_void, stride: u64,
+                                           d_sizes: *const u64, n: usize, d_keys: *mut u64,
+                                           d_rep: *mut u32, d_overflow: *mut u32,
+                                           stream: *mut c_void) -> c_int;
+    pub fn sd_cas_group_regions_dev(ctx: *mut sd_cas_ctx, n: usize, d_rep: *mut u32,
+                                    out_objects: *mut u64, stream: *mut c_void) -> c_int;
     pub fn sd_cas_group_min_dev(ctx: *mut sd_cas_ctx, d_keys: *const u64, d_vals: *const u32, n: usize,
                                 d_out: *mut u32, out_objects: *mut u64, stream: *mut c_void) -> c_int;
     pub fn sd_cas_partition_dev(ctx: *mut sd_cas_ctx, d_keys: *const u64, n: usize, parts: u32,

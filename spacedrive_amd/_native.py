@@ -47,6 +47,9 @@ SIGNATURES = [
     ("sd_cas_hash_sampled_dev", _i, [_vp, _vp, _u64, _vp, _sz, _vp, _vp]),
     ("sd_cas_hash_packed_dev", _i, [_vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp]),
     ("sd_cas_group_dev", _i, [_vp, _vp, _sz, _vp, _vp, _vp]),
+    ("sd_cas_hash_group_sampled_dev", _i, [_vp, _vp, _u64, _vp, _sz, _vp, _vp, _vp, _vp, _vp]),
+    ("sd_cas_hash_regions_sampled_dev", _i, [_vp, _vp, _u64, _vp, _sz, _vp, _vp, _vp, _vp]),
+    ("sd_cas_group_regions_dev", _i, [_vp, _sz, _vp, _vp, _vp]),
     ("sd_cas_group_min_dev", _i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     ("sd_cas_partition_dev", _i, [_vp, _vp, _sz, _u32, _vp, _vp, _vp, _vp]),
     ("sd_cas_exchange_pack_dev", _i, [_vp, _vp, _vp, _sz, _u64, _vp, _vp]),

@@ -254,6 +254,38 @@ class CasEngine:
                     "group")
         return int(obj.value) if want_objects else None
 
+    def hash_group_sampled(self, content, sizes, keys, rep, overflow, stream: Optional[int] = None,
+                           want_objects: bool = True) -> Optional[int]:
+        """K1 with the grouping partition fused into its epilogue + one bucket-table launch
+        (sd_cas_hash_group_sampled_dev): keys as hash_sampled, rep as group.  overflow: int32
+        [1] device tensor, zeroed by the caller — set if a coarse bucket outgrew its region
+        (then regroup with group(keys, rep)); want_objects blocks and regroups itself."""
+        n = int(sizes.numel())
+        stride = int(content.shape[-1]) if content.dim() == 2 else SAMPLED_CONTENT_LEN
+        obj = ctypes.c_uint64(0)
+        self._check(self.L.sd_cas_hash_group_sampled_dev(
+            self.h, _ptr(content), stride, _ptr(sizes), n, _ptr(keys), _ptr(rep), _ptr(overflow),
+            ctypes.byref(obj) if want_objects else None, _stream(stream)), "hash_group_sampled")
+        return int(obj.value) if want_objects else None
+
+    def hash_regions_sampled(self, content, sizes, keys, rep, overflow,
+                             stream: Optional[int] = None) -> None:
+        """The first half of hash_group_sampled: K1G into the next region set (async)."""
+        n = int(sizes.numel())
+        stride = int(content.shape[-1]) if content.dim() == 2 else SAMPLED_CONTENT_LEN
+        self._check(self.L.sd_cas_hash_regions_sampled_dev(
+            self.h, _ptr(content), stride, _ptr(sizes), n, _ptr(keys), _ptr(rep), _ptr(overflow),
+            _stream(stream)), "hash_regions_sampled")
+
+    def group_regions(self, n: int, rep, stream: Optional[int] = None,
+                      want_objects: bool = True) -> Optional[int]:
+        """The second half: the bucket tables over the last hash_regions batch."""
+        obj = ctypes.c_uint64(0)
+        self._check(self.L.sd_cas_group_regions_dev(self.h, int(n), _ptr(rep),
+                                                    ctypes.byref(obj) if want_objects else None,
+                                                    _stream(stream)), "group_regions")
+        return int(obj.value) if want_objects else None
+
     def group_min(self, keys, vals, out, stream: Optional[int] = None,
                   want_objects: bool = True) -> Optional[int]:
         """out[i] = min{ vals[j] : keys[j] == keys[i] } (vals None = identity)."""

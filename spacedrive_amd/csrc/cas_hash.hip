@@ -25,6 +25,7 @@
 
 #include "blake3_device.hpp"
 #include "sd_kernels.h"
+#include "sd_mix.h"
 
 namespace sdcas {
 
@@ -187,6 +188,84 @@ sd_cas_sampled_kernel_256(const uint8_t* __restrict__ content, uint64_t stride,
                           const uint64_t* __restrict__ sizes, uint64_t n,
                           uint64_t* __restrict__ keys) {
   sampled_kernel_body<SAMPLED_BLOCK_NARROW>(content, stride, sizes, n, keys);
+}
+
+// ---- K1G: K1 + the grouping's partition, fused (sd_cas_hash_group_sampled_dev) ----------
+// The Object grouping needs each key once more after K1 has written it: the standalone chain
+// reads the keys back (bucket totals, 8 B/key), prefills rep (4 B/key), then scatters the
+// keys into coarse-bucket order (8 B read + 12 B write) before the bucket tables.  K1 holds
+// every key in a register when it finishes, so K1G does that partition in its epilogue
+// instead: the lane's (mixed key, file) row goes straight into a FIXED-capacity region of
+// its coarse bucket (the top 8 bits of mix64(key)); the workgroup ranks its lanes per bucket
+// in LDS (the CV stack's LDS, dead by then) and reserves each bucket's run with one device
+// atomic.  The chain after K1G is one bucket-table launch.  Regions are sized mean + 8
+// sigma + 64 rows for uniform keys; a bucket that outgrows its region (heavily duplicated
+// content: every copy of a file lands in one bucket) sets *overflow, and the caller
+// regroups with the standalone chain (the fixed-capacity exchange's contract).
+struct RegionOut {
+  uint64_t* rkeys;     // [REGIONS][cap] mixed keys
+  uint32_t* rfile;     // [REGIONS][cap] file index
+  uint32_t* cursor;    // [REGIONS] rows reserved; zero on entry (the bucket tables re-zero it)
+  uint64_t cap;
+  uint32_t* rep;       // rep[f] = f: the bucket tables store only where a key's minimum differs
+  uint32_t* overflow;  // set when a region is full
+  unsigned long long* objects;  // zeroed here; the bucket tables add the distinct keys
+};
+
+template <int B>
+__device__ __forceinline__ void sampled_group_kernel_body(const uint8_t* __restrict__ content,
+                                                          uint64_t stride,
+                                                          const uint64_t* __restrict__ sizes,
+                                                          uint64_t n, uint64_t* __restrict__ keys,
+                                                          RegionOut ro) {
+  __shared__ uint32_t stack_lds[SAMPLED_DEPTH][8][B];
+  const uint64_t f = (uint64_t)blockIdx.x * B + threadIdx.x;
+  const bool live = f < n;
+  uint64_t key = 0;
+  if (live) {  // exactly K1's lane program
+    LdsStack<B> stk{stack_lds, threadIdx.x};
+    const uint4* q = reinterpret_cast<const uint4*>(content + f * stride);
+    key = cas_lane_sampled<false, LAYOUT_ROW, B>(q, sizes[f], stk);
+    keys[f] = key;
+    ro.rep[f] = (uint32_t)f;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ro.objects = 0;
+  // epilogue: the stack columns are dead once every lane has its root
+  uint32_t* hist = &stack_lds[0][0][0];  // REGIONS counters, then REGIONS run bases
+  uint32_t* base = hist + REGIONS;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < REGIONS; i += B) hist[i] = 0;
+  __syncthreads();
+  const uint64_t m = mix64(key);
+  const uint32_t bkt = (uint32_t)(m >> (64 - REGION_BITS));
+  const uint32_t r = live ? atomicAdd(&hist[bkt], 1u) : 0u;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < REGIONS; i += B)
+    base[i] = hist[i] ? atomicAdd(&ro.cursor[i], hist[i]) : 0u;
+  __syncthreads();
+  if (live) {
+    const uint64_t slot = (uint64_t)base[bkt] + r;
+    if (slot < ro.cap) {
+      ro.rkeys[(uint64_t)bkt * ro.cap + slot] = m;
+      ro.rfile[(uint64_t)bkt * ro.cap + slot] = (uint32_t)f;
+    } else {
+      atomicOr(ro.overflow, 1u);
+    }
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(SAMPLED_BLOCK)
+sd_cas_sampled_group_kernel(const uint8_t* __restrict__ content, uint64_t stride,
+                            const uint64_t* __restrict__ sizes, uint64_t n,
+                            uint64_t* __restrict__ keys, RegionOut ro) {
+  sampled_group_kernel_body<SAMPLED_BLOCK>(content, stride, sizes, n, keys, ro);
+}
+
+extern "C" __global__ void __launch_bounds__(SAMPLED_BLOCK_NARROW)
+sd_cas_sampled_group_kernel_256(const uint8_t* __restrict__ content, uint64_t stride,
+                                const uint64_t* __restrict__ sizes, uint64_t n,
+                                uint64_t* __restrict__ keys, RegionOut ro) {
+  sampled_group_kernel_body<SAMPLED_BLOCK_NARROW>(content, stride, sizes, n, keys, ro);
 }
 
 // ---- K2: the whole-file (packed) path ------------------------------------------------
@@ -579,6 +658,25 @@ hipError_t hash_sampled(const uint8_t* content, uint64_t stride, const uint64_t*
                                                                            n, keys);
   } else {
     sd_cas_sampled_kernel<<<(uint32_t)blocks, SAMPLED_BLOCK, 0, s>>>(content, stride, sizes, n, keys);
+  }
+  return hipGetLastError();
+}
+
+hipError_t hash_sampled_regions(const uint8_t* content, uint64_t stride, const uint64_t* sizes,
+                                uint64_t n, uint64_t* keys, uint32_t* rep, uint64_t* rkeys,
+                                uint32_t* rfile, uint32_t* cursor, uint64_t cap, uint32_t* overflow,
+                                uint64_t* objects, hipStream_t s, uint32_t cus) {
+  if (n == 0) return hipSuccess;
+  const RegionOut ro{rkeys, rfile, cursor, cap, rep, overflow, (unsigned long long*)objects};
+  const uint64_t blocks = (n + SAMPLED_BLOCK - 1) / SAMPLED_BLOCK;
+  const uint64_t quanta = cus ? (n + (uint64_t)cus * 256 - 1) / ((uint64_t)cus * 256) : 0;
+  if (cus && (blocks < cus || (quanta & 1))) {  // the grid choice of hash_sampled
+    const uint64_t nb = (n + SAMPLED_BLOCK_NARROW - 1) / SAMPLED_BLOCK_NARROW;
+    sd_cas_sampled_group_kernel_256<<<(uint32_t)nb, SAMPLED_BLOCK_NARROW, 0, s>>>(content, stride,
+                                                                                 sizes, n, keys, ro);
+  } else {
+    sd_cas_sampled_group_kernel<<<(uint32_t)blocks, SAMPLED_BLOCK, 0, s>>>(content, stride, sizes, n,
+                                                                          keys, ro);
   }
   return hipGetLastError();
 }

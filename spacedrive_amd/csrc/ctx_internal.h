@@ -90,6 +90,20 @@ struct sd_cas_ctx {
   // the hash grouping's bucket totals: zero between calls (each call's last kernel re-zeroes
   // them), so the chain has no zeroing launch; ordered across streams like ws
   uint32_t* gtotals = nullptr;
+  // The fused hash + group chain (sd_cas_hash_regions_sampled_dev / sd_cas_group_regions_dev):
+  // two region sets used alternately, so set k's bucket tables can run on a side stream while
+  // the next batch's K1G fills set k^1; region_done[k] orders set k's reuse after its tables.
+  // gcursor holds both sets' cursors (2 x 256 u32), zero between calls (the tables re-zero).
+  uint32_t* gcursor = nullptr;
+  DevBuf regions[2];
+  uint64_t region_n[2] = {0, 0};
+  hipEvent_t region_done[2] = {nullptr, nullptr};
+  bool region_pending[2] = {false, false};
+  bool region_grouped[2] = {true, true};  // set k's tables have been enqueued since its K1G
+  int region_cur = -1;
+  // the Object counter of the last grouping call (d_scalar, or a region set's): what
+  // sd_cas_copy_objects_dev copies; region_obj_set = that set (-1: d_scalar)
+  int region_obj_set = -1;
   // ws and d_scalar are shared by every device call of the context, whatever stream the
   // caller passes: the last enqueued use is recorded here and a use on another stream
   // waits for it first (sd_ws_acquire / sd_ws_release)

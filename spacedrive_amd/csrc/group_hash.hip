@@ -39,6 +39,7 @@
 
 #include "sd_debug.h"
 #include "sd_group.h"
+#include "sd_mix.h"
 
 namespace sdcas {
 
@@ -63,12 +64,6 @@ constexpr uint32_t MAX_BITS = 19;
 constexpr uint32_t MAX_B2 = 9;
 constexpr uint64_t MAX_MEAN_PER_BUCKET = 2500;
 
-// splitmix64 finalizer: a bijection on u64, so distinct keys stay distinct
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
 
 // mode 0 (grouping): bucket = top bits of mix64(key), the stored key is mix64(key)
 // mode 1 (range partition): bucket = floor(key * nb / 2^64), the stored key is the key
@@ -548,6 +543,9 @@ __device__ __forceinline__ uint64_t g_find(const uint64_t* tk, uint64_t cap, uin
 // instead of probing again — faster for the big tables (1.31M keys: 0.064 -> 0.060
 // ms), slower for the 4,096-slot ones (12.5M keys: 0.369 -> 0.398 ms; A/B in
 // profiles/r02_group_ab.log), so only sd_bucket_min_big keeps it.
+// Regions (the fused hash + group chain): counts != nullptr — bucket b's keys are rows
+// [b * region_cap, b * region_cap + min(counts[b], region_cap)) and the workgroup re-zeroes
+// counts[b] after reading it (the region cursors' persistent-zero invariant).
 template <uint32_t TBL, int THREADS, bool KEEP_SLOT>
 __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict__ rezero,
                                            uint32_t rezero_words,
@@ -558,7 +556,9 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
                                            uint32_t bits, uint64_t n, uint32_t* __restrict__ out,
                                            unsigned long long* __restrict__ objects,
                                            uint64_t* __restrict__ gkeys,
-                                           uint32_t* __restrict__ gvals) {
+                                           uint32_t* __restrict__ gvals,
+                                           uint32_t* __restrict__ counts = nullptr,
+                                           uint64_t region_cap = 0) {
   constexpr uint32_t TILE = THREADS * ITEMS;
   constexpr uint32_t FILL = TBL / 8 * 7;  // above this the bucket goes to global memory
   __shared__ uint64_t tk[TBL];
@@ -568,13 +568,25 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
   // single flag could be raised by a fast wave's trip-(t+1) insert while a slower wave was
   // still reading it for trip t+1, splitting the waves over different barriers
   __shared__ int ovf[2];
+  __shared__ uint32_t region_n;
   const uint32_t b = bucket;
   // the chain's bucket totals were last read by the scatter: zero them for the next call
   // (the persistent buffer's invariant, see hash_group_min)
   if (bucket == 0)
     for (uint32_t i = threadIdx.x; i < rezero_words; i += THREADS) rezero[i] = 0;
-  const uint64_t s = starts[b];
-  const uint64_t e = b + 1 < nb ? starts[b + 1] : n;
+  uint64_t s, e;
+  if (counts) {
+    if (threadIdx.x == 0) {
+      region_n = counts[b];
+      counts[b] = 0;
+    }
+    __syncthreads();
+    s = (uint64_t)b * region_cap;
+    e = s + (region_n < region_cap ? region_n : region_cap);
+  } else {
+    s = starts[b];
+    e = b + 1 < nb ? starts[b + 1] : n;
+  }
   if (s == e) return;  // uniform for the whole workgroup
   // every stored key of this bucket has top bits == b, so a key from bucket b^1 is never stored
   const uint64_t empty = (uint64_t)(b ^ 1u) << (64 - bits);
@@ -708,12 +720,60 @@ sd_bucket_min_big(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict
                                            starts, nb, bits, n, out, objects, gkeys, gvals);
 }
 
+// The fused chain's bucket tables: one 1,024-thread workgroup per region (the coarse
+// buckets K1G wrote), straight from the regions — no totals, scatter or refine launch.
+extern "C" __global__ void __launch_bounds__(BIG_THREADS)
+sd_bucket_min_regions(const uint64_t* __restrict__ rkeys, const uint32_t* __restrict__ rfile,
+                      uint32_t* __restrict__ cursor, uint64_t cap, uint32_t* __restrict__ out,
+                      unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
+                      uint32_t* __restrict__ gvals) {
+  bucket_min<BIG_TABLE, BIG_THREADS, true>(blockIdx.x, nullptr, 0, rkeys, rfile, nullptr, nullptr,
+                                           REGIONS, REGION_BITS, 0, out, objects, gkeys, gvals,
+                                           cursor, cap);
+}
+
 }  // namespace sdcas
 
 // ---- host launchers ----------------------------------------------------------------
 namespace sdcas {
 
 static inline size_t al256(size_t x) { return (x + 255) / 256 * 256; }
+
+// Fixed region capacity of the fused chain for a batch of n uniform keys: the mean coarse
+// bucket + 8 standard deviations (binomial) + 64 rows (the exchange's fixed_capacity rule).
+uint64_t region_capacity(uint64_t n) {
+  const double mean = (double)n / REGIONS;
+  const double var = mean * (1.0 - 1.0 / REGIONS);
+  uint64_t sd = 1;
+  while ((double)(sd * sd) < var) ++sd;
+  return (uint64_t)mean + 1 + 8 * sd + 64;
+}
+
+bool region_group_supported(uint64_t n) { return n > 0 && n <= BIG_MAX_KEYS; }
+
+// workspace: rkeys | rfile | global overflow tables (2 slots per region row)
+size_t region_group_workspace_bytes(uint64_t n) {
+  const uint64_t rows = (uint64_t)REGIONS * region_capacity(n);
+  return al256(rows * 8) + al256(rows * 4) + al256(2 * rows * 8) + al256(2 * rows * 4);
+}
+
+void region_group_layout(void* ws, uint64_t n, uint64_t** rkeys, uint32_t** rfile, uint64_t** gkeys,
+                         uint32_t** gvals) {
+  const uint64_t rows = (uint64_t)REGIONS * region_capacity(n);
+  char* q = (char*)ws;
+  *rkeys = (uint64_t*)q; q += al256(rows * 8);
+  *rfile = (uint32_t*)q; q += al256(rows * 4);
+  *gkeys = (uint64_t*)q; q += al256(2 * rows * 8);
+  *gvals = (uint32_t*)q;
+}
+
+hipError_t region_group_min(const uint64_t* rkeys, const uint32_t* rfile, uint32_t* cursor,
+                            uint64_t cap, uint32_t* out, uint64_t* d_objects, uint64_t* gkeys,
+                            uint32_t* gvals, hipStream_t s) {
+  sd_bucket_min_regions<<<REGIONS, BIG_THREADS, 0, s>>>(rkeys, rfile, cursor, cap, out,
+                                                        (unsigned long long*)d_objects, gkeys, gvals);
+  return hipGetLastError();
+}
 
 struct PartPlan {
   uint32_t nb, nblk;

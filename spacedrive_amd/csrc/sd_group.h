@@ -51,6 +51,17 @@ constexpr uint32_t GROUP_TOTALS_WORDS = 16 * 1024;
 hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n, uint32_t* out,
                           uint64_t* d_objects, void* ws, uint32_t* totals, hipStream_t stream,
                           uint64_t target = 0);
+// The fused hash + group chain (K1G writes the regions, sd_bucket_min_regions groups them):
+// n <= 1,441,792 keys; regions of region_capacity(n) rows per coarse bucket; `cursor`
+// (REGIONS u32, persistent, zero between calls) is re-zeroed by the bucket tables.
+uint64_t region_capacity(uint64_t n);
+bool region_group_supported(uint64_t n);
+size_t region_group_workspace_bytes(uint64_t n);
+void region_group_layout(void* ws, uint64_t n, uint64_t** rkeys, uint32_t** rfile, uint64_t** gkeys,
+                         uint32_t** gvals);
+hipError_t region_group_min(const uint64_t* rkeys, const uint32_t* rfile, uint32_t* cursor,
+                            uint64_t cap, uint32_t* out, uint64_t* d_objects, uint64_t* gkeys,
+                            uint32_t* gvals, hipStream_t stream);
 // Key-range partition: part(k) = floor(k * parts / 2^64); out_keys/out_pos hold the keys and
 // their input positions part-contiguous (order inside a part unspecified), d_counts[p] the
 // part sizes.  ws: partition_workspace_bytes(n, parts).

@@ -92,7 +92,11 @@ int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
       hipEventCreateWithFlags(&c->ws_ev, hipEventDisableTiming) != hipSuccess ||
       hipMalloc((void**)&c->d_scalar, 64) != hipSuccess ||
       hipMalloc((void**)&c->gtotals, GROUP_TOTALS_WORDS * 4) != hipSuccess ||
-      hipMemset(c->gtotals, 0, GROUP_TOTALS_WORDS * 4) != hipSuccess) {
+      hipMemset(c->gtotals, 0, GROUP_TOTALS_WORDS * 4) != hipSuccess ||
+      hipMalloc((void**)&c->gcursor, 4096) != hipSuccess ||
+      hipMemset(c->gcursor, 0, 4096) != hipSuccess ||
+      hipEventCreateWithFlags(&c->region_done[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->region_done[1], hipEventDisableTiming) != hipSuccess) {
     sd_cas_ctx_destroy(c);
     g_ctx_create_err = "stream/event/scratch creation failed on device " + std::to_string(device);
     return SD_CAS_EHIP;
@@ -141,6 +145,11 @@ void sd_cas_ctx_destroy(sd_cas_ctx* c) {
   if (c->io.p) (void)hipFree(c->io.p);
   if (c->d_scalar) (void)hipFree(c->d_scalar);
   if (c->gtotals) (void)hipFree(c->gtotals);
+  if (c->gcursor) (void)hipFree(c->gcursor);
+  for (int k = 0; k < 2; k++) {
+    if (c->regions[k].p) (void)hipFree(c->regions[k].p);
+    if (c->region_done[k]) (void)hipEventDestroy(c->region_done[k]);
+  }
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->h2d_done) (void)hipEventDestroy(c->h2d_done);
   if (c->ws_ev) (void)hipEventDestroy(c->ws_ev);
@@ -310,9 +319,114 @@ int sd_cas_group_dev(sd_cas_ctx* c, const uint64_t* d_keys, size_t n, uint32_t* 
     HIP_TRY(c, group_keys(d_keys, n, d_rep, c->d_scalar, c->ws.p, s));
   }
   HIP_TRY(c, sd_ws_release(c, s));
+  c->region_obj_set = -1;
   if (out_objects) {
     HIP_TRY(c, hipMemcpyAsync(out_objects, c->d_scalar, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
+  }
+  return SD_CAS_OK;
+}
+
+// ---- the fused hash + group chain -------------------------------------------------
+static bool fused_eligible(const sd_cas_ctx* c, size_t n) {
+  return n && n % c->quantum == 0 && region_group_supported(n) &&
+         (c->group_method == SD_CAS_GROUP_AUTO || c->group_method == SD_CAS_GROUP_HASH) &&
+         c->group_target == 0;
+}
+
+// region set k's buffer: rkeys | rfile | gkeys | gvals (region_group_layout) | objects u64
+static uint64_t* region_objects(sd_cas_ctx* c, int k) {
+  return (uint64_t*)((char*)c->regions[k].p + region_group_workspace_bytes(c->region_n[k]));
+}
+
+int sd_cas_hash_regions_sampled_dev(sd_cas_ctx* c, const void* d_content, uint64_t stride,
+                                    const uint64_t* d_sizes, size_t n, uint64_t* d_keys,
+                                    uint32_t* d_rep, uint32_t* d_overflow, void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (!fused_eligible(c, n))
+    return fail(c, SD_CAS_EINVAL,
+                "hash_regions: %zu files (a multiple of %zu up to 1,441,792, default group method)",
+                n, c->quantum);
+  if (!d_content || !d_sizes || !d_keys || !d_rep || !d_overflow || stride < SAMPLED_CONTENT_LEN ||
+      (stride & 15) || ((uintptr_t)d_content & 15))
+    return fail(c, SD_CAS_EINVAL, "hash_regions: bad arguments (stride=%llu)",
+                (unsigned long long)stride);
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  const int k = (c->region_cur + 1) & 1;
+  // set k was last grouped two batches ago: its tables must be done before it is refilled
+  if (c->region_pending[k]) HIP_TRY(c, hipStreamWaitEvent(s, c->region_done[k], 0));
+  c->region_n[k] = n;  // sizes the layout (ensure below grows the set if needed)
+  int rc = ensure(c, c->regions[k], region_group_workspace_bytes(n) + 256);
+  if (rc) return rc;
+  uint64_t *rkeys, *gkeys;
+  uint32_t *rfile, *gvals;
+  region_group_layout(c->regions[k].p, n, &rkeys, &rfile, &gkeys, &gvals);
+  hipError_t e = hash_sampled_regions((const uint8_t*)d_content, stride, d_sizes, n, d_keys, d_rep,
+                                      rkeys, rfile, c->gcursor + 256 * k, region_capacity(n), d_overflow,
+                                      region_objects(c, k), s, (uint32_t)(c->quantum / 256));
+  if (e != hipSuccess) {
+    (void)hipMemsetAsync(c->gcursor + 256 * k, 0, 1024, s);  // restore the cursors' invariant
+    return fail(c, SD_CAS_EHIP, "hash_regions: %s", hipGetErrorString(e));
+  }
+  c->region_cur = k;
+  c->region_grouped[k] = false;
+  return SD_CAS_OK;
+}
+
+int sd_cas_group_regions_dev(sd_cas_ctx* c, size_t n, uint32_t* d_rep, uint64_t* out_objects,
+                             void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  const int k = c->region_cur;
+  if (k < 0 || c->region_grouped[k] || c->region_n[k] != n || !d_rep)
+    return fail(c, SD_CAS_EINVAL, "group_regions: no ungrouped hash_regions batch of %zu files", n);
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  uint64_t *rkeys, *gkeys;
+  uint32_t *rfile, *gvals;
+  region_group_layout(c->regions[k].p, n, &rkeys, &rfile, &gkeys, &gvals);
+  uint64_t* obj = region_objects(c, k);
+  hipError_t e = region_group_min(rkeys, rfile, c->gcursor + 256 * k, region_capacity(n), d_rep, obj,
+                                  gkeys, gvals, s);
+  if (e != hipSuccess) {
+    (void)hipMemsetAsync(c->gcursor + 256 * k, 0, 1024, s);
+    return fail(c, SD_CAS_EHIP, "group_regions: %s", hipGetErrorString(e));
+  }
+  HIP_TRY(c, hipEventRecord(c->region_done[k], s));
+  c->region_pending[k] = true;
+  c->region_grouped[k] = true;
+  c->region_obj_set = k;
+  if (out_objects) {
+    HIP_TRY(c, hipMemcpyAsync(out_objects, obj, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+  }
+  return SD_CAS_OK;
+}
+
+int sd_cas_hash_group_sampled_dev(sd_cas_ctx* c, const void* d_content, uint64_t stride,
+                                  const uint64_t* d_sizes, size_t n, uint64_t* d_keys,
+                                  uint32_t* d_rep, uint32_t* d_overflow, uint64_t* out_objects,
+                                  void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (n && (!d_rep || !d_overflow))
+    return fail(c, SD_CAS_EINVAL, "hash_group_sampled: null rep/overflow");
+  if (!fused_eligible(c, n)) {  // the two calls in sequence
+    int rc = sd_cas_hash_sampled_dev(c, d_content, stride, d_sizes, n, d_keys, stream);
+    if (rc) return rc;
+    return sd_cas_group_dev(c, d_keys, n, d_rep, out_objects, stream);
+  }
+  int rc = sd_cas_hash_regions_sampled_dev(c, d_content, stride, d_sizes, n, d_keys, d_rep,
+                                           d_overflow, stream);
+  if (rc) return rc;
+  uint64_t obj = 0;
+  if ((rc = sd_cas_group_regions_dev(c, n, d_rep, out_objects ? &obj : nullptr, stream))) return rc;
+  if (out_objects) {
+    uint32_t ovf = 0;
+    hipStream_t s = pick(c, stream);
+    HIP_TRY(c, hipMemcpyAsync(&ovf, d_overflow, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    if (ovf) return sd_cas_group_dev(c, d_keys, n, d_rep, out_objects, stream);  // exact regroup
+    *out_objects = obj;
   }
   return SD_CAS_OK;
 }
@@ -338,6 +452,7 @@ int sd_cas_group_min_dev(sd_cas_ctx* c, const uint64_t* d_keys, const uint32_t* 
     HIP_TRY(c, group_min_by_sort(d_keys, d_vals, n, d_out, c->d_scalar, c->ws.p, s));
   }
   HIP_TRY(c, sd_ws_release(c, s));
+  c->region_obj_set = -1;
   if (out_objects) {
     HIP_TRY(c, hipMemcpyAsync(out_objects, c->d_scalar, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
@@ -373,6 +488,7 @@ int sd_cas_group_sorted_dev(sd_cas_ctx* c, const uint64_t* d_sorted_keys,
   HIP_TRY(c, sd_ws_acquire(c, s));
   HIP_TRY(c, group_sorted(d_sorted_keys, d_sorted_vals, n, d_rep, c->d_scalar, c->ws.p, s));
   HIP_TRY(c, sd_ws_release(c, s));
+  c->region_obj_set = -1;
   if (out_objects) {
     HIP_TRY(c, hipMemcpyAsync(out_objects, c->d_scalar, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));

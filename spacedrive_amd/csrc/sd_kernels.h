@@ -28,6 +28,14 @@ namespace sdcas {
 // 256-lane grid (one wave per SIMD instead of half the CUs at two)
 hipError_t hash_sampled(const uint8_t* content, uint64_t stride, const uint64_t* sizes,
                         uint64_t n, uint64_t* keys, hipStream_t s, uint32_t cus);
+// K1G: K1 + the grouping partition in its epilogue (cas_hash.hip): keys, rep[f] = f, and
+// each key's (mix64(key), f) row in the fixed-capacity region of its coarse bucket
+// (rkeys/rfile [REGIONS][cap], cursor [REGIONS] zero on entry); *overflow |= 1 when a region
+// is full; *objects = 0 (the bucket tables count).
+hipError_t hash_sampled_regions(const uint8_t* content, uint64_t stride, const uint64_t* sizes,
+                                uint64_t n, uint64_t* keys, uint32_t* rep, uint64_t* rkeys,
+                                uint32_t* rfile, uint32_t* cursor, uint64_t cap, uint32_t* overflow,
+                                uint64_t* objects, hipStream_t s, uint32_t cus);
 hipError_t hash_packed(const uint8_t* arena, const uint64_t* offs, const uint32_t* lens,
                        const uint64_t* sizes, const uint32_t* order, uint64_t n, uint64_t* keys,
                        hipStream_t s);

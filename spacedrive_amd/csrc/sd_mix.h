@@ -1,0 +1,22 @@
+// sd_mix.h — the grouping's key mix and coarse-bucket function, shared by the grouping
+// kernels (group_hash.hip) and the hash kernels that partition their own output
+// (cas_hash.hip, the fused hash + group chain).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sdcas {
+
+// splitmix64 finalizer: a bijection on u64, so distinct keys stay distinct
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// The fused chain's coarse buckets: the top REGION_BITS bits of the mixed key, each with a
+// fixed-capacity region of rows (mixed key u64, file u32) written by the hash kernel.
+constexpr uint32_t REGION_BITS = 8;
+constexpr uint32_t REGIONS = 1u << REGION_BITS;
+
+}  // namespace sdcas

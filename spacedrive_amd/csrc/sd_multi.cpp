@@ -430,6 +430,14 @@ int sd_cas_exchange_unpack_fixed_dev(sd_cas_ctx* c, const uint32_t* d_back,
 int sd_cas_copy_objects_dev(sd_cas_ctx* c, uint64_t* d_dst, void* stream) {
   if (!c || !d_dst) return SD_CAS_EINVAL;
   hipStream_t s = sd_pick(c, stream);
+  const int k = c->region_obj_set;
+  if (k >= 0) {  // the fused chain's last grouping: its region set's counter, after its tables
+    HIP_TRY(c, hipStreamWaitEvent(s, c->region_done[k], 0));
+    const uint64_t* obj = (const uint64_t*)((const char*)c->regions[k].p +
+                                            sdcas::region_group_workspace_bytes(c->region_n[k]));
+    HIP_TRY(c, hipMemcpyAsync(d_dst, obj, 8, hipMemcpyDeviceToDevice, s));
+    return SD_CAS_OK;
+  }
   HIP_TRY(c, sd_ws_acquire(c, s));
   HIP_TRY(c, hipMemcpyAsync(d_dst, c->d_scalar, 8, hipMemcpyDeviceToDevice, s));
   HIP_TRY(c, sd_ws_release(c, s));

@@ -415,6 +415,87 @@ def test_group_methods_and_deep_plans(eng, oracle, method, target, n):
         eng.set_group_method()
 
 
+@pytest.mark.parametrize("quanta", [1, 2, 3])
+def test_hash_group_fused_vs_standalone(eng, oracle, quanta):
+    """sd_cas_hash_group_sampled_dev (K1G: K1 with the grouping partition in its epilogue, then
+    one bucket-table launch over the fixed-capacity regions): keys == K1's, rep and Objects ==
+    the standalone grouping's, on 30 %-duplicate batches of 1, 2 (512-lane grid) and 3
+    (256-lane grid) quanta; async use leaves the overflow flag 0; oracle parity on a sample."""
+    q = eng.batch_quantum
+    n = quanta * q
+    content = torch.empty((n, SAMPLED_CONTENT_LEN), dtype=torch.uint8, device="cuda")
+    sizes = torch.empty(n, dtype=torch.int64, device="cuda")
+    eng.synth_sampled(61 + quanta, 0, n, content, sizes, SAMPLED_CONTENT_LEN, dup_permille=300)
+    keys = torch.empty(n, dtype=torch.int64, device="cuda")
+    rep = torch.empty(n, dtype=torch.int32, device="cuda")
+    keys2 = torch.zeros(n, dtype=torch.int64, device="cuda")
+    rep2 = torch.zeros(n, dtype=torch.int32, device="cuda")
+    ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
+    eng.hash_sampled(content, sizes, keys)
+    objects = eng.group(keys, rep)
+    assert eng.hash_group_sampled(content, sizes, keys2, rep2, ovf, want_objects=False) is None
+    torch.cuda.synchronize()
+    assert int(ovf.item()) == 0
+    assert torch.equal(keys, keys2) and torch.equal(rep, rep2)
+    out = torch.empty(1, dtype=torch.int64, device="cuda")
+    eng._check(eng.L.sd_cas_copy_objects_dev(eng.h, out.data_ptr(), eng.stream), "copy_objects")
+    torch.cuda.synchronize()
+    assert int(out.item()) == objects
+    # blocking form, twice (the region cursors are left zero by each call)
+    for _ in range(2):
+        rep2.zero_()
+        assert eng.hash_group_sampled(content, sizes, keys2, rep2, ovf) == objects
+        assert torch.equal(rep, rep2)
+    rng = np.random.default_rng(quanta)
+    idx = rng.integers(0, n, 200)
+    host = content[torch.from_numpy(idx).cuda()].cpu().numpy()
+    hs = sizes.cpu().numpy().view(np.uint64)[idx]
+    want = oracle.cas_keys_strided(host.reshape(-1), SAMPLED_CONTENT_LEN, SAMPLED_CONTENT_LEN, hs)
+    assert (keys2.cpu().numpy().view(np.uint64)[idx] == want).all()
+    orep, oobj = oracle.group_canonical(keys2.cpu().numpy().view(np.uint64))
+    assert oobj == objects and (rep2.cpu().numpy().astype(np.uint32) == orep).all()
+    del content
+    torch.cuda.empty_cache()
+
+
+def test_hash_group_fused_overflow_and_fallback(eng, oracle):
+    """A coarse bucket outgrowing its fixed region (one file copied 20,000 times in a batch of
+    one quantum: region capacity ~450 rows): the async call raises the overflow flag and the
+    caller's regroup gives the exact result; the blocking call regroups by itself.  A batch
+    that is not a multiple of the quantum runs K1 + the standalone chain (flag untouched)."""
+    q = eng.batch_quantum
+    for n, copies in [(q, 20_000), (q + 1000, 0)]:
+        content = torch.empty((n, SAMPLED_CONTENT_LEN), dtype=torch.uint8, device="cuda")
+        sizes = torch.empty(n, dtype=torch.int64, device="cuda")
+        eng.synth_sampled(71, 0, n, content, sizes, SAMPLED_CONTENT_LEN, dup_permille=100)
+        if copies:
+            content[1:copies + 1] = content[0]
+            sizes[1:copies + 1] = sizes[0]
+        keys = torch.empty(n, dtype=torch.int64, device="cuda")
+        rep = torch.empty(n, dtype=torch.int32, device="cuda")
+        eng.hash_sampled(content, sizes, keys)
+        objects = eng.group(keys, rep)
+        keys2 = torch.empty(n, dtype=torch.int64, device="cuda")
+        rep2 = torch.empty(n, dtype=torch.int32, device="cuda")
+        ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
+        eng.hash_group_sampled(content, sizes, keys2, rep2, ovf, want_objects=False)
+        torch.cuda.synchronize()
+        assert torch.equal(keys, keys2)
+        if copies:
+            assert int(ovf.item()) == 1
+            assert eng.group(keys2, rep2) == objects and torch.equal(rep, rep2)  # the caller's regroup
+            rep2.zero_()
+            ovf.zero_()
+            assert eng.hash_group_sampled(content, sizes, keys2, rep2, ovf) == objects
+        else:
+            assert int(ovf.item()) == 0
+        assert torch.equal(rep, rep2)
+        orep, oobj = oracle.group_canonical(keys.cpu().numpy().view(np.uint64))
+        assert oobj == objects and (rep.cpu().numpy().astype(np.uint32) == orep).all()
+        del content
+        torch.cuda.empty_cache()
+
+
 def test_workspace_ordered_across_streams(eng, oracle):
     """One context, device calls on two streams with no host sync between them: grouping,
     group_min and the packed hash's length sort share the context workspace, which the

@@ -15,17 +15,22 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--files", type=int, default=1_250_000)
 ap.add_argument("--iters", type=int, default=3)
 ap.add_argument("--group", action="store_true")
+ap.add_argument("--fused", action="store_true", help="K1G + bucket tables (hash_group_sampled)")
 a = ap.parse_args()
 eng = CasEngine(0)
 content = torch.empty((a.files, 57344), dtype=torch.uint8, device="cuda")
 sizes = torch.empty(a.files, dtype=torch.int64, device="cuda")
 keys = torch.empty(a.files, dtype=torch.int64, device="cuda")
 rep = torch.empty(a.files, dtype=torch.int32, device="cuda")
+ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
 eng.synth_sampled(7, 0, a.files, content, sizes, 57344, dup_permille=300)
 torch.cuda.synchronize()
 for i in range(a.iters):
     t = time.perf_counter()
-    eng.hash_sampled(content, sizes, keys)
+    if a.fused:
+        eng.hash_group_sampled(content, sizes, keys, rep, ovf, want_objects=False)
+    else:
+        eng.hash_sampled(content, sizes, keys)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t
     print(f"iter {i}: {dt*1e3:.2f} ms  {a.files*57352/dt/1e9:.0f} GB/s  {a.files/dt/1e6:.1f} M files/s", flush=True)
