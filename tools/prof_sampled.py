@@ -36,3 +36,6 @@ for i in range(a.iters):
     print(f"iter {i}: {dt*1e3:.2f} ms  {a.files*57352/dt/1e9:.0f} GB/s  {a.files/dt/1e6:.1f} M files/s", flush=True)
     if a.group:
         eng.group(keys, rep)
+# keys digest: variants of the kernel must agree (A/B parity)
+k = keys.cpu().numpy().view("uint64")
+print(f"keys_digest {int((k * 0x9E3779B97F4A7C15).sum() & 0xFFFFFFFFFFFFFFFF):016x}", flush=True)
