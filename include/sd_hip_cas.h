@@ -219,8 +219,9 @@ int sd_cas_hash_group_sampled_dev(sd_cas_ctx* ctx, const void* d_content, uint64
 /* The same chain in its two halves, for callers that pipeline batches: hash_regions = K1 +
  * the partition into one of the context's two region sets (n a multiple of the quantum, <=
  * 1,441,792, default group method: else SD_CAS_EINVAL), async; group_regions = the bucket
- * tables over the regions of the LAST hash_regions batch (same n), on any stream ordered
- * after it (an event), async unless out_objects != NULL.  The sets alternate, so batch i's
+ * tables over the regions of the LAST hash_regions batch (same n and d_rep: hash_regions
+ * prefilled it), on any stream ordered after it (an event), async unless out_objects != NULL;
+ * a batch that is hashed but never grouped is simply dropped by the next hash_regions.  The sets alternate, so batch i's
  * tables may run on a side stream while batch i+1 hashes; a set is refilled only after its
  * previous tables finished (the library orders that itself).  d_overflow as above. */
 int sd_cas_hash_regions_sampled_dev(sd_cas_ctx* ctx, const void* d_content, uint64_t stride,

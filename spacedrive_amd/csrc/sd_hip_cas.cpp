@@ -356,6 +356,8 @@ int sd_cas_hash_regions_sampled_dev(sd_cas_ctx* c, const void* d_content, uint64
   const int k = (c->region_cur + 1) & 1;
   // set k was last grouped two batches ago: its tables must be done before it is refilled
   if (c->region_pending[k]) HIP_TRY(c, hipStreamWaitEvent(s, c->region_done[k], 0));
+  // a batch hashed into set k but never grouped left its cursors counted: clear them
+  if (!c->region_grouped[k]) HIP_TRY(c, hipMemsetAsync(c->gcursor + 256 * k, 0, 1024, s));
   c->region_n[k] = n;  // sizes the layout (ensure below grows the set if needed)
   int rc = ensure(c, c->regions[k], region_group_workspace_bytes(n) + 256);
   if (rc) return rc;

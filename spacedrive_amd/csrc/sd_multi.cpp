@@ -436,6 +436,8 @@ int sd_cas_copy_objects_dev(sd_cas_ctx* c, uint64_t* d_dst, void* stream) {
     const uint64_t* obj = (const uint64_t*)((const char*)c->regions[k].p +
                                             sdcas::region_group_workspace_bytes(c->region_n[k]));
     HIP_TRY(c, hipMemcpyAsync(d_dst, obj, 8, hipMemcpyDeviceToDevice, s));
+    // the set's next refill (its K1G zeroes this counter) must also wait for this copy
+    HIP_TRY(c, hipEventRecord(c->region_done[k], s));
     return SD_CAS_OK;
   }
   HIP_TRY(c, sd_ws_acquire(c, s));

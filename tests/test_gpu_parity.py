@@ -458,6 +458,53 @@ def test_hash_group_fused_vs_standalone(eng, oracle, quanta):
     torch.cuda.empty_cache()
 
 
+def test_hash_regions_split_pipelined(eng, oracle):
+    """The fused chain's two halves as a pipelining caller uses them: batch i's bucket tables
+    on a side stream while batch i+1 hashes into the other region set (the library orders a
+    set's refill after its tables), a batch hashed but never grouped (its set's cursors must
+    not leak into the next batch), and the async Object count via copy_objects — every rep ==
+    the standalone grouping's."""
+    q = eng.batch_quantum
+    n = 2 * q
+    side = torch.cuda.Stream()
+    main = torch.cuda.current_stream()
+    batches = []
+    for j in range(4):
+        content = torch.empty((n, SAMPLED_CONTENT_LEN), dtype=torch.uint8, device="cuda")
+        sizes = torch.empty(n, dtype=torch.int64, device="cuda")
+        eng.synth_sampled(80 + j, j * n, n, content, sizes, SAMPLED_CONTENT_LEN, dup_permille=300)
+        batches.append((content, sizes))
+    torch.cuda.synchronize()
+    ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
+    keys = [torch.empty(n, dtype=torch.int64, device="cuda") for _ in range(4)]
+    reps = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(4)]
+    objs = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(4)]
+    done = []
+    for j, (content, sizes) in enumerate(batches):
+        eng.hash_regions_sampled(content, sizes, keys[j], reps[j], ovf, stream=main.cuda_stream)
+        if j == 1:
+            continue  # hashed, never grouped: dropped by the next hash_regions
+        ev = torch.cuda.Event()
+        ev.record(main)
+        side.wait_event(ev)
+        eng.group_regions(n, reps[j], stream=side.cuda_stream, want_objects=False)
+        eng._check(eng.L.sd_cas_copy_objects_dev(eng.h, objs[j].data_ptr(), side.cuda_stream), "copy")
+        done.append(j)
+    torch.cuda.synchronize()
+    assert int(ovf.item()) == 0
+    with pytest.raises(Exception):  # the last batch is grouped already
+        eng.group_regions(n, reps[3])
+    for j in done:
+        rep = torch.empty(n, dtype=torch.int32, device="cuda")
+        objects = eng.group(keys[j], rep)
+        assert torch.equal(rep, reps[j]) and int(objs[j].item()) == objects, j
+    kh = keys[0].cpu().numpy().view(np.uint64)
+    orep, oobj = oracle.group_canonical(kh)
+    assert (reps[0].cpu().numpy().astype(np.uint32) == orep).all() and oobj == int(objs[0].item())
+    del batches
+    torch.cuda.empty_cache()
+
+
 def test_hash_group_fused_overflow_and_fallback(eng, oracle):
     """A coarse bucket outgrowing its fixed region (one file copied 20,000 times in a batch of
     one quantum: region capacity ~450 rows): the async call raises the overflow flag and the
