@@ -822,10 +822,30 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
   std::vector<uint8_t> redo(n, 0);
   for (size_t i = 0; i < n; i++)
     lens[i] = status[i] ? 0 : sizes[i] > MINIMUM_FILE_SIZE ? SAMPLED_CONTENT_LEN : sizes[i];
-  // Windows of GATHER_WINDOW files, double-buffered: the pool gathers window w into one
-  // pinned slot while the GPU copies and hashes window w-1 from the other.
+  // Windows of files, double-buffered: the pool gathers window w into one pinned slot while
+  // the GPU copies and hashes window w-1 from the other.  The call takes about (gather of all
+  // windows) + (H2D + hash of the last one), so windows are cut by staged BYTES — about a
+  // twelfth of the batch each (2-64 MiB, <= GATHER_WINDOW files): config 1's 10k tmpfs files
+  // (~40 KB staged each) run in ~12 windows of ~830 files instead of 5 of 2,048, and the
+  // un-overlapped tail shrinks with the last window.
   constexpr size_t GATHER_WINDOW = 2048;
-  const size_t nw = (n + GATHER_WINDOW - 1) / GATHER_WINDOW;
+  std::vector<size_t> wstart{0};
+  {
+    uint64_t total = 0;
+    for (size_t i = 0; i < n; i++) total += up128(lens[i]);
+    const uint64_t target = std::min<uint64_t>(64ull << 20, std::max<uint64_t>(2ull << 20, total / 12));
+    uint64_t bytes = 0;
+    for (size_t i = 0; i < n; i++) {
+      const size_t files = i - wstart.back();
+      if (files && (files == GATHER_WINDOW || bytes + up128(lens[i]) > target)) {
+        wstart.push_back(i);
+        bytes = 0;
+      }
+      bytes += up128(lens[i]);
+    }
+    wstart.push_back(n);
+  }
+  const size_t nw = wstart.size() - 1;
   std::vector<Plan> plans(nw);
   size_t slot = 0;
   // decided rows plan as empty whole files (their metadata size may be anything)
@@ -833,7 +853,7 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
   for (size_t i = 0; i < n; i++)
     if (status[i]) psize[i] = 0;
   for (size_t w = 0; w < nw; w++) {
-    const size_t f0 = w * GATHER_WINDOW, m = std::min(GATHER_WINDOW, n - f0);
+    const size_t f0 = wstart[w], m = wstart[w + 1] - wstart[w];
     int rc = plan_batch(c, lens.data() + f0, psize.data() + f0, m, plans[w]);
     if (rc) return rc;
     slot = std::max(slot, up256(staged_pinned_bytes(plans[w], m)));
@@ -847,7 +867,7 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
     HIP_TRY(c, hipEventCreateWithFlags(&done[b], hipEventDisableTiming));
   auto gather = [&](size_t w, char* pin) {
     const Plan& pl = plans[w];
-    const size_t f0 = w * GATHER_WINDOW, m = std::min(GATHER_WINDOW, n - f0);
+    const size_t f0 = wstart[w], m = wstart[w + 1] - wstart[w];
     const size_t ns = pl.sampled.size(), np = pl.packed.size();
     const size_t content_bytes = pl.sampled_bytes + up256(pl.packed_bytes);
     uint32_t* h_plens = (uint32_t*)(pin + content_bytes + up256((ns + np) * 8) + up256(np * 8));
@@ -922,14 +942,14 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
   auto finish = [&](size_t w) -> int {
     const int b = (int)(w & 1);
     HIP_TRY(c, hipEventSynchronize(done[b]));
-    scatter_keys(plans[w], pin0 + b * slot, out_keys + w * GATHER_WINDOW);
+    scatter_keys(plans[w], pin0 + b * slot, out_keys + wstart[w]);
     return SD_CAS_OK;
   };
   for (size_t w = 0; w < nw && rc == 0; w++) {
     const int b = (int)(w & 1);
     if (w >= 2 && (rc = finish(w - 2))) break;  // slot b free again
     gather(w, pin0 + b * slot);
-    const size_t f0 = w * GATHER_WINDOW, m = std::min(GATHER_WINDOW, n - f0);
+    const size_t f0 = wstart[w], m = wstart[w + 1] - wstart[w];
     rc = enqueue_staged(c, plans[w], psize.data() + f0, m, pin0 + b * slot, dev0 + b * slot, done[b]);
   }
   for (size_t w = nw >= 2 ? nw - 2 : 0; w < nw && rc == 0; w++) rc = finish(w);
