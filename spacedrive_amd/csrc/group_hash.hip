@@ -49,8 +49,24 @@ namespace sdcas {
 constexpr int PART_THREADS = 512;
 constexpr int ITEMS = 8;
 constexpr uint32_t PART_TILE = PART_THREADS * ITEMS;  // 4096 keys per block trip
-constexpr int MIN_THREADS = 512;
-constexpr uint32_t TABLE = 4096;          // LDS slots per bucket (48 KiB: 3 workgroups/CU)
+#ifndef SD_MIN_THREADS
+#define SD_MIN_THREADS 512
+#endif
+#ifndef SD_MIN_TABLE
+#define SD_MIN_TABLE 4096
+#endif
+constexpr int MIN_THREADS = SD_MIN_THREADS;
+// keys per thread per trip of the fine-bucket tables (mean bucket <= 1,536 keys: one trip of
+// 2,048) and whether their lookup reuses the insert's slots (A/B: DESIGN.md §2.2)
+#ifndef SD_MIN_ITEMS
+#define SD_MIN_ITEMS 4
+#endif
+#ifndef SD_MIN_KEEP_SLOT
+#define SD_MIN_KEEP_SLOT 1
+#endif
+constexpr int MIN_ITEMS = SD_MIN_ITEMS;
+constexpr bool MIN_KEEP_SLOT = SD_MIN_KEEP_SLOT;
+constexpr uint32_t TABLE = SD_MIN_TABLE;  // LDS slots per bucket (4,096: 48 KiB, 3 workgroups/CU)
 constexpr uint32_t BIG_TABLE = 12288;     // sd_bucket_min_big: 144 KiB LDS, 1 workgroup/CU
 constexpr int BIG_THREADS = 1024;
 constexpr uint64_t BIG_MAX_KEYS = 256ull * 5632;  // mean coarse bucket <= 5,632 keys
@@ -62,6 +78,10 @@ constexpr uint32_t TOTALS_REPL = 16;                  // interleaved copies of t
 // plan the mean bucket may grow to MAX_MEAN_PER_BUCKET distinct keys (LDS table fill 3,584)
 constexpr uint32_t MAX_BITS = 19;
 constexpr uint32_t MAX_B2 = 9;
+#ifndef SD_COARSE10_KEYS
+#define SD_COARSE10_KEYS 40000000
+#endif
+constexpr uint64_t COARSE10_KEYS = SD_COARSE10_KEYS;
 constexpr uint64_t MAX_MEAN_PER_BUCKET = 2500;
 
 
@@ -206,6 +226,8 @@ __device__ __forceinline__ void staged_trip(const uint64_t (&k)[ITEMS], const ui
     for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS)
       if (tcnt[b]) gcur[b] = bstart[b] + atomicAdd(&fill[b], tcnt[b]);
   }
+  // (consuming each reservation only after the LDS scan and staging below, so its round trip
+  // overlapped them, changed nothing: profiles/r03b_group_ab/abg5)
   lds_exclusive_scan(tcnt, tstart, nb);  // (its barriers also publish gcur)
   // conservation: the trip's per-bucket counts add up to the trip
   SD_DBG_CHECK(threadIdx.x != 0 || tstart[nb - 1] + tcnt[nb - 1] == trip_n,
@@ -463,45 +485,56 @@ __device__ __forceinline__ uint32_t next_slot(uint32_t s) {
   return s + 1 == TBL ? 0u : s + 1;
 }
 
-// Linear-probing tables: LDS (the normal case) and global memory (overflow).  `fresh`
-// counts keys this thread inserted first.  Returns false if the table has no room.  The
-// LDS insert CASes first (one LDS round trip per probe; at the tables' fill most first
-// probes find the slot empty) — reading the slot before the CAS was 1-2 % slower
-// (profiles/r02_group_ab3.log).
+// Linear-probing tables: LDS (the normal case) and global memory (overflow).
+// lds_claim: the slot holding k after inserting it (CAS-first: one LDS round trip per probe;
+// at the tables' fill most first probes find the slot empty — reading the slot before the
+// CAS was 1-2 % slower, profiles/r02_group_ab3.log), or TBL if the table has no room;
+// `fresh` counts keys this thread inserted first.  The probe loop is one exec-masked region
+// per round with no branch inside: the table's value (the minimum) is updated after the
+// loop, once per key.  PMC (profiles/r03b_group_ab/): the earlier form, with the atomic min
+// and a read-first branch inside the loop, issued ~680 scalar instructions per wave — exec
+// mask bookkeeping of the nested divergent branches — against one scalar issue per cycle
+// per CU, the bucket tables' binding limit (SQ_INSTS_SALU 1.6x SQ_INSTS_VALU).
 // READ_FIRST (buckets of more than one trip, i.e. a key repeated thousands of times): read
-// the slot and CAS only if it is empty, and skip the atomic min when the slot already holds
-// a smaller value — one hot key otherwise serialises every lane's CAS and min on one LDS
-// address (a key making up 40 % of 1.31 M keys: 1.19 -> 0.49 ms); uniform buckets keep the
-// CAS-first form.
+// the slot and CAS only if it is empty — one hot key otherwise serialises every lane's CAS
+// on one LDS address (a key making up 40 % of 1.31 M keys: 1.19 -> 0.49 ms).
 template <uint32_t TBL, bool READ_FIRST = false>
-__device__ __forceinline__ bool lds_insert(uint64_t* tk, uint32_t* tv, uint32_t& slot, uint64_t k,
-                                           uint32_t v, uint64_t empty, uint32_t& fresh) {
-  for (uint32_t probe = 0; probe < TBL; ++probe) {
-    uint64_t cur;
-    if (READ_FIRST) {
-      cur = tk[slot];
-      if (cur == empty) {
-        cur = atomicCAS((unsigned long long*)&tk[slot], (unsigned long long)empty,
-                        (unsigned long long)k);
-        if (cur == empty) { ++fresh; cur = k; }
-      }
-    } else {
-      cur = atomicCAS((unsigned long long*)&tk[slot], (unsigned long long)empty,
-                      (unsigned long long)k);
-      if (cur == empty) { ++fresh; cur = k; }
-    }
-    if (cur == k) {
-      if (!READ_FIRST || tv[slot] > v) atomicMin(&tv[slot], v);
-      return true;
-    }
-    slot = next_slot<TBL>(slot);
+__device__ __forceinline__ uint32_t lds_claim(uint64_t* tk, uint32_t slot, uint64_t k, uint64_t empty,
+                                              uint32_t& fresh) {
+  uint64_t cur;
+  bool done;
+  if (!READ_FIRST) {
+    // one-trip buckets: at most TILE < TBL keys ever enter the table, so an empty slot
+    // always exists and the loop needs no probe bound (which costs a branch per round)
+#pragma unroll 1
+    do {
+      cur = atomicCAS((unsigned long long*)&tk[slot], (unsigned long long)empty, (unsigned long long)k);
+      done = cur == empty || cur == k;
+      slot = done ? slot : next_slot<TBL>(slot);
+    } while (!done);
+    fresh += cur == empty;
+    return slot;
   }
-  return false;
+  // multi-trip buckets: up to FILL keys from earlier trips plus this trip's may exceed TBL
+  uint32_t probe = 0;
+#pragma unroll 1
+  do {
+    cur = tk[slot];
+    if (cur == empty) {
+      cur = atomicCAS((unsigned long long*)&tk[slot], (unsigned long long)empty, (unsigned long long)k);
+      fresh += cur == empty;
+    }
+    done = cur == empty || cur == k;
+    slot = done ? slot : next_slot<TBL>(slot);
+  } while (!done && ++probe < TBL);
+  return done ? slot : TBL;
 }
 
 template <uint32_t TBL>
 __device__ __forceinline__ uint32_t lds_find(const uint64_t* tk, uint32_t slot, uint64_t k) {
-  while (tk[slot] != k) slot = next_slot<TBL>(slot);  // present by construction
+  uint32_t probe = 0;  // present by construction; bounded anyway
+#pragma unroll 1
+  while (tk[slot] != k && ++probe < TBL) slot = next_slot<TBL>(slot);
   return slot;
 }
 
@@ -540,13 +573,13 @@ __device__ __forceinline__ uint64_t g_find(const uint64_t* tk, uint64_t cap, uin
 // A bucket of <= TILE keys (all but pathological ones) is loaded once and kept in
 // registers for the lookup; larger buckets stream in TILE trips.
 // KEEP_SLOT: the one-trip lookup reads the slot each key landed in during the insert
-// instead of probing again — faster for the big tables (1.31M keys: 0.064 -> 0.060
-// ms), slower for the 4,096-slot ones (12.5M keys: 0.369 -> 0.398 ms; A/B in
-// profiles/r02_group_ab.log), so only sd_bucket_min_big keeps it.
+// instead of probing again (round 2 measured it slower for the 4,096-slot tables: with 8
+// keys per lane it cost occupancy; at 4 keys per lane it is the same or faster,
+// profiles/r03b_group_ab/).
 // Regions (the fused hash + group chain): counts != nullptr — bucket b's keys are rows
 // [b * region_cap, b * region_cap + min(counts[b], region_cap)) and the workgroup re-zeroes
 // counts[b] after reading it (the region cursors' persistent-zero invariant).
-template <uint32_t TBL, int THREADS, bool KEEP_SLOT>
+template <uint32_t TBL, int THREADS, int NI, bool KEEP_SLOT>
 __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict__ rezero,
                                            uint32_t rezero_words,
                                            const uint64_t* __restrict__ pkeys,
@@ -559,8 +592,9 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
                                            uint32_t* __restrict__ gvals,
                                            uint32_t* __restrict__ counts = nullptr,
                                            uint64_t region_cap = 0) {
-  constexpr uint32_t TILE = THREADS * ITEMS;
+  constexpr uint32_t TILE = THREADS * NI;
   constexpr uint32_t FILL = TBL / 8 * 7;  // above this the bucket goes to global memory
+  static_assert(TILE < TBL, "one-trip buckets must leave an empty slot (lds_claim's unbounded probe)");
   __shared__ uint64_t tk[TBL];
   __shared__ uint32_t tv[TBL];
   __shared__ uint32_t distinct;
@@ -587,49 +621,57 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
     s = starts[b];
     e = b + 1 < nb ? starts[b + 1] : n;
   }
-  if (s == e) return;  // uniform for the whole workgroup
-  // every stored key of this bucket has top bits == b, so a key from bucket b^1 is never stored
+  // every stored key of this bucket has top bits == b, so a key from bucket b^1 is never
+  // stored; the table is initialised while the bucket bounds are in flight
   const uint64_t empty = (uint64_t)(b ^ 1u) << (64 - bits);
   for (uint32_t i = threadIdx.x; i < TBL; i += THREADS) { tk[i] = empty; tv[i] = 0xFFFFFFFFu; }
   if (threadIdx.x == 0) { distinct = 0; ovf[0] = 0; ovf[1] = 0; }
+  if (s == e) return;  // uniform for the whole workgroup
 #if SD_DBG
   __shared__ unsigned int dbg_seen;  // keys inserted: must be the bucket's e - s
   if (threadIdx.x == 0) dbg_seen = 0;
 #endif
-  uint64_t k[ITEMS];
-  uint32_t p[ITEMS], v[ITEMS], sl[ITEMS];
+  uint64_t k[NI];
+  uint32_t p[NI], v[NI], sl[NI];
   uint32_t trip = 0;
   for (uint64_t base = s; base < e; base += TILE, ++trip) {
 #pragma unroll
-    for (int j = 0; j < ITEMS; ++j) {
+    for (int j = 0; j < NI; ++j) {
       const uint64_t i = base + (uint64_t)j * THREADS + threadIdx.x;
       k[j] = i < e ? pkeys[i] : empty;
       p[j] = i < e ? ppos[i] : 0u;
     }
 #pragma unroll
-    for (int j = 0; j < ITEMS; ++j) v[j] = (vals && k[j] != empty) ? vals[p[j]] : p[j];
+    for (int j = 0; j < NI; ++j) v[j] = (vals && k[j] != empty) ? vals[p[j]] : p[j];
     __syncthreads();  // table initialised (first trip) / the previous trip's flag visible
     if (ovf[(trip + 1) & 1]) break;  // raised by trip - 1 (ovf[1] = 0 on the first trip)
     uint32_t fresh = 0;
     bool ok = true;
+    // -> each key's slot (kept for the one-trip lookup), then its minimum
     if (e - s <= TILE) {
 #pragma unroll
-      for (int j = 0; j < ITEMS; ++j) {
-        sl[j] = home_slot<TBL>(k[j]);  // -> the key's slot (kept for the one-trip lookup)
-        if (k[j] != empty) ok &= lds_insert<TBL>(tk, tv, sl[j], k[j], v[j], empty, fresh);
+      for (int j = 0; j < NI; ++j)
+        if (k[j] != empty) sl[j] = lds_claim<TBL>(tk, home_slot<TBL>(k[j]), k[j], empty, fresh);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        if (k[j] != empty && sl[j] < TBL) atomicMin(&tv[sl[j]], v[j]);
+        ok &= k[j] == empty || sl[j] < TBL;
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < ITEMS; ++j) {
-        sl[j] = home_slot<TBL>(k[j]);
-        if (k[j] != empty) ok &= lds_insert<TBL, true>(tk, tv, sl[j], k[j], v[j], empty, fresh);
+      for (int j = 0; j < NI; ++j)
+        if (k[j] != empty) sl[j] = lds_claim<TBL, true>(tk, home_slot<TBL>(k[j]), k[j], empty, fresh);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        if (k[j] != empty && sl[j] < TBL && tv[sl[j]] > v[j]) atomicMin(&tv[sl[j]], v[j]);
+        ok &= k[j] == empty || sl[j] < TBL;
       }
     }
     if ((fresh && atomicAdd(&distinct, fresh) + fresh > FILL) || !ok) ovf[trip & 1] = 1;
 #if SD_DBG
     unsigned int seen = 0;
 #pragma unroll
-    for (int j = 0; j < ITEMS; ++j) seen += k[j] != empty;
+    for (int j = 0; j < NI; ++j) seen += k[j] != empty;
     if (seen) atomicAdd(&dbg_seen, seen);
 #endif
   }
@@ -641,7 +683,7 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
   if (!overflow) {
     if (e - s <= TILE) {  // the one trip's keys and their slots are still in registers
 #pragma unroll
-      for (int j = 0; j < ITEMS; ++j)
+      for (int j = 0; j < NI; ++j)
         if (k[j] != empty) {
           const uint32_t mv =
               tv[KEEP_SLOT ? sl[j] : lds_find<TBL>(tk, home_slot<TBL>(k[j]), k[j])];
@@ -650,13 +692,13 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
     } else {
       for (uint64_t base = s; base < e; base += TILE) {
 #pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
+        for (int j = 0; j < NI; ++j) {
           const uint64_t i = base + (uint64_t)j * THREADS + threadIdx.x;
           k[j] = i < e ? pkeys[i] : empty;
           p[j] = i < e ? ppos[i] : 0u;
         }
 #pragma unroll
-        for (int j = 0; j < ITEMS; ++j)
+        for (int j = 0; j < NI; ++j)
           if (k[j] != empty) {
             const uint32_t mv = tv[lds_find<TBL>(tk, home_slot<TBL>(k[j]), k[j])];
             if (mv != (vals ? vals[p[j]] : p[j])) out[p[j]] = mv;
@@ -700,7 +742,7 @@ sd_bucket_min(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ p
               uint32_t bits, uint64_t n, uint32_t* __restrict__ out,
               unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
               uint32_t* __restrict__ gvals, uint32_t* __restrict__ rezero, uint32_t rezero_words) {
-  bucket_min<TABLE, MIN_THREADS, false>(blockIdx.x, rezero, rezero_words, pkeys, ppos, vals, starts,
+  bucket_min<TABLE, MIN_THREADS, MIN_ITEMS, MIN_KEEP_SLOT>(blockIdx.x, rezero, rezero_words, pkeys, ppos, vals, starts,
                                         nb, bits, n, out, objects, gkeys, gvals);
 }
 
@@ -716,7 +758,7 @@ sd_bucket_min_big(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict
                   unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
                   uint32_t* __restrict__ gvals, uint32_t* __restrict__ rezero,
                   uint32_t rezero_words) {
-  bucket_min<BIG_TABLE, BIG_THREADS, true>(blockIdx.x, rezero, rezero_words, pkeys, ppos, vals,
+  bucket_min<BIG_TABLE, BIG_THREADS, ITEMS, true>(blockIdx.x, rezero, rezero_words, pkeys, ppos, vals,
                                            starts, nb, bits, n, out, objects, gkeys, gvals);
 }
 
@@ -727,7 +769,7 @@ sd_bucket_min_regions(const uint64_t* __restrict__ rkeys, const uint32_t* __rest
                       uint32_t* __restrict__ cursor, uint64_t cap, uint32_t* __restrict__ out,
                       unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
                       uint32_t* __restrict__ gvals) {
-  bucket_min<BIG_TABLE, BIG_THREADS, true>(blockIdx.x, nullptr, 0, rkeys, rfile, nullptr, nullptr,
+  bucket_min<BIG_TABLE, BIG_THREADS, ITEMS, true>(blockIdx.x, nullptr, 0, rkeys, rfile, nullptr, nullptr,
                                            REGIONS, REGION_BITS, 0, out, objects, gkeys, gvals,
                                            cursor, cap);
 }
@@ -810,9 +852,14 @@ static GroupPlan group_plan(uint64_t n, uint64_t target) {
   uint32_t bits = 1;
   while (bits < MAX_BITS && ((uint64_t)1 << bits) * target < n) ++bits;
   GroupPlan g;
-  // coarse level: 2^8 buckets (runs of ~16 keys per 4,096-key trip), more only when the
-  // refine level would exceed 2^MAX_B2 fine buckets per coarse bucket (> ~200M keys)
-  g.b1 = bits < 8 ? bits : (bits - 8 > MAX_B2 ? bits - MAX_B2 : 8);
+  // coarse level: 2^8 buckets (runs of ~16 keys per 4,096-key trip); above COARSE10_KEYS,
+  // 2^10 (one refine workgroup per coarse bucket walks ~100 K keys instead of ~400 K at 100 M
+  // keys: 2.96 -> 2.89 ms; at 12.5 M the 1,024-bucket scatter's shorter runs cost more than
+  // the refine saves, 0.307 -> 0.327 ms, profiles/r03b_group_ab/abg5); more only when the
+  // refine level would exceed 2^MAX_B2 fine buckets per coarse bucket (> ~200M keys);
+  // b1 <= 10 whatever n (MAX_BITS - MAX_B2)
+  const uint32_t cb = n <= COARSE10_KEYS ? 8u : 10u;
+  g.b1 = bits < cb ? bits : (bits - cb > MAX_B2 ? bits - MAX_B2 : cb);
   g.b2 = bits - g.b1;
   g.big = g.b2 > 0 && n <= BIG_MAX_KEYS;
   if (g.big) g.b2 = 0;

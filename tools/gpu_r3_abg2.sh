@@ -2,7 +2,7 @@
 # Round 3: grouping-table rework.  (1) the grouping GPU tests on the in-tree build, (2) the
 # chain at 1.31 M / 12.5 M / 100 M keys: in-tree vs every tools/ablib/g_*.so, interleaved 2
 # rounds (tools/ab_group.py), (3) rocprofv3 kernel stats of the in-tree chain at 12.5 M.
-# Usage: <tag>
+# Usage: <tag>   (env SIZES = key counts, PROF=0 skips (3))
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/${1:-r3_abg2}
@@ -14,10 +14,11 @@ for round in 1 2; do
   for lib in current $R/tools/ablib/g_*.so; do
     name=$(basename $lib .so)
     if [ $lib = current ]; then unset SD_HIP_CAS_LIB; else export SD_HIP_CAS_LIB=$lib; fi
-    timeout -k 10 200 python3 -u tools/ab_group.py 1310720 12500000 100000000 > $OUT/g_${name}_r$round.log 2>&1 || { echo "FAIL $name"; tail -5 $OUT/g_${name}_r$round.log; exit 1; }
+    timeout -k 10 200 python3 -u tools/ab_group.py ${SIZES:-1310720 12500000 100000000} > $OUT/g_${name}_r$round.log 2>&1 || { echo "FAIL $name"; tail -5 $OUT/g_${name}_r$round.log; exit 1; }
     tail -1 $OUT/g_${name}_r$round.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['lib'], 'r$round', {k: (round(v['ms'],4), round(v['hbm_frac'],3), v['objects'], v['rep_digest']) for k, v in d.items() if k != 'lib'})"
   done
 done
+[ "${PROF:-1}" = 0 ] && { echo ABG2_OK; exit 0; }
 cd /tmp && export TMPDIR=/tmp
 for lib in current $R/tools/ablib/g_*.so; do
   name=$(basename $lib .so)
