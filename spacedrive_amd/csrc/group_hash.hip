@@ -65,6 +65,9 @@ constexpr int MIN_THREADS = SD_MIN_THREADS;
 #define SD_MIN_KEEP_SLOT 1
 #endif
 constexpr int MIN_ITEMS = SD_MIN_ITEMS;
+#ifndef SD_ONE_TRIP_READ_FIRST
+#define SD_ONE_TRIP_READ_FIRST 0
+#endif
 constexpr bool MIN_KEEP_SLOT = SD_MIN_KEEP_SLOT;
 constexpr uint32_t TABLE = SD_MIN_TABLE;  // LDS slots per bucket (4,096: 48 KiB, 3 workgroups/CU)
 constexpr uint32_t BIG_TABLE = 12288;     // sd_bucket_min_big: 144 KiB LDS, 1 workgroup/CU
@@ -651,7 +654,8 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
     if (e - s <= TILE) {
 #pragma unroll
       for (int j = 0; j < NI; ++j)
-        if (k[j] != empty) sl[j] = lds_claim<TBL>(tk, home_slot<TBL>(k[j]), k[j], empty, fresh);
+        if (k[j] != empty)
+          sl[j] = lds_claim<TBL, SD_ONE_TRIP_READ_FIRST>(tk, home_slot<TBL>(k[j]), k[j], empty, fresh);
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         if (k[j] != empty && sl[j] < TBL) atomicMin(&tv[sl[j]], v[j]);
@@ -667,7 +671,22 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
         ok &= k[j] == empty || sl[j] < TBL;
       }
     }
-    if ((fresh && atomicAdd(&distinct, fresh) + fresh > FILL) || !ok) ovf[trip & 1] = 1;
+    if (THREADS >= 1024) {
+      // the big tables (one 16-wave workgroup per CU, latency-bound): the wave's fresh keys
+      // summed by ballots (fresh <= NI <= 15 per lane), one returning LDS atomic per wave
+      // instead of one per lane on one address — insert phase 6.6 -> 3.4 us, 1.31 M keys
+      // 0.0466 -> 0.0433-0.0441 ms.  The fine tables keep one per lane: their insert phase
+      // halved too (3.9 -> 1.8 us), but the kernel ran 6-9 % LONGER, its bounds and stores
+      // phases stretching (profiles/r03b_group_ab/abg8, abg10)
+      static_assert(NI <= 15, "fresh fits 4 bits");
+      const uint32_t wfresh = __popcll(__ballot(fresh & 1u)) + 2u * __popcll(__ballot(fresh & 2u)) +
+                              4u * __popcll(__ballot(fresh & 4u)) + 8u * __popcll(__ballot(fresh & 8u));
+      if ((threadIdx.x & 63u) == 0 && wfresh && atomicAdd(&distinct, wfresh) + wfresh > FILL)
+        ovf[trip & 1] = 1;
+      if (!ok) ovf[trip & 1] = 1;
+    } else if ((fresh && atomicAdd(&distinct, fresh) + fresh > FILL) || !ok) {
+      ovf[trip & 1] = 1;
+    }
 #if SD_DBG
     unsigned int seen = 0;
 #pragma unroll
@@ -742,8 +761,9 @@ sd_bucket_min(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ p
               uint32_t bits, uint64_t n, uint32_t* __restrict__ out,
               unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
               uint32_t* __restrict__ gvals, uint32_t* __restrict__ rezero, uint32_t rezero_words) {
-  bucket_min<TABLE, MIN_THREADS, MIN_ITEMS, MIN_KEEP_SLOT>(blockIdx.x, rezero, rezero_words, pkeys, ppos, vals, starts,
-                                        nb, bits, n, out, objects, gkeys, gvals);
+  bucket_min<TABLE, MIN_THREADS, MIN_ITEMS, MIN_KEEP_SLOT>(blockIdx.x, rezero, rezero_words, pkeys, ppos,
+                                                          vals, starts, nb, bits, n, out, objects,
+                                                          gkeys, gvals);
 }
 
 // Small batches (<= BIG_MAX_KEYS): the 2^8 coarse buckets of the first partition level

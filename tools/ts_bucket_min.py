@@ -29,6 +29,8 @@ L = _native.lib()
 nb = 1
 while nb * 1536 < n:
     nb *= 2
+if n <= 256 * 5632:  # the big tables: 256 coarse buckets (instrumented build ts_big)
+    nb = 256
 buf = np.zeros(65536 * 5, dtype=np.uint64)
 assert L.sd_dbg_bucket_ts(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes)) == 0
 ts = buf[: nb * 5].reshape(nb, 5).astype(np.int64)
