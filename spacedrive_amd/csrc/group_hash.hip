@@ -86,6 +86,19 @@ constexpr uint32_t MAX_B2 = 9;
 #endif
 constexpr uint64_t COARSE10_KEYS = SD_COARSE10_KEYS;
 constexpr uint64_t MAX_MEAN_PER_BUCKET = 2500;
+// The fine-bucket tables (one workgroup per ~1,500 keys: 8,192 at 12.5 M keys, 65,536 at
+// 100 M) add their distinct-key counts into OBJ_SHARDS counters, each on a 128-B line of its
+// own (workgroup b into shard b % OBJ_SHARDS), summed into the Object count by one 64-lane
+// launch after them.  Device-scope atomics on ONE counter complete one per ~12.8 ns: 8,192 of
+// them took 105 us where the same workgroups' loads alone took 27 us, and 29 us with 64
+// counters (tools/ubench_bucketload.hip, profiles/r03b_group_ab/).  SD_GROUP_OBJ_SHARDS=1:
+// one counter (the A/B base).
+#ifndef SD_GROUP_OBJ_SHARDS
+#define SD_GROUP_OBJ_SHARDS 64
+#endif
+constexpr uint32_t OBJ_SHARDS = SD_GROUP_OBJ_SHARDS;
+static_assert(OBJ_SHARDS >= 1 && OBJ_SHARDS <= 64, "sd_objects_sum is one wave");
+constexpr uint32_t OBJ_STRIDE = 16;  // u64 words: one 128-B line per shard
 
 
 // mode 0 (grouping): bucket = top bits of mix64(key), the stored key is mix64(key)
@@ -121,12 +134,13 @@ template <int MODE>
 __device__ void part_totals_body(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb,
                                  uint64_t per_block, uint32_t* __restrict__ totals, uint32_t repl,
                                  uint32_t* __restrict__ fill, unsigned long long* __restrict__ objects,
-                                 const uint32_t* __restrict__ vals, uint32_t* __restrict__ prefill) {
+                                 uint32_t nobj, const uint32_t* __restrict__ vals,
+                                 uint32_t* __restrict__ prefill) {
   extern __shared__ uint32_t cnt[];
   for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS) cnt[b] = 0;
   if (blockIdx.x == 0) {
     for (uint32_t b = threadIdx.x; b < repl * nb; b += PART_THREADS) fill[b] = 0;
-    if (objects && threadIdx.x == 0) *objects = 0;
+    if (objects && threadIdx.x < nobj) objects[threadIdx.x * OBJ_STRIDE] = 0;  // the shards
   }
   __syncthreads();
   const uint64_t lo = (uint64_t)blockIdx.x * per_block;
@@ -366,14 +380,14 @@ __device__ void part_scatter_body(const uint64_t* __restrict__ keys, uint64_t n,
 extern "C" __global__ void __launch_bounds__(PART_THREADS)
 sd_part_totals_mix(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb, uint64_t per_block,
                    uint32_t* __restrict__ totals, uint32_t repl, uint32_t* __restrict__ fill,
-                   unsigned long long* __restrict__ objects, const uint32_t* __restrict__ vals,
-                   uint32_t* __restrict__ prefill) {
-  part_totals_body<0>(keys, n, nb, per_block, totals, repl, fill, objects, vals, prefill);
+                   unsigned long long* __restrict__ objects, uint32_t nobj,
+                   const uint32_t* __restrict__ vals, uint32_t* __restrict__ prefill) {
+  part_totals_body<0>(keys, n, nb, per_block, totals, repl, fill, objects, nobj, vals, prefill);
 }
 extern "C" __global__ void __launch_bounds__(PART_THREADS)
 sd_part_totals_range(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb, uint64_t per_block,
                      uint32_t* __restrict__ totals, uint32_t repl, uint32_t* __restrict__ fill) {
-  part_totals_body<1>(keys, n, nb, per_block, totals, repl, fill, nullptr, nullptr, nullptr);
+  part_totals_body<1>(keys, n, nb, per_block, totals, repl, fill, nullptr, 0, nullptr, nullptr);
 }
 extern "C" __global__ void __launch_bounds__(PART_THREADS)
 sd_part_scatter_mix(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb, uint64_t per_block,
@@ -671,22 +685,17 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
         ok &= k[j] == empty || sl[j] < TBL;
       }
     }
-    if (THREADS >= 1024) {
-      // the big tables (one 16-wave workgroup per CU, latency-bound): the wave's fresh keys
-      // summed by ballots (fresh <= NI <= 15 per lane), one returning LDS atomic per wave
-      // instead of one per lane on one address — insert phase 6.6 -> 3.4 us, 1.31 M keys
-      // 0.0466 -> 0.0433-0.0441 ms.  The fine tables keep one per lane: their insert phase
-      // halved too (3.9 -> 1.8 us), but the kernel ran 6-9 % LONGER, its bounds and stores
-      // phases stretching (profiles/r03b_group_ab/abg8, abg10)
-      static_assert(NI <= 15, "fresh fits 4 bits");
-      const uint32_t wfresh = __popcll(__ballot(fresh & 1u)) + 2u * __popcll(__ballot(fresh & 2u)) +
-                              4u * __popcll(__ballot(fresh & 4u)) + 8u * __popcll(__ballot(fresh & 8u));
-      if ((threadIdx.x & 63u) == 0 && wfresh && atomicAdd(&distinct, wfresh) + wfresh > FILL)
-        ovf[trip & 1] = 1;
-      if (!ok) ovf[trip & 1] = 1;
-    } else if ((fresh && atomicAdd(&distinct, fresh) + fresh > FILL) || !ok) {
+    // the wave's fresh keys summed by ballots (fresh <= NI <= 15 per lane), one returning LDS
+    // atomic per wave instead of one per lane on one address: the insert phase halved (fine
+    // tables 3.9 -> 1.8 us, big 6.6 -> 3.4 us per workgroup); sd_bucket_min at 12.5 M keys
+    // 106.6 -> 87.8 us once its Object count is sharded (before that the one device counter
+    // bound the kernel either way, profiles/r03b_group_ab/abg16)
+    static_assert(NI <= 15, "fresh fits 4 bits");
+    const uint32_t wfresh = __popcll(__ballot(fresh & 1u)) + 2u * __popcll(__ballot(fresh & 2u)) +
+                            4u * __popcll(__ballot(fresh & 4u)) + 8u * __popcll(__ballot(fresh & 8u));
+    if ((threadIdx.x & 63u) == 0 && wfresh && atomicAdd(&distinct, wfresh) + wfresh > FILL)
       ovf[trip & 1] = 1;
-    }
+    if (!ok) ovf[trip & 1] = 1;
 #if SD_DBG
     unsigned int seen = 0;
 #pragma unroll
@@ -762,7 +771,8 @@ sd_bucket_min(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict__ p
               unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
               uint32_t* __restrict__ gvals, uint32_t* __restrict__ rezero, uint32_t rezero_words) {
   bucket_min<TABLE, MIN_THREADS, MIN_ITEMS, MIN_KEEP_SLOT>(blockIdx.x, rezero, rezero_words, pkeys, ppos,
-                                                          vals, starts, nb, bits, n, out, objects,
+                                                          vals, starts, nb, bits, n, out,
+                                                          objects + (blockIdx.x % OBJ_SHARDS) * OBJ_STRIDE,
                                                           gkeys, gvals);
 }
 
@@ -894,18 +904,30 @@ bool hash_group_supported(uint64_t n) {
 
 static uint32_t totals_repl(uint32_t nb) { return nb <= STAGED_MAX_NB ? TOTALS_REPL : 1; }
 
-// workspace: k1 | p1 | k2 | p2 | fill (repl copies) | starts1 | starts | overflow tables (the
-// bucket totals live in a persistent buffer of the caller, GROUP_TOTALS_WORDS)
+// workspace: k1 | p1 | k2 | p2 | fill (repl copies) | starts1 | starts | Object-count shards |
+// overflow tables (the bucket totals live in a persistent buffer of the caller,
+// GROUP_TOTALS_WORDS)
 size_t hash_group_workspace_bytes(uint64_t n, uint64_t target) {
   const GroupPlan g = group_plan(n, target);
   const size_t nb1 = g.l1.nb;
   return 2 * (al256(n * 8) + al256(n * 4)) + al256(totals_repl(nb1) * nb1 * 4) +
-         al256(nb1 * 4) + al256((size_t)g.nb() * 4) + al256(2 * n * 8) + al256(2 * n * 4);
+         al256(nb1 * 4) + al256((size_t)g.nb() * 4) + al256(OBJ_SHARDS * OBJ_STRIDE * 8) +
+         al256(2 * n * 8) + al256(2 * n * 4);
 }
 
 size_t partition_workspace_bytes(uint64_t n, uint32_t parts) {
   (void)n;
   return 2 * al256((size_t)totals_repl(parts) * parts * 4);
+}
+
+// the Object count of a sharded chain: *objects = the sum of its shards
+extern "C" __global__ void __launch_bounds__(64)
+sd_objects_sum(const unsigned long long* __restrict__ shards, uint32_t nshards,
+               unsigned long long* __restrict__ objects) {
+  unsigned long long x = threadIdx.x < nshards ? shards[threadIdx.x * OBJ_STRIDE] : 0ull;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  if (threadIdx.x == 0) *objects = x;
 }
 
 // Zeroes the bucket totals ahead of the chain: a kernel of our own, because a
@@ -933,7 +955,8 @@ SD_DBG_ACCESSOR(sd_dbg_violations_group_hash)
 static hipError_t run_partition(const uint64_t* keys, uint64_t n, const PartPlan& p, int mode,
                                 uint64_t* out_keys, uint32_t* out_pos, uint32_t* totals,
                                 bool totals_zero, uint32_t* fill, uint32_t* starts_out,
-                                uint64_t* counts_out, unsigned long long* objects, hipStream_t s,
+                                uint64_t* counts_out, unsigned long long* objects, uint32_t nobj,
+                                hipStream_t s,
                                 const uint32_t* vals = nullptr, uint32_t* prefill = nullptr) {
   const uint32_t repl = totals_repl(p.nb);
   const uint32_t words = repl * p.nb;
@@ -942,7 +965,7 @@ static hipError_t run_partition(const uint64_t* keys, uint64_t n, const PartPlan
   const size_t lds = (size_t)p.nb * 4, slds = scatter_lds_bytes(p.nb);
   if (mode == 0) {
     sd_part_totals_mix<<<p.nblk, PART_THREADS, lds, s>>>(keys, n, p.nb, p.per_block, totals, repl,
-                                                         fill, objects, vals, prefill);
+                                                         fill, objects, nobj, vals, prefill);
     sd_part_scatter_mix<<<p.nblk, PART_THREADS, slds, s>>>(keys, n, p.nb, p.per_block, totals, repl,
                                                            fill, out_keys, out_pos, starts_out);
   } else {
@@ -976,11 +999,16 @@ hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n
   uint32_t* fill = (uint32_t*)q; q += al256(totals_repl(nb1) * nb1 * 4);
   uint32_t* starts1 = (uint32_t*)q; q += al256(nb1 * 4);
   uint32_t* starts = (uint32_t*)q; q += al256((size_t)g.nb() * 4);
+  unsigned long long* shards = (unsigned long long*)q; q += al256(OBJ_SHARDS * OBJ_STRIDE * 8);
   uint64_t* gkeys = (uint64_t*)q; q += al256(2 * n * 8);
   uint32_t* gvals = (uint32_t*)q;
   const uint32_t twords = totals_repl((uint32_t)nb1) * (uint32_t)nb1;  // <= GROUP_TOTALS_WORDS
+  // the fine-bucket tables count into the shards (summed after them); the big tables (<= 256
+  // workgroups) straight into d_objects
+  const bool sharded = !g.big && OBJ_SHARDS > 1;
+  unsigned long long* objects = sharded ? shards : (unsigned long long*)d_objects;
   hipError_t e = run_partition(keys, n, g.l1, 0, k1, p1, totals, true, fill, starts1, nullptr,
-                               (unsigned long long*)d_objects, s, vals, out);
+                               objects, sharded ? OBJ_SHARDS : 1, s, vals, out);
   if (e != hipSuccess) {
     (void)hipMemsetAsync(totals, 0, GROUP_TOTALS_WORDS * 4, s);  // restore the invariant
     return e;
@@ -1007,9 +1035,11 @@ hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n
     // (profiles/r02b_bucket_min_persist_ab.log)
     // (2,048-slot tables in 256-lane workgroups, twice the buckets: 1.28x slower,
     // profiles/r02b_group_small_tables_ab.log)
+  {
     sd_bucket_min<<<g.nb(), MIN_THREADS, 0, s>>>(fk, fp, vals, fstarts, g.nb(), g.b1 + g.b2, n, out,
-                                                 (unsigned long long*)d_objects, gkeys, gvals,
-                                                 totals, twords);
+                                                 objects, gkeys, gvals, totals, twords);
+    if (sharded) sd_objects_sum<<<1, 64, 0, s>>>(shards, OBJ_SHARDS, (unsigned long long*)d_objects);
+  }
   e = hipGetLastError();
   if (e != hipSuccess) (void)hipMemsetAsync(totals, 0, GROUP_TOTALS_WORDS * 4, s);  // restore
   return e;
@@ -1023,7 +1053,7 @@ hipError_t partition_range(const uint64_t* keys, uint64_t n, uint32_t parts, uin
   uint32_t* totals = (uint32_t*)ws;
   uint32_t* fill = (uint32_t*)((char*)ws + al256((size_t)totals_repl(parts) * parts * 4));
   return run_partition(keys, n, p, 1, out_keys, out_pos, totals, false, fill, nullptr, d_counts,
-                       nullptr, s);
+                       nullptr, 0, s);
 }
 
 }  // namespace sdcas
