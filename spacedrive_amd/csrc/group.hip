@@ -378,19 +378,35 @@ sd_sum_u32_block(const uint32_t* __restrict__ v, uint64_t m, unsigned long long*
 }
 
 // chunk-of-`chunk` reference emulation (mod.rs:202-311):
-// rep_c[i] = i if canonical rep is in i's own chunk, else canonical rep.
-extern "C" __global__ void __launch_bounds__(256)
+// rep_c[i] = i if canonical rep is in i's own chunk, else canonical rep.  The created count
+// is summed per workgroup (CHUNKED_ROWS rows) and added with one device atomic: one per wave
+// on one counter serialised (same-address device atomics complete one per ~12.8 ns,
+// tools/ubench_bucketload.hip).
+constexpr int CHUNKED_THREADS = 1024, CHUNKED_ITEMS = 8;
+constexpr uint32_t CHUNKED_ROWS = CHUNKED_THREADS * CHUNKED_ITEMS;
+extern "C" __global__ void __launch_bounds__(CHUNKED_THREADS)
 sd_group_chunked(const uint32_t* __restrict__ rep, uint64_t n, uint32_t chunk,
                  uint32_t* __restrict__ rep_chunked, unsigned long long* __restrict__ created) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool own = false;
-  if (i < n) {
-    const uint32_t r = rep[i];
-    own = (r / chunk) == ((uint32_t)i / chunk);
-    rep_chunked[i] = own ? (uint32_t)i : r;
+  __shared__ unsigned int wsum;
+  if (threadIdx.x == 0) wsum = 0;
+  __syncthreads();
+  uint32_t mine = 0;
+#pragma unroll
+  for (int j = 0; j < CHUNKED_ITEMS; ++j) {
+    const uint64_t i = (uint64_t)blockIdx.x * CHUNKED_ROWS + (uint64_t)j * CHUNKED_THREADS + threadIdx.x;
+    if (i < n) {
+      const uint32_t r = rep[i];
+      const bool own = (r / chunk) == ((uint32_t)i / chunk);
+      rep_chunked[i] = own ? (uint32_t)i : r;
+      mine += own;
+    }
   }
-  const uint64_t b = __ballot(own);
-  if ((threadIdx.x & 63u) == 0 && b) atomicAdd(created, (unsigned long long)__popcll(b));
+  // the wave's sum by ballots of the bits of `mine` (<= CHUNKED_ITEMS < 16)
+  const uint32_t wave = __popcll(__ballot(mine & 1u)) + 2u * __popcll(__ballot(mine & 2u)) +
+                        4u * __popcll(__ballot(mine & 4u)) + 8u * __popcll(__ballot(mine & 8u));
+  if ((threadIdx.x & 63u) == 0 && wave) atomicAdd(&wsum, wave);
+  __syncthreads();
+  if (threadIdx.x == 0 && wsum) atomicAdd(created, (unsigned long long)wsum);
 }
 
 // helpers of group_min_by_sort: widen the values to sort keys, gather keys by position,
@@ -552,7 +568,7 @@ hipError_t group_chunked(const uint32_t* rep, uint64_t n, uint32_t chunk, uint32
                          uint64_t* d_created, hipStream_t s) {
   if (n == 0) return hipSuccess;
   if (chunk == 0) return hipErrorInvalidValue;
-  sd_group_chunked<<<tiles_of(n, 256), 256, 0, s>>>(rep, n, chunk, rep_chunked,
+  sd_group_chunked<<<(uint32_t)((n + CHUNKED_ROWS - 1) / CHUNKED_ROWS), CHUNKED_THREADS, 0, s>>>(rep, n, chunk, rep_chunked,
                                                    (unsigned long long*)d_created);
   return hipGetLastError();
 }

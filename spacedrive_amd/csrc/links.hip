@@ -15,34 +15,68 @@
 
 namespace sdcas {
 
-// Appends with one atomic per wave: lanes that hold an item get consecutive slots.
-__device__ __forceinline__ uint64_t wave_append(bool take, unsigned long long* counter) {
-  const uint64_t mask = __ballot(take);
-  if (!mask) return 0;
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t leader = (uint32_t)__ffsll((unsigned long long)mask) - 1u;
-  unsigned long long base = 0;
-  if (lane == leader) base = atomicAdd(counter, (unsigned long long)__popcll(mask));
-  base = __shfl(base, (int)leader, 64);
-  return base + (uint64_t)__popcll(mask & ((1ull << lane) - 1ull));
-}
-
 // Split the rows by state: hashed rows -> (key, row) pairs for the grouping; every other
 // row -> (row << 8 | state) for the host's cursor walk (they stay orphan after a step).
-extern "C" __global__ void __launch_bounds__(256)
+// Both lists are unordered (the grouping's minimum does not depend on the order; the host
+// sorts the orphans).  A workgroup takes SPLIT_ROWS rows, counts them per wave with ballots,
+// and reserves its runs with ONE device atomic per list: appending per wave (one returning
+// atomic per 64 rows on one counter) took 2 ms of a 10 M-row job — same-address device
+// atomics complete one per ~12.8 ns (tools/ubench_bucketload.hip).
+constexpr int SPLIT_THREADS = 1024, SPLIT_ITEMS = 16;
+constexpr uint32_t SPLIT_ROWS = SPLIT_THREADS * SPLIT_ITEMS;
+constexpr int SPLIT_WAVES = SPLIT_THREADS / 64;
+extern "C" __global__ void __launch_bounds__(SPLIT_THREADS)
 sd_links_split(const uint64_t* __restrict__ keys, const uint8_t* __restrict__ state, uint64_t n,
                uint64_t* __restrict__ hkeys, uint32_t* __restrict__ hrows,
                unsigned long long* __restrict__ hcount, uint64_t* __restrict__ orphans,
                unsigned long long* __restrict__ ocount) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool valid = i < n;
-  const uint8_t st = valid ? state[i] : (uint8_t)SD_LINKS_HASHED;
-  const bool hashed = valid && st == SD_LINKS_HASHED;
-  const bool orphan = valid && st != SD_LINKS_HASHED;
-  const uint64_t h = wave_append(hashed, hcount);
-  const uint64_t o = wave_append(orphan, ocount);
-  if (hashed) { hkeys[h] = keys[i]; hrows[h] = (uint32_t)i; }
-  if (orphan) orphans[o] = (i << 8) | st;
+  __shared__ uint32_t wh[SPLIT_WAVES], wo[SPLIT_WAVES];
+  __shared__ unsigned long long base[2];
+  const uint64_t row0 = (uint64_t)blockIdx.x * SPLIT_ROWS;
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint64_t below = (1ull << lane) - 1ull;
+  uint8_t st[SPLIT_ITEMS];
+  uint32_t th = 0, to = 0;  // the wave's hashed / orphan rows
+#pragma unroll
+  for (int j = 0; j < SPLIT_ITEMS; ++j) {
+    const uint64_t i = row0 + (uint64_t)j * SPLIT_THREADS + threadIdx.x;
+    st[j] = i < n ? state[i] : (uint8_t)SD_LINKS_HASHED;
+  }
+#pragma unroll
+  for (int j = 0; j < SPLIT_ITEMS; ++j) {
+    const bool valid = row0 + (uint64_t)j * SPLIT_THREADS + threadIdx.x < n;
+    th += (uint32_t)__popcll(__ballot(valid && st[j] == SD_LINKS_HASHED));
+    to += (uint32_t)__popcll(__ballot(valid && st[j] != SD_LINKS_HASHED));
+  }
+  if (lane == 0) { wh[w] = th; wo[w] = to; }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // wave prefixes in place, then the block's two runs
+    uint32_t ph = 0, po = 0;
+    for (int k = 0; k < SPLIT_WAVES; ++k) {
+      const uint32_t a = wh[k], b = wo[k];
+      wh[k] = ph; wo[k] = po;
+      ph += a; po += b;
+    }
+    base[0] = ph ? atomicAdd(hcount, (unsigned long long)ph) : 0ull;
+    base[1] = po ? atomicAdd(ocount, (unsigned long long)po) : 0ull;
+  }
+  __syncthreads();
+  uint64_t h = base[0] + wh[w], o = base[1] + wo[w];
+#pragma unroll
+  for (int j = 0; j < SPLIT_ITEMS; ++j) {
+    const uint64_t i = row0 + (uint64_t)j * SPLIT_THREADS + threadIdx.x;
+    const bool valid = i < n;
+    const bool hashed = valid && st[j] == SD_LINKS_HASHED, orphan = valid && st[j] != SD_LINKS_HASHED;
+    const uint64_t hm = __ballot(hashed), om = __ballot(orphan);
+    if (hashed) {
+      const uint64_t d = h + (uint64_t)__popcll(hm & below);
+      hkeys[d] = keys[i];
+      hrows[d] = (uint32_t)i;
+    }
+    if (orphan) orphans[o + (uint64_t)__popcll(om & below)] = (i << 8) | st[j];
+    h += (uint64_t)__popcll(hm);
+    o += (uint64_t)__popcll(om);
+  }
 }
 
 extern "C" __global__ void __launch_bounds__(256)
@@ -124,7 +158,7 @@ hipError_t links_split(const uint64_t* keys, const uint8_t* state, uint64_t n, u
                        uint32_t* hrows, uint64_t* d_hcount, uint64_t* orphans, uint64_t* d_ocount,
                        hipStream_t s) {
   if (n == 0) return hipSuccess;
-  sd_links_split<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(
+  sd_links_split<<<(uint32_t)((n + SPLIT_ROWS - 1) / SPLIT_ROWS), SPLIT_THREADS, 0, s>>>(
       keys, state, n, hkeys, hrows, (unsigned long long*)d_hcount, orphans,
       (unsigned long long*)d_ocount);
   return hipGetLastError();

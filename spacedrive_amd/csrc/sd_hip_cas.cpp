@@ -583,10 +583,14 @@ int sd_cas_identifier_links_dev(sd_cas_ctx* c, const uint64_t* d_keys, const uin
   // 2. the cursor walk (host; O(steps + orphans)): step k covers [start, start + chunk);
   //    the next cursor is its last row, which the next query returns again iff it is
   //    still orphan; an empty query ends the job
+  // the rows asked about only increase (each step's last row), so one forward pointer into
+  // the sorted orphan list answers them all: O(steps + orphans) (a binary search per step
+  // cost ~2 ms of a 10 M-row job)
+  size_t sp = 0;
   auto stays = [&](uint64_t row, uint8_t* st) {
-    auto it = std::lower_bound(stay.begin(), stay.end(), row << 8);
-    if (it == stay.end() || (*it >> 8) != row) return false;
-    *st = (uint8_t)(*it & 0xFF);
+    while (sp < stay.size() && (stay[sp] >> 8) < row) ++sp;
+    if (sp == stay.size() || (stay[sp] >> 8) != row) return false;
+    *st = (uint8_t)(stay[sp] & 0xFF);
     return true;
   };
   std::vector<uint32_t> h_starts;
