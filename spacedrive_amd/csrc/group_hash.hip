@@ -130,7 +130,7 @@ __device__ __forceinline__ uint32_t bucket_of(uint64_t stored, uint32_t nb) {
 // block b reserves inside sub-run b % repl with its own cursor fill[b % repl][c]: 1/repl
 // of the blocks contend on each cursor (all of them did: every block's reservation waited
 // behind ~nblk same-address returning atomics).
-template <int MODE>
+template <int MODE, bool HAS_VALS>
 __device__ void part_totals_body(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb,
                                  uint64_t per_block, uint32_t* __restrict__ totals, uint32_t repl,
                                  uint32_t* __restrict__ fill, unsigned long long* __restrict__ objects,
@@ -147,11 +147,14 @@ __device__ void part_totals_body(const uint64_t* __restrict__ keys, uint64_t n, 
   const uint64_t hi = lo + per_block < n ? lo + per_block : n;
   // the next trip's keys are loaded before this trip's counting atomics
   uint64_t kn[ITEMS];
+  // every lane loads and stores (rows past the slice use its last row: the prefill then
+  // rewrites that row's own value) — loads and stores under a branch leave the compiler
+  // unable to count what is in flight, and it waits for all of it (the prefetch included)
   auto load = [&](uint64_t base) {
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
       const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
-      kn[j] = i < hi ? keys[i] : 0;
+      kn[j] = keys[i < hi ? i : hi - 1];
     }
   };
   if (lo < hi) load(lo);
@@ -159,12 +162,13 @@ __device__ void part_totals_body(const uint64_t* __restrict__ keys, uint64_t n, 
     uint64_t k[ITEMS];
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) k[j] = kn[j];
-    if (base + PART_TILE < hi) load(base + PART_TILE);
-    if (prefill) {
+    load(base + PART_TILE < hi ? base + PART_TILE : base);  // (a last trip re-reads itself)
+    if (MODE == 0) {  // the grouping always prefills; HAS_VALS picks the value source
 #pragma unroll
       for (int j = 0; j < ITEMS; ++j) {
         const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
-        if (i < hi) prefill[i] = vals ? vals[i] : (uint32_t)i;
+        const uint64_t c = i < hi ? i : hi - 1;
+        prefill[c] = HAS_VALS ? vals[c] : (uint32_t)c;
       }
     }
 #pragma unroll
@@ -223,14 +227,17 @@ __device__ void lds_exclusive_scan(const uint32_t* cnt, uint32_t* out, uint32_t 
 // otherwise gcur[b] is this workgroup's running cursor (the refine level: one workgroup
 // owns the segment).  tcnt must be zero on entry and is left zero.
 constexpr uint32_t STAGED_MAX_NB = 1024;
-template <bool RESERVE, typename BucketFn>
+// `prefetch` issues the next trip's loads: after this trip's reservation atomics (whose
+// results are consumed after it, so the compiler's in-order wait for them does not also wait
+// out the prefetch) and before its LDS scan, staging and stores.
+template <bool RESERVE, bool STORE_ALL, typename BucketFn, typename Prefetch>
 __device__ __forceinline__ void staged_trip(const uint64_t (&k)[ITEMS], const uint32_t (&pos)[ITEMS],
                                             uint32_t trip_n, uint32_t nb, BucketFn bfn,
                                             uint32_t* gcur, uint32_t* tcnt, uint32_t* tstart,
                                             uint64_t* skey, uint32_t* spos,
                                             const uint32_t* bstart, uint32_t* __restrict__ fill,
                                             uint64_t* __restrict__ out_keys,
-                                            uint32_t* __restrict__ out_pos) {
+                                            uint32_t* __restrict__ out_pos, Prefetch prefetch) {
   uint32_t bk[ITEMS], r[ITEMS];
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
@@ -239,12 +246,23 @@ __device__ __forceinline__ void staged_trip(const uint64_t (&k)[ITEMS], const ui
     r[j] = t < trip_n ? atomicAdd(&tcnt[bk[j]], 1u) : 0u;
   }
   __syncthreads();
+  constexpr int RPT = (STAGED_MAX_NB + PART_THREADS - 1) / PART_THREADS;
+  uint32_t resv[RPT];
   if (RESERVE) {
-    for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS)
-      if (tcnt[b]) gcur[b] = bstart[b] + atomicAdd(&fill[b], tcnt[b]);
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      const uint32_t b = threadIdx.x + (uint32_t)q * PART_THREADS;
+      resv[q] = b < nb && tcnt[b] ? atomicAdd(&fill[b], tcnt[b]) : 0u;
+    }
   }
-  // (consuming each reservation only after the LDS scan and staging below, so its round trip
-  // overlapped them, changed nothing: profiles/r03b_group_ab/abg5)
+  prefetch();
+  if (RESERVE) {
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      const uint32_t b = threadIdx.x + (uint32_t)q * PART_THREADS;
+      if (b < nb && tcnt[b]) gcur[b] = bstart[b] + resv[q];
+    }
+  }
   lds_exclusive_scan(tcnt, tstart, nb);  // (its barriers also publish gcur)
   // conservation: the trip's per-bucket counts add up to the trip
   SD_DBG_CHECK(threadIdx.x != 0 || tstart[nb - 1] + tcnt[nb - 1] == trip_n,
@@ -260,10 +278,16 @@ __device__ __forceinline__ void staged_trip(const uint64_t (&k)[ITEMS], const ui
     }
   }
   __syncthreads();
+  // STORE_ALL: every lane stores, one past the trip rewriting the trip's last row (same slot,
+  // same data), so the compiler can count the stores and keeps the next trip's loads in
+  // flight past them.  It pays in the 2^10-bucket coarse scatter (100 M keys: 756 -> 557 us)
+  // and costs in the 2^8-bucket one (12.5 M: 62 -> 75 us); the refine is the same either way
+  // (profiles/r03b_group_ab/abg17_21)
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
-    const uint32_t t = (uint32_t)j * PART_THREADS + threadIdx.x;
-    if (t < trip_n) {
+    const uint32_t t0 = (uint32_t)j * PART_THREADS + threadIdx.x;
+    if (STORE_ALL || t0 < trip_n) {
+      const uint32_t t = t0 < trip_n ? t0 : trip_n - 1;
       const uint64_t kk = skey[t];
       const uint32_t b = bfn(kk);
       const uint32_t dest = gcur[b] + (t - tstart[b]);
@@ -288,7 +312,7 @@ __host__ __device__ constexpr size_t scatter_lds_bytes(uint32_t nb) {
 // Bucket-contiguous scatter.  Every block derives the bucket starts from the totals (an
 // LDS scan); block 0 publishes them (starts_out, the coarse level's segments) and, for the
 // range partition, the part sizes (counts_out, u64).
-template <int MODE>
+template <int MODE, bool STORE_ALL>
 __device__ void part_scatter_body(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb,
                                   uint64_t per_block, const uint32_t* __restrict__ totals,
                                   uint32_t repl, uint32_t* __restrict__ fill,
@@ -306,21 +330,30 @@ __device__ void part_scatter_body(const uint64_t* __restrict__ keys, uint64_t n,
   // the first trip's keys are loaded before the totals, so both latencies overlap
   uint64_t k[ITEMS];
   uint32_t q[ITEMS];
+  // raw keys, every lane loading (rows past the slice re-read its last row; staged_trip
+  // ignores them): a load under a branch, or the mix applied where it is loaded, made the
+  // compiler wait for each load in turn — the next trip's loads did not overlap this one
   auto load_trip = [&](uint64_t base) {
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
       const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
-      k[j] = i < hi ? stored_key<MODE>(keys[i]) : 0;
+      k[j] = keys[i < hi ? i : hi - 1];
       q[j] = (uint32_t)i;
     }
   };
   if (staged) load_trip(lo);
+  // the replicas' counts of a bucket: all TOTALS_REPL loads issued before any is summed (a
+  // loop over the runtime `repl` waited out each load in turn: the prologue took 8.4 us of a
+  // block's ~33, profiles/r03b_group_ab/ts_scatter.log)
   for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS) {
+    uint32_t t[TOTALS_REPL];
+#pragma unroll
+    for (uint32_t r = 0; r < TOTALS_REPL; ++r) t[r] = r < repl ? totals[(uint64_t)r * nb + b] : 0u;
     uint32_t x = 0, pre = 0;
-    for (uint32_t r = 0; r < repl; ++r) {
-      const uint32_t t = totals[(uint64_t)r * nb + b];
-      pre += r < mine ? t : 0u;
-      x += t;
+#pragma unroll
+    for (uint32_t r = 0; r < TOTALS_REPL; ++r) {
+      pre += r < mine ? t[r] : 0u;
+      x += t[r];
     }
     if (staged) { tcnt[b] = x; rbase[b] = pre; }
     if (blockIdx.x == 0 && counts_out) counts_out[b] = x;
@@ -349,11 +382,12 @@ __device__ void part_scatter_body(const uint64_t* __restrict__ keys, uint64_t n,
       uint64_t kc[ITEMS];
       uint32_t qc[ITEMS];
 #pragma unroll
-      for (int j = 0; j < ITEMS; ++j) { kc[j] = k[j]; qc[j] = q[j]; }
-      if (base + PART_TILE < hi) load_trip(base + PART_TILE);  // in flight during this trip
+      for (int j = 0; j < ITEMS; ++j) { kc[j] = stored_key<MODE>(k[j]); qc[j] = q[j]; }
       const uint64_t left = hi - base;
-      staged_trip<true>(kc, qc, left < PART_TILE ? (uint32_t)left : PART_TILE, nb, bfn, gcur, tcnt,
-                        tstart, skey, spos, rbase, myfill, out_keys, out_pos);
+      const uint64_t nbase = base + PART_TILE < hi ? base + PART_TILE : base;  // (a last trip re-reads itself)
+      staged_trip<true, STORE_ALL>(kc, qc, left < PART_TILE ? (uint32_t)left : PART_TILE, nb, bfn, gcur, tcnt,
+                        tstart, skey, spos, rbase, myfill, out_keys, out_pos,
+                        [&]() { load_trip(nbase); });  // in flight during this trip
     }
     return;
   }
@@ -382,28 +416,44 @@ sd_part_totals_mix(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb, u
                    uint32_t* __restrict__ totals, uint32_t repl, uint32_t* __restrict__ fill,
                    unsigned long long* __restrict__ objects, uint32_t nobj,
                    const uint32_t* __restrict__ vals, uint32_t* __restrict__ prefill) {
-  part_totals_body<0>(keys, n, nb, per_block, totals, repl, fill, objects, nobj, vals, prefill);
+  part_totals_body<0, false>(keys, n, nb, per_block, totals, repl, fill, objects, nobj, vals, prefill);
+}
+extern "C" __global__ void __launch_bounds__(PART_THREADS)
+sd_part_totals_mix_vals(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb, uint64_t per_block,
+                        uint32_t* __restrict__ totals, uint32_t repl, uint32_t* __restrict__ fill,
+                        unsigned long long* __restrict__ objects, uint32_t nobj,
+                        const uint32_t* __restrict__ vals, uint32_t* __restrict__ prefill) {
+  part_totals_body<0, true>(keys, n, nb, per_block, totals, repl, fill, objects, nobj, vals, prefill);
 }
 extern "C" __global__ void __launch_bounds__(PART_THREADS)
 sd_part_totals_range(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb, uint64_t per_block,
                      uint32_t* __restrict__ totals, uint32_t repl, uint32_t* __restrict__ fill) {
-  part_totals_body<1>(keys, n, nb, per_block, totals, repl, fill, nullptr, 0, nullptr, nullptr);
+  part_totals_body<1, false>(keys, n, nb, per_block, totals, repl, fill, nullptr, 0, nullptr, nullptr);
 }
 extern "C" __global__ void __launch_bounds__(PART_THREADS)
 sd_part_scatter_mix(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb, uint64_t per_block,
                     const uint32_t* __restrict__ totals, uint32_t repl, uint32_t* __restrict__ fill,
                     uint64_t* __restrict__ out_keys, uint32_t* __restrict__ out_pos,
                     uint32_t* __restrict__ starts_out) {
-  part_scatter_body<0>(keys, n, nb, per_block, totals, repl, fill, out_keys, out_pos, starts_out,
-                       nullptr);
+  part_scatter_body<0, false>(keys, n, nb, per_block, totals, repl, fill, out_keys, out_pos, starts_out,
+                              nullptr);
+}
+// the same for 2^10 coarse buckets (above COARSE10_KEYS): every lane stores (STORE_ALL)
+extern "C" __global__ void __launch_bounds__(PART_THREADS)
+sd_part_scatter_mix_wide(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb, uint64_t per_block,
+                         const uint32_t* __restrict__ totals, uint32_t repl, uint32_t* __restrict__ fill,
+                         uint64_t* __restrict__ out_keys, uint32_t* __restrict__ out_pos,
+                         uint32_t* __restrict__ starts_out) {
+  part_scatter_body<0, true>(keys, n, nb, per_block, totals, repl, fill, out_keys, out_pos, starts_out,
+                             nullptr);
 }
 extern "C" __global__ void __launch_bounds__(PART_THREADS)
 sd_part_scatter_range(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb, uint64_t per_block,
                       const uint32_t* __restrict__ totals, uint32_t repl, uint32_t* __restrict__ fill,
                       uint64_t* __restrict__ out_keys, uint32_t* __restrict__ out_pos,
                       uint64_t* __restrict__ counts_out) {
-  part_scatter_body<1>(keys, n, nb, per_block, totals, repl, fill, out_keys, out_pos, nullptr,
-                       counts_out);
+  part_scatter_body<1, false>(keys, n, nb, per_block, totals, repl, fill, out_keys, out_pos, nullptr,
+                              counts_out);
 }
 
 // Second partition level: one workgroup per coarse bucket (top b1 bits of the stored key)
@@ -430,12 +480,13 @@ sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict_
   // so the ~12 trips of a 12.5M-key refine do not each wait out an HBM round trip
   uint64_t kn[ITEMS];
   uint32_t qn[ITEMS];
-  auto load = [&](uint64_t base, bool with_pos) {
+  auto load = [&](uint64_t base, bool with_pos) {  // every lane loads (clamped, as in the totals)
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
       const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
-      kn[j] = i < e ? in_keys[i] : 0;
-      if (with_pos) qn[j] = i < e ? in_pos[i] : 0;
+      const uint64_t c = i < e ? i : e - 1;
+      kn[j] = in_keys[c];
+      if (with_pos) qn[j] = in_pos[c];
     }
   };
   if (s < e) load(s, false);
@@ -443,7 +494,7 @@ sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict_
     uint64_t k[ITEMS];
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) k[j] = kn[j];
-    if (base + PART_TILE < e) load(base + PART_TILE, false);
+    load(base + PART_TILE < e ? base + PART_TILE : base, false);  // (a last trip re-reads itself)
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
       const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
@@ -477,10 +528,10 @@ sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict_
     uint32_t q[ITEMS];
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) { k[j] = kn[j]; q[j] = qn[j]; }
-    if (base + PART_TILE < e) load(base + PART_TILE, true);
+    load(base + PART_TILE < e ? base + PART_TILE : base, true);
     const uint64_t left = e - base;
-    staged_trip<false>(k, q, left < PART_TILE ? (uint32_t)left : PART_TILE, nb2, bfn, gcur, tcnt,
-                       tstart, skey, spos, nullptr, nullptr, out_keys, out_pos);
+    staged_trip<false, false>(k, q, left < PART_TILE ? (uint32_t)left : PART_TILE, nb2, bfn, gcur, tcnt,
+                       tstart, skey, spos, nullptr, nullptr, out_keys, out_pos, []() {});
   }
   // conservation: every fine bucket's cursor advanced by exactly its count (rows written ==
   // rows counted); staged_trip's last barrier published gcur
@@ -964,10 +1015,18 @@ static hipError_t run_partition(const uint64_t* keys, uint64_t n, const PartPlan
     sd_zero_words<<<(words + 255) / 256 < 64 ? (words + 255) / 256 : 64, 256, 0, s>>>(totals, words);
   const size_t lds = (size_t)p.nb * 4, slds = scatter_lds_bytes(p.nb);
   if (mode == 0) {
-    sd_part_totals_mix<<<p.nblk, PART_THREADS, lds, s>>>(keys, n, p.nb, p.per_block, totals, repl,
-                                                         fill, objects, nobj, vals, prefill);
-    sd_part_scatter_mix<<<p.nblk, PART_THREADS, slds, s>>>(keys, n, p.nb, p.per_block, totals, repl,
-                                                           fill, out_keys, out_pos, starts_out);
+    if (vals)
+      sd_part_totals_mix_vals<<<p.nblk, PART_THREADS, lds, s>>>(keys, n, p.nb, p.per_block, totals, repl,
+                                                                fill, objects, nobj, vals, prefill);
+    else
+      sd_part_totals_mix<<<p.nblk, PART_THREADS, lds, s>>>(keys, n, p.nb, p.per_block, totals, repl,
+                                                           fill, objects, nobj, vals, prefill);
+    if (p.nb >= 1024)
+      sd_part_scatter_mix_wide<<<p.nblk, PART_THREADS, slds, s>>>(keys, n, p.nb, p.per_block, totals, repl,
+                                                                  fill, out_keys, out_pos, starts_out);
+    else
+      sd_part_scatter_mix<<<p.nblk, PART_THREADS, slds, s>>>(keys, n, p.nb, p.per_block, totals, repl,
+                                                             fill, out_keys, out_pos, starts_out);
   } else {
     sd_part_totals_range<<<p.nblk, PART_THREADS, lds, s>>>(keys, n, p.nb, p.per_block, totals, repl,
                                                            fill);

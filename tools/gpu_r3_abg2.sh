@@ -23,7 +23,7 @@ cd /tmp && export TMPDIR=/tmp
 for lib in current $R/tools/ablib/g_*.so; do
   name=$(basename $lib .so)
   if [ $lib = current ]; then unset SD_HIP_CAS_LIB; else export SD_HIP_CAS_LIB=$lib; fi
-  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/prof_$name -o run --output-format csv -- python3 $R/tools/ab_group.py 12500000 > $OUT/prof_$name.log 2>&1 || { echo "PROF_FAIL $name"; exit 1; }
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/prof_$name -o run --output-format csv -- python3 $R/tools/ab_group.py ${PROFN:-12500000} > $OUT/prof_$name.log 2>&1 || { echo "PROF_FAIL $name"; exit 1; }
   f=$(find $OUT/prof_$name -name 'run_kernel_stats.csv' | head -1)
   echo "== $name"; grep '"sd_' $f | cut -d, -f1-4
 done
