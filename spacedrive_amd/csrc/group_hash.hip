@@ -162,7 +162,7 @@ __device__ void part_totals_body(const uint64_t* __restrict__ keys, uint64_t n, 
     uint64_t k[ITEMS];
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) k[j] = kn[j];
-    load(base + PART_TILE < hi ? base + PART_TILE : base);  // (a last trip re-reads itself)
+    load(base + PART_TILE < hi ? base + PART_TILE : hi);  // (past the end: one line, row hi - 1)
     if (MODE == 0) {  // the grouping always prefills; HAS_VALS picks the value source
 #pragma unroll
       for (int j = 0; j < ITEMS; ++j) {
@@ -384,7 +384,7 @@ __device__ void part_scatter_body(const uint64_t* __restrict__ keys, uint64_t n,
 #pragma unroll
       for (int j = 0; j < ITEMS; ++j) { kc[j] = stored_key<MODE>(k[j]); qc[j] = q[j]; }
       const uint64_t left = hi - base;
-      const uint64_t nbase = base + PART_TILE < hi ? base + PART_TILE : base;  // (a last trip re-reads itself)
+      const uint64_t nbase = base + PART_TILE < hi ? base + PART_TILE : hi;  // (past the end: one line)
       staged_trip<true, STORE_ALL>(kc, qc, left < PART_TILE ? (uint32_t)left : PART_TILE, nb, bfn, gcur, tcnt,
                         tstart, skey, spos, rbase, myfill, out_keys, out_pos,
                         [&]() { load_trip(nbase); });  // in flight during this trip
@@ -494,7 +494,7 @@ sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict_
     uint64_t k[ITEMS];
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) k[j] = kn[j];
-    load(base + PART_TILE < e ? base + PART_TILE : base, false);  // (a last trip re-reads itself)
+    load(base + PART_TILE < e ? base + PART_TILE : e, false);  // (past the end: one line, row e - 1)
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
       const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
@@ -528,7 +528,7 @@ sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict_
     uint32_t q[ITEMS];
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) { k[j] = kn[j]; q[j] = qn[j]; }
-    load(base + PART_TILE < e ? base + PART_TILE : base, true);
+    load(base + PART_TILE < e ? base + PART_TILE : e, true);
     const uint64_t left = e - base;
     staged_trip<false, false>(k, q, left < PART_TILE ? (uint32_t)left : PART_TILE, nb2, bfn, gcur, tcnt,
                        tstart, skey, spos, nullptr, nullptr, out_keys, out_pos, []() {});
