@@ -6,11 +6,11 @@ def rep(a, b):
     global s
     assert s.count(a) == 1, a
     s = s.replace(a, b)
-rep("""template <int MODE>
+rep("""template <int MODE, bool STORE_ALL>
 __device__ void part_scatter_body(""", """__device__ unsigned long long sd_scatter_ts[4096 * 8];
 #define STS(i) do { if (MODE == 0 && threadIdx.x == 0 && (i) < 8) { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \\
   sd_scatter_ts[(uint64_t)blockIdx.x * 8 + (i)] = wall_clock64(); } } while (0)
-template <int MODE>
+template <int MODE, bool STORE_ALL>
 __device__ void part_scatter_body(""")
 rep("""  const bool staged = nb <= STAGED_MAX_NB;
   const uint32_t mine = blockIdx.x % repl;""", """  const bool staged = nb <= STAGED_MAX_NB;
@@ -23,11 +23,9 @@ rep("""    for (uint32_t b = threadIdx.x; b < nb; b += PART_THREADS) tcnt[b] = 0
     STS(1);
     uint32_t tno = 0;
     auto bfn = [nb](uint64_t x) { return bucket_of(x, nb); };""")
-rep("""      staged_trip<true>(kc, qc, left < PART_TILE ? (uint32_t)left : PART_TILE, nb, bfn, gcur, tcnt,
-                        tstart, skey, spos, rbase, myfill, out_keys, out_pos);
+rep("""                        [&]() { load_trip(nbase); });  // in flight during this trip
     }
-    return;""", """      staged_trip<true>(kc, qc, left < PART_TILE ? (uint32_t)left : PART_TILE, nb, bfn, gcur, tcnt,
-                        tstart, skey, spos, rbase, myfill, out_keys, out_pos);
+    return;""", """                        [&]() { load_trip(nbase); });  // in flight during this trip
       ++tno;
       STS(1 + tno);
     }
