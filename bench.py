@@ -57,13 +57,15 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 # read 12 / write 12 = 76 B/key (the minima of duplicates are the only other stores)
 def group_bytes_per_key(n: int) -> int:
     return 44 if n <= 256 * 5632 else 76
+FUSED_REGION_BITS = 8  # sd_mix.h REGION_BITS
 FUSED_MAX_FILES = 256 * 5632  # the fused chain's single-level regions (sd_cas_hash_group_sampled_dev)
 
 
 def eng_region_capacity(n: int) -> int:
     """Rows per coarse-bucket region of the fused chain (group_hash.hip region_capacity)."""
-    mean = n / 256
-    var = mean * (1 - 1 / 256)
+    regions = 1 << FUSED_REGION_BITS
+    mean = n / regions
+    var = mean * (1 - 1 / regions)
     sd = 1
     while sd * sd < var:
         sd += 1

@@ -93,7 +93,7 @@ struct sd_cas_ctx {
   // The fused hash + group chain (sd_cas_hash_regions_sampled_dev / sd_cas_group_regions_dev):
   // two region sets used alternately, so set k's bucket tables can run on a side stream while
   // the next batch's K1G fills set k^1; region_done[k] orders set k's reuse after its tables.
-  // gcursor holds both sets' cursors (2 x 256 u32), zero between calls (the tables re-zero).
+  // gcursor holds both sets' cursors (2 x REGIONS u32, <= 1,024), zero between calls (the tables re-zero).
   uint32_t* gcursor = nullptr;
   DevBuf regions[2];
   uint64_t region_n[2] = {0, 0};

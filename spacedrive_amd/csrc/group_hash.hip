@@ -843,16 +843,21 @@ sd_bucket_min_big(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict
                                            starts, nb, bits, n, out, objects, gkeys, gvals);
 }
 
-// The fused chain's bucket tables: one 1,024-thread workgroup per region (the coarse
-// buckets K1G wrote), straight from the regions — no totals, scatter or refine launch.
-extern "C" __global__ void __launch_bounds__(BIG_THREADS)
+// The fused chain's bucket tables: one workgroup per region (the coarse buckets K1G wrote),
+// straight from the regions — no totals, scatter or refine launch.  2^9 regions: 512 lanes x 7
+// keys over a 6,144-slot table (72 KiB, two workgroups per CU; a region of <= 3,584 keys, every
+// batch up to BIG_MAX_KEYS, is one trip).  2^8 regions: the 1,024-lane big table.
+constexpr uint32_t REG_TABLE = REGION_BITS >= 9 ? 6144 : BIG_TABLE;
+constexpr int REG_THREADS = REGION_BITS >= 9 ? 512 : BIG_THREADS;
+constexpr int REG_ITEMS = REGION_BITS >= 9 ? 7 : ITEMS;
+extern "C" __global__ void __launch_bounds__(REG_THREADS)
 sd_bucket_min_regions(const uint64_t* __restrict__ rkeys, const uint32_t* __restrict__ rfile,
                       uint32_t* __restrict__ cursor, uint64_t cap, uint32_t* __restrict__ out,
                       unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
                       uint32_t* __restrict__ gvals) {
-  bucket_min<BIG_TABLE, BIG_THREADS, ITEMS, true>(blockIdx.x, nullptr, 0, rkeys, rfile, nullptr, nullptr,
-                                           REGIONS, REGION_BITS, 0, out, objects, gkeys, gvals,
-                                           cursor, cap);
+  bucket_min<REG_TABLE, REG_THREADS, REG_ITEMS, true>(blockIdx.x, nullptr, 0, rkeys, rfile, nullptr,
+                                                      nullptr, REGIONS, REGION_BITS, 0, out, objects,
+                                                      gkeys, gvals, cursor, cap);
 }
 
 }  // namespace sdcas
@@ -893,7 +898,7 @@ void region_group_layout(void* ws, uint64_t n, uint64_t** rkeys, uint32_t** rfil
 hipError_t region_group_min(const uint64_t* rkeys, const uint32_t* rfile, uint32_t* cursor,
                             uint64_t cap, uint32_t* out, uint64_t* d_objects, uint64_t* gkeys,
                             uint32_t* gvals, hipStream_t s) {
-  sd_bucket_min_regions<<<REGIONS, BIG_THREADS, 0, s>>>(rkeys, rfile, cursor, cap, out,
+  sd_bucket_min_regions<<<REGIONS, REG_THREADS, 0, s>>>(rkeys, rfile, cursor, cap, out,
                                                         (unsigned long long*)d_objects, gkeys, gvals);
   return hipGetLastError();
 }

@@ -28,6 +28,7 @@
 #include "sd_group.h"
 #include "sd_kernels.h"
 #include "sd_links.h"
+#include "sd_mix.h"
 #include "sd_synth.h"
 
 using namespace sdcas;
@@ -93,8 +94,8 @@ int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
       hipMalloc((void**)&c->d_scalar, 64) != hipSuccess ||
       hipMalloc((void**)&c->gtotals, GROUP_TOTALS_WORDS * 4) != hipSuccess ||
       hipMemset(c->gtotals, 0, GROUP_TOTALS_WORDS * 4) != hipSuccess ||
-      hipMalloc((void**)&c->gcursor, 4096) != hipSuccess ||
-      hipMemset(c->gcursor, 0, 4096) != hipSuccess ||
+      hipMalloc((void**)&c->gcursor, 2 * REGIONS * 4) != hipSuccess ||
+      hipMemset(c->gcursor, 0, 2 * REGIONS * 4) != hipSuccess ||
       hipEventCreateWithFlags(&c->region_done[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->region_done[1], hipEventDisableTiming) != hipSuccess) {
     sd_cas_ctx_destroy(c);
@@ -357,7 +358,7 @@ int sd_cas_hash_regions_sampled_dev(sd_cas_ctx* c, const void* d_content, uint64
   // set k was last grouped two batches ago: its tables must be done before it is refilled
   if (c->region_pending[k]) HIP_TRY(c, hipStreamWaitEvent(s, c->region_done[k], 0));
   // a batch hashed into set k but never grouped left its cursors counted: clear them
-  if (!c->region_grouped[k]) HIP_TRY(c, hipMemsetAsync(c->gcursor + 256 * k, 0, 1024, s));
+  if (!c->region_grouped[k]) HIP_TRY(c, hipMemsetAsync(c->gcursor + REGIONS * k, 0, REGIONS * 4, s));
   c->region_n[k] = n;  // sizes the layout (ensure below grows the set if needed)
   int rc = ensure(c, c->regions[k], region_group_workspace_bytes(n) + 256);
   if (rc) return rc;
@@ -365,10 +366,10 @@ int sd_cas_hash_regions_sampled_dev(sd_cas_ctx* c, const void* d_content, uint64
   uint32_t *rfile, *gvals;
   region_group_layout(c->regions[k].p, n, &rkeys, &rfile, &gkeys, &gvals);
   hipError_t e = hash_sampled_regions((const uint8_t*)d_content, stride, d_sizes, n, d_keys, d_rep,
-                                      rkeys, rfile, c->gcursor + 256 * k, region_capacity(n), d_overflow,
+                                      rkeys, rfile, c->gcursor + REGIONS * k, region_capacity(n), d_overflow,
                                       region_objects(c, k), s, (uint32_t)(c->quantum / 256));
   if (e != hipSuccess) {
-    (void)hipMemsetAsync(c->gcursor + 256 * k, 0, 1024, s);  // restore the cursors' invariant
+    (void)hipMemsetAsync(c->gcursor + REGIONS * k, 0, REGIONS * 4, s);  // restore the cursors' invariant
     return fail(c, SD_CAS_EHIP, "hash_regions: %s", hipGetErrorString(e));
   }
   c->region_cur = k;
@@ -388,10 +389,10 @@ int sd_cas_group_regions_dev(sd_cas_ctx* c, size_t n, uint32_t* d_rep, uint64_t*
   uint32_t *rfile, *gvals;
   region_group_layout(c->regions[k].p, n, &rkeys, &rfile, &gkeys, &gvals);
   uint64_t* obj = region_objects(c, k);
-  hipError_t e = region_group_min(rkeys, rfile, c->gcursor + 256 * k, region_capacity(n), d_rep, obj,
+  hipError_t e = region_group_min(rkeys, rfile, c->gcursor + REGIONS * k, region_capacity(n), d_rep, obj,
                                   gkeys, gvals, s);
   if (e != hipSuccess) {
-    (void)hipMemsetAsync(c->gcursor + 256 * k, 0, 1024, s);
+    (void)hipMemsetAsync(c->gcursor + REGIONS * k, 0, REGIONS * 4, s);
     return fail(c, SD_CAS_EHIP, "group_regions: %s", hipGetErrorString(e));
   }
   HIP_TRY(c, hipEventRecord(c->region_done[k], s));

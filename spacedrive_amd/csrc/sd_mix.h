@@ -16,7 +16,13 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 
 // The fused chain's coarse buckets: the top REGION_BITS bits of the mixed key, each with a
 // fixed-capacity region of rows (mixed key u64, file u32) written by the hash kernel.
-constexpr uint32_t REGION_BITS = 8;
+// 2^8 regions: one 1,024-lane table workgroup per CU over ~5,100 keys.  SD_REGION_BITS=9 (two
+// 512-lane workgroups per CU over ~2,560 keys each) measured slower: 0.0224 vs 0.0213 ms at
+// 1.31M keys, K1G unchanged (profiles/r03b_group_ab/README.md)
+#ifndef SD_REGION_BITS
+#define SD_REGION_BITS 8
+#endif
+constexpr uint32_t REGION_BITS = SD_REGION_BITS;
 constexpr uint32_t REGIONS = 1u << REGION_BITS;
 
 }  // namespace sdcas
