@@ -37,6 +37,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "sd_debug.h"
 #include "sd_group.h"
 #include "sd_mix.h"
@@ -646,7 +648,10 @@ __device__ __forceinline__ uint64_t g_find(const uint64_t* tk, uint64_t cap, uin
 // profiles/r03b_group_ab/).
 // Regions (the fused hash + group chain): counts != nullptr — bucket b's keys are rows
 // [b * region_cap, b * region_cap + min(counts[b], region_cap)) and the workgroup re-zeroes
-// counts[b] after reading it (the region cursors' persistent-zero invariant).
+// counts[b] after reading it (the region cursors' persistent-zero invariant).  With `rescan`
+// (the standalone small-batch chain) a region whose count passed its capacity is regrouped
+// exactly from the whole input rescan[0, rescan_n) (keys of this bucket only) in a global
+// table of 2 x count slots carved from *spill.
 template <uint32_t TBL, int THREADS, int NI, bool KEEP_SLOT>
 __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict__ rezero,
                                            uint32_t rezero_words,
@@ -659,7 +664,11 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
                                            uint64_t* __restrict__ gkeys,
                                            uint32_t* __restrict__ gvals,
                                            uint32_t* __restrict__ counts = nullptr,
-                                           uint64_t region_cap = 0) {
+                                           uint64_t region_cap = 0,
+                                           const uint64_t* __restrict__ rescan = nullptr,
+                                           uint64_t rescan_n = 0,
+                                           unsigned long long* __restrict__ spill = nullptr,
+                                           uint32_t count_stride = 1) {
   constexpr uint32_t TILE = THREADS * NI;
   constexpr uint32_t FILL = TBL / 8 * 7;  // above this the bucket goes to global memory
   static_assert(TILE < TBL, "one-trip buckets must leave an empty slot (lds_claim's unbounded probe)");
@@ -671,6 +680,7 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
   // still reading it for trip t+1, splitting the waves over different barriers
   __shared__ int ovf[2];
   __shared__ uint32_t region_n;
+  __shared__ unsigned long long spill_off;
   const uint32_t b = bucket;
   // the chain's bucket totals were last read by the scatter: zero them for the next call
   // (the persistent buffer's invariant, see hash_group_min)
@@ -679,12 +689,13 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
   uint64_t s, e;
   if (counts) {
     if (threadIdx.x == 0) {
-      region_n = counts[b];
-      counts[b] = 0;
+      region_n = counts[b * count_stride];
+      counts[b * count_stride] = 0;
     }
     __syncthreads();
     s = (uint64_t)b * region_cap;
     e = s + (region_n < region_cap ? region_n : region_cap);
+    if (rescan && region_n > region_cap) e = s;  // (uniform) straight to the whole-input regroup
   } else {
     s = starts[b];
     e = b + 1 < nb ? starts[b + 1] : n;
@@ -694,7 +705,8 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
   const uint64_t empty = (uint64_t)(b ^ 1u) << (64 - bits);
   for (uint32_t i = threadIdx.x; i < TBL; i += THREADS) { tk[i] = empty; tv[i] = 0xFFFFFFFFu; }
   if (threadIdx.x == 0) { distinct = 0; ovf[0] = 0; ovf[1] = 0; }
-  if (s == e) return;  // uniform for the whole workgroup
+  const bool whole = counts && rescan && region_n > region_cap;
+  if (s == e && !whole) return;  // uniform for the whole workgroup
 #if SD_DBG
   __shared__ unsigned int dbg_seen;  // keys inserted: must be the bucket's e - s
   if (threadIdx.x == 0) dbg_seen = 0;
@@ -755,7 +767,7 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
 #endif
   }
   __syncthreads();
-  const bool overflow = ovf[0] | ovf[1];
+  const bool overflow = whole || (ovf[0] | ovf[1]);
   SD_DBG_CHECK(threadIdx.x != 0 || overflow || (dbg_seen == e - s && distinct <= e - s),
                "bucket %u: inserted %u of %llu keys, %u distinct", b, dbg_seen,
                (unsigned long long)(e - s), distinct);
@@ -787,26 +799,32 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
     if (threadIdx.x == 0) atomicAdd(objects, (unsigned long long)distinct);
     return;
   }
-  // Overflow: redo the bucket in its own 2m-slot global table (load <= 1/2).
-  const uint64_t m = e - s, cap = 2 * m;
-  uint64_t* gk = gkeys + 2 * s;
-  uint32_t* gv = gvals + 2 * s;
+  // Overflow: redo the bucket in its own 2m-slot global table (load <= 1/2); a region past
+  // its capacity (whole) from the whole input, in 2 x count slots carved from *spill
+  const uint64_t m = whole ? (uint64_t)region_n : e - s, cap = 2 * m;
+  if (whole && threadIdx.x == 0) spill_off = atomicAdd(spill, (unsigned long long)cap);
+  __syncthreads();
+  uint64_t* gk = gkeys + (whole ? (uint64_t)spill_off : 2 * s);
+  uint32_t* gv = gvals + (whole ? (uint64_t)spill_off : 2 * s);
   for (uint64_t i = threadIdx.x; i < cap; i += THREADS) { gk[i] = empty; gv[i] = 0xFFFFFFFFu; }
   if (threadIdx.x == 0) distinct = 0;
   __threadfence();
   __syncthreads();
+  const uint64_t lo = whole ? 0 : s, hi = whole ? rescan_n : e;
   uint32_t fresh = 0;
-  for (uint64_t i = s + threadIdx.x; i < e; i += THREADS) {
-    const uint64_t kk = pkeys[i];
-    const uint32_t pp = ppos[i];
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += THREADS) {
+    const uint64_t kk = whole ? mix64(rescan[i]) : pkeys[i];
+    if (whole && (uint32_t)(kk >> (64 - bits)) != b) continue;
+    const uint32_t pp = whole ? (uint32_t)i : ppos[i];
     g_insert(gk, gv, cap, (kk & 0xFFFFFFFFull) % cap, kk, vals ? vals[pp] : pp, empty, fresh);
   }
   if (fresh) atomicAdd(&distinct, fresh);
   __threadfence();
   __syncthreads();
-  for (uint64_t i = s + threadIdx.x; i < e; i += THREADS) {
-    const uint64_t kk = pkeys[i];
-    const uint32_t pp = ppos[i];
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += THREADS) {
+    const uint64_t kk = whole ? mix64(rescan[i]) : pkeys[i];
+    if (whole && (uint32_t)(kk >> (64 - bits)) != b) continue;
+    const uint32_t pp = whole ? (uint32_t)i : ppos[i];
     const uint64_t slot = g_find(gk, cap, (kk & 0xFFFFFFFFull) % cap, kk);
     const uint32_t mv = __hip_atomic_load(&gv[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (mv != (vals ? vals[pp] : pp)) out[pp] = mv;
@@ -858,6 +876,105 @@ sd_bucket_min_regions(const uint64_t* __restrict__ rkeys, const uint32_t* __rest
   bucket_min<REG_TABLE, REG_THREADS, REG_ITEMS, true>(blockIdx.x, nullptr, 0, rkeys, rfile, nullptr,
                                                       nullptr, REGIONS, REGION_BITS, 0, out, objects,
                                                       gkeys, gvals, cursor, cap);
+}
+
+// The standalone chain for small batches (<= BIG_MAX_KEYS keys, default plan): the keys
+// already in HBM go through K1G's region epilogue — one pass into the fixed-capacity regions
+// (mixed key, row), out[] prefilled, one LDS histogram per 4,096 keys and one reservation
+// atomic per (workgroup, non-empty region) — then the region tables: two launches instead
+// of totals + scatter + tables.  A region past its capacity (a key repeated thousands of
+// times) keeps counting in its cursor and its table workgroup regroups it from the whole
+// input.  cursor: REGIONS u32 CURSOR_STRIDE apart (own 128-B lines), zero on entry (the
+// tables re-zero them).
+#ifndef SD_REGION_CURSOR_STRIDE
+#define SD_REGION_CURSOR_STRIDE 32
+#endif
+constexpr uint32_t CURSOR_STRIDE = SD_REGION_CURSOR_STRIDE;
+constexpr int RPART_THREADS = 512;
+constexpr int RPART_ITEMS = 8;
+constexpr uint32_t RPART_TILE = RPART_THREADS * RPART_ITEMS;
+extern "C" __global__ void __launch_bounds__(RPART_THREADS)
+sd_region_partition(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ vals, uint64_t n,
+                    uint64_t* __restrict__ rkeys, uint32_t* __restrict__ rfile,
+                    uint32_t* __restrict__ cursor, uint64_t cap, uint32_t* __restrict__ out,
+                    unsigned long long* __restrict__ objects, unsigned long long* __restrict__ spill) {
+  static_assert(RPART_THREADS == PART_THREADS, "lds_exclusive_scan runs on PART_THREADS lanes");
+  __shared__ uint32_t tcnt[REGIONS], tstart[REGIONS], gbase[REGIONS];
+  __shared__ uint64_t skey[RPART_TILE];
+  __shared__ uint32_t sfile[RPART_TILE];
+  const uint64_t b0 = (uint64_t)blockIdx.x * RPART_TILE;
+  const uint32_t tile_n = n - b0 < RPART_TILE ? (uint32_t)(n - b0) : RPART_TILE;
+  uint64_t k[RPART_ITEMS];
+  uint32_t v[RPART_ITEMS], r[RPART_ITEMS];
+  // clamped, unconditional loads (no per-lane branch around them: one wait for all)
+#pragma unroll
+  for (int j = 0; j < RPART_ITEMS; ++j) {
+    const uint64_t i = b0 + (uint64_t)j * RPART_THREADS + threadIdx.x;
+    k[j] = keys[i < n ? i : n - 1];
+  }
+  if (vals) {
+#pragma unroll
+    for (int j = 0; j < RPART_ITEMS; ++j) {
+      const uint64_t i = b0 + (uint64_t)j * RPART_THREADS + threadIdx.x;
+      v[j] = vals[i < n ? i : n - 1];
+    }
+  }
+  for (uint32_t i = threadIdx.x; i < REGIONS; i += RPART_THREADS) tcnt[i] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) { *objects = 0; *spill = 0; }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RPART_ITEMS; ++j) {
+    const uint32_t t = (uint32_t)j * RPART_THREADS + threadIdx.x;
+    k[j] = mix64(k[j]);
+    if (t < tile_n) {
+      r[j] = atomicAdd(&tcnt[(uint32_t)(k[j] >> (64 - REGION_BITS))], 1u);
+      out[b0 + t] = vals ? v[j] : (uint32_t)(b0 + t);
+    }
+  }
+  __syncthreads();
+  // one reservation per non-empty region, then the tile counting-sorted by region in LDS so
+  // that consecutive lanes store consecutive rows of one region's run
+  for (uint32_t b = threadIdx.x; b < REGIONS; b += RPART_THREADS) {
+    const uint32_t h = tcnt[b];
+    gbase[b] = h ? atomicAdd(&cursor[b * CURSOR_STRIDE], h) : 0u;
+  }
+  lds_exclusive_scan(tcnt, tstart, REGIONS);  // (its barriers also publish gbase)
+#pragma unroll
+  for (int j = 0; j < RPART_ITEMS; ++j) {
+    const uint32_t t = (uint32_t)j * RPART_THREADS + threadIdx.x;
+    if (t < tile_n) {
+      const uint32_t slot = tstart[(uint32_t)(k[j] >> (64 - REGION_BITS))] + r[j];
+      skey[slot] = k[j];
+      sfile[slot] = (uint32_t)(b0 + t);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RPART_ITEMS; ++j) {
+    const uint32_t t = (uint32_t)j * RPART_THREADS + threadIdx.x;
+    if (t < tile_n) {
+      const uint64_t kk = skey[t];
+      const uint32_t b = (uint32_t)(kk >> (64 - REGION_BITS));
+      const uint64_t o = (uint64_t)gbase[b] + (t - tstart[b]);
+      if (o < cap) {  // rows past the capacity only counted (the table regroups the region)
+        rkeys[(uint64_t)b * cap + o] = kk;
+        rfile[(uint64_t)b * cap + o] = sfile[t];
+      }
+    }
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(REG_THREADS)
+sd_bucket_min_regions_keys(const uint64_t* __restrict__ rkeys, const uint32_t* __restrict__ rfile,
+                           uint32_t* __restrict__ cursor, uint64_t cap,
+                           const uint64_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                           uint64_t n, uint32_t* __restrict__ out,
+                           unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
+                           uint32_t* __restrict__ gvals, unsigned long long* __restrict__ spill) {
+  bucket_min<REG_TABLE, REG_THREADS, REG_ITEMS, true>(blockIdx.x, nullptr, 0, rkeys, rfile, vals,
+                                                      nullptr, REGIONS, REGION_BITS, 0, out, objects,
+                                                      gkeys, gvals, cursor, cap, keys, n, spill,
+                                                      CURSOR_STRIDE);
 }
 
 }  // namespace sdcas
@@ -960,15 +1077,34 @@ bool hash_group_supported(uint64_t n) {
 
 static uint32_t totals_repl(uint32_t nb) { return nb <= STAGED_MAX_NB ? TOTALS_REPL : 1; }
 
+// The small-batch region chain (sd_region_partition + sd_bucket_min_regions_keys) serves the
+// default plan's batches of (SD_SMALL_REGIONS_MIN, BIG_MAX_KEYS] keys
+#ifndef SD_SMALL_REGIONS
+#define SD_SMALL_REGIONS 1
+#endif
+#ifndef SD_SMALL_REGIONS_MIN
+#define SD_SMALL_REGIONS_MIN (256ull * 1536)
+#endif
+static bool small_regions(uint64_t n, uint64_t target) {
+  return SD_SMALL_REGIONS && target == 0 && n > SD_SMALL_REGIONS_MIN && n <= BIG_MAX_KEYS;
+}
+
+// its workspace: rkeys | rfile | overflow tables (2n slots) | spill cursor
+static size_t small_regions_bytes(uint64_t n) {
+  const uint64_t rows = (uint64_t)REGIONS * region_capacity(n);
+  return al256(rows * 8) + al256(rows * 4) + al256(2 * n * 8) + al256(2 * n * 4) + 256;
+}
+
 // workspace: k1 | p1 | k2 | p2 | fill (repl copies) | starts1 | starts | Object-count shards |
 // overflow tables (the bucket totals live in a persistent buffer of the caller,
 // GROUP_TOTALS_WORDS)
 size_t hash_group_workspace_bytes(uint64_t n, uint64_t target) {
   const GroupPlan g = group_plan(n, target);
   const size_t nb1 = g.l1.nb;
-  return 2 * (al256(n * 8) + al256(n * 4)) + al256(totals_repl(nb1) * nb1 * 4) +
-         al256(nb1 * 4) + al256((size_t)g.nb() * 4) + al256(OBJ_SHARDS * OBJ_STRIDE * 8) +
-         al256(2 * n * 8) + al256(2 * n * 4);
+  const size_t chain = 2 * (al256(n * 8) + al256(n * 4)) + al256(totals_repl(nb1) * nb1 * 4) +
+                       al256(nb1 * 4) + al256((size_t)g.nb() * 4) +
+                       al256(OBJ_SHARDS * OBJ_STRIDE * 8) + al256(2 * n * 8) + al256(2 * n * 4);
+  return small_regions(n, target) ? std::max(chain, small_regions_bytes(n)) : chain;
 }
 
 size_t partition_workspace_bytes(uint64_t n, uint32_t parts) {
@@ -1053,6 +1189,24 @@ hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n
                           uint64_t target) {
   if (n == 0) return hipMemsetAsync(d_objects, 0, 8, s);
   if (!hash_group_supported(n)) return hipErrorInvalidValue;
+  static_assert(REGIONS * CURSOR_STRIDE <= GROUP_TOTALS_WORDS, "the cursors fit the totals buffer");
+  if (small_regions(n, target)) {  // `totals` (zero, left zero) holds the region cursors
+    const uint64_t cap = region_capacity(n), rows = (uint64_t)REGIONS * cap;
+    char* q = (char*)ws;
+    uint64_t* rkeys = (uint64_t*)q; q += al256(rows * 8);
+    uint32_t* rfile = (uint32_t*)q; q += al256(rows * 4);
+    uint64_t* gkeys = (uint64_t*)q; q += al256(2 * n * 8);
+    uint32_t* gvals = (uint32_t*)q; q += al256(2 * n * 4);
+    unsigned long long* spill = (unsigned long long*)q;
+    unsigned long long* obj = (unsigned long long*)d_objects;
+    sd_region_partition<<<(uint32_t)((n + RPART_TILE - 1) / RPART_TILE), RPART_THREADS, 0, s>>>(
+        keys, vals, n, rkeys, rfile, totals, cap, out, obj, spill);
+    sd_bucket_min_regions_keys<<<REGIONS, REG_THREADS, 0, s>>>(rkeys, rfile, totals, cap, keys, vals,
+                                                               n, out, obj, gkeys, gvals, spill);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) (void)hipMemsetAsync(totals, 0, GROUP_TOTALS_WORDS * 4, s);  // restore
+    return e;
+  }
   const GroupPlan g = group_plan(n, target);
   const size_t nb1 = g.l1.nb;
   char* q = (char*)ws;

@@ -605,6 +605,42 @@ def test_group_min_vs_numpy(eng):
         assert (out.cpu().numpy().view(np.uint32) == mins[inv]).all()
 
 
+def test_group_small_regions_overflow(eng, oracle):
+    """The small-batch region chain (393K < n <= 1.44M keys: sd_region_partition into fixed-
+    capacity regions, then sd_bucket_min_regions_keys): regions pushed past their capacity —
+    one key repeated 300K times, and 3 regions each given 20K crafted distinct keys — are
+    regrouped from the whole input; sd_cas_group vs the oracle and sd_cas_group_min (random
+    u32 vals) vs numpy, twice in a row (the region cursors are left zero)."""
+    rng = np.random.default_rng(43)
+    crafted = []
+    for top in (3, 77, 200):  # mixed top byte = the region
+        low = rng.integers(0, 2 ** 56, 20_000, dtype=np.uint64)
+        crafted.append(np.array([unmix64((top << 56) | int(x)) for x in low], dtype=np.uint64))
+    uni = rng.integers(0, 2 ** 64, 900_000, dtype=np.uint64)
+    cases = {
+        "one key x300K": np.concatenate([uni, np.full(300_000, 0x1234567, dtype=np.uint64)]),
+        "3 crafted regions": np.concatenate([uni] + crafted),
+        "uniform 30% dup": uni[rng.integers(0, 630_000, 1_100_000)],
+    }
+    for name, keys in cases.items():
+        keys = keys[rng.permutation(len(keys))]
+        n = len(keys)
+        for _ in range(2):
+            rep = torch.empty(n, dtype=torch.int32, device="cuda")
+            objects = eng.group(dev64(keys), rep)
+            orep, oobj = oracle.group_canonical(keys)
+            assert objects == oobj, name
+            assert (rep.cpu().numpy().astype(np.uint32) == orep).all(), name
+        vals = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+        out = torch.empty(n, dtype=torch.int32, device="cuda")
+        objects = eng.group_min(dev64(keys), torch.from_numpy(vals.view(np.int32)).cuda(), out)
+        uniq, inv = np.unique(keys, return_inverse=True)
+        mins = np.full(len(uniq), 0xFFFFFFFF, dtype=np.uint32)
+        np.minimum.at(mins, inv, vals)
+        assert objects == len(uniq), name
+        assert (out.cpu().numpy().view(np.uint32) == mins[inv]).all(), name
+
+
 def test_partition_range_vs_numpy(eng):
     from tests.test_shard_cpu import range_part
     rng = np.random.default_rng(42)
