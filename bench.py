@@ -56,7 +56,12 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 # the 12,288-slot tables, sd_bucket_min_big); above, the refine level adds count read 8 +
 # read 12 / write 12 = 76 B/key (the minima of duplicates are the only other stores)
 def group_bytes_per_key(n: int) -> int:
-    return 44 if n <= 256 * 5632 else 76
+    """Algorithmic HBM bytes per key of the standalone grouping: up to 1.44 M
+    keys the region chain (read key 8, prefill rep 4, region row 12, tables read it 12); above,
+    the partition chain (totals 8 + prefill 4 + scatter 8/12 + refine 12/12 + count 8 + read 12)."""
+    return 36 if n <= 256 * 5632 else 76
+
+
 FUSED_REGION_BITS = 8  # sd_mix.h REGION_BITS
 FUSED_MAX_FILES = 256 * 5632  # the fused chain's single-level regions (sd_cas_hash_group_sampled_dev)
 

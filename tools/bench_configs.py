@@ -218,10 +218,9 @@ def config4(eng, orc, n_total: int, batch: int, dup: int, shards: int = 1):
     np.minimum.at(first, inv, np.arange(n_total))
     ok = objects == len(uniq) and bool((rep.cpu().numpy() == first[inv]).all())
     del roots, r, inv, first
-    # K4h/K5h algorithmic bytes per key (bench.group_bytes_per_key): totals read 8 + rep
-    # prefill 4 + scatter 8/12 + bucket read 12 = 44 up to 1,441,792 keys; above, the refine
-    # level adds count read 8 + read 12 / write 12 = 76
-    bpk = 44 if n_total <= 256 * 5632 else 76
+    # grouping algorithmic bytes per key (bench.group_bytes_per_key): 36 up to 1,441,792 keys
+    # (the region chain), 76 above (the partition chain with its refine level)
+    bpk = 36 if n_total <= 256 * 5632 else 76
     out = {"config": "4-rank-share" if n_total < 100_000_000 else "4-full-library",
            "files": n_total, "dup_permille": dup,
            "hash_kernel_s": hash_s, "hash_files_per_s": n_total / hash_s,
