@@ -465,17 +465,21 @@ sd_part_scatter_range(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nb
 // writes runs of ~1-3 keys per bucket per block, which costs 5-10x in scattered stores
 // (tools/ubench_scatter.hip); two coalesced levels move more bytes in less time.
 constexpr uint32_t MAX_FINE = 1u << MAX_B2;
-extern "C" __global__ void __launch_bounds__(PART_THREADS)
-sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict__ in_pos,
-               const uint32_t* __restrict__ starts1, uint32_t nb1, uint64_t n, uint32_t b1,
-               uint32_t b2, uint64_t* __restrict__ out_keys, uint32_t* __restrict__ out_pos,
-               uint32_t* __restrict__ starts) {
+// refine_body: coarse bucket c's rows in_keys/in_pos[is, ie) -> out rows from os on (bucket-
+// contiguous by the next b2 bits); with a spill list (the region chain: rows past the region's
+// capacity), its rows of bucket c follow them (filtered, stored one by one: only inputs where
+// one key repeats thousands of times have any).
+__device__ __forceinline__ void refine_body(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict__ in_pos,
+                            uint64_t is, uint64_t ie, uint64_t os, uint32_t c, uint32_t b1,
+                            uint32_t b2, uint64_t* __restrict__ out_keys,
+                            uint32_t* __restrict__ out_pos, uint32_t* __restrict__ starts,
+                            const uint64_t* __restrict__ spill_keys = nullptr,
+                            const uint32_t* __restrict__ spill_pos = nullptr, uint64_t spill_n = 0) {
   __shared__ uint32_t cnt[MAX_FINE], gcur[MAX_FINE], tcnt[MAX_FINE], tstart[MAX_FINE];
   __shared__ uint64_t skey[PART_TILE];
   __shared__ uint32_t spos[PART_TILE];
-  const uint32_t c = blockIdx.x, nb2 = 1u << b2;
-  const uint64_t s = starts1[c];
-  const uint64_t e = c + 1 < nb1 ? starts1[c + 1] : n;
+  const uint32_t nb2 = 1u << b2;
+  const uint64_t s = is, e = ie;
   if (threadIdx.x < nb2) cnt[threadIdx.x] = 0;
   __syncthreads();
   // one workgroup per coarse bucket (~1 per CU): each trip's loads are issued a trip ahead,
@@ -491,6 +495,8 @@ sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict_
       if (with_pos) qn[j] = in_pos[c];
     }
   };
+  auto fine = [b1, b2](uint64_t x) { return (uint32_t)((x << b1) >> (64 - b2)); };
+  auto mine = [b1, c](uint64_t x) { return (uint32_t)(x >> (64 - b1)) == c; };
   if (s < e) load(s, false);
   for (uint64_t base = s; base < e; base += PART_TILE) {
     uint64_t k[ITEMS];
@@ -500,8 +506,12 @@ sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict_
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
       const uint64_t i = base + (uint64_t)j * PART_THREADS + threadIdx.x;
-      if (i < e) atomicAdd(&cnt[(uint32_t)((k[j] << b1) >> (64 - b2))], 1u);
+      if (i < e) atomicAdd(&cnt[fine(k[j])], 1u);
     }
+  }
+  for (uint64_t i = threadIdx.x; i < spill_n; i += PART_THREADS) {
+    const uint64_t x = spill_keys[i];
+    if (mine(x)) atomicAdd(&cnt[fine(x)], 1u);
   }
   if (s < e) load(s, true);  // the scatter pass's first trip, in flight during the plan
   __syncthreads();
@@ -509,7 +519,7 @@ sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict_
   __shared__ uint32_t dbg_end[MAX_FINE];  // where each fine bucket's cursor must end
 #endif
   if (threadIdx.x == 0) {
-    uint32_t run = (uint32_t)s;
+    uint32_t run = (uint32_t)os;
     for (uint32_t j = 0; j < nb2; ++j) {
       const uint32_t x = cnt[j];
       gcur[j] = run;
@@ -519,12 +529,12 @@ sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict_
       dbg_end[j] = run;
 #endif
     }
-    SD_DBG_CHECK(run == (uint32_t)e, "refine bucket %u: fine counts add to %u, segment ends at %llu",
-                 c, run, (unsigned long long)e);
+    SD_DBG_CHECK(spill_n || run == (uint32_t)(os + (e - s)),
+                 "refine bucket %u: fine counts add to %u, segment ends at %llu", c, run,
+                 (unsigned long long)(os + (e - s)));
   }
   if (threadIdx.x < nb2) tcnt[threadIdx.x] = 0;
   __syncthreads();
-  auto bfn = [b1, b2](uint64_t x) { return (uint32_t)((x << b1) >> (64 - b2)); };
   for (uint64_t base = s; base < e; base += PART_TILE) {
     uint64_t k[ITEMS];
     uint32_t q[ITEMS];
@@ -532,14 +542,36 @@ sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict_
     for (int j = 0; j < ITEMS; ++j) { k[j] = kn[j]; q[j] = qn[j]; }
     load(base + PART_TILE < e ? base + PART_TILE : e, true);
     const uint64_t left = e - base;
-    staged_trip<false, false>(k, q, left < PART_TILE ? (uint32_t)left : PART_TILE, nb2, bfn, gcur, tcnt,
+    staged_trip<false, false>(k, q, left < PART_TILE ? (uint32_t)left : PART_TILE, nb2, fine, gcur, tcnt,
                        tstart, skey, spos, nullptr, nullptr, out_keys, out_pos, []() {});
+  }
+  if (spill_n) {  // (uniform) after the last trip's barrier: gcur is final for the region rows
+    for (uint64_t i = threadIdx.x; i < spill_n; i += PART_THREADS) {
+      const uint64_t x = spill_keys[i];
+      if (mine(x)) {
+        const uint32_t d = atomicAdd(&gcur[fine(x)], 1u);
+        out_keys[d] = x;
+        out_pos[d] = spill_pos[i];
+      }
+    }
+    __syncthreads();
   }
   // conservation: every fine bucket's cursor advanced by exactly its count (rows written ==
   // rows counted); staged_trip's last barrier published gcur
   SD_DBG_CHECK(threadIdx.x >= nb2 || gcur[threadIdx.x] == dbg_end[threadIdx.x],
                "refine bucket %u.%u: cursor %u, expected %u", c, threadIdx.x, gcur[threadIdx.x],
                dbg_end[threadIdx.x]);
+}
+
+extern "C" __global__ void __launch_bounds__(PART_THREADS)
+sd_part_refine(const uint64_t* __restrict__ in_keys, const uint32_t* __restrict__ in_pos,
+               const uint32_t* __restrict__ starts1, uint32_t nb1, uint64_t n, uint32_t b1,
+               uint32_t b2, uint64_t* __restrict__ out_keys, uint32_t* __restrict__ out_pos,
+               uint32_t* __restrict__ starts) {
+  const uint32_t c = blockIdx.x;
+  const uint64_t s = starts1[c];
+  const uint64_t e = c + 1 < nb1 ? starts1[c + 1] : n;
+  refine_body(in_keys, in_pos, s, e, s, c, b1, b2, out_keys, out_pos, starts);
 }
 
 // Home slot of a (mixed, uniform) key in a TBL-slot table — its low bits for a power of two,
@@ -981,6 +1013,278 @@ sd_bucket_min_regions_keys(const uint64_t* __restrict__ rkeys, const uint32_t* _
                                                       CURSOR_STRIDE);
 }
 
+// The region chain above 1.44 M keys (default plan): one pass of the keys into 2^b1 fixed-
+// capacity coarse regions (sd_region_partition_big: 8,192 keys per 1,024-lane workgroup,
+// LDS-staged), the refine over each region (its output segment starts at the sum of the
+// preceding regions' counts), then the fine tables — no totals pass.  Rows past a region's
+// capacity go to a spill list (one reservation per workgroup that has any) that the refine of
+// their region reads after its region rows.  The cursors (CURSOR_STRIDE apart) and the spill
+// count live in the persistent totals buffer, zero on entry; the tables re-zero them.
+#ifndef SD_RBIG_THREADS
+#define SD_RBIG_THREADS 1024
+#endif
+#ifndef SD_RBIG_ITEMS
+#define SD_RBIG_ITEMS 8
+#endif
+#ifndef SD_RBIG_MAX_NB
+#define SD_RBIG_MAX_NB 256
+#endif
+constexpr int RBIG_THREADS = SD_RBIG_THREADS;
+constexpr int RBIG_ITEMS = SD_RBIG_ITEMS;
+constexpr uint32_t RBIG_TILE = RBIG_THREADS * RBIG_ITEMS;
+constexpr uint32_t RBIG_MAX_NB = SD_RBIG_MAX_NB;
+
+// Exclusive scan of cnt[0..nb) into out (both LDS) by a THREADS-lane block.
+template <int THREADS>
+__device__ void lds_exclusive_scan_t(const uint32_t* cnt, uint32_t* out, uint32_t nb) {
+  __shared__ uint32_t wsum[THREADS / 64];
+  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+  const uint32_t per = (nb + THREADS - 1) / THREADS;
+  const uint32_t lo = t * per < nb ? t * per : nb, hi = lo + per < nb ? lo + per : nb;
+  uint32_t sum = 0;
+  for (uint32_t i = lo; i < hi; ++i) sum += cnt[i];
+  uint32_t inc = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= (uint32_t)o) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t run = inc - sum;
+  for (uint32_t i = 0; i < w; ++i) run += wsum[i];
+  for (uint32_t i = lo; i < hi; ++i) { out[i] = run; run += cnt[i]; }
+  __syncthreads();
+}
+
+extern "C" __global__ void __launch_bounds__(RBIG_THREADS)
+sd_region_partition_big(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                        uint64_t n, uint32_t rbits, uint64_t* __restrict__ rkeys,
+                        uint32_t* __restrict__ rfile, uint32_t* __restrict__ cursor, uint64_t cap,
+                        uint32_t* __restrict__ out, unsigned long long* __restrict__ shards,
+                        uint32_t nshards, uint32_t* __restrict__ spill_cnt,
+                        uint64_t* __restrict__ spill_keys, uint32_t* __restrict__ spill_pos) {
+  __shared__ uint32_t tcnt[RBIG_MAX_NB], tstart[RBIG_MAX_NB], gbase[RBIG_MAX_NB];
+  __shared__ uint64_t skey[RBIG_TILE];
+  __shared__ uint32_t sfile[RBIG_TILE];
+  __shared__ uint32_t sp_n, sp_i, sp_base;
+  const uint32_t nb = 1u << rbits;
+  const uint64_t b0 = (uint64_t)blockIdx.x * RBIG_TILE;
+  const uint32_t tile_n = n - b0 < RBIG_TILE ? (uint32_t)(n - b0) : RBIG_TILE;
+  uint64_t k[RBIG_ITEMS];
+  uint32_t v[RBIG_ITEMS], r[RBIG_ITEMS];
+#pragma unroll
+  for (int j = 0; j < RBIG_ITEMS; ++j) {
+    const uint64_t i = b0 + (uint64_t)j * RBIG_THREADS + threadIdx.x;
+    k[j] = keys[i < n ? i : n - 1];
+  }
+  if (vals) {
+#pragma unroll
+    for (int j = 0; j < RBIG_ITEMS; ++j) {
+      const uint64_t i = b0 + (uint64_t)j * RBIG_THREADS + threadIdx.x;
+      v[j] = vals[i < n ? i : n - 1];
+    }
+  }
+  for (uint32_t i = threadIdx.x; i < nb; i += RBIG_THREADS) tcnt[i] = 0;
+  if (threadIdx.x == 0) { sp_n = 0; sp_i = 0; }
+  if (blockIdx.x == 0 && threadIdx.x < nshards) shards[threadIdx.x * OBJ_STRIDE] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RBIG_ITEMS; ++j) {
+    const uint32_t t = (uint32_t)j * RBIG_THREADS + threadIdx.x;
+    k[j] = mix64(k[j]);
+    if (t < tile_n) {
+      r[j] = atomicAdd(&tcnt[(uint32_t)(k[j] >> (64 - rbits))], 1u);
+      out[b0 + t] = vals ? v[j] : (uint32_t)(b0 + t);
+    }
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nb; b += RBIG_THREADS) {
+    const uint32_t h = tcnt[b];
+    const uint32_t g = h ? atomicAdd(&cursor[b * CURSOR_STRIDE], h) : 0u;
+    gbase[b] = g;
+    if ((uint64_t)g + h > cap) atomicAdd(&sp_n, (uint32_t)((uint64_t)g + h - (g > cap ? g : cap)));
+  }
+  lds_exclusive_scan_t<RBIG_THREADS>(tcnt, tstart, nb);  // (its barriers publish gbase, sp_n)
+  SD_DBG_CHECK(threadIdx.x != 0 || tstart[nb - 1] + tcnt[nb - 1] == tile_n,
+               "region partition (block %u) counted %u of %u keys", blockIdx.x,
+               tstart[nb - 1] + tcnt[nb - 1], tile_n);
+  if (threadIdx.x == 0 && sp_n) sp_base = atomicAdd(spill_cnt, sp_n);
+#pragma unroll
+  for (int j = 0; j < RBIG_ITEMS; ++j) {
+    const uint32_t t = (uint32_t)j * RBIG_THREADS + threadIdx.x;
+    if (t < tile_n) {
+      const uint32_t slot = tstart[(uint32_t)(k[j] >> (64 - rbits))] + r[j];
+      skey[slot] = k[j];
+      sfile[slot] = (uint32_t)(b0 + t);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RBIG_ITEMS; ++j) {
+    const uint32_t t = (uint32_t)j * RBIG_THREADS + threadIdx.x;
+    if (t < tile_n) {
+      const uint64_t kk = skey[t];
+      const uint32_t b = (uint32_t)(kk >> (64 - rbits));
+      const uint64_t o = (uint64_t)gbase[b] + (t - tstart[b]);
+      if (o < cap) {
+        rkeys[(uint64_t)b * cap + o] = kk;
+        rfile[(uint64_t)b * cap + o] = sfile[t];
+      } else {
+        const uint32_t d = sp_base + atomicAdd(&sp_i, 1u);
+        spill_keys[d] = kk;
+        spill_pos[d] = sfile[t];
+      }
+    }
+  }
+}
+
+// The same as a resident grid (SD_RBIG_PERSIST): each workgroup walks tiles blockIdx.x,
+// + gridDim.x, ..., the next tile's keys loaded behind this tile's reservation atomics.
+#ifndef SD_RBIG_PERSIST
+#define SD_RBIG_PERSIST 0
+#endif
+constexpr uint32_t RPERS_PER_CU = 3;
+// (HAS_VALS a template parameter: a runtime `if (vals)` between the prefetch's loads made the
+// compiler wait for each in turn)
+template <bool HAS_VALS>
+__device__ __forceinline__ void region_partition_pers(
+    const uint64_t* __restrict__ keys, const uint32_t* __restrict__ vals, uint64_t n, uint32_t rbits,
+    uint64_t* __restrict__ rkeys, uint32_t* __restrict__ rfile, uint32_t* __restrict__ cursor,
+    uint64_t cap, uint32_t* __restrict__ out, unsigned long long* __restrict__ shards,
+    uint32_t nshards, uint32_t* __restrict__ spill_cnt, uint64_t* __restrict__ spill_keys,
+    uint32_t* __restrict__ spill_pos) {
+  __shared__ uint32_t tcnt[RBIG_MAX_NB], tstart[RBIG_MAX_NB], gbase[RBIG_MAX_NB];
+  __shared__ uint64_t skey[RBIG_TILE];
+  __shared__ uint32_t sfile[RBIG_TILE];
+  __shared__ uint32_t sp_n, sp_i, sp_base;
+  constexpr int RPT = (RBIG_MAX_NB + RBIG_THREADS - 1) / RBIG_THREADS;
+  const uint32_t nb = 1u << rbits;
+  const uint64_t ntiles = (n + RBIG_TILE - 1) / RBIG_TILE;
+  uint64_t kn[RBIG_ITEMS];
+  uint32_t vn[RBIG_ITEMS];
+  auto load = [&](uint64_t tile) {  // raw, unconditional (clamped to the last key)
+#pragma unroll
+    for (int j = 0; j < RBIG_ITEMS; ++j) {
+      const uint64_t i = tile * RBIG_TILE + (uint64_t)j * RBIG_THREADS + threadIdx.x;
+      kn[j] = keys[i < n ? i : n - 1];
+      if (HAS_VALS) vn[j] = vals[i < n ? i : n - 1];
+    }
+  };
+  for (uint32_t i = threadIdx.x; i < nb; i += RBIG_THREADS) tcnt[i] = 0;
+  if (threadIdx.x == 0) { sp_n = 0; sp_i = 0; }
+  if (blockIdx.x == 0 && threadIdx.x < nshards) shards[threadIdx.x * OBJ_STRIDE] = 0;
+  load(blockIdx.x);
+  __syncthreads();
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint64_t b0 = tile * RBIG_TILE;
+    const uint32_t tile_n = n - b0 < RBIG_TILE ? (uint32_t)(n - b0) : RBIG_TILE;
+    uint64_t k[RBIG_ITEMS];
+    uint32_t r[RBIG_ITEMS];
+#pragma unroll
+    for (int j = 0; j < RBIG_ITEMS; ++j) {
+      const uint32_t t = (uint32_t)j * RBIG_THREADS + threadIdx.x;
+      k[j] = mix64(kn[j]);
+      if (t < tile_n) {
+        r[j] = atomicAdd(&tcnt[(uint32_t)(k[j] >> (64 - rbits))], 1u);
+        out[b0 + t] = HAS_VALS ? vn[j] : (uint32_t)(b0 + t);
+      }
+    }
+    __syncthreads();
+    uint32_t res[RPT];
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      const uint32_t b = threadIdx.x + (uint32_t)q * RBIG_THREADS;
+      res[q] = b < nb && tcnt[b] ? atomicAdd(&cursor[b * CURSOR_STRIDE], tcnt[b]) : 0u;
+    }
+    load(tile + gridDim.x < ntiles ? tile + gridDim.x : tile);  // in flight during this tile
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      const uint32_t b = threadIdx.x + (uint32_t)q * RBIG_THREADS;
+      if (b < nb) {
+        const uint32_t h = tcnt[b], g = res[q];
+        gbase[b] = g;
+        if ((uint64_t)g + h > cap) atomicAdd(&sp_n, (uint32_t)((uint64_t)g + h - (g > cap ? g : cap)));
+      }
+    }
+    lds_exclusive_scan_t<RBIG_THREADS>(tcnt, tstart, nb);  // (its barriers publish gbase, sp_n)
+    SD_DBG_CHECK(threadIdx.x != 0 || tstart[nb - 1] + tcnt[nb - 1] == tile_n,
+                 "region partition (tile %llu) counted %u of %u keys", (unsigned long long)tile,
+                 tstart[nb - 1] + tcnt[nb - 1], tile_n);
+    if (threadIdx.x == 0 && sp_n) sp_base = atomicAdd(spill_cnt, sp_n);
+#pragma unroll
+    for (int j = 0; j < RBIG_ITEMS; ++j) {
+      const uint32_t t = (uint32_t)j * RBIG_THREADS + threadIdx.x;
+      if (t < tile_n) {
+        const uint32_t slot = tstart[(uint32_t)(k[j] >> (64 - rbits))] + r[j];
+        skey[slot] = k[j];
+        sfile[slot] = (uint32_t)(b0 + t);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RBIG_ITEMS; ++j) {
+      const uint32_t t = (uint32_t)j * RBIG_THREADS + threadIdx.x;
+      if (t < tile_n) {
+        const uint64_t kk = skey[t];
+        const uint32_t b = (uint32_t)(kk >> (64 - rbits));
+        const uint64_t o = (uint64_t)gbase[b] + (t - tstart[b]);
+        if (o < cap) {
+          rkeys[(uint64_t)b * cap + o] = kk;
+          rfile[(uint64_t)b * cap + o] = sfile[t];
+        } else {
+          const uint32_t d = sp_base + atomicAdd(&sp_i, 1u);
+          spill_keys[d] = kk;
+          spill_pos[d] = sfile[t];
+        }
+      }
+    }
+    __syncthreads();  // the tile's LDS fully read before the next tile rewrites it
+    for (uint32_t i = threadIdx.x; i < nb; i += RBIG_THREADS) tcnt[i] = 0;
+    if (threadIdx.x == 0) { sp_n = 0; sp_i = 0; }
+    __syncthreads();
+  }
+}
+
+#define SD_RPERS_KERNEL(name, HV)                                                                   \
+  extern "C" __global__ void __launch_bounds__(RBIG_THREADS)                                      \
+  name(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ vals, uint64_t n,          \
+       uint32_t rbits, uint64_t* __restrict__ rkeys, uint32_t* __restrict__ rfile,                \
+       uint32_t* __restrict__ cursor, uint64_t cap, uint32_t* __restrict__ out,                   \
+       unsigned long long* __restrict__ shards, uint32_t nshards, uint32_t* __restrict__ spill_cnt, \
+       uint64_t* __restrict__ spill_keys, uint32_t* __restrict__ spill_pos) {                     \
+    region_partition_pers<HV>(keys, vals, n, rbits, rkeys, rfile, cursor, cap, out, shards, nshards, \
+                              spill_cnt, spill_keys, spill_pos);                                   \
+  }
+SD_RPERS_KERNEL(sd_region_partition_pers, false)
+SD_RPERS_KERNEL(sd_region_partition_pers_vals, true)
+
+// The refine of region c: its output segment starts at the preceding regions' counts.
+extern "C" __global__ void __launch_bounds__(PART_THREADS)
+sd_part_refine_regions(const uint64_t* __restrict__ rkeys, const uint32_t* __restrict__ rfile,
+                       const uint32_t* __restrict__ cursor, uint64_t cap, uint32_t b1, uint32_t b2,
+                       const uint32_t* __restrict__ spill_cnt,
+                       const uint64_t* __restrict__ spill_keys,
+                       const uint32_t* __restrict__ spill_pos, uint64_t* __restrict__ out_keys,
+                       uint32_t* __restrict__ out_pos, uint32_t* __restrict__ starts) {
+  __shared__ uint32_t wsum[PART_THREADS / 64];
+  const uint32_t c = blockIdx.x;
+  uint32_t part = 0;
+  for (uint32_t b = threadIdx.x; b < c; b += PART_THREADS) part += cursor[b * CURSOR_STRIDE];
+  const uint32_t cnt = cursor[c * CURSOR_STRIDE];
+  const uint32_t sp = cnt > cap ? *spill_cnt : 0u;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+  if ((threadIdx.x & 63u) == 0) wsum[threadIdx.x >> 6] = part;
+  __syncthreads();
+  uint32_t os = 0;
+#pragma unroll
+  for (int w = 0; w < PART_THREADS / 64; ++w) os += wsum[w];
+  const uint64_t is = (uint64_t)c * cap;
+  refine_body(rkeys, rfile, is, is + (cnt < cap ? cnt : cap), os, c, b1, b2, out_keys, out_pos, starts,
+              spill_keys, spill_pos, sp);
+}
+
 }  // namespace sdcas
 
 // ---- host launchers ----------------------------------------------------------------
@@ -1095,10 +1399,35 @@ static bool small_regions(uint64_t n, uint64_t target) {
   return SD_SMALL_REGIONS && target == 0 && n > SD_SMALL_REGIONS_MIN && n <= BIG_MAX_KEYS;
 }
 
+// the region chain above 1.44 M keys: the default plan's two-level shapes
+#ifndef SD_BIG_REGIONS
+#define SD_BIG_REGIONS 1
+#endif
+static uint64_t region_capacity_nb(uint64_t n, uint32_t nb) {
+  const double mean = (double)n / nb;
+  const double var = mean * (1.0 - 1.0 / nb);
+  uint64_t sd = 1;
+  while ((double)(sd * sd) < var) ++sd;
+  return (uint64_t)mean + 1 + 8 * sd + 64;
+}
+
 // its workspace: rkeys | rfile | overflow tables (2n slots) | spill cursor
 static size_t small_regions_bytes(uint64_t n) {
   const uint64_t rows = (uint64_t)REGIONS * region_capacity(n);
   return al256(rows * 8) + al256(rows * 4) + al256(2 * n * 8) + al256(2 * n * 4) + 256;
+}
+
+static bool big_regions(const GroupPlan& g, uint64_t target) {
+  return SD_BIG_REGIONS && target == 0 && !g.big && g.b2 > 0 && g.l1.nb <= RBIG_MAX_NB;
+}
+
+// rkeys | rfile | spill keys | spill rows | k2 | p2 | starts | Object-count shards | overflow
+// tables (2n slots)
+static size_t big_regions_bytes(uint64_t n, const GroupPlan& g) {
+  const uint64_t rows = (uint64_t)g.l1.nb * region_capacity_nb(n, g.l1.nb);
+  return al256(rows * 8) + al256(rows * 4) + 2 * (al256(n * 8) + al256(n * 4)) +
+         al256((size_t)g.nb() * 4) + al256(OBJ_SHARDS * OBJ_STRIDE * 8) + al256(2 * n * 8) +
+         al256(2 * n * 4);
 }
 
 // workspace: k1 | p1 | k2 | p2 | fill (repl copies) | starts1 | starts | Object-count shards |
@@ -1110,7 +1439,9 @@ size_t hash_group_workspace_bytes(uint64_t n, uint64_t target) {
   const size_t chain = 2 * (al256(n * 8) + al256(n * 4)) + al256(totals_repl(nb1) * nb1 * 4) +
                        al256(nb1 * 4) + al256((size_t)g.nb() * 4) +
                        al256(OBJ_SHARDS * OBJ_STRIDE * 8) + al256(2 * n * 8) + al256(2 * n * 4);
-  return small_regions(n, target) ? std::max(chain, small_regions_bytes(n)) : chain;
+  if (small_regions(n, target)) return std::max(chain, small_regions_bytes(n));
+  if (big_regions(g, target)) return std::max(chain, big_regions_bytes(n, g));
+  return chain;
 }
 
 size_t partition_workspace_bytes(uint64_t n, uint32_t parts) {
@@ -1196,6 +1527,8 @@ hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n
   if (n == 0) return hipMemsetAsync(d_objects, 0, 8, s);
   if (!hash_group_supported(n)) return hipErrorInvalidValue;
   static_assert(REGIONS * CURSOR_STRIDE <= GROUP_TOTALS_WORDS, "the cursors fit the totals buffer");
+  static_assert((1024 + 1) * CURSOR_STRIDE <= GROUP_TOTALS_WORDS,
+                "the big chain's cursors and spill count fit the totals buffer");
   if (small_regions(n, target)) {  // `totals` (zero, left zero) holds the region cursors
     const uint64_t cap = region_capacity(n), rows = (uint64_t)REGIONS * cap;
     char* q = (char*)ws;
@@ -1215,6 +1548,38 @@ hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n
   }
   const GroupPlan g = group_plan(n, target);
   const size_t nb1 = g.l1.nb;
+  if (big_regions(g, target)) {  // `totals` (zero, left zero) holds the cursors + spill count
+    const uint64_t cap = region_capacity_nb(n, (uint32_t)nb1), rows = nb1 * cap;
+    char* q = (char*)ws;
+    uint64_t* rkeys = (uint64_t*)q; q += al256(rows * 8);
+    uint32_t* rfile = (uint32_t*)q; q += al256(rows * 4);
+    uint64_t* skeys = (uint64_t*)q; q += al256(n * 8);
+    uint32_t* spos = (uint32_t*)q; q += al256(n * 4);
+    uint64_t* k2 = (uint64_t*)q; q += al256(n * 8);
+    uint32_t* p2 = (uint32_t*)q; q += al256(n * 4);
+    uint32_t* starts = (uint32_t*)q; q += al256((size_t)g.nb() * 4);
+    unsigned long long* shards = (unsigned long long*)q; q += al256(OBJ_SHARDS * OBJ_STRIDE * 8);
+    uint64_t* gkeys = (uint64_t*)q; q += al256(2 * n * 8);
+    uint32_t* gvals = (uint32_t*)q;
+    uint32_t* spill_cnt = totals + nb1 * CURSOR_STRIDE;
+    const uint32_t twords = (uint32_t)(nb1 * CURSOR_STRIDE + CURSOR_STRIDE);
+    const uint64_t tiles = (n + RBIG_TILE - 1) / RBIG_TILE;
+    if (SD_RBIG_PERSIST)
+      (vals ? sd_region_partition_pers_vals : sd_region_partition_pers)<<<
+          (uint32_t)std::min<uint64_t>(tiles, 256 * RPERS_PER_CU), RBIG_THREADS, 0, s>>>(
+          keys, vals, n, g.b1, rkeys, rfile, totals, cap, out, shards, OBJ_SHARDS, spill_cnt, skeys, spos);
+    else
+      sd_region_partition_big<<<(uint32_t)tiles, RBIG_THREADS, 0, s>>>(
+          keys, vals, n, g.b1, rkeys, rfile, totals, cap, out, shards, OBJ_SHARDS, spill_cnt, skeys, spos);
+    sd_part_refine_regions<<<(uint32_t)nb1, PART_THREADS, 0, s>>>(rkeys, rfile, totals, cap, g.b1, g.b2,
+                                                                  spill_cnt, skeys, spos, k2, p2, starts);
+    sd_bucket_min<<<g.nb(), MIN_THREADS, 0, s>>>(k2, p2, vals, starts, g.nb(), g.b1 + g.b2, n, out,
+                                                 shards, gkeys, gvals, totals, twords);
+    sd_objects_sum<<<1, 64, 0, s>>>(shards, OBJ_SHARDS, (unsigned long long*)d_objects);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) (void)hipMemsetAsync(totals, 0, GROUP_TOTALS_WORDS * 4, s);  // restore
+    return e;
+  }
   char* q = (char*)ws;
   uint64_t* k1 = (uint64_t*)q; q += al256(n * 8);
   uint32_t* p1 = (uint32_t*)q; q += al256(n * 4);

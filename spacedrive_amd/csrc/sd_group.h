@@ -47,7 +47,7 @@ size_t partition_workspace_bytes(uint64_t n, uint32_t parts);
 // *d_objects = #distinct keys (written on the device).  n < 2^32.  `totals`: a persistent
 // device buffer of GROUP_TOTALS_WORDS u32, all zero before the first call (every call leaves
 // it zero again); calls using it must be stream-ordered.
-constexpr uint32_t GROUP_TOTALS_WORDS = 16 * 1024;
+constexpr uint32_t GROUP_TOTALS_WORDS = 33 * 1024;
 hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n, uint32_t* out,
                           uint64_t* d_objects, void* ws, uint32_t* totals, hipStream_t stream,
                           uint64_t target = 0);

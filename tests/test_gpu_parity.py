@@ -605,22 +605,25 @@ def test_group_min_vs_numpy(eng):
         assert (out.cpu().numpy().view(np.uint32) == mins[inv]).all()
 
 
-def test_group_small_regions_overflow(eng, oracle):
-    """The small-batch region chain (393K < n <= 1.44M keys: sd_region_partition into fixed-
-    capacity regions, then sd_bucket_min_regions_keys): regions pushed past their capacity —
-    one key repeated 300K times, and 3 regions each given 20K crafted distinct keys — are
-    regrouped from the whole input; sd_cas_group vs the oracle and sd_cas_group_min (random
-    u32 vals) vs numpy, twice in a row (the region cursors are left zero)."""
+@pytest.mark.parametrize("n_uni", [900_000, 2_400_000])
+def test_group_regions_overflow(eng, oracle, n_uni):
+    """The region chains: up to 1.44M keys sd_region_partition into 256 fixed-capacity regions
+    + sd_bucket_min_regions_keys (a region past capacity regrouped from the whole input);
+    above, sd_region_partition_big + sd_part_refine_regions + the fine tables (rows past a
+    region's capacity through the spill list).  Regions pushed past capacity — one key
+    repeated 300K times, and 3 regions each given 20K crafted distinct keys — plus a uniform
+    30 %-duplicate batch; sd_cas_group vs the oracle and sd_cas_group_min (random u32 vals) vs
+    numpy, twice in a row (the region cursors are left zero)."""
     rng = np.random.default_rng(43)
     crafted = []
-    for top in (3, 77, 200):  # mixed top byte = the region
+    for top in (3, 77, 200):  # mixed top byte = the region (2^8 coarse regions at these sizes)
         low = rng.integers(0, 2 ** 56, 20_000, dtype=np.uint64)
         crafted.append(np.array([unmix64((top << 56) | int(x)) for x in low], dtype=np.uint64))
-    uni = rng.integers(0, 2 ** 64, 900_000, dtype=np.uint64)
+    uni = rng.integers(0, 2 ** 64, n_uni, dtype=np.uint64)
     cases = {
         "one key x300K": np.concatenate([uni, np.full(300_000, 0x1234567, dtype=np.uint64)]),
         "3 crafted regions": np.concatenate([uni] + crafted),
-        "uniform 30% dup": uni[rng.integers(0, 630_000, 1_100_000)],
+        "uniform 30% dup": uni[rng.integers(0, int(n_uni * 0.7), int(n_uni * 1.2))],
     }
     for name, keys in cases.items():
         keys = keys[rng.permutation(len(keys))]
