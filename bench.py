@@ -57,9 +57,12 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 # read 12 / write 12 = 76 B/key (the minima of duplicates are the only other stores)
 def group_bytes_per_key(n: int) -> int:
     """Algorithmic HBM bytes per key of the standalone grouping: up to 1.44 M
-    keys the region chain (read key 8, prefill rep 4, region row 12, tables read it 12); above,
-    the partition chain (totals 8 + prefill 4 + scatter 8/12 + refine 12/12 + count 8 + read 12)."""
-    return 36 if n <= 256 * 5632 else 76
+    keys the region chain (read key 8, prefill rep 4, region row 12, tables read it 12); up to
+    40 M the two-level region chain (+ the refine: count pass 8, rows 12/12); above, the
+    partition chain (totals 8 + prefill 4 + scatter 8/12 + count 8 + refine 12/12 + read 12)."""
+    if n <= 256 * 5632:
+        return 36
+    return 68 if n <= 40_000_000 else 76
 
 
 FUSED_REGION_BITS = 8  # sd_mix.h REGION_BITS

@@ -33,7 +33,7 @@ for n in [int(x) for x in (sys.argv[1:] or ["1310720", "12500000"])]:
         b.synchronize()
         ts.append(a.elapsed_time(b) / 10)
     ms = float(np.median(ts))
-    bpk = 76 if n > 256 * 5632 else 36
+    bpk = 36 if n <= 256 * 5632 else (68 if n <= 40_000_000 else 76)
     r = rep.cpu().numpy().astype(np.uint64)
     out[str(n)] = {"ms": ms, "all": ts, "objects": obj, "hbm_frac": n * bpk / (ms / 1e3) / 8e12,
                    "rep_digest": f"{int((r * 0x9E3779B97F4A7C15).sum() & 0xFFFFFFFFFFFFFFFF):016x}"}

@@ -219,8 +219,8 @@ def config4(eng, orc, n_total: int, batch: int, dup: int, shards: int = 1):
     ok = objects == len(uniq) and bool((rep.cpu().numpy() == first[inv]).all())
     del roots, r, inv, first
     # grouping algorithmic bytes per key (bench.group_bytes_per_key): 36 up to 1,441,792 keys
-    # (the region chain), 76 above (the partition chain with its refine level)
-    bpk = 36 if n_total <= 256 * 5632 else 76
+    # (the region chain), 68 up to 40 M (two-level region chain), 76 above (the partition chain)
+    bpk = 36 if n_total <= 256 * 5632 else (68 if n_total <= 40_000_000 else 76)
     out = {"config": "4-rank-share" if n_total < 100_000_000 else "4-full-library",
            "files": n_total, "dup_permille": dup,
            "hash_kernel_s": hash_s, "hash_files_per_s": n_total / hash_s,

@@ -47,7 +47,7 @@ def main():
         legacy()
         t_lsd = timed(legacy)
         same = bool(torch.equal(rep, rep2))
-        bpk = 76 if n > 256 * 5632 else 36  # region chain up to 1,441,792 keys; refine level above
+        bpk = 36 if n <= 256 * 5632 else (68 if n <= 40_000_000 else 76)  # bench.group_bytes_per_key
         print(json.dumps({"keys": n, "objects": obj, "hash_group_ms": t_hash, "lsd_group_ms": t_lsd,
                           "speedup": t_lsd / t_hash, "hash_gkeys_per_s": n / t_hash / 1e6,
                           "hash_bytes_per_key": bpk,
