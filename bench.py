@@ -51,10 +51,8 @@ HW_OPS = 680                 # VALU instructions per compression as compiled (ad
 # 224 v_alignbit + 112 v_add3 (half rate on gfx950, 2 slots; profiles/r01_ubench_valu.log)
 SLOTS = 230 + 112 + 2 * (224 + 112)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
-# grouping (group_hash.hip): totals read 8 + prefill write 4 + scatter read 8 / write 12 +
-# bucket read 12 = 44 B/key up to 1,441,792 keys (the 256 coarse buckets go straight to
-# the 12,288-slot tables, sd_bucket_min_big); above, the refine level adds count read 8 +
-# read 12 / write 12 = 76 B/key (the minima of duplicates are the only other stores)
+# grouping (group_hash.hip): see group_bytes_per_key (the minima of duplicates are the only
+# other stores)
 def group_bytes_per_key(n: int) -> int:
     """Algorithmic HBM bytes per key of the standalone grouping: up to 1.44 M
     keys the region chain (read key 8, prefill rep 4, region row 12, tables read it 12); up to
@@ -315,7 +313,7 @@ def main() -> None:
     # on a side stream and shares the CUs with it, so its own speed is measured serially)
     group_ms = group_ms_sync = group12_ms = group12_objects = None
     if not sharded:
-        # (a) each call synchronised: includes the host's enqueue latency of its 4-5 launches
+        # (a) each call synchronised: includes the host's enqueue latency of its 2-4 launches
         # (the GPU idles ~4 us between the first two: profiles/r02b_group_chain_trace.txt);
         # (b) 10 calls back to back: the GPU time per grouping as the pipelined steps see it,
         # where the chain is enqueued ahead behind the hashing
@@ -521,8 +519,8 @@ def main() -> None:
             "e2e": e2e,
             "group": None if group_ms is None else {
                 "fused": fused_rec,
-                # Object grouping of one step's keys alone (K4h partition + K5h LDS hash
-                # min), HIP events on the stream it runs on, after the timed region: `ms` per
+                # Object grouping of one step's keys alone (region partition + LDS hash
+                # min; DESIGN.md 2.2), HIP events on the stream it runs on, after the timed region: `ms` per
                 # call over 10 back-to-back calls, `ms_each_synced` one call at a time
                 "ms": group_ms, "ms_each_synced": group_ms_sync, "keys": F,
                 "algorithmic_bytes_per_key": group_bytes_per_key(F),
