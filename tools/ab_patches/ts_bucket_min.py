@@ -17,15 +17,15 @@ rep("""  const uint32_t b = bucket;
   // the chain's bucket totals""", """  const uint32_t b = bucket;
   TS(0);
   // the chain's bucket totals""")
-rep("""  if (s == e) return;  // uniform for the whole workgroup""", """  if (threadIdx.x == 0 && s == 0xFFFFFFFFFFFFull) sd_bucket_ts[0] = e;
+rep("""  if (s == e && !whole) return;  // uniform for the whole workgroup""", """  if (threadIdx.x == 0 && s == 0xFFFFFFFFFFFFull) sd_bucket_ts[0] = e;
   TS(1);
-  if (s == e) return;  // uniform for the whole workgroup""")
+  if (s == e && !whole) return;  // uniform for the whole workgroup""")
 rep("""    __syncthreads();  // table initialised (first trip) / the previous trip's flag visible
 """, """    __syncthreads();  // table initialised (first trip) / the previous trip's flag visible
     if (trip == 0) TS(2);
 """)
-rep("""  const bool overflow = ovf[0] | ovf[1];""", """  TS(3);
-  const bool overflow = ovf[0] | ovf[1];""")
+rep("""  const bool overflow = whole || (ovf[0] | ovf[1]);""", """  TS(3);
+  const bool overflow = whole || (ovf[0] | ovf[1]);""")
 rep("""    if (threadIdx.x == 0) atomicAdd(objects, (unsigned long long)distinct);
     return;""", """    TS(4);
     if (threadIdx.x == 0) atomicAdd(objects, (unsigned long long)distinct);

@@ -2,6 +2,10 @@
 # 100 MHz, thread 0 after a full wait): entry, keys loaded, histogram + prefill, reservations +
 # scan, LDS staging, stores drained; read back with sd_dbg_rpart_ts (tools/ts_region_part.py).
 s = open("group_hash.hip").read()
+# only sd_region_partition (the big-batch partition below it repeats some of its lines)
+CUT = 'extern "C" __global__ void __launch_bounds__(RBIG_THREADS)\nsd_region_partition_big('
+s, rest = s.split(CUT, 1)
+rest = CUT + rest
 def rep(a, b):
     global s
     assert s.count(a) == 1, a
@@ -24,9 +28,9 @@ rep("""  // one reservation per non-empty region, then the tile counting-sorted 
 """  RTS(2);
   // one reservation per non-empty region, then the tile counting-sorted by region in LDS so""")
 rep("""  lds_exclusive_scan(tcnt, tstart, REGIONS);  // (its barriers also publish gbase)
-#pragma unroll""", """  lds_exclusive_scan(tcnt, tstart, REGIONS);  // (its barriers also publish gbase)
+""", """  lds_exclusive_scan(tcnt, tstart, REGIONS);  // (its barriers also publish gbase)
   RTS(3);
-#pragma unroll""")
+""")
 rep("""      const uint64_t o = (uint64_t)gbase[b] + (t - tstart[b]);
       if (o < cap) {  // rows past the capacity only counted (the table regroups the region)
         rkeys[(uint64_t)b * cap + o] = kk;
@@ -51,6 +55,7 @@ rep("""      sfile[slot] = (uint32_t)(b0 + t);
   }
   __syncthreads();
   RTS(4);""")
+s += rest
 s += """
 extern "C" int sd_dbg_rpart_ts(void* host, size_t bytes) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(sdcas::sd_rpart_ts), bytes, 0, hipMemcpyDeviceToHost);
