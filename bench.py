@@ -207,9 +207,13 @@ def main() -> None:
                 eng.group(keys[b], rep, want_objects=False)  # K4h + K5h, async
             else:
                 r = sharded_group(keys[b], file0, ops, capacity=capacity)
-                results[:] = [r]
                 if r.overflow is not None:
-                    overflows.append(r.overflow)
+                    # an overflowed fixed-capacity part is redone with the exact exchange
+                    # inside the step (collective, on this worker thread; the flag read is
+                    # the worker's only host sync), so every timed step's rep is exact
+                    overflows.append(int(r.overflow.item()))
+                    r.resolve()
+                results[:] = [r]
             grouped[b].record(side)
 
     def launch_group(i: int):
@@ -282,6 +286,7 @@ def main() -> None:
         # every timed step's regions must have held their keys (else the step's rep would
         # need the standalone regroup); the last step's rep == the standalone grouping's
         timed_overflow = int(ovf.item())
+        ovf.zero_()
         last_rep = reps[(args.steps - 1) % NBUF]
         rep_parity = bool(torch.equal(last_rep, rep))
         # the bucket tables alone, serially after K1G (inside the steps they share the CUs
@@ -295,9 +300,14 @@ def main() -> None:
             b_.record(main)
             b_.synchronize()
             tabs.append(a_.elapsed_time(b_))
+        ovf.zero_()
         fobj = eng.hash_group_sampled(content, sizes, last_keys, last_rep, ovf)
+        fobj_rep_parity = bool(torch.equal(last_rep, rep))
         fused_rec = {"tables_ms": float(np.median(tabs)), "tables_ms_all": tabs,
-                     "objects": fobj, "parity_vs_standalone": rep_parity and fobj == objects,
+                     "objects": fobj,
+                     "parity_vs_standalone": rep_parity and fobj_rep_parity and fobj == objects,
+                     # an overflowed region is regrouped by its table workgroup inside the step
+                     # (exact, on the device): the flag counts the slower path, never a wrong rep
                      "timed_steps_overflowed": timed_overflow,
                      "region_capacity": eng_region_capacity(F),
                      "note": "K1G (sd_cas_sampled_group_kernel: K1 + the coarse-bucket partition "
@@ -307,7 +317,7 @@ def main() -> None:
     if sharded:
         # every timed step's fixed-capacity exchange must have fit (else it would have been
         # redone exactly outside the timed region, and the step time would not stand)
-        n_overflow = sum(int(f.item()) for f in overflows)
+        n_overflow = sum(overflows)
         objects = res.objects
     # the grouping alone (after the timed region: inside the steps it overlaps the next K1
     # on a side stream and shares the CUs with it, so its own speed is measured serially)
@@ -430,9 +440,15 @@ def main() -> None:
             if per_file is not None:
                 traffic = per_file * F
 
+    # the host-CPU baseline beside the line at EVERY world size (the reference path cas.rs:23-62
+    # on the host cores): rank 0 runs it after the timed region, the other ranks wait for it
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(content, sizes, last_keys, args.cpu_seconds)
+        if world > 1:
+            cpu["ranks_idle_meanwhile"] = world - 1
+    if world > 1:
+        dist.barrier()
 
     n_gpus = dist.get_world_size() if sharded else 1
     if rank == 0:
@@ -517,7 +533,14 @@ def main() -> None:
             },
             "sustained": sustained,
             "e2e": e2e,
-            "group": None if group_ms is None else {
+            "group": ({
+                # the N > 1 grouping: partition + fixed-capacity RCCL all-to-all + grouping of
+                # the received keys + mirror all-to-all, one step alone after the timed region
+                "mode": "exchange", "ms": exchange_ms, "keys_per_rank": F, "keys": world * F,
+                "keys_per_s": world * F / (exchange_ms / 1e3), "phases_ms": exchange_phases,
+                "objects": objects, "timed_steps_overflowed": n_overflow,
+                "note": "max over ranks; inside the steps it overlaps the next K1 on a side stream"}
+                if sharded else None) if group_ms is None else {
                 "fused": fused_rec,
                 # Object grouping of one step's keys alone (region partition + LDS hash
                 # min), HIP events on the stream it runs on, after the timed region: `ms` per
@@ -547,16 +570,38 @@ def fail(msg: str) -> None:
     sys.exit(2)
 
 
+def visible_gpus(topology: str = "/sys/class/kfd/kfd/topology/nodes") -> int:
+    """GPUs this process would see, counted WITHOUT touching HIP: the KFD topology's GPU
+    nodes (a non-zero gfx_target_version; CPU nodes have 0), narrowed by
+    ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES as the runtime would.
+    No KFD topology = no ROCm GPU."""
+    import glob
+    gpus = 0
+    for p in glob.glob(os.path.join(topology, "*", "properties")):
+        try:
+            with open(p) as fh:
+                for line in fh:
+                    k, _, v = line.partition(" ")
+                    if k == "gfx_target_version" and int(v) != 0:
+                        gpus += 1
+        except (OSError, ValueError):
+            continue
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            gpus = min(gpus, len([x for x in v.split(",") if x.strip()]))
+    return gpus
+
+
 def spawn_ranks(n: int, rehearsal: bool) -> int:
     """Run this bench as n ranks (one process per GPU) under torch.distributed.run, the way
-    the driver launches it, and return the launcher's exit status.  The parent makes no GPU
-    call and does not exec: it counts devices (no HIP initialisation on this image),
-    starts the launcher as a child, lets rank 0's one JSON line through to its own stdout
-    and exits with the child's code."""
+    the driver launches it, and return the launcher's exit status.  The parent never
+    initialises the GPU (it counts devices from the KFD topology in sysfs, visible_gpus) and
+    does not exec: it starts the launcher as a child, lets rank 0's one JSON line through to
+    its own stdout and exits with the child's code."""
     import socket
     import subprocess
-    import torch
-    have = torch.cuda.device_count()
+    have = visible_gpus()
     if have < n and not rehearsal:
         print(f"bench: --gpus {n} needs {n} visible GPUs, found {have} "
               "(SD_BENCH_ONE_DEVICE=1 rehearses the N > 1 path on one GPU)",

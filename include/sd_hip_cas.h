@@ -131,6 +131,12 @@ int sd_cas_generate_cas_ids(sd_cas_ctx* ctx, const uint8_t* const* bufs, const u
 int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* ctx, const char* const* paths,
                                        const uint64_t* sizes, size_t n, uint64_t* out_keys,
                                        int32_t* status);
+/* FileMetadata::new over a batch with the metadata taken by the library (sizes == NULL
+ * above) and returned: out_sizes[i] = the fs::metadata().len() the row was decided from
+ * (FileMetadata's fs_metadata, mod.rs:48-53,63), 0 for a row whose metadata failed — one stat
+ * per path, so the caller's record can never disagree with the status it got. */
+int sd_cas_file_metadata_from_paths(sd_cas_ctx* ctx, const char* const* paths, size_t n,
+                                    uint64_t* out_keys, int32_t* status, uint64_t* out_sizes);
 
 /* End-to-end sampled path from host memory (BASELINE config 3 "pre-staged in pinned host
  * memory"): n contents of 57,344 B at h_content + i*stride (pin it with
@@ -206,9 +212,9 @@ int sd_cas_group_dev(sd_cas_ctx* ctx, const uint64_t* d_keys, size_t n, uint32_t
  * row goes to a fixed-capacity region of its coarse bucket — so the grouping after it is one
  * bucket-table launch (no key read-back, totals, prefill or scatter pass).  Async unless
  * out_objects != NULL.  d_overflow (u32, device; zero it first) is set when a region filled
- * (more than mean + 8 sigma + 64 keys in one coarse bucket: heavily duplicated content) —
- * d_rep is then not complete and the caller regroups with sd_cas_group_dev(d_keys); with
- * out_objects != NULL the call blocks and does that itself.  Batches the fused chain does not
+ * (more than mean + 8 sigma + 64 keys in one coarse bucket: heavily duplicated content); the
+ * grouping stays exact — that region's table workgroup regroups it from the whole d_keys
+ * array on the device — so the flag only reports the slower path.  Batches the fused chain does not
  * take (n not a multiple of sd_cas_batch_quantum, n > 1,441,792, or a non-AUTO/HASH group
  * method) run the two calls in sequence, d_overflow untouched.  The Object count of an async
  * call: sd_cas_copy_objects_dev. */
@@ -220,10 +226,12 @@ int sd_cas_hash_group_sampled_dev(sd_cas_ctx* ctx, const void* d_content, uint64
  * the partition into one of the context's two region sets (n a multiple of the quantum, <=
  * 1,441,792, default group method: else SD_CAS_EINVAL), async; group_regions = the bucket
  * tables over the regions of the LAST hash_regions batch (same n and d_rep: hash_regions
- * prefilled it), on any stream ordered after it (an event), async unless out_objects != NULL;
- * a batch that is hashed but never grouped is simply dropped by the next hash_regions.  The sets alternate, so batch i's
+ * prefilled it), on any stream (the library orders it after that batch's K1), async unless
+ * out_objects != NULL; d_keys of that batch must stay unchanged until its tables completed
+ * (an overflowed region is regrouped from them).  A batch that is hashed but never grouped is
+ * simply dropped by the next hash_regions into its set.  The sets alternate, so batch i's
  * tables may run on a side stream while batch i+1 hashes; a set is refilled only after its
- * previous tables finished (the library orders that itself).  d_overflow as above. */
+ * previous K1 and tables finished (the library orders that itself).  d_overflow as above. */
 int sd_cas_hash_regions_sampled_dev(sd_cas_ctx* ctx, const void* d_content, uint64_t stride,
                                     const uint64_t* d_sizes, size_t n, uint64_t* d_keys,
                                     uint32_t* d_rep, uint32_t* d_overflow, void* stream);
@@ -293,7 +301,8 @@ int sd_cas_group_chunked_dev(sd_cas_ctx* ctx, const uint32_t* d_rep, size_t n, u
                              uint64_t* out_linked, void* stream);
 /* ---- Object-link emission of a file-identifier job ------------------
  * The decisions of file_identifier_job.rs:180-236 (the step loop) and identifier_job_step
- * (mod.rs:98-350) over n orphan file_path rows in ascending id order on a fresh library,
+ * (mod.rs:98-350) over n orphan file_path rows in ascending id order on a fresh library
+ * (a library that already holds Objects: sd_cas_identifier_links_seeded below),
  * `chunk` rows per step (CHUNK_SIZE = 100, mod.rs:34), with the reference's cursor: step k
  * queries the orphan rows with `id >= cursor` (file_identifier_job.rs:268, 307-315) and
  * the next cursor is the chunk's LAST row (mod.rs:401-405), so a last row that stays
@@ -326,6 +335,7 @@ int sd_cas_group_chunked_dev(sd_cas_ctx* ctx, const uint32_t* d_rep, size_t n, u
 #define SD_CAS_LINK_LINKED 1
 #define SD_CAS_LINK_DROPPED 2
 #define SD_CAS_LINK_NOT_REACHED 3
+#define SD_CAS_LINK_EXISTING 4
 #define SD_CAS_NO_STEP 0xFFFFFFFFu
 #define SD_CAS_NO_OBJECT 0xFFFFFFFFu
 size_t sd_cas_identifier_max_steps(size_t n, uint32_t chunk);
@@ -340,6 +350,27 @@ int sd_cas_identifier_links(sd_cas_ctx* ctx, const uint64_t* h_keys, const uint8
                             size_t n, uint32_t chunk, uint32_t* h_step, uint32_t* h_object,
                             uint8_t* h_action, uint64_t* h_step_counts, size_t max_steps,
                             uint64_t* out_steps);
+/* The same job on a library that already holds Objects (an incremental job, or a second
+ * location of the same library): every step's find_many (mod.rs:180-198) returns the
+ * Objects already connected to ANY file_path with one of the step's cas_ids — there is no
+ * location filter — so a row whose key such an Object carries links to it (mod.rs:202-238,
+ * find() = the first Object in id order) and its key never creates (mod.rs:246-253).
+ * seed_keys[j] / seed_objects[j] (n_seed pairs, any order, repeats allowed) = (cas key, id)
+ * of each Object that exists before the job and is connected to a file_path with that
+ * cas_id, as the DB returns them; ids < 2^31, ascending in the DB's row order.  Such a row
+ * gets action SD_CAS_LINK_EXISTING, object = the SMALLEST id seeded for its key, and counts
+ * as linked in its step.  n_seed = 0 is the fresh-library call above; seeded calls need
+ * n < 2^31. */
+int sd_cas_identifier_links_seeded_dev(sd_cas_ctx* ctx, const uint64_t* d_keys, const uint8_t* d_state,
+                                       size_t n, uint32_t chunk, const uint64_t* d_seed_keys,
+                                       const uint32_t* d_seed_objects, size_t n_seed, uint32_t* d_step,
+                                       uint32_t* d_object, uint8_t* d_action, uint64_t* h_step_counts,
+                                       size_t max_steps, uint64_t* out_steps, void* stream);
+int sd_cas_identifier_links_seeded(sd_cas_ctx* ctx, const uint64_t* h_keys, const uint8_t* h_state,
+                                   size_t n, uint32_t chunk, const uint64_t* h_seed_keys,
+                                   const uint32_t* h_seed_objects, size_t n_seed, uint32_t* h_step,
+                                   uint32_t* h_object, uint8_t* h_action, uint64_t* h_step_counts,
+                                   size_t max_steps, uint64_t* out_steps);
 
 /* Stable LSD radix sort of (u64 key, u32 val) on bits [begin_bit, end_bit).
  * d_vals_in == NULL sorts the identity 0..n-1. */

@@ -32,6 +32,7 @@ pub const SD_CAS_LINK_CREATED: u8 = 0;
 pub const SD_CAS_LINK_LINKED: u8 = 1;
 pub const SD_CAS_LINK_DROPPED: u8 = 2;
 pub const SD_CAS_LINK_NOT_REACHED: u8 = 3;
+pub const SD_CAS_LINK_EXISTING: u8 = 4;
 pub const SD_CAS_NO_OBJECT: u32 = 0xFFFF_FFFF;
 pub const SD_CAS_NO_STEP: u32 = 0xFFFF_FFFF;
 pub const SD_CAS_CHUNK_SIZE: u32 = 100;
@@ -56,6 +57,9 @@ extern "C" {
     pub fn sd_cas_generate_cas_ids_from_paths(ctx: *mut sd_cas_ctx, paths: *const *const c_char,
                                               sizes: *const u64, n: usize, out_keys: *mut u64,
                                               status: *mut i32) -> c_int;
+    pub fn sd_cas_file_metadata_from_paths(ctx: *mut sd_cas_ctx, paths: *const *const c_char, n: usize,
+                                           out_keys: *mut u64, status: *mut i32,
+                                           out_sizes: *mut u64) -> c_int;
     pub fn sd_cas_hash_sampled_host(ctx: *mut sd_cas_ctx, h_content: *const c_void, stride: u64,
                                     h_sizes: *const u64, n: usize, h_keys: *mut u64,
                                     batch_files: usize) -> c_int;
@@ -128,6 +132,18 @@ extern "C" {
                                    n: usize, chunk: u32, h_step: *mut u32, h_object: *mut u32,
                                    h_action: *mut u8, h_step_counts: *mut u64, max_steps: usize,
                                    out_steps: *mut u64) -> c_int;
+    pub fn sd_cas_identifier_links_seeded_dev(ctx: *mut sd_cas_ctx, d_keys: *const u64, d_state: *const u8,
+                                              n: usize, chunk: u32, d_seed_keys: *const u64,
+                                              d_seed_objects: *const u32, n_seed: usize,
+                                              d_step: *mut u32, d_object: *mut u32, d_action: *mut u8,
+                                              h_step_counts: *mut u64, max_steps: usize,
+                                              out_steps: *mut u64, stream: *mut c_void) -> c_int;
+    pub fn sd_cas_identifier_links_seeded(ctx: *mut sd_cas_ctx, h_keys: *const u64, h_state: *const u8,
+                                          n: usize, chunk: u32, h_seed_keys: *const u64,
+                                          h_seed_objects: *const u32, n_seed: usize, h_step: *mut u32,
+                                          h_object: *mut u32, h_action: *mut u8,
+                                          h_step_counts: *mut u64, max_steps: usize,
+                                          out_steps: *mut u64) -> c_int;
     pub fn sd_cas_sort_pairs_dev(ctx: *mut sd_cas_ctx, d_keys_in: *const u64, d_vals_in: *const u32,
                                  n: usize, d_keys_out: *mut u64, d_vals_out: *mut u32, begin_bit: c_int,
                                  end_bit: c_int, stream: *mut c_void) -> c_int;
@@ -211,13 +227,25 @@ pub enum RowState {
 }
 
 /// One job step's DB batches (mod.rs:157-347): `creates` feed `create_many` + the link
-/// updates of the new Objects, `links` connect rows to the Object created for `.1`.
+/// updates of the new Objects, `links` connect rows to the Object created for `.1`,
+/// `links_existing` connect rows to an Object that existed before the job (`.1` = its id as
+/// given in `ExistingObject`, mod.rs:202-238).
 #[derive(Clone, Debug, Default, PartialEq, Eq)]
 pub struct StepBatch {
     pub creates: Vec<usize>,
     pub links: Vec<(usize, usize)>,
+    pub links_existing: Vec<(usize, u32)>,
     pub total_created: u64,
     pub total_linked: u64,
+}
+
+/// An Object the library holds before the job, as the step's `find_many` would return it
+/// (mod.rs:180-198): one pair per (Object, cas_id of one of its file_paths).  `id` < 2^31,
+/// ascending in the DB's row order (`find()` picks the smallest, mod.rs:214-224).
+#[derive(Clone, Copy, Debug, PartialEq, Eq)]
+pub struct ExistingObject {
+    pub cas_id: CasId,
+    pub id: u32,
 }
 
 /// One context per (job thread, device).  Not Sync; Send is fine.
@@ -304,10 +332,49 @@ impl HipCas {
             .collect())
     }
 
+    /// `FileMetadata::new` over a batch with the metadata taken by the library: per path the
+    /// cas_id result and the `fs::metadata().len()` it was decided from (one stat per path).
+    pub fn file_metadata(&mut self, paths: &[&Path])
+        -> io::Result<Vec<(Result<Option<CasId>, io::Error>, u64)>> {
+        let cpaths: Vec<CString> = paths
+            .iter()
+            .map(|p| CString::new(p.as_os_str().as_encoded_bytes()).expect("NUL in path"))
+            .collect();
+        let ptrs: Vec<*const c_char> = cpaths.iter().map(|c| c.as_ptr()).collect();
+        let n = paths.len();
+        let (mut keys, mut status, mut sizes) = (vec![0u64; n], vec![0i32; n], vec![0u64; n]);
+        let rc = unsafe {
+            sd_cas_file_metadata_from_paths(self.ctx, ptrs.as_ptr(), n, keys.as_mut_ptr(),
+                                            status.as_mut_ptr(), sizes.as_mut_ptr())
+        };
+        if rc != 0 {
+            return Err(self.err(rc));
+        }
+        Ok((0..n)
+            .map(|i| {
+                let r = match status[i] {
+                    0 => Ok(Some(CasId(keys[i]))),
+                    SD_CAS_STATUS_NO_CAS => Ok(None),
+                    e => Err(io::Error::from_raw_os_error(-e)),
+                };
+                (r, sizes[i])
+            })
+            .collect())
+    }
+
     /// The Object decisions of a whole file-identifier job over `rows` (orphan file_paths in
     /// ascending id order, fresh library), `chunk` rows per step with the reference's cursor:
     /// the batches each step hands to the DB (file_identifier_job.rs:180-236, mod.rs:157-347).
     pub fn identifier_links(&mut self, rows: &[RowState], chunk: u32) -> io::Result<Vec<StepBatch>> {
+        self.identifier_links_existing(rows, chunk, &[])
+    }
+
+    /// The same job on a library that already holds Objects (`existing`: every Object
+    /// connected to a file_path with some cas_id, from the DB): a row whose cas_id one of them
+    /// carries links to the smallest such id in `links_existing` and its key never creates
+    /// (mod.rs:180-253; the query has no location filter).
+    pub fn identifier_links_existing(&mut self, rows: &[RowState], chunk: u32,
+                                     existing: &[ExistingObject]) -> io::Result<Vec<StepBatch>> {
         let n = rows.len();
         let keys: Vec<u64> = rows.iter().map(|r| if let RowState::Hashed(k) = r { k.0 } else { 0 }).collect();
         let state: Vec<u8> = rows
@@ -322,10 +389,13 @@ impl HipCas {
         let (mut step, mut object, mut action) = (vec![0u32; n], vec![0u32; n], vec![0u8; n]);
         let mut counts = vec![0u64; 2 * max_steps.max(1)];
         let mut steps = 0u64;
+        let seed_keys: Vec<u64> = existing.iter().map(|e| e.cas_id.0).collect();
+        let seed_ids: Vec<u32> = existing.iter().map(|e| e.id).collect();
         let rc = unsafe {
-            sd_cas_identifier_links(self.ctx, keys.as_ptr(), state.as_ptr(), n, chunk, step.as_mut_ptr(),
-                                    object.as_mut_ptr(), action.as_mut_ptr(), counts.as_mut_ptr(),
-                                    max_steps, &mut steps)
+            sd_cas_identifier_links_seeded(self.ctx, keys.as_ptr(), state.as_ptr(), n, chunk,
+                                           seed_keys.as_ptr(), seed_ids.as_ptr(), existing.len(),
+                                           step.as_mut_ptr(), object.as_mut_ptr(), action.as_mut_ptr(),
+                                           counts.as_mut_ptr(), max_steps, &mut steps)
         };
         if rc != 0 {
             return Err(self.err(rc));
@@ -337,6 +407,7 @@ impl HipCas {
             match action[i] {
                 SD_CAS_LINK_CREATED => out[step[i] as usize].creates.push(i),
                 SD_CAS_LINK_LINKED => out[step[i] as usize].links.push((i, object[i] as usize)),
+                SD_CAS_LINK_EXISTING => out[step[i] as usize].links_existing.push((i, object[i])),
                 _ => {}
             }
         }

@@ -36,6 +36,7 @@ SIGNATURES = [
     ("sd_cas_free_pinned", _i, [_vp, _vp]),
     ("sd_cas_generate_cas_ids", _i, [_vp, _vp, _vp, _vp, _sz, _vp]),
     ("sd_cas_generate_cas_ids_from_paths", _i, [_vp, _vp, _vp, _sz, _vp, _vp]),
+    ("sd_cas_file_metadata_from_paths", _i, [_vp, _vp, _sz, _vp, _vp, _vp]),
     ("sd_cas_hash_sampled_host", _i, [_vp, _vp, _u64, _vp, _sz, _vp, _sz]),
     ("sd_cas_hash_sampled_host_ring", _i, [_vp, _vp, _u64, _sz, _vp, _sz, _vp, _sz]),
     ("sd_cas_key_to_hex", None, [_u64, _cp]),
@@ -64,6 +65,10 @@ SIGNATURES = [
     ("sd_cas_identifier_max_steps", _sz, [_sz, _u32]),
     ("sd_cas_identifier_links_dev", _i, [_vp, _vp, _vp, _sz, _u32, _vp, _vp, _vp, _vp, _sz, _vp, _vp]),
     ("sd_cas_identifier_links", _i, [_vp, _vp, _vp, _sz, _u32, _vp, _vp, _vp, _vp, _sz, _vp]),
+    ("sd_cas_identifier_links_seeded_dev", _i,
+     [_vp, _vp, _vp, _sz, _u32, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _sz, _vp, _vp]),
+    ("sd_cas_identifier_links_seeded", _i,
+     [_vp, _vp, _vp, _sz, _u32, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _sz, _vp]),
     ("sd_cas_sort_pairs_dev", _i, [_vp, _vp, _vp, _sz, _vp, _vp, _i, _i, _vp]),
     ("sd_cas_checksum_dev", _i, [_vp, _vp, _u64, _vp, _vp]),
     ("sd_cas_file_checksum", _i, [_vp, _cp, _cp, ctypes.POINTER(_i)]),

@@ -172,6 +172,22 @@ class CasEngine:
             self._check(rc, "generate_cas_ids_from_paths")
         return keys, status
 
+    def file_metadata_from_paths(self, paths: Sequence[str]):
+        """FileMetadata::new over a batch (mod.rs:55-95), metadata taken by the library:
+        (keys, status, sizes) — sizes = the fs::metadata length each row was decided from
+        (sd_cas_file_metadata_from_paths: one stat per path)."""
+        n = len(paths)
+        enc = [os.fsencode(p) for p in paths]
+        parr = (ctypes.c_char_p * n)(*enc)
+        keys = np.zeros(n, dtype=np.uint64)
+        status = np.zeros(n, dtype=np.int32)
+        sizes = np.zeros(n, dtype=np.uint64)
+        if n:
+            self._check(self.L.sd_cas_file_metadata_from_paths(
+                self.h, ctypes.cast(parr, ctypes.c_void_p), n, _np_ptr(keys), _np_ptr(status),
+                _np_ptr(sizes)), "file_metadata_from_paths")
+        return keys, status, sizes
+
     def alloc_pinned(self, nbytes: int) -> np.ndarray:
         """Page-locked host buffer (uint8 numpy view); free with free_pinned."""
         p = ctypes.c_void_p()
@@ -259,7 +275,8 @@ class CasEngine:
         """K1 with the grouping partition fused into its epilogue + one bucket-table launch
         (sd_cas_hash_group_sampled_dev): keys as hash_sampled, rep as group.  overflow: int32
         [1] device tensor, zeroed by the caller — set if a coarse bucket outgrew its region
-        (then regroup with group(keys, rep)); want_objects blocks and regroups itself."""
+        (the result is exact either way: that region is regrouped on the device from the
+        whole key array); want_objects blocks and returns the Object count."""
         n = int(sizes.numel())
         stride = int(content.shape[-1]) if content.dim() == 2 else SAMPLED_CONTENT_LEN
         obj = ctypes.c_uint64(0)
@@ -335,11 +352,15 @@ class CasEngine:
         return int(c.value), int(ln.value)
 
     def identifier_links(self, keys, state=None, chunk: int = CHUNK_SIZE,
-                         stream: Optional[int] = None):
+                         stream: Optional[int] = None, existing=None):
         """Object-link emission of one file-identifier job over the rows (ascending
-        file_path.id) — sd_cas_identifier_links_dev: returns (step, object, action) device
-        tensors (int32, int32, uint8) and the per-step (created, linked) counts as an
-        int64 numpy array [steps, 2].  state: uint8 ROW_* per row (None = all hashed)."""
+        file_path.id) — sd_cas_identifier_links[_seeded]_dev: returns (step, object, action)
+        device tensors (int32, int32, uint8) and the per-step (created, linked) counts as an
+        int64 numpy array [steps, 2].  state: uint8 ROW_* per row (None = all hashed).
+        existing: None (a fresh library) or (seed_keys int64, seed_objects int32) device
+        tensors — the Objects the library holds before the job, as (cas key, Object id)
+        pairs (mod.rs:180-198); a row whose key one carries links to the smallest such id
+        (action LINK_EXISTING)."""
         import torch
         n = int(keys.numel())
         dev = keys.device
@@ -349,17 +370,21 @@ class CasEngine:
         ms = int(self.L.sd_cas_identifier_max_steps(n, int(chunk)))
         counts = np.zeros(2 * max(ms, 1), dtype=np.uint64)
         steps = ctypes.c_uint64(0)
-        self._check(self.L.sd_cas_identifier_links_dev(
+        sk, so = existing if existing is not None else (None, None)
+        ns = 0 if sk is None else int(sk.numel())
+        self._check(self.L.sd_cas_identifier_links_seeded_dev(
             self.h, _ptr(keys), _ptr(state) if state is not None else None, n, int(chunk),
+            _ptr(sk) if ns else None, _ptr(so) if ns else None, ns,
             _ptr(step), _ptr(obj), _ptr(act), _np_ptr(counts), ms, ctypes.byref(steps),
             _stream(stream)), "identifier_links")
         k = int(steps.value)
         return step, obj, act, counts[:2 * k].reshape(k, 2).astype(np.int64)
 
     def identifier_links_host(self, keys: np.ndarray, state: Optional[np.ndarray] = None,
-                              chunk: int = CHUNK_SIZE):
-        """sd_cas_identifier_links (host arrays): (step u32, object u32, action u8, counts
-        int64 [steps, 2]) — the DB layer's view of the same emission."""
+                              chunk: int = CHUNK_SIZE, existing=None):
+        """sd_cas_identifier_links[_seeded] (host arrays): (step u32, object u32, action u8,
+        counts int64 [steps, 2]) — the DB layer's view of the same emission.  existing: None
+        or (seed_keys, seed_objects) numpy arrays (see identifier_links)."""
         n = len(keys)
         k = np.ascontiguousarray(keys, dtype=np.uint64)
         st = None if state is None else np.ascontiguousarray(state, dtype=np.uint8)
@@ -369,8 +394,17 @@ class CasEngine:
         ms = int(self.L.sd_cas_identifier_max_steps(n, int(chunk)))
         counts = np.zeros(2 * max(ms, 1), dtype=np.uint64)
         steps = ctypes.c_uint64(0)
-        self._check(self.L.sd_cas_identifier_links(
+        if existing is not None:
+            sk = np.ascontiguousarray(existing[0], dtype=np.uint64)
+            so = np.ascontiguousarray(existing[1], dtype=np.uint32)
+            if len(sk) != len(so):
+                raise ValueError("existing: as many Object ids as cas keys")
+        else:
+            sk = so = np.zeros(0, dtype=np.uint64)
+        ns = len(sk)
+        self._check(self.L.sd_cas_identifier_links_seeded(
             self.h, _np_ptr(k), _np_ptr(st) if st is not None else None, n, int(chunk),
+            _np_ptr(sk) if ns else None, _np_ptr(so) if ns else None, ns,
             _np_ptr(step), _np_ptr(obj), _np_ptr(act), _np_ptr(counts), ms, ctypes.byref(steps)),
             "identifier_links")
         s = int(steps.value)
@@ -489,7 +523,7 @@ class FileMetadata:
 
 ROW_HASHED, ROW_NO_CAS, ROW_ERROR = 0, 1, 2                          # SD_CAS_ROW_*
 STATUS_NO_CAS = 1                                                    # SD_CAS_STATUS_NO_CAS
-LINK_CREATED, LINK_LINKED, LINK_DROPPED, LINK_NOT_REACHED = 0, 1, 2, 3  # SD_CAS_LINK_*
+LINK_CREATED, LINK_LINKED, LINK_DROPPED, LINK_NOT_REACHED, LINK_EXISTING = 0, 1, 2, 3, 4  # SD_CAS_LINK_*
 
 
 @dataclass
@@ -498,6 +532,7 @@ class StepBatch:
     step: int
     creates: list = field(default_factory=list)   # rows getting a new Object (create_many)
     links: list = field(default_factory=list)     # (row, row owning the existing Object)
+    links_existing: list = field(default_factory=list)  # (row, id of an Object older than the job)
     total_created: int = 0                        # mod.rs:349 (total_created, total_linked)
     total_linked: int = 0
 
@@ -508,6 +543,7 @@ class StepResult:
     mod.rs:98-350) decides for its orphan file_paths."""
     metadata: dict = field(default_factory=dict)   # idx -> FileMetadata (errors dropped)
     object_of: dict = field(default_factory=dict)  # idx -> idx of the file owning its Object
+    existing_of: dict = field(default_factory=dict)  # idx -> id of the pre-job Object it links to
     total_created: int = 0
     total_linked: int = 0
     errors: dict = field(default_factory=dict)     # idx -> errno (logged + dropped, :125-141)
@@ -516,30 +552,26 @@ class StepResult:
 
 
 def identifier_job_step(paths: Sequence[str], chunk: int = CHUNK_SIZE,
-                        eng: Optional[CasEngine] = None) -> StepResult:
+                        eng: Optional[CasEngine] = None, existing=None) -> StepResult:
     """Run the file identifier over ``paths`` (ascending file_path.id order: the rows the
     job's orphan query returns — object/cas NULL and indexed size != 0, orphan_path_filters,
-    file_identifier_job.rs:251-277) on a fresh library, as file_identifier_job.rs:180-236 /
-    mod.rs:98-350 would: fs::metadata
-    per row (mod.rs:63), cas_ids from the GPU (len 0 -> no cas_id, mod.rs:78-86; an I/O
-    error drops the row, :125-141), and the Object decisions of every step from the GPU
-    link emission (sd_cas_identifier_links: grouping + the cursor walk, a last row that
-    stays orphan is queried again by the next step).  Returns the per-file decisions, the
-    per-step batches and the summed (created, linked)."""
+    file_identifier_job.rs:251-277) as file_identifier_job.rs:180-236 / mod.rs:98-350 would:
+    fs::metadata per row (mod.rs:63), cas_ids from the GPU (len 0 -> no cas_id, mod.rs:78-86;
+    an I/O error drops the row, :125-141), and the Object decisions of every step from the
+    GPU link emission (sd_cas_identifier_links: grouping + the cursor walk, a last row that
+    stays orphan is queried again by the next step).  existing: None for a fresh library,
+    else (cas_ids or keys, Object ids) of the Objects the library already holds
+    (mod.rs:180-238: a row whose cas_id one carries links to the lowest such id).  Returns
+    the per-file decisions, the per-step batches and the summed (created, linked)."""
     eng = eng or engine()
     res = StepResult()
     n = len(paths)
     if n == 0:
         return res
     # FileMetadata::new per row, behind the ABI: fs::metadata (mod.rs:63), a directory or an
-    # error drops the row, length 0 -> no cas_id (mod.rs:78-86), else generate_cas_id
-    all_keys, status = eng.generate_cas_keys_from_paths(paths, None)
-    sizes = []
-    for p in paths:
-        try:
-            sizes.append(os.stat(p).st_size)  # FileMetadata.size, for the record
-        except OSError:
-            sizes.append(-1)
+    # error drops the row, length 0 -> no cas_id (mod.rs:78-86), else generate_cas_id; the
+    # metadata length each row was decided from comes back with it (one stat per path)
+    all_keys, status, sizes = eng.file_metadata_from_paths(paths)
     state = np.full(n, ROW_HASHED, dtype=np.uint8)
     for i in range(n):
         if status[i] == STATUS_NO_CAS:
@@ -547,7 +579,12 @@ def identifier_job_step(paths: Sequence[str], chunk: int = CHUNK_SIZE,
         elif status[i] < 0:
             res.errors[i] = int(-status[i])
             state[i] = ROW_ERROR
-    step, obj, act, counts = eng.identifier_links_host(all_keys, state, chunk)
+    seed = None
+    if existing is not None:
+        ek, eo = existing
+        ek = np.array([cas_id_to_key(x) if isinstance(x, str) else int(x) for x in ek], dtype=np.uint64)
+        seed = (ek, np.asarray(eo, dtype=np.uint32))
+    step, obj, act, counts = eng.identifier_links_host(all_keys, state, chunk, existing=seed)
     res.steps = [StepBatch(k, total_created=int(c), total_linked=int(ln))
                  for k, (c, ln) in enumerate(counts)]
     for i in range(n):
@@ -558,9 +595,13 @@ def identifier_job_step(paths: Sequence[str], chunk: int = CHUNK_SIZE,
         if a == LINK_DROPPED:
             continue
         res.metadata[i] = FileMetadata(key_to_cas_id(all_keys[i]) if state[i] == ROW_HASHED else None,
-                                       sizes[i])
-        res.object_of[i] = int(obj[i])
+                                       int(sizes[i]))
         b = res.steps[int(step[i])]
+        if a == LINK_EXISTING:
+            res.existing_of[i] = int(obj[i])
+            b.links_existing.append((i, int(obj[i])))
+            continue
+        res.object_of[i] = int(obj[i])
         if a == LINK_CREATED:
             b.creates.append(i)
         else:

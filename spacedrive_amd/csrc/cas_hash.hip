@@ -200,8 +200,9 @@ sd_cas_sampled_kernel_256(const uint8_t* __restrict__ content, uint64_t stride,
 // in LDS (the CV stack's LDS, dead by then) and reserves each bucket's run with one device
 // atomic.  The chain after K1G is one bucket-table launch.  Regions are sized mean + 8
 // sigma + 64 rows for uniform keys; a bucket that outgrows its region (heavily duplicated
-// content: every copy of a file lands in one bucket) sets *overflow, and the caller
-// regroups with the standalone chain (the fixed-capacity exchange's contract).
+// content: every copy of a file lands in one bucket) keeps counting in its cursor and sets
+// *overflow, and that region's table workgroup regroups it exactly from the whole key array
+// (sd_bucket_min_regions) — only the overflowed regions pay, on the device, no host regroup.
 struct RegionOut {
   uint64_t* rkeys;     // [REGIONS][cap] mixed keys
   uint32_t* rfile;     // [REGIONS][cap] file index
@@ -209,7 +210,9 @@ struct RegionOut {
   uint64_t cap;
   uint32_t* rep;       // rep[f] = f: the bucket tables store only where a key's minimum differs
   uint32_t* overflow;  // set when a region is full
-  unsigned long long* objects;  // zeroed here; the bucket tables add the distinct keys
+  // objects[0]: zeroed here, the bucket tables add the distinct keys; objects[1]: zeroed
+  // here, the tables' carve cursor for the global tables of overflowed regions
+  unsigned long long* objects;
 };
 
 template <int B>
@@ -229,7 +232,7 @@ __device__ __forceinline__ void sampled_group_kernel_body(const uint8_t* __restr
     keys[f] = key;
     ro.rep[f] = (uint32_t)f;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) *ro.objects = 0;
+  if (blockIdx.x == 0 && threadIdx.x < 2) ro.objects[threadIdx.x] = 0;
   // epilogue: the stack columns are dead once every lane has its root
   uint32_t* hist = &stack_lds[0][0][0];  // REGIONS counters, then REGIONS run bases
   uint32_t* base = hist + REGIONS;

@@ -6,6 +6,7 @@
 #include <stdio.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -97,7 +98,10 @@ struct sd_cas_ctx {
   uint32_t* gcursor = nullptr;
   DevBuf regions[2];
   uint64_t region_n[2] = {0, 0};
+  const uint64_t* region_keys[2] = {nullptr, nullptr};  // the batch's keys (an overflowed region's regroup)
   hipEvent_t region_done[2] = {nullptr, nullptr};
+  // recorded after set k's K1G: its tables (any stream) and its refill wait for it
+  hipEvent_t region_hashed[2] = {nullptr, nullptr};
   bool region_pending[2] = {false, false};
   bool region_grouped[2] = {true, true};  // set k's tables have been enqueued since its K1G
   int region_cur = -1;
@@ -126,7 +130,38 @@ struct sd_cas_ctx {
     return n >= (sampled ? seg16_sampled : seg16_packed) ? 16 : 64;
   }
   HostPool pool;  // I/O gather workers
+  // the path gather's two window-slot events (persistent: creating them per call cost a
+  // 100-file job step ~10 us)
+  hipEvent_t gather_done[2] = {nullptr, nullptr};
+  bool trace = false;  // SD_CAS_TRACE=1: per-phase host timestamps of host-buffer calls on stderr
   std::string err;
+};
+
+// Host phase timestamps of one blocking call (SD_CAS_TRACE=1): mark(name) after each phase,
+// one stderr line at the end — "sd_cas_trace <call> n=<files> <phase>=<us> ...".
+struct SdTrace {
+  bool on;
+  const char* call;
+  size_t n;
+  std::chrono::steady_clock::time_point t0, last;
+  std::string line;
+  SdTrace(bool on_, const char* call_, size_t n_) : on(on_), call(call_), n(n_) {
+    if (on) t0 = last = std::chrono::steady_clock::now();
+  }
+  void mark(const char* name) {
+    if (!on) return;
+    const auto t = std::chrono::steady_clock::now();
+    char buf[64];
+    snprintf(buf, sizeof buf, " %s=%.1f", name,
+             std::chrono::duration<double, std::micro>(t - last).count());
+    line += buf;
+    last = t;
+  }
+  ~SdTrace() {
+    if (!on) return;
+    fprintf(stderr, "sd_cas_trace %s n=%zu%s total=%.1f\n", call, n, line.c_str(),
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+  }
 };
 
 inline int sd_fail(sd_cas_ctx* c, int code, const char* fmt, ...) {

@@ -896,7 +896,11 @@ sd_bucket_min_big(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict
 // The fused chain's bucket tables: one workgroup per region (the coarse buckets K1G wrote),
 // straight from the regions — no totals, scatter or refine launch.  2^9 regions: 512 lanes x 7
 // keys over a 6,144-slot table (72 KiB, two workgroups per CU; a region of <= 3,584 keys, every
-// batch up to BIG_MAX_KEYS, is one trip).  2^8 regions: the 1,024-lane big table.
+// batch up to BIG_MAX_KEYS, is one trip).  2^8 regions: the 1,024-lane big table.  A region
+// whose cursor passed its capacity (K1G counted rows it could not store) is regrouped by its
+// workgroup from the whole key array `keys` (K1G's output, unmixed) in a global table carved
+// from the region set's 2 x rows overflow slots by *spill (objects[1], zeroed by K1G): the
+// batch's grouping is exact whatever the key distribution, with no host regroup.
 constexpr uint32_t REG_TABLE = REGION_BITS >= 9 ? 6144 : BIG_TABLE;
 constexpr int REG_THREADS = REGION_BITS >= 9 ? 512 : BIG_THREADS;
 constexpr int REG_ITEMS = REGION_BITS >= 9 ? 7 : ITEMS;
@@ -904,10 +908,10 @@ extern "C" __global__ void __launch_bounds__(REG_THREADS)
 sd_bucket_min_regions(const uint64_t* __restrict__ rkeys, const uint32_t* __restrict__ rfile,
                       uint32_t* __restrict__ cursor, uint64_t cap, uint32_t* __restrict__ out,
                       unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
-                      uint32_t* __restrict__ gvals) {
+                      uint32_t* __restrict__ gvals, const uint64_t* __restrict__ keys, uint64_t n) {
   bucket_min<REG_TABLE, REG_THREADS, REG_ITEMS, true>(blockIdx.x, nullptr, 0, rkeys, rfile, nullptr,
                                                       nullptr, REGIONS, REGION_BITS, 0, out, objects,
-                                                      gkeys, gvals, cursor, cap);
+                                                      gkeys, gvals, cursor, cap, keys, n, objects + 1);
 }
 
 // The standalone chain for small batches (<= BIG_MAX_KEYS keys, default plan): the keys
@@ -1310,9 +1314,10 @@ void region_group_layout(void* ws, uint64_t n, uint64_t** rkeys, uint32_t** rfil
 
 hipError_t region_group_min(const uint64_t* rkeys, const uint32_t* rfile, uint32_t* cursor,
                             uint64_t cap, uint32_t* out, uint64_t* d_objects, uint64_t* gkeys,
-                            uint32_t* gvals, hipStream_t s) {
+                            uint32_t* gvals, const uint64_t* keys, uint64_t n, hipStream_t s) {
   sd_bucket_min_regions<<<REGIONS, REG_THREADS, 0, s>>>(rkeys, rfile, cursor, cap, out,
-                                                        (unsigned long long*)d_objects, gkeys, gvals);
+                                                        (unsigned long long*)d_objects, gkeys, gvals,
+                                                        keys, n);
   return hipGetLastError();
 }
 

@@ -29,7 +29,7 @@ extern "C" __global__ void __launch_bounds__(SPLIT_THREADS)
 sd_links_split(const uint64_t* __restrict__ keys, const uint8_t* __restrict__ state, uint64_t n,
                uint64_t* __restrict__ hkeys, uint32_t* __restrict__ hrows,
                unsigned long long* __restrict__ hcount, uint64_t* __restrict__ orphans,
-               unsigned long long* __restrict__ ocount) {
+               unsigned long long* __restrict__ ocount, uint32_t row_flag) {
   __shared__ uint32_t wh[SPLIT_WAVES], wo[SPLIT_WAVES];
   __shared__ unsigned long long base[2];
   const uint64_t row0 = (uint64_t)blockIdx.x * SPLIT_ROWS;
@@ -40,7 +40,7 @@ sd_links_split(const uint64_t* __restrict__ keys, const uint8_t* __restrict__ st
 #pragma unroll
   for (int j = 0; j < SPLIT_ITEMS; ++j) {
     const uint64_t i = row0 + (uint64_t)j * SPLIT_THREADS + threadIdx.x;
-    st[j] = i < n ? state[i] : (uint8_t)SD_LINKS_HASHED;
+    st[j] = i < n && state ? state[i] : (uint8_t)SD_LINKS_HASHED;
   }
 #pragma unroll
   for (int j = 0; j < SPLIT_ITEMS; ++j) {
@@ -71,7 +71,7 @@ sd_links_split(const uint64_t* __restrict__ keys, const uint8_t* __restrict__ st
     if (hashed) {
       const uint64_t d = h + (uint64_t)__popcll(hm & below);
       hkeys[d] = keys[i];
-      hrows[d] = (uint32_t)i;
+      hrows[d] = (uint32_t)i | row_flag;
     }
     if (orphan) orphans[o + (uint64_t)__popcll(om & below)] = (i << 8) | st[j];
     h += (uint64_t)__popcll(hm);
@@ -81,9 +81,9 @@ sd_links_split(const uint64_t* __restrict__ keys, const uint8_t* __restrict__ st
 
 extern "C" __global__ void __launch_bounds__(256)
 sd_links_scatter(const uint32_t* __restrict__ minrow, const uint32_t* __restrict__ hrows,
-                 uint64_t m, uint32_t* __restrict__ rep) {
+                 uint64_t m, uint32_t* __restrict__ rep, uint32_t row_flag) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < m) rep[hrows[i]] = minrow[i];
+  if (i < m) rep[hrows[i] & ~row_flag] = minrow[i];
 }
 
 // Final step of row i = the largest k with starts[k] <= i (steps are consecutive windows
@@ -98,6 +98,10 @@ __device__ __forceinline__ uint32_t step_of(const uint32_t* starts, uint32_t nst
 }
 
 // Per-row decision (mod.rs:202-347 replayed with HashMap order := ascending row):
+//   hashed, key held by an Object that existed before the job (seeded: rep < ROW_FLAG is the
+//           lowest such Object id): EXISTING — the step's find_many returns it (:180-198, no
+//           location filter), find() picks the first Object in id order (:214-224) and the
+//           key never creates (:246-253);
 //   hashed: CREATED iff its key's first row (rep) is in the same step — no intra-step dedup,
 //           mod.rs:246-311 — else LINKED to the Object of rep (find() = the lowest Object
 //           id, created for the key's lowest row, :214-224);
@@ -108,7 +112,7 @@ extern "C" __global__ void __launch_bounds__(256)
 sd_links_decide(const uint8_t* __restrict__ state, const uint32_t* __restrict__ rep, uint64_t n,
                 const uint32_t* __restrict__ starts, uint32_t nsteps, uint64_t reached,
                 uint32_t* __restrict__ step_out, uint32_t* __restrict__ object_out,
-                uint8_t* __restrict__ action_out, unsigned int* __restrict__ counts) {
+                uint8_t* __restrict__ action_out, unsigned int* __restrict__ counts, bool seeded) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t step = SD_LINKS_NO_STEP, object = SD_LINKS_NO_OBJECT;
   uint8_t action = SD_LINKS_NOT_REACHED;
@@ -121,8 +125,12 @@ sd_links_decide(const uint8_t* __restrict__ state, const uint32_t* __restrict__ 
       action = SD_LINKS_CREATED;
       object = (uint32_t)i;
     } else {
-      const uint32_t r = rep[i];
-      if (r == (uint32_t)i || step_of(starts, nsteps, r) == step) {
+      const uint32_t v = rep[i];
+      const uint32_t r = seeded ? v & ~LINKS_ROW_FLAG : v;  // the key's first row
+      if (seeded && v < LINKS_ROW_FLAG) {
+        action = SD_LINKS_EXISTING;
+        object = v;
+      } else if (r == (uint32_t)i || step_of(starts, nsteps, r) == step) {
         action = SD_LINKS_CREATED;
         object = (uint32_t)i;
       } else {
@@ -138,7 +146,8 @@ sd_links_decide(const uint8_t* __restrict__ state, const uint32_t* __restrict__ 
   }
   // per-step counts: runs of equal steps inside a wave are the common case (steps are
   // CHUNK_SIZE rows wide), so count per (wave, step) with ballots and one atomic per run
-  const bool created = action == SD_LINKS_CREATED, linked = action == SD_LINKS_LINKED;
+  const bool created = action == SD_LINKS_CREATED,
+             linked = action == SD_LINKS_LINKED || action == SD_LINKS_EXISTING;
   uint64_t todo = __ballot(created || linked);
   const uint32_t lane = threadIdx.x & 63u;
   while (todo) {
@@ -156,28 +165,28 @@ sd_links_decide(const uint8_t* __restrict__ state, const uint32_t* __restrict__ 
 
 hipError_t links_split(const uint64_t* keys, const uint8_t* state, uint64_t n, uint64_t* hkeys,
                        uint32_t* hrows, uint64_t* d_hcount, uint64_t* orphans, uint64_t* d_ocount,
-                       hipStream_t s) {
+                       uint32_t row_flag, hipStream_t s) {
   if (n == 0) return hipSuccess;
   sd_links_split<<<(uint32_t)((n + SPLIT_ROWS - 1) / SPLIT_ROWS), SPLIT_THREADS, 0, s>>>(
       keys, state, n, hkeys, hrows, (unsigned long long*)d_hcount, orphans,
-      (unsigned long long*)d_ocount);
+      (unsigned long long*)d_ocount, row_flag);
   return hipGetLastError();
 }
 
 hipError_t links_scatter(const uint32_t* minrow, const uint32_t* hrows, uint64_t m, uint32_t* rep,
-                         hipStream_t s) {
+                         uint32_t row_flag, hipStream_t s) {
   if (m == 0) return hipSuccess;
-  sd_links_scatter<<<(uint32_t)((m + 255) / 256), 256, 0, s>>>(minrow, hrows, m, rep);
+  sd_links_scatter<<<(uint32_t)((m + 255) / 256), 256, 0, s>>>(minrow, hrows, m, rep, row_flag);
   return hipGetLastError();
 }
 
 hipError_t links_decide(const uint8_t* state, const uint32_t* rep, uint64_t n,
                         const uint32_t* starts, uint32_t nsteps, uint64_t reached,
                         uint32_t* step_out, uint32_t* object_out, uint8_t* action_out,
-                        uint32_t* counts, hipStream_t s) {
+                        uint32_t* counts, bool seeded, hipStream_t s) {
   if (n == 0) return hipSuccess;
   sd_links_decide<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(
-      state, rep, n, starts, nsteps, reached, step_out, object_out, action_out, counts);
+      state, rep, n, starts, nsteps, reached, step_out, object_out, action_out, counts, seeded);
   return hipGetLastError();
 }
 

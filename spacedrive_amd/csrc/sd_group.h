@@ -59,9 +59,11 @@ bool region_group_supported(uint64_t n);
 size_t region_group_workspace_bytes(uint64_t n);
 void region_group_layout(void* ws, uint64_t n, uint64_t** rkeys, uint32_t** rfile, uint64_t** gkeys,
                          uint32_t** gvals);
+// d_objects: 2 u64 (count, overflow carve cursor; K1G zeroed both); keys/n: the batch's key
+// array, read only for a region K1G overflowed
 hipError_t region_group_min(const uint64_t* rkeys, const uint32_t* rfile, uint32_t* cursor,
                             uint64_t cap, uint32_t* out, uint64_t* d_objects, uint64_t* gkeys,
-                            uint32_t* gvals, hipStream_t stream);
+                            uint32_t* gvals, const uint64_t* keys, uint64_t n, hipStream_t stream);
 // Key-range partition: part(k) = floor(k * parts / 2^64); out_keys/out_pos hold the keys and
 // their input positions part-contiguous (order inside a part unspecified), d_counts[p] the
 // part sizes.  ws: partition_workspace_bytes(n, parts).

@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -97,12 +98,20 @@ int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
       hipMalloc((void**)&c->gcursor, 2 * REGIONS * 4) != hipSuccess ||
       hipMemset(c->gcursor, 0, 2 * REGIONS * 4) != hipSuccess ||
       hipEventCreateWithFlags(&c->region_done[0], hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->region_done[1], hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->region_done[1], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->region_hashed[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->region_hashed[1], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->gather_done[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->gather_done[1], hipEventDisableTiming) != hipSuccess) {
     sd_cas_ctx_destroy(c);
     g_ctx_create_err = "stream/event/scratch creation failed on device " + std::to_string(device);
     return SD_CAS_EHIP;
   }
   c->quantum = (size_t)prop.multiProcessorCount * 4 * 64;
+  {
+    const char* t = getenv("SD_CAS_TRACE");
+    c->trace = t && *t && strcmp(t, "0") != 0;
+  }
   sd_cas_set_latency_threshold(c, SD_CAS_THRESHOLD_DEFAULT, SD_CAS_THRESHOLD_DEFAULT);
   sd_cas_set_chunkpar_split(c, SD_CAS_THRESHOLD_DEFAULT, SD_CAS_THRESHOLD_DEFAULT);
   *out = c;
@@ -150,7 +159,10 @@ void sd_cas_ctx_destroy(sd_cas_ctx* c) {
   for (int k = 0; k < 2; k++) {
     if (c->regions[k].p) (void)hipFree(c->regions[k].p);
     if (c->region_done[k]) (void)hipEventDestroy(c->region_done[k]);
+    if (c->region_hashed[k]) (void)hipEventDestroy(c->region_hashed[k]);
   }
+  for (int b = 0; b < 2; b++)
+    if (c->gather_done[b]) (void)hipEventDestroy(c->gather_done[b]);
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->h2d_done) (void)hipEventDestroy(c->h2d_done);
   if (c->ws_ev) (void)hipEventDestroy(c->ws_ev);
@@ -335,7 +347,8 @@ static bool fused_eligible(const sd_cas_ctx* c, size_t n) {
          c->group_target == 0;
 }
 
-// region set k's buffer: rkeys | rfile | gkeys | gvals (region_group_layout) | objects u64
+// region set k's buffer: rkeys | rfile | gkeys | gvals (region_group_layout) | objects u64 |
+// overflow carve cursor u64
 static uint64_t* region_objects(sd_cas_ctx* c, int k) {
   return (uint64_t*)((char*)c->regions[k].p + region_group_workspace_bytes(c->region_n[k]));
 }
@@ -355,10 +368,22 @@ int sd_cas_hash_regions_sampled_dev(sd_cas_ctx* c, const void* d_content, uint64
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t s = pick(c, stream);
   const int k = (c->region_cur + 1) & 1;
-  // set k was last grouped two batches ago: its tables must be done before it is refilled
+  // set k was last grouped two batches ago: its tables must be done before it is refilled;
+  // a batch hashed into it but never grouped: its K1G (on whatever stream) must be done
   if (c->region_pending[k]) HIP_TRY(c, hipStreamWaitEvent(s, c->region_done[k], 0));
-  // a batch hashed into set k but never grouped left its cursors counted: clear them
-  if (!c->region_grouped[k]) HIP_TRY(c, hipMemsetAsync(c->gcursor + REGIONS * k, 0, REGIONS * 4, s));
+  if (!c->region_grouped[k]) {
+    HIP_TRY(c, hipStreamWaitEvent(s, c->region_hashed[k], 0));
+    // its cursors were left counted: clear them
+    HIP_TRY(c, hipMemsetAsync(c->gcursor + REGIONS * k, 0, REGIONS * 4, s));
+  }
+  if (c->region_obj_set == k) {
+    // set k holds the Object count of the context's last grouping, which this refill's K1G
+    // zeroes: keep it in d_scalar for sd_cas_copy_objects_dev
+    HIP_TRY(c, sd_ws_acquire(c, s));
+    HIP_TRY(c, hipMemcpyAsync(c->d_scalar, region_objects(c, k), 8, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(c, sd_ws_release(c, s));
+    c->region_obj_set = -1;
+  }
   c->region_n[k] = n;  // sizes the layout (ensure below grows the set if needed)
   int rc = ensure(c, c->regions[k], region_group_workspace_bytes(n) + 256);
   if (rc) return rc;
@@ -372,6 +397,8 @@ int sd_cas_hash_regions_sampled_dev(sd_cas_ctx* c, const void* d_content, uint64
     (void)hipMemsetAsync(c->gcursor + REGIONS * k, 0, REGIONS * 4, s);  // restore the cursors' invariant
     return fail(c, SD_CAS_EHIP, "hash_regions: %s", hipGetErrorString(e));
   }
+  HIP_TRY(c, hipEventRecord(c->region_hashed[k], s));
+  c->region_keys[k] = d_keys;
   c->region_cur = k;
   c->region_grouped[k] = false;
   return SD_CAS_OK;
@@ -389,8 +416,9 @@ int sd_cas_group_regions_dev(sd_cas_ctx* c, size_t n, uint32_t* d_rep, uint64_t*
   uint32_t *rfile, *gvals;
   region_group_layout(c->regions[k].p, n, &rkeys, &rfile, &gkeys, &gvals);
   uint64_t* obj = region_objects(c, k);
+  HIP_TRY(c, hipStreamWaitEvent(s, c->region_hashed[k], 0));  // after its K1G, whatever stream
   hipError_t e = region_group_min(rkeys, rfile, c->gcursor + REGIONS * k, region_capacity(n), d_rep, obj,
-                                  gkeys, gvals, s);
+                                  gkeys, gvals, c->region_keys[k], n, s);
   if (e != hipSuccess) {
     (void)hipMemsetAsync(c->gcursor + REGIONS * k, 0, REGIONS * 4, s);
     return fail(c, SD_CAS_EHIP, "group_regions: %s", hipGetErrorString(e));
@@ -421,17 +449,8 @@ int sd_cas_hash_group_sampled_dev(sd_cas_ctx* c, const void* d_content, uint64_t
   int rc = sd_cas_hash_regions_sampled_dev(c, d_content, stride, d_sizes, n, d_keys, d_rep,
                                            d_overflow, stream);
   if (rc) return rc;
-  uint64_t obj = 0;
-  if ((rc = sd_cas_group_regions_dev(c, n, d_rep, out_objects ? &obj : nullptr, stream))) return rc;
-  if (out_objects) {
-    uint32_t ovf = 0;
-    hipStream_t s = pick(c, stream);
-    HIP_TRY(c, hipMemcpyAsync(&ovf, d_overflow, 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(c, hipStreamSynchronize(s));
-    if (ovf) return sd_cas_group_dev(c, d_keys, n, d_rep, out_objects, stream);  // exact regroup
-    *out_objects = obj;
-  }
-  return SD_CAS_OK;
+  // (an overflowed region is regrouped by its own table workgroup: exact either way)
+  return sd_cas_group_regions_dev(c, n, d_rep, out_objects, stream);
 }
 
 int sd_cas_group_min_dev(sd_cas_ctx* c, const uint64_t* d_keys, const uint32_t* d_vals, size_t n,
@@ -525,6 +544,7 @@ static_assert(SD_CAS_ROW_HASHED == SD_LINKS_HASHED && SD_CAS_ROW_NO_CAS == SD_LI
                   SD_CAS_ROW_ERROR == SD_LINKS_ERROR && SD_CAS_LINK_CREATED == SD_LINKS_CREATED &&
                   SD_CAS_LINK_LINKED == SD_LINKS_LINKED && SD_CAS_LINK_DROPPED == SD_LINKS_DROPPED &&
                   SD_CAS_LINK_NOT_REACHED == SD_LINKS_NOT_REACHED &&
+                  SD_CAS_LINK_EXISTING == SD_LINKS_EXISTING &&
                   SD_CAS_NO_STEP == SD_LINKS_NO_STEP && SD_CAS_NO_OBJECT == SD_LINKS_NO_OBJECT,
               "link constants");
 
@@ -532,21 +552,30 @@ size_t sd_cas_identifier_max_steps(size_t n, uint32_t chunk) {
   return chunk ? (n + chunk - 1) / chunk : 0;
 }
 
-int sd_cas_identifier_links_dev(sd_cas_ctx* c, const uint64_t* d_keys, const uint8_t* d_state,
-                                size_t n, uint32_t chunk, uint32_t* d_step, uint32_t* d_object,
-                                uint8_t* d_action, uint64_t* h_step_counts, size_t max_steps,
-                                uint64_t* out_steps, void* stream) {
+int sd_cas_identifier_links_seeded_dev(sd_cas_ctx* c, const uint64_t* d_keys, const uint8_t* d_state,
+                                       size_t n, uint32_t chunk, const uint64_t* d_seed_keys,
+                                       const uint32_t* d_seed_objects, size_t n_seed, uint32_t* d_step,
+                                       uint32_t* d_object, uint8_t* d_action, uint64_t* h_step_counts,
+                                       size_t max_steps, uint64_t* out_steps, void* stream) {
   if (!c) return SD_CAS_EINVAL;
   const size_t steps_total = sd_cas_identifier_max_steps(n, chunk);
   if (chunk == 0 || n >= (1ull << 32) || !out_steps || max_steps < steps_total ||
-      (n && (!d_keys || !d_step || !d_object || !d_action || !h_step_counts)))
+      (n && (!d_keys || !d_step || !d_object || !d_action || !h_step_counts)) ||
+      (n_seed && (!d_seed_keys || !d_seed_objects)))
     return fail(c, SD_CAS_EINVAL, "identifier_links: bad arguments");
+  // a seeded grouping tags rows with LINKS_ROW_FLAG: rows and Object ids below 2^31
+  if (n_seed && (n >= LINKS_ROW_FLAG || n_seed >= LINKS_ROW_FLAG || n + n_seed >= (1ull << 32)))
+    return fail(c, SD_CAS_EINVAL, "identifier_links: %zu rows + %zu existing Objects exceed 2^31",
+                n, n_seed);
   *out_steps = 0;
   for (size_t k = 0; k < 2 * steps_total; k++) h_step_counts[k] = 0;
   if (n == 0) return SD_CAS_OK;
   hipStream_t s = pick(c, stream);
-  // staging (this call is blocking): rep | hkeys | hrows | minrow | orphans | starts | counts | 2 counters
-  const size_t b_rep = up256(n * 4), b_hk = up256(n * 8), b_hr = up256(n * 4), b_mr = up256(n * 4),
+  const bool seeded = n_seed > 0;
+  // staging (this call is blocking): rep | hkeys | hrows | minrow | orphans | starts | counts |
+  // 2 counters; the seeded grouping runs over the hashed rows + the existing Objects' keys
+  const size_t m = n + n_seed;
+  const size_t b_rep = up256(n * 4), b_hk = up256(m * 8), b_hr = up256(m * 4), b_mr = up256(m * 4),
                b_or = up256(n * 8), b_st = up256((steps_total + 1) * 4), b_ct = up256(steps_total * 8);
   int rc = ensure(c, c->staging, b_rep + b_hk + b_hr + b_mr + b_or + b_st + b_ct + 256);
   if (rc) return rc;
@@ -559,22 +588,28 @@ int sd_cas_identifier_links_dev(sd_cas_ctx* c, const uint64_t* d_keys, const uin
   uint32_t* starts = (uint32_t*)p; p += b_st;
   uint32_t* counts = (uint32_t*)p; p += b_ct;
   uint64_t* counters = (uint64_t*)p;
-  // 1. grouping over the hashed rows (rep = the key's first row), and the rows that stay
-  //    orphan after being processed (they steer the cursor)
+  // 1. grouping over the hashed rows (rep = the key's first row; seeded: the lowest existing
+  //    Object id when the key has one — mod.rs:180-198 finds Objects by cas over the whole
+  //    library), and the rows that stay orphan after being processed (they steer the cursor)
   std::vector<uint64_t> stay;  // row << 8 | state, ascending
-  if (d_state) {
+  if (d_state || seeded) {
     uint64_t cnt[2] = {0, 0};
     HIP_TRY(c, hipMemsetAsync(counters, 0, 16, s));
-    HIP_TRY(c, links_split(d_keys, d_state, n, hkeys, hrows, counters, orphans, counters + 1, s));
+    HIP_TRY(c, links_split(d_keys, d_state, n, hkeys, hrows, counters, orphans, counters + 1,
+                           seeded ? LINKS_ROW_FLAG : 0u, s));
     HIP_TRY(c, hipMemcpyAsync(cnt, counters, 16, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
     stay.resize(cnt[1]);
     if (cnt[1]) {
       HIP_TRY(c, hipMemcpyAsync(stay.data(), orphans, cnt[1] * 8, hipMemcpyDeviceToHost, s));
     }
+    if (seeded) {  // the existing Objects' (cas key, id) pairs after the hashed rows
+      HIP_TRY(c, hipMemcpyAsync(hkeys + cnt[0], d_seed_keys, n_seed * 8, hipMemcpyDeviceToDevice, s));
+      HIP_TRY(c, hipMemcpyAsync(hrows + cnt[0], d_seed_objects, n_seed * 4, hipMemcpyDeviceToDevice, s));
+    }
     if (cnt[0]) {
-      if ((rc = sd_cas_group_min_dev(c, hkeys, hrows, cnt[0], minrow, nullptr, s))) return rc;
-      HIP_TRY(c, links_scatter(minrow, hrows, cnt[0], rep, s));
+      if ((rc = sd_cas_group_min_dev(c, hkeys, hrows, cnt[0] + n_seed, minrow, nullptr, s))) return rc;
+      HIP_TRY(c, links_scatter(minrow, hrows, cnt[0], rep, seeded ? LINKS_ROW_FLAG : 0u, s));
     }
     HIP_TRY(c, hipStreamSynchronize(s));
     std::sort(stay.begin(), stay.end());
@@ -616,7 +651,7 @@ int sd_cas_identifier_links_dev(sd_cas_ctx* c, const uint64_t* d_keys, const uin
   HIP_TRY(c, hipMemcpyAsync(starts, h_starts.data(), h_starts.size() * 4, hipMemcpyHostToDevice, s));
   HIP_TRY(c, hipMemsetAsync(counts, 0, std::max<size_t>(nsteps, 1) * 8, s));
   HIP_TRY(c, links_decide(d_state, rep, n, starts, (uint32_t)nsteps, reached, d_step, d_object,
-                          d_action, counts, s));
+                          d_action, counts, seeded, s));
   std::vector<uint32_t> hc(2 * std::max<size_t>(nsteps, 1));
   HIP_TRY(c, hipMemcpyAsync(hc.data(), counts, hc.size() * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
@@ -628,38 +663,68 @@ int sd_cas_identifier_links_dev(sd_cas_ctx* c, const uint64_t* d_keys, const uin
   return SD_CAS_OK;
 }
 
-int sd_cas_identifier_links(sd_cas_ctx* c, const uint64_t* h_keys, const uint8_t* h_state,
-                            size_t n, uint32_t chunk, uint32_t* h_step, uint32_t* h_object,
-                            uint8_t* h_action, uint64_t* h_step_counts, size_t max_steps,
-                            uint64_t* out_steps) {
+int sd_cas_identifier_links_dev(sd_cas_ctx* c, const uint64_t* d_keys, const uint8_t* d_state,
+                                size_t n, uint32_t chunk, uint32_t* d_step, uint32_t* d_object,
+                                uint8_t* d_action, uint64_t* h_step_counts, size_t max_steps,
+                                uint64_t* out_steps, void* stream) {
+  return sd_cas_identifier_links_seeded_dev(c, d_keys, d_state, n, chunk, nullptr, nullptr, 0, d_step,
+                                            d_object, d_action, h_step_counts, max_steps, out_steps,
+                                            stream);
+}
+
+int sd_cas_identifier_links_seeded(sd_cas_ctx* c, const uint64_t* h_keys, const uint8_t* h_state,
+                                   size_t n, uint32_t chunk, const uint64_t* h_seed_keys,
+                                   const uint32_t* h_seed_objects, size_t n_seed, uint32_t* h_step,
+                                   uint32_t* h_object, uint8_t* h_action, uint64_t* h_step_counts,
+                                   size_t max_steps, uint64_t* out_steps) {
   if (!c) return SD_CAS_EINVAL;
-  if (n && (!h_keys || !h_step || !h_object || !h_action))
+  if ((n && (!h_keys || !h_step || !h_object || !h_action)) ||
+      (n_seed && (!h_seed_keys || !h_seed_objects)))
     return fail(c, SD_CAS_EINVAL, "identifier_links: bad arguments");
+  for (size_t j = 0; j < n_seed; j++)
+    if (h_seed_objects[j] >= LINKS_ROW_FLAG)
+      return fail(c, SD_CAS_EINVAL, "identifier_links: existing Object id %u >= 2^31", h_seed_objects[j]);
   if (n == 0 || n >= (1ull << 32))
     return sd_cas_identifier_links_dev(c, nullptr, nullptr, n, chunk, nullptr, nullptr, nullptr,
                                        h_step_counts, max_steps, out_steps, c->stream);
   HIP_TRY(c, hipSetDevice(c->device));
-  // device copies (c->io): keys | state | step | object | action
+  // device copies (c->io): keys | state | step | object | action | seed keys | seed ids
   const size_t bk = up256(n * 8), bs = up256(n), b4 = up256(n * 4);
-  int rc = ensure(c, c->io, bk + 2 * bs + 2 * b4);
+  const size_t bsk = up256(n_seed * 8), bso = up256(n_seed * 4);
+  int rc = ensure(c, c->io, bk + 2 * bs + 2 * b4 + bsk + bso);
   if (rc) return rc;
   char* p = (char*)c->io.p;
   uint64_t* d_keys = (uint64_t*)p; p += bk;
   uint8_t* d_state = h_state ? (uint8_t*)p : nullptr; p += bs;
   uint32_t* d_step = (uint32_t*)p; p += b4;
   uint32_t* d_object = (uint32_t*)p; p += b4;
-  uint8_t* d_action = (uint8_t*)p;
+  uint8_t* d_action = (uint8_t*)p; p += bs;
+  uint64_t* d_seed_keys = (uint64_t*)p; p += bsk;
+  uint32_t* d_seed_objects = (uint32_t*)p;
   hipStream_t s = c->stream;
   HIP_TRY(c, hipMemcpyAsync(d_keys, h_keys, n * 8, hipMemcpyHostToDevice, s));
   if (h_state) HIP_TRY(c, hipMemcpyAsync(d_state, h_state, n, hipMemcpyHostToDevice, s));
-  rc = sd_cas_identifier_links_dev(c, d_keys, d_state, n, chunk, d_step, d_object, d_action,
-                                   h_step_counts, max_steps, out_steps, s);
+  if (n_seed) {
+    HIP_TRY(c, hipMemcpyAsync(d_seed_keys, h_seed_keys, n_seed * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(d_seed_objects, h_seed_objects, n_seed * 4, hipMemcpyHostToDevice, s));
+  }
+  rc = sd_cas_identifier_links_seeded_dev(c, d_keys, d_state, n, chunk, d_seed_keys, d_seed_objects,
+                                          n_seed, d_step, d_object, d_action, h_step_counts,
+                                          max_steps, out_steps, s);
   if (rc) return rc;
   HIP_TRY(c, hipMemcpyAsync(h_step, d_step, n * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipMemcpyAsync(h_object, d_object, n * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipMemcpyAsync(h_action, d_action, n, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
   return SD_CAS_OK;
+}
+
+int sd_cas_identifier_links(sd_cas_ctx* c, const uint64_t* h_keys, const uint8_t* h_state,
+                            size_t n, uint32_t chunk, uint32_t* h_step, uint32_t* h_object,
+                            uint8_t* h_action, uint64_t* h_step_counts, size_t max_steps,
+                            uint64_t* out_steps) {
+  return sd_cas_identifier_links_seeded(c, h_keys, h_state, n, chunk, nullptr, nullptr, 0, h_step,
+                                        h_object, h_action, h_step_counts, max_steps, out_steps);
 }
 
 // ---- host-buffer cas (blocking) -----------------------------------------------------
@@ -784,13 +849,28 @@ int sd_cas_generate_cas_ids(sd_cas_ctx* c, const uint8_t* const* bufs, const uin
   return run_staged(c, pl, sizes, n, out_keys);
 }
 
+static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uint64_t* sizes,
+                              size_t n, uint64_t* out_keys, int32_t* status, uint64_t* out_sizes);
+
 int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
                                        const uint64_t* sizes, size_t n, uint64_t* out_keys,
                                        int32_t* status) {
+  return cas_ids_from_paths(c, paths, sizes, n, out_keys, status, nullptr);
+}
+
+int sd_cas_file_metadata_from_paths(sd_cas_ctx* c, const char* const* paths, size_t n,
+                                    uint64_t* out_keys, int32_t* status, uint64_t* out_sizes) {
+  if (c && n && !out_sizes) return fail(c, SD_CAS_EINVAL, "file_metadata_from_paths: null out_sizes");
+  return cas_ids_from_paths(c, paths, nullptr, n, out_keys, status, out_sizes);
+}
+
+static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uint64_t* sizes,
+                              size_t n, uint64_t* out_keys, int32_t* status, uint64_t* out_sizes) {
   if (!c) return SD_CAS_EINVAL;
   if (n == 0) return SD_CAS_OK;
   if (!paths || !out_keys || !status || n >= (1ull << 32))
     return fail(c, SD_CAS_EINVAL, "generate_cas_ids_from_paths: null argument");
+  SdTrace tr(c->trace, "from_paths", n);
   HIP_TRY(c, hipSetDevice(c->device));
   for (size_t i = 0; i < n; i++) {
     status[i] = 0;
@@ -814,7 +894,9 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
       }
     });
     sizes = msize.data();
+    tr.mark("stat");
   }
+  if (out_sizes) std::copy(sizes, sizes + n, out_sizes);
   for (size_t i = 0; i < n; i++)
     if (status[i] == 0 && sizes[i] == 0) status[i] = SD_CAS_STATUS_NO_CAS;
   // Content length per file: sampled 57,344; whole file = its actual length (cas.rs:29
@@ -832,13 +914,21 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
   // windows) + (H2D + hash of the last one), so windows are cut by staged BYTES — about a
   // twelfth of the batch each (2-64 MiB, <= GATHER_WINDOW files): config 1's 10k tmpfs files
   // (~40 KB staged each) run in ~12 windows of ~830 files instead of 5 of 2,048, and the
-  // un-overlapped tail shrinks with the last window.
+  // un-overlapped tail shrinks with the last window.  A batch whose whole gather is shorter
+  // than what a second window's launch chain costs — the reference's 100-file job step
+  // (mod.rs:34), up to SMALL_BATCH_FILES files and SMALL_BATCH_BYTES staged — is one window:
+  // cutting its ~4 MB in two added a second H2D/hash/D2H chain and its serial tail
+  // (0.36-0.41 -> 0.48-0.52 ms per step).
   constexpr size_t GATHER_WINDOW = 2048;
+  constexpr size_t SMALL_BATCH_FILES = 2048;
+  constexpr uint64_t SMALL_BATCH_BYTES = 16ull << 20;
   std::vector<size_t> wstart{0};
   {
     uint64_t total = 0;
     for (size_t i = 0; i < n; i++) total += up128(lens[i]);
-    const uint64_t target = std::min<uint64_t>(64ull << 20, std::max<uint64_t>(2ull << 20, total / 12));
+    const bool one_window = n <= SMALL_BATCH_FILES && total <= SMALL_BATCH_BYTES;
+    const uint64_t target = one_window ? SMALL_BATCH_BYTES
+                                       : std::min<uint64_t>(64ull << 20, std::max<uint64_t>(2ull << 20, total / 12));
     uint64_t bytes = 0;
     for (size_t i = 0; i < n; i++) {
       const size_t files = i - wstart.back();
@@ -867,9 +957,8 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
   int rc = ensure_pinned(c, nslots * slot);
   if (rc) return rc;
   if ((rc = ensure(c, c->staging, nslots * slot))) return rc;
-  hipEvent_t done[2] = {nullptr, nullptr};
-  for (int b = 0; b < nslots; b++)
-    HIP_TRY(c, hipEventCreateWithFlags(&done[b], hipEventDisableTiming));
+  hipEvent_t* done = c->gather_done;
+  tr.mark("plan");
   auto gather = [&](size_t w, char* pin) {
     const Plan& pl = plans[w];
     const size_t f0 = wstart[w], m = wstart[w + 1] - wstart[w];
@@ -954,12 +1043,14 @@ int sd_cas_generate_cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths,
     const int b = (int)(w & 1);
     if (w >= 2 && (rc = finish(w - 2))) break;  // slot b free again
     gather(w, pin0 + b * slot);
+    tr.mark("gather");
     const size_t f0 = wstart[w], m = wstart[w + 1] - wstart[w];
     rc = enqueue_staged(c, plans[w], psize.data() + f0, m, pin0 + b * slot, dev0 + b * slot, done[b]);
+    tr.mark("enqueue");
   }
   for (size_t w = nw >= 2 ? nw - 2 : 0; w < nw && rc == 0; w++) rc = finish(w);
+  tr.mark("wait");
   if (rc) (void)hipStreamSynchronize(c->stream);
-  for (int b = 0; b < nslots; b++) (void)hipEventDestroy(done[b]);
   if (rc) return rc;
   // whole files whose length is not their metadata size: read them as they are now
   // (fs::read, cas.rs:29) and hash the few of them as one host batch

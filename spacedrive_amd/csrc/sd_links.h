@@ -11,23 +11,31 @@
 #define SD_LINKS_LINKED 1
 #define SD_LINKS_DROPPED 2
 #define SD_LINKS_NOT_REACHED 3
+#define SD_LINKS_EXISTING 4
 #define SD_LINKS_NO_STEP 0xFFFFFFFFu
 #define SD_LINKS_NO_OBJECT 0xFFFFFFFFu
 
 namespace sdcas {
 
-// hashed rows -> (hkeys, hrows) (unordered), other rows -> orphans[] = row << 8 | state;
-// *d_hcount / *d_ocount (u64, zeroed by the caller) = counts
+// A seeded job (Objects that exist before it) tags its rows with ROW_FLAG in the grouping's
+// values, so one minimum per key tells an existing Object (< ROW_FLAG: its id) from the
+// key's first row (ROW_FLAG | row)
+constexpr uint32_t LINKS_ROW_FLAG = 0x80000000u;
+
+// hashed rows -> (hkeys, hrows = row | row_flag) (unordered), other rows -> orphans[] =
+// row << 8 | state (state NULL: every row hashed); *d_hcount / *d_ocount (u64, zeroed by the
+// caller) = counts
 hipError_t links_split(const uint64_t* keys, const uint8_t* state, uint64_t n, uint64_t* hkeys,
                        uint32_t* hrows, uint64_t* d_hcount, uint64_t* orphans, uint64_t* d_ocount,
-                       hipStream_t s);
-// rep[hrows[i]] = minrow[i]
+                       uint32_t row_flag, hipStream_t s);
+// rep[hrows[i] & ~row_flag] = minrow[i]
 hipError_t links_scatter(const uint32_t* minrow, const uint32_t* hrows, uint64_t m, uint32_t* rep,
-                         hipStream_t s);
-// per-row decisions; counts[2k], counts[2k+1] (u32, zeroed by the caller) += created, linked
+                         uint32_t row_flag, hipStream_t s);
+// per-row decisions; counts[2k], counts[2k+1] (u32, zeroed by the caller) += created, linked.
+// seeded: rep[i] < LINKS_ROW_FLAG is an existing Object's id, else LINKS_ROW_FLAG | first row
 hipError_t links_decide(const uint8_t* state, const uint32_t* rep, uint64_t n,
                         const uint32_t* starts, uint32_t nsteps, uint64_t reached,
                         uint32_t* step_out, uint32_t* object_out, uint8_t* action_out,
-                        uint32_t* counts, hipStream_t s);
+                        uint32_t* counts, bool seeded, hipStream_t s);
 
 }  // namespace sdcas

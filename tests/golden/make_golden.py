@@ -91,12 +91,13 @@ def replay_identifier(keys: list[int], chunk: int = 100):
 
 
 ROW_HASHED, ROW_NO_CAS, ROW_ERROR = 0, 1, 2
-LINK_CREATED, LINK_LINKED, LINK_DROPPED, LINK_NOT_REACHED = 0, 1, 2, 3
+LINK_CREATED, LINK_LINKED, LINK_DROPPED, LINK_NOT_REACHED, LINK_EXISTING = 0, 1, 2, 3, 4
 NO_STEP = NO_OBJECT = 0xFFFFFFFF
 
 
-def replay_identifier_job(keys, states, chunk: int = 100, with_creates: bool = False):
-    """Literal replay of one file-identifier job over a fresh library, DB state included:
+def replay_identifier_job(keys, states, chunk: int = 100, with_creates: bool = False,
+                          existing=None):
+    """Literal replay of one file-identifier job, DB state included:
     file_identifier_job.rs:86-178 (init: orphan count, ceil(n/chunk) steps, cursor = first
     orphan id), :180-236 (execute_step: get_orphan_file_paths = orphan rows with id >=
     cursor, ascending, LIMIT chunk (:251-319); an empty query ends the job), mod.rs:98-350
@@ -104,15 +105,28 @@ def replay_identifier_job(keys, states, chunk: int = 100, with_creates: bool = F
     found by cas; links to the first; one new Object per remaining row, HashMap order :=
     ascending row) and mod.rs:401-405 (the next cursor = the chunk's last row).
     Rows: file_path ids 0..n-1, all orphan at init (object_id and cas_id NULL).
+    existing: None (a fresh library) or (cas key, Object id) pairs — Objects the library
+    holds before the job, each connected to a file_path (outside the job's rows) with that
+    cas.  They take the Object table's first rows in id order, so a later find_many returns
+    them ahead of the job's own Objects (:181-188; the query has no location filter).
     Returns (step[], object[], action[], [(created, linked)] per step) where object[i] is
-    the row that created the Object row i is connected to; with_creates: also the rows that
-    created an Object in each step (a re-queried empty row appears in every step it was
-    processed in)."""
+    the row that created the Object row i is connected to, or (LINK_EXISTING) the id of the
+    pre-job Object; with_creates: also the rows that created an Object in each step (a
+    re-queried empty row appears in every step it was processed in)."""
     n = len(keys)
     cas_col = [None] * n         # file_path.cas_id
     obj_col = [None] * n         # file_path.object_id
-    creator = []                 # Object table: id -> creating row
+    creator = []                 # Object table: id -> creating row (None: a pre-job Object)
     cas_objects = {}             # cas -> Object ids having a file_path with that cas, in id order
+    pre_id = []                  # pre-job Objects' own ids, by Object-table row
+    for oid in sorted({int(o) for _, o in existing or ()}):
+        pre_id.append(oid)
+        creator.append(None)
+    pos = {oid: t for t, oid in enumerate(pre_id)}
+    for c, o in sorted(existing or (), key=lambda e: int(e[1])):
+        lst = cas_objects.setdefault(int(c), [])
+        if pos[int(o)] not in lst:
+            lst.append(pos[int(o)])
     step = [NO_STEP] * n
     processed_ok = [False] * n   # last processing of the row succeeded
     processed = [False] * n
@@ -139,18 +153,18 @@ def replay_identifier_job(keys, states, chunk: int = 100, with_creates: bool = F
         for r, c in meta.items():                    # cas_id write (mod.rs:157-178)
             cas_col[r] = c
         unique = {c for c in meta.values() if c is not None}
-        existing = {c: cas_objects[c] for c in unique if c in cas_objects}  # :181-198
+        found = {c: cas_objects[c] for c in unique if c in cas_objects}  # :181-198
         linked = 0
         for r in sorted(meta):                       # :202-238 link to the FIRST Object
             c = meta[r]
-            if c is not None and c in existing:
-                obj_col[r] = existing[c][0]
+            if c is not None and c in found:
+                obj_col[r] = found[c][0]
                 linked += 1
         created = 0
         step_creates.append([])
         for r in sorted(meta):                       # :246-347 one new Object per remaining row
             c = meta[r]
-            if c is None or c not in existing:
+            if c is None or c not in found:
                 oid = len(creator)
                 creator.append(r)
                 obj_col[r] = oid
@@ -167,6 +181,10 @@ def replay_identifier_job(keys, states, chunk: int = 100, with_creates: bool = F
             continue
         if not processed_ok[r]:
             act[r] = LINK_DROPPED
+            continue
+        if creator[obj_col[r]] is None:
+            obj[r] = pre_id[obj_col[r]]
+            act[r] = LINK_EXISTING
             continue
         obj[r] = creator[obj_col[r]]
         act[r] = LINK_CREATED if obj[r] == r else LINK_LINKED

@@ -36,3 +36,20 @@ def test_rank_refuses_world_mismatch():
 def test_gpus_zero_is_an_error():
     r = _run(["--gpus", "0"])
     assert r.returncode != 0
+
+
+def test_visible_gpus_from_kfd_topology(tmp_path, monkeypatch):
+    """spawn_ranks counts GPUs from the KFD topology (no HIP call in the parent): GPU nodes
+    have a non-zero gfx_target_version, the CPU node 0; the *_VISIBLE_DEVICES lists narrow it."""
+    sys.path.insert(0, ROOT)
+    import bench
+    for i, ver in enumerate([0, 90500, 90500, 90500]):
+        d = tmp_path / str(i)
+        d.mkdir()
+        (d / "properties").write_text(f"cpu_cores_count 0\ngfx_target_version {ver}\nsimd_count 1024\n")
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    assert bench.visible_gpus(str(tmp_path)) == 3
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")
+    assert bench.visible_gpus(str(tmp_path)) == 1
+    assert bench.visible_gpus(str(tmp_path / "none")) == 0

@@ -505,19 +505,28 @@ def test_hash_regions_split_pipelined(eng, oracle):
     torch.cuda.empty_cache()
 
 
-def test_hash_group_fused_overflow_and_fallback(eng, oracle):
-    """A coarse bucket outgrowing its fixed region (one file copied 20,000 times in a batch of
-    one quantum: region capacity ~450 rows): the async call raises the overflow flag and the
-    caller's regroup gives the exact result; the blocking call regroups by itself.  A batch
-    that is not a multiple of the quantum runs K1 + the standalone chain (flag untouched)."""
+@pytest.mark.parametrize("hot", [[20_000], [9_000, 7_000, 5_000, 3_000], []])
+def test_hash_group_fused_overflow_and_fallback(eng, oracle, hot):
+    """Coarse buckets outgrowing their fixed regions (files copied thousands of times in a
+    batch of one quantum: region capacity ~450 rows): the flag is raised and the grouping is
+    still exact — the async call's rep and Object count (copy_objects) equal the standalone
+    grouping's with no caller regroup (each overflowed region is regrouped from the whole key
+    array by its table workgroup; several hot keys carve several global tables).  A batch that
+    is not a multiple of the quantum runs K1 + the standalone chain (flag untouched)."""
     q = eng.batch_quantum
-    for n, copies in [(q, 20_000), (q + 1000, 0)]:
+    for n in ([q, q + 1000] if not hot else [q]):
         content = torch.empty((n, SAMPLED_CONTENT_LEN), dtype=torch.uint8, device="cuda")
         sizes = torch.empty(n, dtype=torch.int64, device="cuda")
         eng.synth_sampled(71, 0, n, content, sizes, SAMPLED_CONTENT_LEN, dup_permille=100)
-        if copies:
-            content[1:copies + 1] = content[0]
-            sizes[1:copies + 1] = sizes[0]
+        at = 1
+        for h, copies in enumerate(hot):
+            src = 40_000 + h  # the hot file's copies spread over the batch
+            idx = torch.from_numpy(np.random.default_rng(h).choice(
+                np.setdiff1d(np.arange(n), [40_000 + j for j in range(len(hot))]), copies,
+                replace=False)).cuda()
+            content[idx] = content[src]
+            sizes[idx] = sizes[src]
+            at += copies
         keys = torch.empty(n, dtype=torch.int64, device="cuda")
         rep = torch.empty(n, dtype=torch.int32, device="cuda")
         eng.hash_sampled(content, sizes, keys)
@@ -526,21 +535,63 @@ def test_hash_group_fused_overflow_and_fallback(eng, oracle):
         rep2 = torch.empty(n, dtype=torch.int32, device="cuda")
         ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
         eng.hash_group_sampled(content, sizes, keys2, rep2, ovf, want_objects=False)
+        out = torch.zeros(1, dtype=torch.int64, device="cuda")
+        eng._check(eng.L.sd_cas_copy_objects_dev(eng.h, out.data_ptr(), eng.stream), "copy_objects")
         torch.cuda.synchronize()
         assert torch.equal(keys, keys2)
-        if copies:
-            assert int(ovf.item()) == 1
-            assert eng.group(keys2, rep2) == objects and torch.equal(rep, rep2)  # the caller's regroup
-            rep2.zero_()
-            ovf.zero_()
-            assert eng.hash_group_sampled(content, sizes, keys2, rep2, ovf) == objects
-        else:
-            assert int(ovf.item()) == 0
+        assert int(ovf.item()) == (1 if hot else 0)
+        assert torch.equal(rep, rep2) and int(out.item()) == objects
+        rep2.zero_()
+        ovf.zero_()
+        assert eng.hash_group_sampled(content, sizes, keys2, rep2, ovf) == objects
         assert torch.equal(rep, rep2)
         orep, oobj = oracle.group_canonical(keys.cpu().numpy().view(np.uint64))
         assert oobj == objects and (rep.cpu().numpy().astype(np.uint32) == orep).all()
         del content
         torch.cuda.empty_cache()
+
+
+def test_hash_regions_streams_and_ungrouped(eng):
+    """K1G batches on two streams with one batch hashed but never grouped — the
+    next hash_regions into its set waits for that K1G (no cursor or row corruption), tables on
+    a third stream wait for their own K1G, and the Object count of the last grouping survives
+    the refill of its set (copy_objects after it)."""
+    q = eng.batch_quantum
+    n = q
+    s1, s2, s3 = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    data = []
+    for j in range(5):
+        c = torch.empty((n, SAMPLED_CONTENT_LEN), dtype=torch.uint8, device="cuda")
+        z = torch.empty(n, dtype=torch.int64, device="cuda")
+        eng.synth_sampled(300 + j, j * n, n, c, z, SAMPLED_CONTENT_LEN, dup_permille=300)
+        data.append((c, z))
+    torch.cuda.synchronize()
+    ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
+    keys = [torch.empty(n, dtype=torch.int64, device="cuda") for _ in range(5)]
+    reps = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(5)]
+    obj = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(5)]
+    # batch 0 on s1 (grouped on s3), batch 1 on s2 never grouped, batch 2 on s1 refills set 0,
+    # batch 3 on s2 refills batch 1's set while its K1G may still run; batch 4 grouped last
+    plan = [(s1, True), (s2, False), (s1, True), (s2, True), (s1, True)]
+    for j, ((c, z), (st, grp)) in enumerate(zip(data, plan)):
+        eng.hash_regions_sampled(c, z, keys[j], reps[j], ovf, stream=st.cuda_stream)
+        if grp:
+            eng.group_regions(n, reps[j], stream=s3.cuda_stream, want_objects=False)
+            eng._check(eng.L.sd_cas_copy_objects_dev(eng.h, obj[j].data_ptr(), s3.cuda_stream), "copy")
+    torch.cuda.synchronize()
+    for j in (0, 2, 3, 4):
+        rep = torch.empty(n, dtype=torch.int32, device="cuda")
+        assert eng.group(keys[j], rep) == int(obj[j].item()) and torch.equal(rep, reps[j]), j
+    # batch 4's count lives in its region set; two more hash_regions (never grouped) refill
+    # that set: copy_objects still returns batch 4's count
+    eng.hash_regions_sampled(data[0][0], data[0][1], keys[0], reps[0], ovf, stream=s1.cuda_stream)
+    eng.hash_regions_sampled(data[1][0], data[1][1], keys[1], reps[1], ovf, stream=s2.cuda_stream)
+    late = torch.zeros(1, dtype=torch.int64, device="cuda")
+    eng._check(eng.L.sd_cas_copy_objects_dev(eng.h, late.data_ptr(), s3.cuda_stream), "copy")
+    torch.cuda.synchronize()
+    assert int(late.item()) == int(obj[4].item())
+    del data
+    torch.cuda.empty_cache()
 
 
 def test_workspace_ordered_across_streams(eng, oracle):
@@ -1278,6 +1329,81 @@ def test_identifier_links_vs_replay(eng, chunk):
     assert (step.cpu().numpy().view(np.uint32) == np.array(want_step, dtype=np.uint32)).all()
     assert (obj.cpu().numpy().view(np.uint32) == np.array(want_obj, dtype=np.uint32)).all()
     assert (act.cpu().numpy() == np.array(want_act, dtype=np.uint8)).all()
+
+
+@pytest.mark.parametrize("chunk", [100, 7, 1])
+def test_identifier_links_existing_vs_replay(eng, chunk):
+    """sd_cas_identifier_links_seeded[_dev] vs the replay on a library that already holds
+    Objects (mod.rs:180-253): ~30 % of the keys carry pre-job Objects (some
+    several, ids in any order), existing keys repeat inside one chunk, NO_CAS/ERROR rows end
+    chunks, and a seed key no row has.  Device and host entry points, with and without
+    per-row states."""
+    rng = np.random.default_rng(180 + chunk)
+    n = 12_000 if chunk > 2 else 2_500
+    pool = rng.integers(1, 2 ** 64, n // 4, dtype=np.uint64)
+    keys = pool[rng.integers(0, len(pool), n)]
+    keys[10:14] = keys[10]  # one existing-or-fresh key four times inside one chunk
+    states = rng.choice(np.array([0, 1, 2], dtype=np.uint8), n, p=[0.9, 0.05, 0.05])
+    last_rows = np.arange(chunk - 1, n, chunk)
+    states[last_rows[rng.random(len(last_rows)) < 0.3]] = 2
+    states[last_rows[rng.random(len(last_rows)) < 0.2]] = 1
+    pre = pool[rng.random(len(pool)) < 0.3]
+    pre = np.concatenate([pre, [keys[10], np.uint64(12345)]]).astype(np.uint64)
+    ids = rng.permutation(3 * len(pre))[:len(pre)].astype(np.uint32)      # unordered ids
+    extra = rng.integers(0, len(pre), len(pre) // 5)                      # several per key
+    sk = np.concatenate([pre, pre[extra]])
+    so = np.concatenate([ids, rng.integers(0, 2 ** 31 - 1, len(extra)).astype(np.uint32)])
+    existing = list(zip((int(k) for k in sk), (int(o) for o in so)))
+    for st in (states, None):
+        want_step, want_obj, want_act, want_counts = replay_identifier_job(
+            [int(k) for k in keys], [int(s) for s in (st if st is not None else np.zeros(n))], chunk,
+            existing=existing)
+        assert 4 in want_act and 0 in want_act and 1 in want_act
+        step, obj, act, counts = eng.identifier_links(
+            dev64(keys), None if st is None else torch.from_numpy(st).cuda(), chunk,
+            existing=(dev64(sk), torch.from_numpy(so.view(np.int32)).cuda()))
+        assert [tuple(c) for c in counts.tolist()] == want_counts
+        assert (step.cpu().numpy().view(np.uint32) == np.array(want_step, dtype=np.uint32)).all()
+        assert (obj.cpu().numpy().view(np.uint32) == np.array(want_obj, dtype=np.uint32)).all()
+        assert (act.cpu().numpy() == np.array(want_act, dtype=np.uint8)).all()
+        hstep, hobj, hact, hcounts = eng.identifier_links_host(keys, st, chunk, existing=(sk, so))
+        assert [tuple(c) for c in hcounts.tolist()] == want_counts
+        assert (hobj == np.array(want_obj, dtype=np.uint32)).all()
+        assert (hact == np.array(want_act, dtype=np.uint8)).all()
+    # an empty seed is the fresh-library call; an id >= 2^31 is refused
+    a = eng.identifier_links_host(keys, states, chunk, existing=(sk[:0], so[:0]))
+    b = eng.identifier_links_host(keys, states, chunk)
+    assert all((x == y).all() for x, y in zip(a, b))
+    from spacedrive_amd import CasError
+    with pytest.raises(CasError):
+        eng.identifier_links_host(keys, states, chunk, existing=(sk[:1], np.array([2 ** 31], np.uint32)))
+
+
+def test_identifier_job_step_existing(eng, oracle, tmp_path):
+    """identifier_job_step on a library whose earlier job already made Objects: the second
+    location's files whose cas_id an older Object carries link to it (LINK_EXISTING), the
+    others follow the fresh rules; FileMetadata.size is the metadata length the library used."""
+    import spacedrive_amd as sd
+    rng = np.random.default_rng(11)
+    blobs = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in [300, 150_000, 7]]
+    paths = []
+    for i in range(150):
+        p = tmp_path / f"q{i:03d}"
+        p.write_bytes(blobs[i % 3] if i % 4 == 0 else
+                      rng.integers(0, 256, int(rng.integers(1, 130_000)), dtype=np.uint8).tobytes())
+        paths.append(str(p))
+    ids = {oracle.generate_cas_id(paths[0], os.path.getsize(paths[0])): 41,
+           oracle.generate_cas_id(paths[4], os.path.getsize(paths[4])): 17}
+    res = sd.identifier_job_step(paths, eng=eng, existing=(list(ids), list(ids.values())))
+    for i, p in enumerate(paths):
+        want = oracle.generate_cas_id(p, os.path.getsize(p))
+        assert res.metadata[i].cas_id == want and res.metadata[i].size == os.path.getsize(p)
+        if want in ids:
+            assert res.existing_of[i] == ids[want] and i not in res.object_of
+        else:
+            assert i in res.object_of
+    assert sum(len(b.links_existing) for b in res.steps) == len(res.existing_of) > 0
+    assert res.total_linked == sum(len(b.links) + len(b.links_existing) for b in res.steps)
 
 
 def test_identifier_links_all_hashed_1m(eng, oracle):

@@ -251,6 +251,30 @@ def test_job_replay_cursor_semantics():
     assert counts[2][0] + counts[2][1] == 100 + 0  # 198 again (new Object) + 199..297
 
 
+def test_job_replay_existing_objects():
+    """The replay on a library that already holds Objects (mod.rs:180-253): a row whose cas
+    an older Object carries links to the lowest such Object id in every step and never
+    creates; keys without one keep the fresh-library behaviour (no intra-step dedup, later
+    steps link to the first creator)."""
+    from tests.golden.make_golden import LINK_EXISTING, replay_identifier_job
+    A, B, C, D = 0xA0, 0xB0, 0xC0, 0xD0
+    keys = [A, C, B, C, A, D, A, C, B, D]
+    states = [0, 0, 0, 0, 1, 0, 0, 0, 2, 0]
+    existing = [(A, 7), (B, 12), (A, 3), (A, 9)]
+    step, obj, act, counts = replay_identifier_job(keys, states, 4, existing=existing)
+    assert step == [0, 0, 0, 0, 1, 1, 1, 1, 2, 2]
+    assert act[0] == act[6] == LINK_EXISTING and obj[0] == obj[6] == 3  # A -> id 3 (lowest)
+    assert act[2] == LINK_EXISTING and obj[2] == 12                     # B -> 12
+    assert act[1] == act[3] == 0 and obj[3] == 3                        # C twice in step 0: two Objects
+    assert act[7] == 1 and obj[7] == 1                                  # later C: the first one
+    assert act[4] == 0 and obj[4] == 4                                  # no cas_id: own Object
+    assert act[5] == 0 and act[9] == 1 and obj[9] == 5 and act[8] == 2  # D fresh; B errors
+    assert counts == [(2, 2), (2, 2), (0, 1)]
+    # unseeded: the same rows as a fresh library
+    _, obj0, act0, _ = replay_identifier_job(keys, states, 4)
+    assert act0[0] == 0 and obj0[6] == 0 and act0[2] == 0
+
+
 def test_simd_baseline_matches_scalar(oracle):
     rng = np.random.default_rng(2)
     n = 48
