@@ -442,6 +442,28 @@ def main() -> None:
 
     # the host-CPU baseline beside the line at EVERY world size (the reference path cas.rs:23-62
     # on the host cores): rank 0 runs it after the timed region, the other ranks wait for it
+    # VALU busy of the headline kernel from the committed PMC pass (tools/pmc_valu.sh ->
+    # profiles/pmc_valu.json; counter conventions in tools/pmc_valu.py)
+    valu_busy = None
+    kname = "sd_cas_sampled_group_kernel" if fused else "sd_cas_sampled_kernel"
+    pv = os.path.join(ROOT, "profiles", "pmc_valu.json")
+    if os.path.exists(pv):
+        with open(pv) as fh:
+            rec = json.load(fh).get(kname)
+        if rec:
+            # issue cycles of K1's measured instruction mix at the PMC pass's own clock:
+            # full-rate v_xor/v_add 2 cycles, half-rate v_alignbit/v_add3 4 (wave64 on SIMD32)
+            mix_cycles = 2 * (230 + 112) + 4 * (224 + 112)
+            wave_comps = rec["counters_mean"]["SQ_WAVES"] * COMPRESSIONS
+            valu_busy = {"valu_busy": rec["valu_busy"], "valu_busy_full_rate": rec["valu_busy_full_rate"],
+                         "valu_pipe_busy_mix": wave_comps * mix_cycles / (1024 * rec["wall_cycles"]),
+                         "clock_ghz": rec.get("clock_ghz"),
+                         "source": "profiles/pmc_valu.json (rocprofv3 --pmc, tools/pmc_valu.sh)",
+                         "note": "valu_busy = SQ_ACTIVE_INST_VALU x 4 / (1,024 SIMDs x GRBM_GUI_ACTIVE/8) "
+                                 "(rocprof VALUBusy, 4 cycles per VALU instruction); "
+                                 "valu_pipe_busy_mix = the ARX mix's issue cycles (2 full-rate, 4 "
+                                 "half-rate per wave64 instruction) over the same SIMD cycles"}
+
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(content, sizes, last_keys, args.cpu_seconds)
@@ -510,6 +532,7 @@ def main() -> None:
                 "unit": "T int32 ops/s",
                 "frac": valu / VALU_PEAK_TOPS,
                 "traffic": traffic,
+                "valu_busy": valu_busy,
                 "kernel_ms": kern_ms,
                 "kernel_ms_ranks": {"min": min(k1_ms_ranks), "max": max(k1_ms_ranks),
                                     "per_rank": k1_ms_ranks},

@@ -200,14 +200,19 @@ sd_cas_sampled_kernel_256(const uint8_t* __restrict__ content, uint64_t stride,
 // in LDS (the CV stack's LDS, dead by then) and reserves each bucket's run with one device
 // atomic.  The chain after K1G is one bucket-table launch.  Regions are sized mean + 8
 // sigma + 64 rows for uniform keys; a bucket that outgrows its region (heavily duplicated
-// content: every copy of a file lands in one bucket) keeps counting in its cursor and sets
-// *overflow, and that region's table workgroup regroups it exactly from the whole key array
+// content: every copy of a file lands in one bucket) keeps counting in its cursor, appends
+// its extra rows to the set's spill list (one reservation per workgroup that has any) and
+// sets *overflow; that region's table workgroup reads its region rows and its spilled rows
 // (sd_bucket_min_regions) — only the overflowed regions pay, on the device, no host regroup.
 struct RegionOut {
   uint64_t* rkeys;     // [REGIONS][cap] mixed keys
   uint32_t* rfile;     // [REGIONS][cap] file index
-  uint32_t* cursor;    // [REGIONS] rows reserved; zero on entry (the bucket tables re-zero it)
+  uint32_t* cursor;    // [REGION_SET_WORDS] rows reserved per region, then the spill count and
+                       // the full-region count at REGION_SPILL_WORD; zero on entry (the bucket
+                       // tables re-zero them)
   uint64_t cap;
+  uint64_t* spill_keys;   // rows past their region's capacity (mixed key, file), unordered
+  uint32_t* spill_file;
   uint32_t* rep;       // rep[f] = f: the bucket tables store only where a key's minimum differs
   uint32_t* overflow;  // set when a region is full
   // objects[0]: zeroed here, the bucket tables add the distinct keys; objects[1]: zeroed
@@ -234,25 +239,47 @@ __device__ __forceinline__ void sampled_group_kernel_body(const uint8_t* __restr
   }
   if (blockIdx.x == 0 && threadIdx.x < 2) ro.objects[threadIdx.x] = 0;
   // epilogue: the stack columns are dead once every lane has its root
-  uint32_t* hist = &stack_lds[0][0][0];  // REGIONS counters, then REGIONS run bases
+  // REGIONS counters, REGIONS run bases, REGIONS spill offsets, the spill total and base
+  uint32_t* hist = &stack_lds[0][0][0];
   uint32_t* base = hist + REGIONS;
+  uint32_t* spoff = base + REGIONS;
+  uint32_t* sp = spoff + REGIONS;  // sp[0] = this workgroup's spilled rows, sp[1] = their base
+  static_assert(3 * REGIONS + 2 <= SAMPLED_DEPTH * 8 * B, "the epilogue fits the stack LDS");
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < REGIONS; i += B) hist[i] = 0;
+  if (threadIdx.x == 0) sp[0] = 0;
   __syncthreads();
   const uint64_t m = mix64(key);
   const uint32_t bkt = (uint32_t)(m >> (64 - REGION_BITS));
   const uint32_t r = live ? atomicAdd(&hist[bkt], 1u) : 0u;
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < REGIONS; i += B)
-    base[i] = hist[i] ? atomicAdd(&ro.cursor[i], hist[i]) : 0u;
+  for (uint32_t i = threadIdx.x; i < REGIONS; i += B) {
+    const uint32_t h = hist[i];
+    const uint32_t g = h ? atomicAdd(&ro.cursor[i], h) : 0u;
+    base[i] = g;
+    // rows past the region's capacity: this workgroup's run of them for region i
+    const uint64_t lo = g > ro.cap ? g : ro.cap;
+    const uint32_t over = g + h > lo ? (uint32_t)(g + h - lo) : 0u;
+    spoff[i] = over ? atomicAdd(&sp[0], over) : 0u;
+    if (g <= ro.cap && g + h > ro.cap) atomicAdd(&ro.cursor[REGION_SPILL_WORD + 1], 1u);  // it filled
+  }
   __syncthreads();
+  if (sp[0]) {  // (uniform) a region is full: one spill reservation for the workgroup
+    if (threadIdx.x == 0) {
+      sp[1] = atomicAdd(&ro.cursor[REGION_SPILL_WORD], sp[0]);
+      atomicOr(ro.overflow, 1u);
+    }
+    __syncthreads();
+  }
   if (live) {
     const uint64_t slot = (uint64_t)base[bkt] + r;
     if (slot < ro.cap) {
       ro.rkeys[(uint64_t)bkt * ro.cap + slot] = m;
       ro.rfile[(uint64_t)bkt * ro.cap + slot] = (uint32_t)f;
     } else {
-      atomicOr(ro.overflow, 1u);
+      const uint64_t d = (uint64_t)sp[1] + spoff[bkt] + (slot - (base[bkt] > ro.cap ? base[bkt] : ro.cap));
+      ro.spill_keys[d] = m;
+      ro.spill_file[d] = (uint32_t)f;
     }
   }
 }
@@ -667,10 +694,12 @@ hipError_t hash_sampled(const uint8_t* content, uint64_t stride, const uint64_t*
 
 hipError_t hash_sampled_regions(const uint8_t* content, uint64_t stride, const uint64_t* sizes,
                                 uint64_t n, uint64_t* keys, uint32_t* rep, uint64_t* rkeys,
-                                uint32_t* rfile, uint32_t* cursor, uint64_t cap, uint32_t* overflow,
-                                uint64_t* objects, hipStream_t s, uint32_t cus) {
+                                uint32_t* rfile, uint32_t* cursor, uint64_t cap, uint64_t* spill_keys,
+                                uint32_t* spill_file, uint32_t* overflow, uint64_t* objects,
+                                hipStream_t s, uint32_t cus) {
   if (n == 0) return hipSuccess;
-  const RegionOut ro{rkeys, rfile, cursor, cap, rep, overflow, (unsigned long long*)objects};
+  const RegionOut ro{rkeys, rfile, cursor, cap, spill_keys, spill_file, rep, overflow,
+                     (unsigned long long*)objects};
   const uint64_t blocks = (n + SAMPLED_BLOCK - 1) / SAMPLED_BLOCK;
   const uint64_t quanta = cus ? (n + (uint64_t)cus * 256 - 1) / ((uint64_t)cus * 256) : 0;
   if (cus && (blocks < cus || (quanta & 1))) {  // the grid choice of hash_sampled

@@ -36,15 +36,19 @@ class HostPool {
   }
   void run(unsigned k, const std::function<void()>& fn) {
     if (k <= 1) { fn(); return; }
+    run2(k - 1, fn, fn);
+  }
+  // `workers` pool threads run fn while the caller runs caller_fn; returns when all are done
+  void run2(unsigned workers, const std::function<void()>& fn, const std::function<void()>& caller_fn) {
     std::unique_lock<std::mutex> lk(mu_);
-    while (th_.size() + 1 < k) th_.emplace_back([this] { loop(); });
+    while (th_.size() < workers) th_.emplace_back([this] { loop(); });
     fn_ = &fn;
-    want_ = k - 1;
-    pending_ = k - 1;
+    want_ = workers;
+    pending_ = workers;
     ++gen_;
     lk.unlock();
     cv_.notify_all();
-    fn();
+    caller_fn();
     lk.lock();
     done_.wait(lk, [this] { return pending_ == 0; });
     fn_ = nullptr;
@@ -147,6 +151,12 @@ struct SdTrace {
   std::string line;
   SdTrace(bool on_, const char* call_, size_t n_) : on(on_), call(call_), n(n_) {
     if (on) t0 = last = std::chrono::steady_clock::now();
+  }
+  void note(const char* name, double v) {
+    if (!on) return;
+    char buf[64];
+    snprintf(buf, sizeof buf, " %s=%.1f", name, v);
+    line += buf;
   }
   void mark(const char* name) {
     if (!on) return;

@@ -680,10 +680,15 @@ __device__ __forceinline__ uint64_t g_find(const uint64_t* tk, uint64_t cap, uin
 // profiles/r03b_group_ab/).
 // Regions (the fused hash + group chain): counts != nullptr — bucket b's keys are rows
 // [b * region_cap, b * region_cap + min(counts[b], region_cap)) and the workgroup re-zeroes
-// counts[b] after reading it (the region cursors' persistent-zero invariant).  With `rescan`
-// (the standalone small-batch chain) a region whose count passed its capacity is regrouped
-// exactly from the whole input rescan[0, rescan_n) (keys of this bucket only) in a global
-// table of 2 x count slots carved from *spill.
+// counts[b] after reading it (the region cursors' persistent-zero invariant).  A region whose
+// count passed its capacity (a key repeated thousands of times) also takes its rows from the
+// spill list (spill_keys/spill_pos[0, *spill_cnt): the rows of every full region, in no
+// order; entries of other regions are skipped) — the same LDS table over region rows +
+// spilled rows, so a hot key costs its own rows, not a pass over the input.  spill_cnt[0]
+// (rows spilled), spill_cnt[1] (full regions, counted by the partition) and spill_cnt[2]
+// (full regions done) are zero on entry; the last full region's workgroup re-zeroes them.  Only when such a region's distinct keys
+// overflow the LDS table too is it regrouped exactly from the whole input rescan[0, rescan_n)
+// (keys of this bucket only) in a global table of 2 x count slots carved from *spill.
 template <uint32_t TBL, int THREADS, int NI, bool KEEP_SLOT>
 __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict__ rezero,
                                            uint32_t rezero_words,
@@ -700,7 +705,10 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
                                            const uint64_t* __restrict__ rescan = nullptr,
                                            uint64_t rescan_n = 0,
                                            unsigned long long* __restrict__ spill = nullptr,
-                                           uint32_t count_stride = 1) {
+                                           uint32_t count_stride = 1,
+                                           const uint64_t* __restrict__ spill_keys = nullptr,
+                                           const uint32_t* __restrict__ spill_pos = nullptr,
+                                           uint32_t* __restrict__ spill_cnt = nullptr) {
   constexpr uint32_t TILE = THREADS * NI;
   constexpr uint32_t FILL = TBL / 8 * 7;  // above this the bucket goes to global memory
   static_assert(TILE < TBL, "one-trip buckets must leave an empty slot (lds_claim's unbounded probe)");
@@ -711,33 +719,71 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
   // single flag could be raised by a fast wave's trip-(t+1) insert while a slower wave was
   // still reading it for trip t+1, splitting the waves over different barriers
   __shared__ int ovf[2];
-  __shared__ uint32_t region_n;
+  __shared__ uint32_t region_n, sp_n;
   __shared__ unsigned long long spill_off;
   const uint32_t b = bucket;
   // the chain's bucket totals were last read by the scatter: zero them for the next call
   // (the persistent buffer's invariant, see hash_group_min)
   if (bucket == 0)
     for (uint32_t i = threadIdx.x; i < rezero_words; i += THREADS) rezero[i] = 0;
-  uint64_t s, e;
+  // rows [s, e_rows) are the bucket's own; [e_rows, e) index the spill list (regions only)
+  uint64_t s, e, e_rows;
   if (counts) {
     if (threadIdx.x == 0) {
       region_n = counts[b * count_stride];
       counts[b * count_stride] = 0;
+      uint32_t c = 0;
+      if (spill_cnt && region_n > region_cap) {
+        // only full regions read the spill count; the partition counted them (spill_cnt[1]),
+        // so the last of them re-zeroes the three counters — regions that fit pay nothing
+        c = __hip_atomic_load(spill_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t full = __hip_atomic_load(spill_cnt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __threadfence();  // the reads land before this workgroup counts itself done
+        if (atomicAdd(spill_cnt + 2, 1u) == full - 1) {
+          spill_cnt[0] = 0;
+          spill_cnt[1] = 0;
+          spill_cnt[2] = 0;
+        }
+      }
+      sp_n = c;
     }
     __syncthreads();
     s = (uint64_t)b * region_cap;
-    e = s + (region_n < region_cap ? region_n : region_cap);
-    if (rescan && region_n > region_cap) e = s;  // (uniform) straight to the whole-input regroup
+    e = e_rows = s + (region_n < region_cap ? region_n : region_cap);
+    if (rescan && region_n > region_cap) {
+      if (spill_keys) e += sp_n;  // region rows + the spilled rows of this region
+      else e = e_rows = s;        // (uniform) no spill list: straight to the whole-input regroup
+    }
   } else {
     s = starts[b];
-    e = b + 1 < nb ? starts[b + 1] : n;
+    e = e_rows = b + 1 < nb ? starts[b + 1] : n;
   }
   // every stored key of this bucket has top bits == b, so a key from bucket b^1 is never
   // stored; the table is initialised while the bucket bounds are in flight
   const uint64_t empty = (uint64_t)(b ^ 1u) << (64 - bits);
+  // row i of the bucket: its own rows, then the spill entries (other regions' read as empty)
+  const bool spilled = e != e_rows;  // (uniform)
+  auto load = [&](uint64_t i, uint64_t& kk, uint32_t& pp) {
+    if (!spilled) {  // every bucket but a full region's: a predicated load
+      kk = i < e ? pkeys[i] : empty;
+      pp = i < e ? ppos[i] : 0u;
+    } else if (i < e_rows) {
+      kk = pkeys[i];
+      pp = ppos[i];
+    } else if (i < e) {
+      kk = spill_keys[i - e_rows];
+      pp = spill_pos[i - e_rows];
+      if ((uint32_t)(kk >> (64 - bits)) != b) { kk = empty; pp = 0u; }
+    } else {
+      kk = empty;
+      pp = 0u;
+    }
+  };
   for (uint32_t i = threadIdx.x; i < TBL; i += THREADS) { tk[i] = empty; tv[i] = 0xFFFFFFFFu; }
   if (threadIdx.x == 0) { distinct = 0; ovf[0] = 0; ovf[1] = 0; }
-  const bool whole = counts && rescan && region_n > region_cap;
+  // a region past its capacity: exact from its rows + spill in LDS, else from the whole input
+  const bool full = counts && rescan && region_n > region_cap;
+  const bool whole = full && !spill_keys;
   if (s == e && !whole) return;  // uniform for the whole workgroup
 #if SD_DBG
   __shared__ unsigned int dbg_seen;  // keys inserted: must be the bucket's e - s
@@ -748,11 +794,7 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
   uint32_t trip = 0;
   for (uint64_t base = s; base < e; base += TILE, ++trip) {
 #pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const uint64_t i = base + (uint64_t)j * THREADS + threadIdx.x;
-      k[j] = i < e ? pkeys[i] : empty;
-      p[j] = i < e ? ppos[i] : 0u;
-    }
+    for (int j = 0; j < NI; ++j) load(base + (uint64_t)j * THREADS + threadIdx.x, k[j], p[j]);
 #pragma unroll
     for (int j = 0; j < NI; ++j) v[j] = (vals && k[j] != empty) ? vals[p[j]] : p[j];
     __syncthreads();  // table initialised (first trip) / the previous trip's flag visible
@@ -800,7 +842,8 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
   }
   __syncthreads();
   const bool overflow = whole || (ovf[0] | ovf[1]);
-  SD_DBG_CHECK(threadIdx.x != 0 || overflow || (dbg_seen == e - s && distinct <= e - s),
+  SD_DBG_CHECK(threadIdx.x != 0 || overflow || spilled ||
+                   (dbg_seen == e - s && distinct <= e - s),
                "bucket %u: inserted %u of %llu keys, %u distinct", b, dbg_seen,
                (unsigned long long)(e - s), distinct);
   if (!overflow) {
@@ -815,11 +858,7 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
     } else {
       for (uint64_t base = s; base < e; base += TILE) {
 #pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          const uint64_t i = base + (uint64_t)j * THREADS + threadIdx.x;
-          k[j] = i < e ? pkeys[i] : empty;
-          p[j] = i < e ? ppos[i] : 0u;
-        }
+        for (int j = 0; j < NI; ++j) load(base + (uint64_t)j * THREADS + threadIdx.x, k[j], p[j]);
 #pragma unroll
         for (int j = 0; j < NI; ++j)
           if (k[j] != empty) {
@@ -832,31 +871,33 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
     return;
   }
   // Overflow: redo the bucket in its own 2m-slot global table (load <= 1/2); a region past
-  // its capacity (whole) from the whole input, in 2 x count slots carved from *spill
-  const uint64_t m = whole ? (uint64_t)region_n : e - s, cap = 2 * m;
-  if (whole && threadIdx.x == 0) spill_off = atomicAdd(spill, (unsigned long long)cap);
+  // its capacity (its rows + spill may exceed the region's own 2 x cap slots) from the whole
+  // input, in 2 x count slots carved from *spill
+  const bool wh = whole || full;
+  const uint64_t m = wh ? (uint64_t)region_n : e - s, cap = 2 * m;
+  if (wh && threadIdx.x == 0) spill_off = atomicAdd(spill, (unsigned long long)cap);
   __syncthreads();
-  uint64_t* gk = gkeys + (whole ? (uint64_t)spill_off : 2 * s);
-  uint32_t* gv = gvals + (whole ? (uint64_t)spill_off : 2 * s);
+  uint64_t* gk = gkeys + (wh ? (uint64_t)spill_off : 2 * s);
+  uint32_t* gv = gvals + (wh ? (uint64_t)spill_off : 2 * s);
   for (uint64_t i = threadIdx.x; i < cap; i += THREADS) { gk[i] = empty; gv[i] = 0xFFFFFFFFu; }
   if (threadIdx.x == 0) distinct = 0;
   __threadfence();
   __syncthreads();
-  const uint64_t lo = whole ? 0 : s, hi = whole ? rescan_n : e;
+  const uint64_t lo = wh ? 0 : s, hi = wh ? rescan_n : e;
   uint32_t fresh = 0;
   for (uint64_t i = lo + threadIdx.x; i < hi; i += THREADS) {
-    const uint64_t kk = whole ? mix64(rescan[i]) : pkeys[i];
-    if (whole && (uint32_t)(kk >> (64 - bits)) != b) continue;
-    const uint32_t pp = whole ? (uint32_t)i : ppos[i];
+    const uint64_t kk = wh ? mix64(rescan[i]) : pkeys[i];
+    if (wh && (uint32_t)(kk >> (64 - bits)) != b) continue;
+    const uint32_t pp = wh ? (uint32_t)i : ppos[i];
     g_insert(gk, gv, cap, (kk & 0xFFFFFFFFull) % cap, kk, vals ? vals[pp] : pp, empty, fresh);
   }
   if (fresh) atomicAdd(&distinct, fresh);
   __threadfence();
   __syncthreads();
   for (uint64_t i = lo + threadIdx.x; i < hi; i += THREADS) {
-    const uint64_t kk = whole ? mix64(rescan[i]) : pkeys[i];
-    if (whole && (uint32_t)(kk >> (64 - bits)) != b) continue;
-    const uint32_t pp = whole ? (uint32_t)i : ppos[i];
+    const uint64_t kk = wh ? mix64(rescan[i]) : pkeys[i];
+    if (wh && (uint32_t)(kk >> (64 - bits)) != b) continue;
+    const uint32_t pp = wh ? (uint32_t)i : ppos[i];
     const uint64_t slot = g_find(gk, cap, (kk & 0xFFFFFFFFull) % cap, kk);
     const uint32_t mv = __hip_atomic_load(&gv[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (mv != (vals ? vals[pp] : pp)) out[pp] = mv;
@@ -897,10 +938,12 @@ sd_bucket_min_big(const uint64_t* __restrict__ pkeys, const uint32_t* __restrict
 // straight from the regions — no totals, scatter or refine launch.  2^9 regions: 512 lanes x 7
 // keys over a 6,144-slot table (72 KiB, two workgroups per CU; a region of <= 3,584 keys, every
 // batch up to BIG_MAX_KEYS, is one trip).  2^8 regions: the 1,024-lane big table.  A region
-// whose cursor passed its capacity (K1G counted rows it could not store) is regrouped by its
-// workgroup from the whole key array `keys` (K1G's output, unmixed) in a global table carved
-// from the region set's 2 x rows overflow slots by *spill (objects[1], zeroed by K1G): the
-// batch's grouping is exact whatever the key distribution, with no host regroup.
+// whose cursor passed its capacity (K1G appended the rows it could not store to the set's
+// spill list) takes its rows from the region and the spill list (bucket_min); only if its
+// distinct keys overflow the LDS table too is it regrouped from the whole key array `keys`
+// (K1G's output, unmixed) in a global table carved from the set's 2 x rows overflow slots by
+// objects[1] (zeroed by K1G): the grouping is exact whatever the key distribution, with no
+// host regroup.
 constexpr uint32_t REG_TABLE = REGION_BITS >= 9 ? 6144 : BIG_TABLE;
 constexpr int REG_THREADS = REGION_BITS >= 9 ? 512 : BIG_THREADS;
 constexpr int REG_ITEMS = REGION_BITS >= 9 ? 7 : ITEMS;
@@ -908,10 +951,13 @@ extern "C" __global__ void __launch_bounds__(REG_THREADS)
 sd_bucket_min_regions(const uint64_t* __restrict__ rkeys, const uint32_t* __restrict__ rfile,
                       uint32_t* __restrict__ cursor, uint64_t cap, uint32_t* __restrict__ out,
                       unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
-                      uint32_t* __restrict__ gvals, const uint64_t* __restrict__ keys, uint64_t n) {
+                      uint32_t* __restrict__ gvals, const uint64_t* __restrict__ keys, uint64_t n,
+                      const uint64_t* __restrict__ spill_keys, const uint32_t* __restrict__ spill_file) {
   bucket_min<REG_TABLE, REG_THREADS, REG_ITEMS, true>(blockIdx.x, nullptr, 0, rkeys, rfile, nullptr,
                                                       nullptr, REGIONS, REGION_BITS, 0, out, objects,
-                                                      gkeys, gvals, cursor, cap, keys, n, objects + 1);
+                                                      gkeys, gvals, cursor, cap, keys, n, objects + 1,
+                                                      1, spill_keys, spill_file,
+                                                      cursor + REGION_SPILL_WORD);
 }
 
 // The standalone chain for small batches (<= BIG_MAX_KEYS keys, default plan): the keys
@@ -919,9 +965,11 @@ sd_bucket_min_regions(const uint64_t* __restrict__ rkeys, const uint32_t* __rest
 // (mixed key, row), out[] prefilled, one LDS histogram per 4,096 keys and one reservation
 // atomic per (workgroup, non-empty region) — then the region tables: two launches instead
 // of totals + scatter + tables.  A region past its capacity (a key repeated thousands of
-// times) keeps counting in its cursor and its table workgroup regroups it from the whole
-// input.  cursor: REGIONS u32 CURSOR_STRIDE apart (own 128-B lines), zero on entry (the
-// tables re-zero them).
+// times) keeps counting in its cursor and its extra rows go to the spill list (one
+// reservation per workgroup that has any), which its table workgroup reads after the region
+// rows.  cursor: REGIONS u32 CURSOR_STRIDE apart (own 128-B lines), then at REGIONS *
+// CURSOR_STRIDE the spill count, the full-region count and the tables' done count; all zero
+// on entry (the tables re-zero them).
 #ifndef SD_REGION_CURSOR_STRIDE
 #define SD_REGION_CURSOR_STRIDE 32
 #endif
@@ -933,9 +981,11 @@ extern "C" __global__ void __launch_bounds__(RPART_THREADS)
 sd_region_partition(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ vals, uint64_t n,
                     uint64_t* __restrict__ rkeys, uint32_t* __restrict__ rfile,
                     uint32_t* __restrict__ cursor, uint64_t cap, uint32_t* __restrict__ out,
-                    unsigned long long* __restrict__ objects, unsigned long long* __restrict__ spill) {
+                    unsigned long long* __restrict__ objects, unsigned long long* __restrict__ spill,
+                    uint64_t* __restrict__ spill_keys, uint32_t* __restrict__ spill_file) {
   static_assert(RPART_THREADS == PART_THREADS, "lds_exclusive_scan runs on PART_THREADS lanes");
-  __shared__ uint32_t tcnt[REGIONS], tstart[REGIONS], gbase[REGIONS];
+  __shared__ uint32_t tcnt[REGIONS], tstart[REGIONS], gbase[REGIONS], spoff[REGIONS];
+  __shared__ uint32_t sp_local, sp_base;
   __shared__ uint64_t skey[RPART_TILE];
   __shared__ uint32_t sfile[RPART_TILE];
   const uint64_t b0 = (uint64_t)blockIdx.x * RPART_TILE;
@@ -956,6 +1006,7 @@ sd_region_partition(const uint64_t* __restrict__ keys, const uint32_t* __restric
     }
   }
   for (uint32_t i = threadIdx.x; i < REGIONS; i += RPART_THREADS) tcnt[i] = 0;
+  if (threadIdx.x == 0) sp_local = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) { *objects = 0; *spill = 0; }
   __syncthreads();
 #pragma unroll
@@ -970,11 +1021,22 @@ sd_region_partition(const uint64_t* __restrict__ keys, const uint32_t* __restric
   __syncthreads();
   // one reservation per non-empty region, then the tile counting-sorted by region in LDS so
   // that consecutive lanes store consecutive rows of one region's run
+  // rows past a region's capacity: the tile's run of them per region (spoff) inside one
+  // spill reservation per workgroup
   for (uint32_t b = threadIdx.x; b < REGIONS; b += RPART_THREADS) {
     const uint32_t h = tcnt[b];
-    gbase[b] = h ? atomicAdd(&cursor[b * CURSOR_STRIDE], h) : 0u;
+    const uint32_t g = h ? atomicAdd(&cursor[b * CURSOR_STRIDE], h) : 0u;
+    gbase[b] = g;
+    const uint64_t lo = g > cap ? g : cap;
+    const uint32_t sp = g + h > lo ? (uint32_t)(g + h - lo) : 0u;
+    spoff[b] = sp ? atomicAdd(&sp_local, sp) : 0u;
+    if (g <= cap && g + h > cap) atomicAdd(&cursor[REGIONS * CURSOR_STRIDE + 1], 1u);  // it filled
   }
-  lds_exclusive_scan(tcnt, tstart, REGIONS);  // (its barriers also publish gbase)
+  lds_exclusive_scan(tcnt, tstart, REGIONS);  // (its barriers also publish gbase, spoff)
+  if (sp_local) {  // (uniform) this tile overflowed a region
+    if (threadIdx.x == 0) sp_base = atomicAdd(&cursor[REGIONS * CURSOR_STRIDE], sp_local);
+    __syncthreads();
+  }
   // conservation: the tile's per-region counts add up to the tile
   SD_DBG_CHECK(threadIdx.x != 0 || tstart[REGIONS - 1] + tcnt[REGIONS - 1] == tile_n,
                "region partition (block %u) counted %u of %u keys", blockIdx.x,
@@ -996,9 +1058,13 @@ sd_region_partition(const uint64_t* __restrict__ keys, const uint32_t* __restric
       const uint64_t kk = skey[t];
       const uint32_t b = (uint32_t)(kk >> (64 - REGION_BITS));
       const uint64_t o = (uint64_t)gbase[b] + (t - tstart[b]);
-      if (o < cap) {  // rows past the capacity only counted (the table regroups the region)
+      if (o < cap) {
         rkeys[(uint64_t)b * cap + o] = kk;
         rfile[(uint64_t)b * cap + o] = sfile[t];
+      } else {  // past the capacity: the spill list (the region's table reads it)
+        const uint64_t d = (uint64_t)sp_base + spoff[b] + (o - (gbase[b] > cap ? gbase[b] : cap));
+        spill_keys[d] = kk;
+        spill_file[d] = sfile[t];
       }
     }
   }
@@ -1010,11 +1076,14 @@ sd_bucket_min_regions_keys(const uint64_t* __restrict__ rkeys, const uint32_t* _
                            const uint64_t* __restrict__ keys, const uint32_t* __restrict__ vals,
                            uint64_t n, uint32_t* __restrict__ out,
                            unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
-                           uint32_t* __restrict__ gvals, unsigned long long* __restrict__ spill) {
+                           uint32_t* __restrict__ gvals, unsigned long long* __restrict__ spill,
+                           const uint64_t* __restrict__ spill_keys,
+                           const uint32_t* __restrict__ spill_file) {
   bucket_min<REG_TABLE, REG_THREADS, REG_ITEMS, true>(blockIdx.x, nullptr, 0, rkeys, rfile, vals,
                                                       nullptr, REGIONS, REGION_BITS, 0, out, objects,
                                                       gkeys, gvals, cursor, cap, keys, n, spill,
-                                                      CURSOR_STRIDE);
+                                                      CURSOR_STRIDE, spill_keys, spill_file,
+                                                      cursor + REGIONS * CURSOR_STRIDE);
 }
 
 // The region chain above 1.44 M keys (default plan): one pass of the keys into 2^b1 fixed-
@@ -1296,28 +1365,33 @@ uint64_t region_capacity(uint64_t n) {
 
 bool region_group_supported(uint64_t n) { return n > 0 && n <= BIG_MAX_KEYS; }
 
-// workspace: rkeys | rfile | global overflow tables (2 slots per region row)
+// workspace: rkeys | rfile | global overflow tables (2 slots per region row) | spill list
+// (keys, files: n rows at most)
 size_t region_group_workspace_bytes(uint64_t n) {
   const uint64_t rows = (uint64_t)REGIONS * region_capacity(n);
-  return al256(rows * 8) + al256(rows * 4) + al256(2 * rows * 8) + al256(2 * rows * 4);
+  return al256(rows * 8) + al256(rows * 4) + al256(2 * rows * 8) + al256(2 * rows * 4) +
+         al256(n * 8) + al256(n * 4);
 }
 
 void region_group_layout(void* ws, uint64_t n, uint64_t** rkeys, uint32_t** rfile, uint64_t** gkeys,
-                         uint32_t** gvals) {
+                         uint32_t** gvals, uint64_t** spill_keys, uint32_t** spill_file) {
   const uint64_t rows = (uint64_t)REGIONS * region_capacity(n);
   char* q = (char*)ws;
   *rkeys = (uint64_t*)q; q += al256(rows * 8);
   *rfile = (uint32_t*)q; q += al256(rows * 4);
   *gkeys = (uint64_t*)q; q += al256(2 * rows * 8);
-  *gvals = (uint32_t*)q;
+  *gvals = (uint32_t*)q; q += al256(2 * rows * 4);
+  *spill_keys = (uint64_t*)q; q += al256(n * 8);
+  *spill_file = (uint32_t*)q;
 }
 
 hipError_t region_group_min(const uint64_t* rkeys, const uint32_t* rfile, uint32_t* cursor,
                             uint64_t cap, uint32_t* out, uint64_t* d_objects, uint64_t* gkeys,
-                            uint32_t* gvals, const uint64_t* keys, uint64_t n, hipStream_t s) {
+                            uint32_t* gvals, const uint64_t* keys, uint64_t n,
+                            const uint64_t* spill_keys, const uint32_t* spill_file, hipStream_t s) {
   sd_bucket_min_regions<<<REGIONS, REG_THREADS, 0, s>>>(rkeys, rfile, cursor, cap, out,
                                                         (unsigned long long*)d_objects, gkeys, gvals,
-                                                        keys, n);
+                                                        keys, n, spill_keys, spill_file);
   return hipGetLastError();
 }
 
@@ -1404,10 +1478,11 @@ static uint64_t region_capacity_nb(uint64_t n, uint32_t nb) {
   return (uint64_t)mean + 1 + 8 * sd + 64;
 }
 
-// its workspace: rkeys | rfile | overflow tables (2n slots) | spill cursor
+// its workspace: rkeys | rfile | overflow tables (2n slots) | carve cursor | spill list (n rows)
 static size_t small_regions_bytes(uint64_t n) {
   const uint64_t rows = (uint64_t)REGIONS * region_capacity(n);
-  return al256(rows * 8) + al256(rows * 4) + al256(2 * n * 8) + al256(2 * n * 4) + 256;
+  return al256(rows * 8) + al256(rows * 4) + al256(2 * n * 8) + al256(2 * n * 4) + 256 +
+         al256(n * 8) + al256(n * 4);
 }
 
 static bool big_regions(const GroupPlan& g, uint64_t target) {
@@ -1519,7 +1594,8 @@ hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n
                           uint64_t target) {
   if (n == 0) return hipMemsetAsync(d_objects, 0, 8, s);
   if (!hash_group_supported(n)) return hipErrorInvalidValue;
-  static_assert(REGIONS * CURSOR_STRIDE <= GROUP_TOTALS_WORDS, "the cursors fit the totals buffer");
+  static_assert(REGIONS * CURSOR_STRIDE + 3 <= GROUP_TOTALS_WORDS,
+                "the cursors, spill and done counts fit the totals buffer");
   static_assert((1024 + 1) * CURSOR_STRIDE <= GROUP_TOTALS_WORDS,
                 "the big chain's cursors and spill count fit the totals buffer");
   if (small_regions(n, target)) {  // `totals` (zero, left zero) holds the region cursors
@@ -1529,12 +1605,15 @@ hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n
     uint32_t* rfile = (uint32_t*)q; q += al256(rows * 4);
     uint64_t* gkeys = (uint64_t*)q; q += al256(2 * n * 8);
     uint32_t* gvals = (uint32_t*)q; q += al256(2 * n * 4);
-    unsigned long long* spill = (unsigned long long*)q;
+    unsigned long long* spill = (unsigned long long*)q; q += 256;
+    uint64_t* skeys = (uint64_t*)q; q += al256(n * 8);
+    uint32_t* sfile = (uint32_t*)q;
     unsigned long long* obj = (unsigned long long*)d_objects;
     sd_region_partition<<<(uint32_t)((n + RPART_TILE - 1) / RPART_TILE), RPART_THREADS, 0, s>>>(
-        keys, vals, n, rkeys, rfile, totals, cap, out, obj, spill);
+        keys, vals, n, rkeys, rfile, totals, cap, out, obj, spill, skeys, sfile);
     sd_bucket_min_regions_keys<<<REGIONS, REG_THREADS, 0, s>>>(rkeys, rfile, totals, cap, keys, vals,
-                                                               n, out, obj, gkeys, gvals, spill);
+                                                               n, out, obj, gkeys, gvals, spill, skeys,
+                                                               sfile);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) (void)hipMemsetAsync(totals, 0, GROUP_TOTALS_WORDS * 4, s);  // restore
     return e;

@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -95,8 +96,8 @@ int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
       hipMalloc((void**)&c->d_scalar, 64) != hipSuccess ||
       hipMalloc((void**)&c->gtotals, GROUP_TOTALS_WORDS * 4) != hipSuccess ||
       hipMemset(c->gtotals, 0, GROUP_TOTALS_WORDS * 4) != hipSuccess ||
-      hipMalloc((void**)&c->gcursor, 2 * REGIONS * 4) != hipSuccess ||
-      hipMemset(c->gcursor, 0, 2 * REGIONS * 4) != hipSuccess ||
+      hipMalloc((void**)&c->gcursor, 2 * REGION_SET_WORDS * 4) != hipSuccess ||
+      hipMemset(c->gcursor, 0, 2 * REGION_SET_WORDS * 4) != hipSuccess ||
       hipEventCreateWithFlags(&c->region_done[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->region_done[1], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->region_hashed[0], hipEventDisableTiming) != hipSuccess ||
@@ -347,8 +348,8 @@ static bool fused_eligible(const sd_cas_ctx* c, size_t n) {
          c->group_target == 0;
 }
 
-// region set k's buffer: rkeys | rfile | gkeys | gvals (region_group_layout) | objects u64 |
-// overflow carve cursor u64
+// region set k's buffer: rkeys | rfile | gkeys | gvals | spill keys | spill files
+// (region_group_layout) | objects u64 | overflow carve cursor u64
 static uint64_t* region_objects(sd_cas_ctx* c, int k) {
   return (uint64_t*)((char*)c->regions[k].p + region_group_workspace_bytes(c->region_n[k]));
 }
@@ -373,8 +374,8 @@ int sd_cas_hash_regions_sampled_dev(sd_cas_ctx* c, const void* d_content, uint64
   if (c->region_pending[k]) HIP_TRY(c, hipStreamWaitEvent(s, c->region_done[k], 0));
   if (!c->region_grouped[k]) {
     HIP_TRY(c, hipStreamWaitEvent(s, c->region_hashed[k], 0));
-    // its cursors were left counted: clear them
-    HIP_TRY(c, hipMemsetAsync(c->gcursor + REGIONS * k, 0, REGIONS * 4, s));
+    // its cursors and spill count were left counted: clear them
+    HIP_TRY(c, hipMemsetAsync(c->gcursor + REGION_SET_WORDS * k, 0, REGION_SET_WORDS * 4, s));
   }
   if (c->region_obj_set == k) {
     // set k holds the Object count of the context's last grouping, which this refill's K1G
@@ -387,14 +388,15 @@ int sd_cas_hash_regions_sampled_dev(sd_cas_ctx* c, const void* d_content, uint64
   c->region_n[k] = n;  // sizes the layout (ensure below grows the set if needed)
   int rc = ensure(c, c->regions[k], region_group_workspace_bytes(n) + 256);
   if (rc) return rc;
-  uint64_t *rkeys, *gkeys;
-  uint32_t *rfile, *gvals;
-  region_group_layout(c->regions[k].p, n, &rkeys, &rfile, &gkeys, &gvals);
+  uint64_t *rkeys, *gkeys, *skeys;
+  uint32_t *rfile, *gvals, *sfile;
+  region_group_layout(c->regions[k].p, n, &rkeys, &rfile, &gkeys, &gvals, &skeys, &sfile);
+  uint32_t* cur = c->gcursor + REGION_SET_WORDS * k;
   hipError_t e = hash_sampled_regions((const uint8_t*)d_content, stride, d_sizes, n, d_keys, d_rep,
-                                      rkeys, rfile, c->gcursor + REGIONS * k, region_capacity(n), d_overflow,
+                                      rkeys, rfile, cur, region_capacity(n), skeys, sfile, d_overflow,
                                       region_objects(c, k), s, (uint32_t)(c->quantum / 256));
   if (e != hipSuccess) {
-    (void)hipMemsetAsync(c->gcursor + REGIONS * k, 0, REGIONS * 4, s);  // restore the cursors' invariant
+    (void)hipMemsetAsync(cur, 0, REGION_SET_WORDS * 4, s);  // restore the cursors' invariant
     return fail(c, SD_CAS_EHIP, "hash_regions: %s", hipGetErrorString(e));
   }
   HIP_TRY(c, hipEventRecord(c->region_hashed[k], s));
@@ -412,15 +414,16 @@ int sd_cas_group_regions_dev(sd_cas_ctx* c, size_t n, uint32_t* d_rep, uint64_t*
     return fail(c, SD_CAS_EINVAL, "group_regions: no ungrouped hash_regions batch of %zu files", n);
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t s = pick(c, stream);
-  uint64_t *rkeys, *gkeys;
-  uint32_t *rfile, *gvals;
-  region_group_layout(c->regions[k].p, n, &rkeys, &rfile, &gkeys, &gvals);
+  uint64_t *rkeys, *gkeys, *skeys;
+  uint32_t *rfile, *gvals, *sfile;
+  region_group_layout(c->regions[k].p, n, &rkeys, &rfile, &gkeys, &gvals, &skeys, &sfile);
   uint64_t* obj = region_objects(c, k);
+  uint32_t* cur = c->gcursor + REGION_SET_WORDS * k;
   HIP_TRY(c, hipStreamWaitEvent(s, c->region_hashed[k], 0));  // after its K1G, whatever stream
-  hipError_t e = region_group_min(rkeys, rfile, c->gcursor + REGIONS * k, region_capacity(n), d_rep, obj,
-                                  gkeys, gvals, c->region_keys[k], n, s);
+  hipError_t e = region_group_min(rkeys, rfile, cur, region_capacity(n), d_rep, obj, gkeys, gvals,
+                                  c->region_keys[k], n, skeys, sfile, s);
   if (e != hipSuccess) {
-    (void)hipMemsetAsync(c->gcursor + REGIONS * k, 0, REGIONS * 4, s);
+    (void)hipMemsetAsync(cur, 0, REGION_SET_WORDS * 4, s);
     return fail(c, SD_CAS_EHIP, "group_regions: %s", hipGetErrorString(e));
   }
   HIP_TRY(c, hipEventRecord(c->region_done[k], s));
@@ -761,26 +764,33 @@ static int plan_batch(sd_cas_ctx* c, const uint64_t* buf_lens, const uint64_t* s
   return SD_CAS_OK;
 }
 
-// Enqueues, for a batch staged in pinned memory at `pin`: H2D to `dev` on the copy stream,
-// both hash sub-batches on the compute stream, and D2H of the keys back to `pin` (the
-// content area is reused).  `done` (optional) is recorded on the compute stream after it.
-static int enqueue_staged(sd_cas_ctx* c, const Plan& pl, const uint64_t* sizes, size_t n,
-                          char* pin, char* dev, hipEvent_t done) {
+// Host side of a staged batch's metadata (sizes of both sub-batches, packed offsets; the
+// packed lens are written by the caller): [content][sizes][poffs][plens][keys].
+static void stage_meta(const Plan& pl, const uint64_t* sizes, char* pin) {
   const size_t ns = pl.sampled.size(), np = pl.packed.size();
   const size_t content_bytes = pl.sampled_bytes + up256(pl.packed_bytes);
-  const size_t meta_bytes = up256((ns + np) * 8) + up256(np * 8) + up256(np * 4) + up256(n * 8);
   uint64_t* h_sizes = (uint64_t*)(pin + content_bytes);
   uint64_t* h_poffs = (uint64_t*)((char*)h_sizes + up256((ns + np) * 8));
   for (size_t k = 0; k < ns; k++) h_sizes[k] = sizes[pl.sampled[k]];
   for (size_t k = 0; k < np; k++) h_sizes[ns + k] = sizes[pl.packed[k]];
   for (size_t k = 0; k < np; k++) h_poffs[k] = pl.poff[k];
-  // (packed lens were written into the staging by the caller)
+}
+
+// Enqueues, for a batch staged in pinned memory at `pin` (stage_meta done): H2D of
+// [h2d_lo, h2d_hi) of the staging to `dev` on the copy stream (the rest is already there),
+// both hash sub-batches on the compute stream after it, and D2H of the keys back to `pin`
+// (the content area is reused).  `done` (optional) is recorded on the compute stream after it.
+static int enqueue_hash(sd_cas_ctx* c, const Plan& pl, size_t n, char* pin, char* dev,
+                        hipEvent_t done, size_t h2d_lo, size_t h2d_hi) {
+  const size_t ns = pl.sampled.size(), np = pl.packed.size();
+  const size_t content_bytes = pl.sampled_bytes + up256(pl.packed_bytes);
   uint64_t* d_sizes = (uint64_t*)(dev + content_bytes);
   uint64_t* d_poffs = (uint64_t*)((char*)d_sizes + up256((ns + np) * 8));
   uint32_t* d_plens = (uint32_t*)((char*)d_poffs + up256(np * 8));
   uint64_t* d_keys = (uint64_t*)((char*)d_plens + up256(np * 4));
-  HIP_TRY(c, hipMemcpyAsync(dev, pin, content_bytes + meta_bytes - up256(n * 8),
-                            hipMemcpyHostToDevice, c->copy));
+  (void)n;
+  if (h2d_hi > h2d_lo)
+    HIP_TRY(c, hipMemcpyAsync(dev + h2d_lo, pin + h2d_lo, h2d_hi - h2d_lo, hipMemcpyHostToDevice, c->copy));
   HIP_TRY(c, hipEventRecord(c->h2d_done, c->copy));
   HIP_TRY(c, hipStreamWaitEvent(c->stream, c->h2d_done, 0));
   int rc;
@@ -793,6 +803,18 @@ static int enqueue_staged(sd_cas_ctx* c, const Plan& pl, const uint64_t* sizes, 
   HIP_TRY(c, hipMemcpyAsync(pin, d_keys, (ns + np) * 8, hipMemcpyDeviceToHost, c->stream));
   if (done) HIP_TRY(c, hipEventRecord(done, c->stream));
   return SD_CAS_OK;
+}
+
+// bytes of the staging before its keys: content + sizes + poffs + plens
+static size_t staged_h2d_bytes(const Plan& pl) {
+  const size_t ns = pl.sampled.size(), np = pl.packed.size();
+  return pl.sampled_bytes + up256(pl.packed_bytes) + up256((ns + np) * 8) + up256(np * 8) + up256(np * 4);
+}
+
+static int enqueue_staged(sd_cas_ctx* c, const Plan& pl, const uint64_t* sizes, size_t n,
+                          char* pin, char* dev, hipEvent_t done) {
+  stage_meta(pl, sizes, pin);
+  return enqueue_hash(c, pl, n, pin, dev, done, 0, staged_h2d_bytes(pl));
 }
 
 static void scatter_keys(const Plan& pl, const char* pin, uint64_t* out_keys) {
@@ -959,31 +981,45 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
   if ((rc = ensure(c, c->staging, nslots * slot))) return rc;
   hipEvent_t* done = c->gather_done;
   tr.mark("plan");
-  auto gather = [&](size_t w, char* pin) {
+  // The single-window batch (up to SMALL_BATCH_FILES: the reference's 100-file job step)
+  // streams its H2D behind the gather instead of after it: the pool threads read the files
+  // while this thread copies each finished prefix of the staging (STREAM_CHUNK bytes or
+  // more at a time) on the copy stream, so the batch costs about max(gather, H2D) + the last
+  // piece + the hash, not gather + H2D + hash.
+  constexpr size_t STREAM_CHUNK = 512u << 10;
+  constexpr size_t STREAM_MIN_FILES = 16;
+  char* pin0 = (char*)c->pinned;
+  char* dev0 = (char*)c->staging.p;
+  auto gather = [&](size_t w, char* pin, char* dev, bool streamed) {
     const Plan& pl = plans[w];
     const size_t f0 = wstart[w], m = wstart[w + 1] - wstart[w];
     const size_t ns = pl.sampled.size(), np = pl.packed.size();
     const size_t content_bytes = pl.sampled_bytes + up256(pl.packed_bytes);
     uint32_t* h_plens = (uint32_t*)(pin + content_bytes + up256((ns + np) * 8) + up256(np * 8));
     for (size_t k = 0; k < np; k++) h_plens[k] = (uint32_t)lens[f0 + pl.packed[k]];
+    const size_t items = ns + np;
     std::atomic<size_t> next{0};
-    c->pool.run(std::max(1u, std::min(16u, (unsigned)((m + 7) / 8))), [&]() {
-      for (size_t t; (t = next.fetch_add(1)) < ns + np;) {
+    std::unique_ptr<std::atomic<uint8_t>[]> fin;
+    if (streamed) {
+      fin.reset(new std::atomic<uint8_t>[items]);
+      for (size_t t = 0; t < items; t++) fin[t].store(0, std::memory_order_relaxed);
+    }
+    auto item = [&](size_t t) {
         const size_t li = t < ns ? pl.sampled[t] : pl.packed[t - ns];
         const size_t i = f0 + li;
-        if (status[i]) continue;
+        if (status[i]) return;
         char* dst = t < ns ? pin + t * (size_t)SAMPLED_CONTENT_LEN
                            : pin + pl.sampled_bytes + pl.poff[t - ns];
         int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
-        if (fd < 0) { status[i] = -errno; continue; }
+        if (fd < 0) { status[i] = -errno; return; }
         {
           struct stat st;
-          if (fstat(fd, &st) != 0) { status[i] = -errno; close(fd); continue; }
-          if (S_ISDIR(st.st_mode)) { status[i] = -EISDIR; close(fd); continue; }
+          if (fstat(fd, &st) != 0) { status[i] = -errno; close(fd); return; }
+          if (S_ISDIR(st.st_mode)) { status[i] = -EISDIR; close(fd); return; }
           if (sizes[i] <= MINIMUM_FILE_SIZE && (uint64_t)st.st_size != lens[i]) {
             redo[i] = 1;
             close(fd);
-            continue;
+            return;
           }
         }
         // cas.rs:35-58 offsets: header at 0, sample k at 8192 + k*jump (both from `size`,
@@ -1028,11 +1064,65 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
           dst += lns[k];
         }
         close(fd);
+    };
+    auto worker = [&]() {
+      for (size_t t; (t = next.fetch_add(1)) < items;) {
+        item(t);
+        if (streamed) fin[t].store(1, std::memory_order_release);
       }
-    });
+    };
+    const unsigned threads = std::max(1u, std::min(16u, (unsigned)((m + 7) / 8)));
+    if (!streamed) {
+      c->pool.run(threads, worker);
+      return SD_CAS_OK;
+    }
+    // the pump: metadata first, then each finished prefix of the content (items are taken
+    // in staging order, so a prefix of items is a prefix of bytes)
+    int prc = SD_CAS_OK;
+    size_t ncopies = 0;
+    double copy_us = 0, first_us = -1, last_us = 0;
+    const auto t_pump = std::chrono::steady_clock::now();
+    auto since = [&](std::chrono::steady_clock::time_point a) {
+      return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - a).count();
+    };
+    auto item_end = [&](size_t t) -> size_t {  // staging bytes of items [0, t)
+      if (t == items) return content_bytes;  // (incl. the packed area's tail pad)
+      return t <= ns ? t * (size_t)SAMPLED_CONTENT_LEN : pl.sampled_bytes + pl.poff[t - ns];
+    };
+    auto pump = [&]() {
+      const size_t meta_hi = staged_h2d_bytes(pl);
+      if (hipMemcpyAsync(dev + content_bytes, pin + content_bytes, meta_hi - content_bytes,
+                         hipMemcpyHostToDevice, c->copy) != hipSuccess)
+        prc = SD_CAS_EHIP;
+      size_t ready = 0, sent = 0;
+      while (sent < content_bytes) {
+        while (ready < items && fin[ready].load(std::memory_order_acquire)) ++ready;
+        const size_t hi = item_end(ready);
+        if (hi > sent && (hi - sent >= STREAM_CHUNK || ready == items)) {
+          const auto t0 = std::chrono::steady_clock::now();
+          if (first_us < 0 && tr.on) first_us = since(t_pump);
+          if (prc == SD_CAS_OK &&
+              hipMemcpyAsync(dev + sent, pin + sent, hi - sent, hipMemcpyHostToDevice, c->copy) != hipSuccess)
+            prc = SD_CAS_EHIP;
+          if (tr.on) { copy_us += since(t0); last_us = since(t_pump); ++ncopies; }
+          sent = hi;
+        } else {
+#if defined(__x86_64__)
+          __builtin_ia32_pause();
+#else
+          std::this_thread::yield();
+#endif
+        }
+      }
+    };
+    c->pool.run2(threads, worker, pump);
+    tr.note("copies", (double)ncopies);
+    tr.note("copy_api_us", copy_us);
+    tr.note("first_copy_at", first_us);
+    tr.note("last_copy_at", last_us);
+    if (prc) return fail(c, prc, "from_paths: streamed H2D failed");
+    return SD_CAS_OK;
   };
-  char* pin0 = (char*)c->pinned;
-  char* dev0 = (char*)c->staging.p;
   auto finish = [&](size_t w) -> int {
     const int b = (int)(w & 1);
     HIP_TRY(c, hipEventSynchronize(done[b]));
@@ -1042,10 +1132,15 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
   for (size_t w = 0; w < nw && rc == 0; w++) {
     const int b = (int)(w & 1);
     if (w >= 2 && (rc = finish(w - 2))) break;  // slot b free again
-    gather(w, pin0 + b * slot);
-    tr.mark("gather");
     const size_t f0 = wstart[w], m = wstart[w + 1] - wstart[w];
-    rc = enqueue_staged(c, plans[w], psize.data() + f0, m, pin0 + b * slot, dev0 + b * slot, done[b]);
+    const bool streamed = nw == 1 && m >= STREAM_MIN_FILES;
+    char* pin = pin0 + b * slot;
+    char* dev = dev0 + b * slot;
+    if (streamed) stage_meta(plans[w], psize.data() + f0, pin);
+    if ((rc = gather(w, pin, dev, streamed))) break;
+    tr.mark("gather");
+    rc = streamed ? enqueue_hash(c, plans[w], m, pin, dev, done[b], 0, 0)
+                  : enqueue_staged(c, plans[w], psize.data() + f0, m, pin, dev, done[b]);
     tr.mark("enqueue");
   }
   for (size_t w = nw >= 2 ? nw - 2 : 0; w < nw && rc == 0; w++) rc = finish(w);

@@ -34,8 +34,9 @@ hipError_t hash_sampled(const uint8_t* content, uint64_t stride, const uint64_t*
 // is full; *objects = 0 (the bucket tables count).
 hipError_t hash_sampled_regions(const uint8_t* content, uint64_t stride, const uint64_t* sizes,
                                 uint64_t n, uint64_t* keys, uint32_t* rep, uint64_t* rkeys,
-                                uint32_t* rfile, uint32_t* cursor, uint64_t cap, uint32_t* overflow,
-                                uint64_t* objects, hipStream_t s, uint32_t cus);
+                                uint32_t* rfile, uint32_t* cursor, uint64_t cap, uint64_t* spill_keys,
+                                uint32_t* spill_file, uint32_t* overflow, uint64_t* objects,
+                                hipStream_t s, uint32_t cus);
 hipError_t hash_packed(const uint8_t* arena, const uint64_t* offs, const uint32_t* lens,
                        const uint64_t* sizes, const uint32_t* order, uint64_t n, uint64_t* keys,
                        hipStream_t s);

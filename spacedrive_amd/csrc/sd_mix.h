@@ -24,5 +24,11 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 #endif
 constexpr uint32_t REGION_BITS = SD_REGION_BITS;
 constexpr uint32_t REGIONS = 1u << REGION_BITS;
+// A region set's persistent counters (zero between calls): REGIONS row cursors, then the
+// spill count (rows past their region's capacity, appended to the set's spill list), the
+// count of full regions and the tables' count of full regions done (the last one re-zeroes
+// the three)
+constexpr uint32_t REGION_SPILL_WORD = REGIONS;
+constexpr uint32_t REGION_SET_WORDS = REGIONS + 32;
 
 }  // namespace sdcas

@@ -200,6 +200,30 @@ def test_from_paths_windowed_pipeline(eng, oracle, tmp_path):
     assert not bad, bad[:5]
 
 
+@pytest.mark.parametrize("kind", ["sampled", "whole", "mixed"])
+def test_from_paths_job_step_shapes(eng, oracle, tmp_path, kind):
+    """The reference's 100-file job step (mod.rs:34) through the single-window path whose H2D
+    streams behind the gather: all-sampled (no packed area but its pad), all-whole, mixed,
+    with a missing file, and 16/17/99/100/101-file batches around the streaming threshold."""
+    rng = np.random.default_rng({"sampled": 31, "whole": 32, "mixed": 33}[kind])
+    lo, hi = {"sampled": (150_000, 3_000_000), "whole": (1, 100_000), "mixed": (1, 3_000_000)}[kind]
+    paths, sizes = [], []
+    for i in range(101):
+        s = int(np.exp(rng.uniform(np.log(lo), np.log(hi))))
+        p = tmp_path / f"{kind}{i:03d}"
+        if i != 57:
+            p.write_bytes(rng.integers(0, 256, s, dtype=np.uint8).tobytes())
+        paths.append(str(p))
+        sizes.append(s)
+    for m in (15, 16, 17, 99, 100, 101):
+        keys, errs = eng.generate_cas_keys_from_paths(paths[:m], sizes[:m])
+        for i in range(m):
+            if i == 57:
+                assert errs[i] == -2 and keys[i] == 0
+            else:
+                assert errs[i] == 0 and f"{keys[i]:016x}" == oracle.generate_cas_id(paths[i], sizes[i]), (m, i)
+
+
 def test_from_paths_file_metadata_rules(eng, oracle, tmp_path):
     """FileMetadata::new's rules behind the ABI (file_identifier/mod.rs:55-95): with the
     metadata taken by the library (sizes NULL) a file emptied after it was indexed gets no
@@ -524,8 +548,8 @@ def test_hash_group_fused_overflow_and_fallback(eng, oracle, hot):
             idx = torch.from_numpy(np.random.default_rng(h).choice(
                 np.setdiff1d(np.arange(n), [40_000 + j for j in range(len(hot))]), copies,
                 replace=False)).cuda()
-            content[idx] = content[src]
-            sizes[idx] = sizes[src]
+            content[idx] = content[src].clone()
+            sizes[idx] = sizes[src].clone()
             at += copies
         keys = torch.empty(n, dtype=torch.int64, device="cuda")
         rep = torch.empty(n, dtype=torch.int32, device="cuda")
@@ -1138,6 +1162,63 @@ def test_k1_grids_agree(eng, oracle):
     assert (runs[n][idx] == want).all()
 
 
+def test_config1_10k_files_tmpfs(eng, oracle):
+    """BASELINE config 1 at its stated size: 10k files, sizes log-uniform in
+    1 KiB..10 MiB (~11 GB) on /dev/shm, seeded as tools/bench_configs.py does, through
+    sd_cas_generate_cas_ids_from_paths (the pread gather at the cas.rs:27-58 offsets) — every
+    cas_id vs the oracle's literal read/seek generate_cas_id (cas.rs:23-62) — then the whole
+    job through identifier_job_step (library-taken metadata, link emission) vs the replay."""
+    import math
+    import shutil
+
+    import spacedrive_amd as sd
+    rng = np.random.default_rng(1)
+    n = 10_000
+    sizes = np.exp(rng.uniform(math.log(1024), math.log(10 * 1024 * 1024), n)).astype(np.int64)
+    root = f"/dev/shm/sdcas_cfg1_{os.getpid()}"
+    os.makedirs(root, exist_ok=True)
+    try:
+        paths = []
+        for i, s in enumerate(sizes):
+            p = os.path.join(root, f"f{i:05d}")
+            with open(p, "wb") as fh:
+                fh.write(rng.integers(0, 256, int(s), dtype=np.uint8).tobytes())
+            paths.append(p)
+        keys, status = eng.generate_cas_keys_from_paths(paths, sizes)
+        assert not status.any()
+        want = [int(oracle.generate_cas_id(p, int(s)), 16) for p, s in zip(paths, sizes)]
+        assert (keys == np.array(want, dtype=np.uint64)).all()
+        res = sd.identifier_job_step(paths, eng=eng)
+        step, obj, act, counts = replay_identifier_job(want, [0] * n, 100)
+        assert [(b.total_created, b.total_linked) for b in res.steps] == counts
+        assert res.object_of == {i: o for i, o in enumerate(obj)}
+        assert all(res.metadata[i].size == int(sizes[i]) for i in range(n))
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+
+
+def test_config2_1m_whole_files(eng, oracle):
+    """BASELINE config 2 at its stated size: 1M whole-file messages (sizes
+    uniform in 1..102,400, ~51 GB, seed as tools/bench_configs.py) resident in HBM through
+    K2 — EVERY key vs the oracle's 16-thread AVX-512 restatement (oracle/cas_fast.c)."""
+    n = 1_000_000
+    sz = torch.empty(n, dtype=torch.int64, device="cuda")
+    ln = torch.empty(n, dtype=torch.int32, device="cuda")
+    of = torch.empty(n, dtype=torch.int64, device="cuda")
+    nb = eng.synth_small(11, 0, n, sz, ln, of, None)
+    arena = torch.empty(nb + 64, dtype=torch.uint8, device="cuda")
+    eng.synth_small(11, 0, n, sz, ln, of, arena)
+    keys = torch.empty(n, dtype=torch.int64, device="cuda")
+    eng.hash_packed(arena, of, ln, sz, keys)
+    lens = ln.cpu().numpy().astype(np.uint64)
+    assert lens.min() <= 1024 and lens.max() >= 100_000 and nb > 45e9
+    host = arena.cpu().numpy()
+    del arena
+    torch.cuda.empty_cache()
+    want = oracle.fast_cas_keys(host, of.cpu().numpy().astype(np.uint64), lens, host64(sz), 16)
+    assert (host64(keys) == want).all()
+
+
 def test_random_cases_1e5(path_eng, oracle):
     """SURVEY §7's minimum-slice bar on every kernel shape: 10^5 random whole-file messages
     (sizes uniform in [0, 102,400]) and 10^5 random sampled files, every cas key vs the
@@ -1347,6 +1428,9 @@ def test_identifier_links_existing_vs_replay(eng, chunk):
     last_rows = np.arange(chunk - 1, n, chunk)
     states[last_rows[rng.random(len(last_rows)) < 0.3]] = 2
     states[last_rows[rng.random(len(last_rows)) < 0.2]] = 1
+    if chunk == 1:  # every row ends its chunk: a row that stays orphan is re-queried until
+        states[:] = 0  # the step budget runs out (the reference's cursor), so only at the end
+        states[-3:] = [1, 0, 2]
     pre = pool[rng.random(len(pool)) < 0.3]
     pre = np.concatenate([pre, [keys[10], np.uint64(12345)]]).astype(np.uint64)
     ids = rng.permutation(3 * len(pre))[:len(pre)].astype(np.uint32)      # unordered ids

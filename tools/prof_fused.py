@@ -37,8 +37,8 @@ eng.synth_sampled(7, 0, F, content, sizes, 57344, dup_permille=300)
 _g = np.random.default_rng(5)
 for h, copies in enumerate(a.hot):
     idx = torch.from_numpy(_g.choice(np.arange(len(a.hot), F), copies, replace=False)).to(dev)
-    content[idx] = content[h]
-    sizes[idx] = sizes[h]
+    content[idx] = content[h].clone()
+    sizes[idx] = sizes[h].clone()
 s = torch.cuda.Stream()
 
 
