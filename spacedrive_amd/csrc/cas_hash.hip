@@ -659,14 +659,23 @@ namespace sdcas {
 // files of one bucket keep their arena order, so a wave's 64 lanes stay close in memory.
 // Measured on 1M ragged files (profiles/r01_k2_order.txt): exact-length global sort 41 ms,
 // per-window exact sort 31.7 ms, chunk buckets 17.4 ms.
-constexpr uint32_t CHUNK_KEY_BITS = 7;  // chunk count <= 104 < 128
+// SD_K2_BLOCK_KEY (default): the key is the message's descending exact 64-B BLOCK count, so
+// the lanes of a wave also share the last chunk's block count — with the chunk count alone
+// they share the trip count of the full chunks but the last chunk's generic loop runs to the
+// longest lane's block count (~half a chunk of idle lane-compressions per file).  One more
+// radix pass (11 key bits).
+#ifndef SD_K2_BLOCK_KEY
+#define SD_K2_BLOCK_KEY 1
+#endif
+constexpr uint32_t CHUNK_KEY_BITS = SD_K2_BLOCK_KEY ? 11 : 7;  // blocks <= 1,664 / chunks <= 104
 
 extern "C" __global__ void __launch_bounds__(256)
 sd_cas_length_keys(const uint32_t* __restrict__ lens, uint64_t n, uint64_t* __restrict__ out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
-    const uint64_t nchunks = ((uint64_t)lens[i] + 8u + 1023u) >> 10;
-    out[i] = ((1ull << CHUNK_KEY_BITS) - 1) - nchunks;
+    const uint64_t units = SD_K2_BLOCK_KEY ? ((uint64_t)lens[i] + 8u + 63u) >> 6
+                                           : ((uint64_t)lens[i] + 8u + 1023u) >> 10;
+    out[i] = ((1ull << CHUNK_KEY_BITS) - 1) - units;
   }
 }
 

@@ -538,8 +538,20 @@ constexpr int ilog2c(uint32_t x) { return x <= 1 ? 0 : 1 + ilog2c(x >> 1); }
 // docs 1.82 / 2.50 / 2.71 / 2.63 TB/s; a 512-lane workgroup (2 waves, 1 per CU) 2.61).
 constexpr int LANE_LDS_DEPTH = ilog2c(LANE_CHUNKS) - 1;
 constexpr int LANE_BLOCK = 256;
-constexpr size_t LANE_LDS_PAD = (80u << 10) - sizeof(uint32_t) * LANE_LDS_DEPTH * 8 * LANE_BLOCK;
-constexpr int LANE_KEY_BITS = ilog2c(MID_CHUNKS) + 1;  // keys 0..MID_CHUNKS: two radix passes
+#ifndef SD_LANE_WAVES
+#define SD_LANE_WAVES 2  // waves per SIMD = 256-lane workgroups per CU (LDS-limited)
+#endif
+constexpr size_t LANE_LDS_PAD = (160u << 10) / SD_LANE_WAVES - sizeof(uint32_t) * LANE_LDS_DEPTH * 8 * LANE_BLOCK;
+static_assert((160u << 10) / SD_LANE_WAVES >= sizeof(uint32_t) * LANE_LDS_DEPTH * 8 * LANE_BLOCK,
+              "the lane stack fits the workgroup's LDS share");
+// SD_LANE_BLOCK_KEY (default): inside the lane class the visiting key is the exact 64-B
+// block count, so a wave's lanes share the last chunk's block count too (K2's rule); the
+// classes stay contiguous (descending blocks implies descending chunks)
+#ifndef SD_LANE_BLOCK_KEY
+#define SD_LANE_BLOCK_KEY 1
+#endif
+constexpr int LANE_KEY_BITS = SD_LANE_BLOCK_KEY ? ilog2c(MID_CHUNKS * 16) + 1   // 0..4,096: 13 bits
+                                                : ilog2c(MID_CHUNKS) + 1;       // 0..256: 9 bits
 
 struct LaneStack {
   uint32_t (*s)[8][LANE_BLOCK];
@@ -688,7 +700,12 @@ sd_b3_lane_keys(const uint64_t* __restrict__ offs, const uint64_t* __restrict__ 
     const uint64_t len = lens[f];
     const uint64_t nch = chunks_of(len);
     const bool ok = nch <= MID_CHUNKS && buffer_ok(offs[f], len, arena_bytes);
-    keys[f] = ok ? MID_CHUNKS - nch : MID_CHUNKS;
+    if (SD_LANE_BLOCK_KEY) {
+      const uint64_t blocks = len == 0 ? 1u : (len + 63u) >> 6;  // a 0-byte buffer: one block
+      keys[f] = ok ? MID_CHUNKS * 16 - blocks : MID_CHUNKS * 16;
+    } else {
+      keys[f] = ok ? MID_CHUNKS - nch : MID_CHUNKS;
+    }
     v[0] += ok && nch <= LANE_CHUNKS ? (uint32_t)nch : 0u;
     v[1] += ok && nch > SMALL_CHUNKS;
     v[2] += ok && nch > 16 && nch <= SMALL_CHUNKS;

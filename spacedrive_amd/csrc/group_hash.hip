@@ -284,7 +284,7 @@ __device__ __forceinline__ void staged_trip(const uint64_t (&k)[ITEMS], const ui
   // same data), so the compiler can count the stores and keeps the next trip's loads in
   // flight past them.  It pays in the 2^10-bucket coarse scatter (100 M keys: 756 -> 557 us)
   // and costs in the 2^8-bucket one (12.5 M: 62 -> 75 us); the refine is the same either way
-  // (profiles/r03b_group_ab/abg17_21)
+  // (profiles/r03b_group_ab/README.md abg17-21)
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const uint32_t t0 = (uint32_t)j * PART_THREADS + threadIdx.x;
@@ -826,7 +826,7 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
     // atomic per wave instead of one per lane on one address: the insert phase halved (fine
     // tables 3.9 -> 1.8 us, big 6.6 -> 3.4 us per workgroup); sd_bucket_min at 12.5 M keys
     // 106.6 -> 87.8 us once its Object count is sharded (before that the one device counter
-    // bound the kernel either way, profiles/r03b_group_ab/abg16)
+    // bound the kernel either way, profiles/r03b_group_ab/README.md abg16)
     static_assert(NI <= 15, "fresh fits 4 bits");
     const uint32_t wfresh = __popcll(__ballot(fresh & 1u)) + 2u * __popcll(__ballot(fresh & 2u)) +
                             4u * __popcll(__ballot(fresh & 4u)) + 8u * __popcll(__ballot(fresh & 8u));
@@ -1212,114 +1212,6 @@ sd_region_partition_big(const uint64_t* __restrict__ keys, const uint32_t* __res
   }
 }
 
-// Two-pass staging (SD_RBIG_TWOPASS = keys per lane): the tile staged through ONE LDS buffer
-// of 8 B per key in two passes (the keys, then the file indices, each row's region kept in a
-// byte array between them) — 8,192-key tiles in 77 KiB, two workgroups per CU; a spilled
-// row's index is fixed by the region's overflow prefix, so both passes agree on it.
-#ifndef SD_RBIG_TWOPASS
-#define SD_RBIG_TWOPASS 0
-#endif
-constexpr int RW_THREADS = 1024;
-constexpr int RW_ITEMS = SD_RBIG_TWOPASS > 0 ? SD_RBIG_TWOPASS : 8;
-constexpr uint32_t RW_TILE = RW_THREADS * RW_ITEMS;
-extern "C" __global__ void __launch_bounds__(RW_THREADS)
-sd_region_partition_wide(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ vals,
-                         uint64_t n, uint32_t rbits, uint64_t* __restrict__ rkeys,
-                         uint32_t* __restrict__ rfile, uint32_t* __restrict__ cursor, uint64_t cap,
-                         uint32_t* __restrict__ out, unsigned long long* __restrict__ shards,
-                         uint32_t nshards, uint32_t* __restrict__ spill_cnt,
-                         uint64_t* __restrict__ spill_keys, uint32_t* __restrict__ spill_pos) {
-  __shared__ uint32_t tcnt[256], tstart[256], gbase[256], ov[256], spoff[256];
-  __shared__ uint64_t stage[RW_TILE];
-  __shared__ uint8_t sreg[RW_TILE];
-  __shared__ uint32_t sp_n, sp_base;
-  uint32_t* sfile = reinterpret_cast<uint32_t*>(stage);
-  const uint32_t nb = 1u << rbits;  // <= 256
-  const uint64_t b0 = (uint64_t)blockIdx.x * RW_TILE;
-  const uint32_t tile_n = n - b0 < RW_TILE ? (uint32_t)(n - b0) : RW_TILE;
-  uint64_t k[RW_ITEMS];
-  uint32_t r[RW_ITEMS];
-#pragma unroll
-  for (int j = 0; j < RW_ITEMS; ++j) {
-    const uint64_t i = b0 + (uint64_t)j * RW_THREADS + threadIdx.x;
-    k[j] = keys[i < n ? i : n - 1];
-  }
-  for (uint32_t i = threadIdx.x; i < nb; i += RW_THREADS) tcnt[i] = 0;
-  if (threadIdx.x == 0) sp_n = 0;
-  if (blockIdx.x == 0 && threadIdx.x < nshards) shards[threadIdx.x * OBJ_STRIDE] = 0;
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < RW_ITEMS; ++j) {
-    const uint32_t t = (uint32_t)j * RW_THREADS + threadIdx.x;
-    k[j] = mix64(k[j]);
-    if (t < tile_n) {
-      r[j] = atomicAdd(&tcnt[(uint32_t)(k[j] >> (64 - rbits))], 1u);
-      out[b0 + t] = vals ? vals[b0 + t] : (uint32_t)(b0 + t);
-    }
-  }
-  __syncthreads();
-  for (uint32_t b = threadIdx.x; b < nb; b += RW_THREADS) {
-    const uint32_t h = tcnt[b];
-    const uint32_t g = h ? atomicAdd(&cursor[b * CURSOR_STRIDE], h) : 0u;
-    gbase[b] = g;
-    const uint32_t o = (uint64_t)g + h > cap ? (uint32_t)((uint64_t)g + h - (g > cap ? g : cap)) : 0u;
-    ov[b] = o;
-    if (o) atomicAdd(&sp_n, o);
-  }
-  lds_exclusive_scan_t<RW_THREADS>(tcnt, tstart, nb);  // (its barriers publish gbase, ov, sp_n)
-  SD_DBG_CHECK(threadIdx.x != 0 || tstart[nb - 1] + tcnt[nb - 1] == tile_n,
-               "region partition (block %u) counted %u of %u keys", blockIdx.x,
-               tstart[nb - 1] + tcnt[nb - 1], tile_n);
-  if (sp_n) {  // (uniform) a region of this tile passes its capacity: rare
-    lds_exclusive_scan_t<RW_THREADS>(ov, spoff, nb);
-    if (threadIdx.x == 0) sp_base = atomicAdd(spill_cnt, sp_n);
-  }
-  // pass 1: the keys (and each staged row's region)
-#pragma unroll
-  for (int j = 0; j < RW_ITEMS; ++j) {
-    const uint32_t t = (uint32_t)j * RW_THREADS + threadIdx.x;
-    if (t < tile_n) stage[tstart[(uint32_t)(k[j] >> (64 - rbits))] + r[j]] = k[j];
-  }
-  __syncthreads();
-  auto dest = [&](uint32_t t, uint32_t b, bool& spilled) -> uint64_t {
-    const uint32_t u = t - tstart[b];
-    const uint64_t o = (uint64_t)gbase[b] + u;
-    spilled = o >= cap;
-    if (!spilled) return (uint64_t)b * cap + o;
-    const uint32_t u0 = gbase[b] >= cap ? 0u : (uint32_t)(cap - gbase[b]);
-    return (uint64_t)sp_base + spoff[b] + (u - u0);
-  };
-#pragma unroll
-  for (int j = 0; j < RW_ITEMS; ++j) {
-    const uint32_t t = (uint32_t)j * RW_THREADS + threadIdx.x;
-    if (t < tile_n) {
-      const uint64_t kk = stage[t];
-      const uint32_t b = (uint32_t)(kk >> (64 - rbits));
-      sreg[t] = (uint8_t)b;
-      bool sp;
-      const uint64_t d = dest(t, b, sp);
-      (sp ? spill_keys : rkeys)[d] = kk;
-    }
-  }
-  __syncthreads();
-  // pass 2: the file indices into the same buffer
-#pragma unroll
-  for (int j = 0; j < RW_ITEMS; ++j) {
-    const uint32_t t = (uint32_t)j * RW_THREADS + threadIdx.x;
-    if (t < tile_n) sfile[tstart[(uint32_t)(k[j] >> (64 - rbits))] + r[j]] = (uint32_t)(b0 + t);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < RW_ITEMS; ++j) {
-    const uint32_t t = (uint32_t)j * RW_THREADS + threadIdx.x;
-    if (t < tile_n) {
-      bool sp;
-      const uint64_t d = dest(t, sreg[t], sp);
-      (sp ? spill_pos : rfile)[d] = sfile[t];
-    }
-  }
-}
-
 // The refine of region c: its output segment starts at the preceding regions' counts.
 extern "C" __global__ void __launch_bounds__(PART_THREADS)
 sd_part_refine_regions(const uint64_t* __restrict__ rkeys, const uint32_t* __restrict__ rfile,
@@ -1433,7 +1325,7 @@ static GroupPlan group_plan(uint64_t n, uint64_t target) {
   // coarse level: 2^8 buckets (runs of ~16 keys per 4,096-key trip); above COARSE10_KEYS,
   // 2^10 (one refine workgroup per coarse bucket walks ~100 K keys instead of ~400 K at 100 M
   // keys: 2.96 -> 2.89 ms; at 12.5 M the 1,024-bucket scatter's shorter runs cost more than
-  // the refine saves, 0.307 -> 0.327 ms, profiles/r03b_group_ab/abg5); more only when the
+  // the refine saves, 0.307 -> 0.327 ms, profiles/r03b_group_ab/README.md abg5); more only when the
   // refine level would exceed 2^MAX_B2 fine buckets per coarse bucket (> ~200M keys);
   // b1 <= 10 whatever n (MAX_BITS - MAX_B2)
   const uint32_t cb = n <= COARSE10_KEYS ? 8u : 10u;
@@ -1455,7 +1347,7 @@ static uint32_t totals_repl(uint32_t nb) { return nb <= STAGED_MAX_NB ? TOTALS_R
 // The small-batch region chain (sd_region_partition + sd_bucket_min_regions_keys) serves the
 // default plan's batches of (SD_SMALL_REGIONS_MIN, BIG_MAX_KEYS] keys: every one (two launches
 // against totals + scatter + tables: 20 K keys 0.0219 -> 0.0177 ms, 393 K 0.0260 -> 0.0217,
-// 1.31 M 0.0392 -> 0.0314, profiles/r03b_group_ab/small)
+// 1.31 M 0.0392 -> 0.0314, profiles/r03b_group_ab/README.md "small")
 #ifndef SD_SMALL_REGIONS
 #define SD_SMALL_REGIONS 1
 #endif
@@ -1637,13 +1529,10 @@ hipError_t hash_group_min(const uint64_t* keys, const uint32_t* vals, uint64_t n
     const uint32_t twords = (uint32_t)(nb1 * CURSOR_STRIDE + CURSOR_STRIDE);
     const uint64_t tiles = (n + RBIG_TILE - 1) / RBIG_TILE;
     // (8,192-key tiles: 512 x 8 and 256 x 8 were slower, a resident grid prefetching the next
-    // tile and 16,384-key tiles staged in two passes no faster: profiles/r03b_group_ab/big)
-    if (SD_RBIG_TWOPASS)
-      sd_region_partition_wide<<<(uint32_t)((n + RW_TILE - 1) / RW_TILE), RW_THREADS, 0, s>>>(
-          keys, vals, n, g.b1, rkeys, rfile, totals, cap, out, shards, OBJ_SHARDS, spill_cnt, skeys, spos);
-    else
-      sd_region_partition_big<<<(uint32_t)tiles, RBIG_THREADS, 0, s>>>(
-          keys, vals, n, g.b1, rkeys, rfile, totals, cap, out, shards, OBJ_SHARDS, spill_cnt, skeys, spos);
+    // tile and 16,384-key tiles staged in two passes no faster: profiles/r03b_group_ab/README.md
+    // "big"; the two-pass variant was removed in round 4)
+    sd_region_partition_big<<<(uint32_t)tiles, RBIG_THREADS, 0, s>>>(
+        keys, vals, n, g.b1, rkeys, rfile, totals, cap, out, shards, OBJ_SHARDS, spill_cnt, skeys, spos);
     sd_part_refine_regions<<<(uint32_t)nb1, PART_THREADS, 0, s>>>(rkeys, rfile, totals, cap, g.b1, g.b2,
                                                                   spill_cnt, skeys, spos, k2, p2, starts);
     sd_bucket_min<<<g.nb(), MIN_THREADS, 0, s>>>(k2, p2, vals, starts, g.nb(), g.b1 + g.b2, n, out,

@@ -986,7 +986,13 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
   // while this thread copies each finished prefix of the staging (STREAM_CHUNK bytes or
   // more at a time) on the copy stream, so the batch costs about max(gather, H2D) + the last
   // piece + the hash, not gather + H2D + hash.
-  constexpr size_t STREAM_CHUNK = 512u << 10;
+#ifndef SD_PATHS_ZERO_COPY
+#define SD_PATHS_ZERO_COPY 0
+#endif
+#ifndef SD_PATHS_STREAM_CHUNK_KB
+#define SD_PATHS_STREAM_CHUNK_KB 512
+#endif
+  constexpr size_t STREAM_CHUNK = (size_t)SD_PATHS_STREAM_CHUNK_KB << 10;
   constexpr size_t STREAM_MIN_FILES = 16;
   char* pin0 = (char*)c->pinned;
   char* dev0 = (char*)c->staging.p;
@@ -1133,14 +1139,23 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
     const int b = (int)(w & 1);
     if (w >= 2 && (rc = finish(w - 2))) break;  // slot b free again
     const size_t f0 = wstart[w], m = wstart[w + 1] - wstart[w];
-    const bool streamed = nw == 1 && m >= STREAM_MIN_FILES;
+    const bool single = nw == 1 && m >= STREAM_MIN_FILES;
     char* pin = pin0 + b * slot;
     char* dev = dev0 + b * slot;
-    if (streamed) stage_meta(plans[w], psize.data() + f0, pin);
-    if ((rc = gather(w, pin, dev, streamed))) break;
-    tr.mark("gather");
-    rc = streamed ? enqueue_hash(c, plans[w], m, pin, dev, done[b], 0, 0)
+    if (single && SD_PATHS_ZERO_COPY) {
+      // A/B (SD_PATHS_ZERO_COPY): no H2D at all — the kernels read the pinned staging
+      // straight over the host link and write the keys into it
+      if ((rc = gather(w, pin, dev, false))) break;
+      tr.mark("gather");
+      stage_meta(plans[w], psize.data() + f0, pin);
+      rc = enqueue_hash(c, plans[w], m, pin, pin, done[b], 0, 0);
+    } else {
+      if (single) stage_meta(plans[w], psize.data() + f0, pin);
+      if ((rc = gather(w, pin, dev, single))) break;
+      tr.mark("gather");
+      rc = single ? enqueue_hash(c, plans[w], m, pin, dev, done[b], 0, 0)
                   : enqueue_staged(c, plans[w], psize.data() + f0, m, pin, dev, done[b]);
+    }
     tr.mark("enqueue");
   }
   for (size_t w = nw >= 2 ? nw - 2 : 0; w < nw && rc == 0; w++) rc = finish(w);
