@@ -32,14 +32,16 @@ constexpr int GROUP = 256;  // threads per workgroup = CVs per reduce workgroup
 constexpr uint64_t GROUP_CHUNKS = (uint64_t)GROUP * K3_LANE_CHUNKS;  // chunks per subtree
 static_assert((K3_LANE_CHUNKS & (K3_LANE_CHUNKS - 1)) == 0, "subtrees must be 2^k chunks");
 
-// CV of one FULL 1 KiB chunk (never a root: a one-chunk input takes chunk_cv below).
-// 8 pair loads (128-B lines) issued one pair ahead, ping-ponged in registers like K1.
-__device__ __forceinline__ void full_chunk_cv(const uint4* __restrict__ q, uint64_t ctr,
-                                              uint32_t (&cv)[8]) {
+// CV of one FULL 1 KiB chunk (never a root: a one-chunk input takes chunk_cv below), with
+// the chunk's first line pair already in A (loaded one chunk ahead), and the
+// first pair of the lane's NEXT chunk (`next`, when non-null) loaded into A during this
+// chunk's last compressions: 8 line pairs (128-B lines) issued one pair ahead, ping-ponged
+// in registers like K1.  A lane's chunks are 256 KiB apart; without the cross-chunk
+// prefetch every chunk started with a full HBM load latency before its first compression.
+__device__ __forceinline__ void full_chunk_cv_pf(const uint4* __restrict__ q, const uint4* __restrict__ next,
+                                                 uint64_t ctr, uint32_t (&cv)[8], uint4 (&A)[8]) {
   set_iv(cv);
-  uint4 A[8], B[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) A[i] = q[i];
+  uint4 B[8];
 #pragma unroll 1
   for (uint32_t p = 0; p < 8; p += 2) {
 #pragma unroll
@@ -54,9 +56,11 @@ __device__ __forceinline__ void full_chunk_cv(const uint4* __restrict__ q, uint6
                               A[6].x, A[6].y, A[6].z, A[6].w, A[7].x, A[7].y, A[7].z, A[7].w};
       compress(cv, m, (uint32_t)ctr, (uint32_t)(ctr >> 32), BLOCK_LEN, 0u);
     }
-    if (p + 2 < 8) {
+    // the next pair of this chunk, or the first pair of the lane's next chunk
+    const uint4* src = p + 2 < 8 ? q + 8u * (p + 2) : next;
+    if (src) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) A[i] = q[8u * (p + 2) + i];
+      for (int i = 0; i < 8; ++i) A[i] = src[i];
     }
     {
       const uint32_t m[16] = {B[0].x, B[0].y, B[0].z, B[0].w, B[1].x, B[1].y, B[1].z, B[1].w,
@@ -159,19 +163,33 @@ __device__ __forceinline__ void group_subtree(const uint8_t* __restrict__ data, 
   const uint32_t count = (uint32_t)min((uint64_t)GC, nchunks - first);
   const uint32_t t = threadIdx.x;
   const bool whole_tree = root_if_single_group && nchunks <= (uint64_t)GC;
+  // a lane's FULL chunks (never the input's last, never a one-chunk input) run with their
+  // first line pair loaded one chunk ahead (full_chunk_cv_pf); the rest take chunk_cv
+  auto full = [&](uint32_t i) {
+    return i < count && first + i + 1 < nchunks;  // not the last chunk: 1,024 bytes
+  };
+  uint4 A[8];
+  if (full(t)) {
+    const uint4* q0 = reinterpret_cast<const uint4*>(data + ((first + t) << 10));
+#pragma unroll
+    for (int k = 0; k < 8; ++k) A[k] = q0[k];
+  }
 #pragma unroll 1
   for (uint32_t j = 0; j < LC; ++j) {
     const uint32_t i = j * GROUP + t;
     if (i < count) {
       const uint64_t c = first + i;
       const uint64_t off = c << 10;
-      const uint32_t clen = (uint32_t)min((uint64_t)1024, len - off);
       uint32_t cv[8];
-      if (clen == 1024 && nchunks > 1)
-        full_chunk_cv(reinterpret_cast<const uint4*>(data + off), chunk0 + c, cv);
-      else
-        chunk_cv(reinterpret_cast<const uint4*>(data + off), clen, chunk0 + c,
-                 whole_tree && nchunks == 1, cv);
+      if (full(i)) {
+        const uint32_t in = i + GROUP;
+        const uint4* next = j + 1 < LC && full(in) ? reinterpret_cast<const uint4*>(data + ((first + in) << 10))
+                                                   : nullptr;
+        full_chunk_cv_pf(reinterpret_cast<const uint4*>(data + off), next, chunk0 + c, cv, A);
+      } else {
+        chunk_cv(reinterpret_cast<const uint4*>(data + off), (uint32_t)min((uint64_t)1024, len - off),
+                 chunk0 + c, whole_tree && nchunks == 1, cv);
+      }
 #pragma unroll
       for (int w = 0; w < 8; ++w) cvs[i][w] = cv[w];
     }
