@@ -1018,11 +1018,13 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
                            : pin + pl.sampled_bytes + pl.poff[t - ns];
         int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
         if (fd < 0) { status[i] = -errno; return; }
-        {
+        // a whole file is checked against its metadata length here; a sampled file needs no
+        // fstat before its reads (a directory's pread fails with EISDIR, the same status)
+        if (sizes[i] <= MINIMUM_FILE_SIZE) {
           struct stat st;
           if (fstat(fd, &st) != 0) { status[i] = -errno; close(fd); return; }
           if (S_ISDIR(st.st_mode)) { status[i] = -EISDIR; close(fd); return; }
-          if (sizes[i] <= MINIMUM_FILE_SIZE && (uint64_t)st.st_size != lens[i]) {
+          if ((uint64_t)st.st_size != lens[i]) {
             redo[i] = 1;
             close(fd);
             return;
@@ -1077,11 +1079,13 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
         if (streamed) fin[t].store(1, std::memory_order_release);
       }
     };
-    const unsigned threads = std::max(1u, std::min(16u, (unsigned)((m + 7) / 8)));
     if (!streamed) {
-      c->pool.run(threads, worker);
+      c->pool.run(std::max(1u, std::min(16u, (unsigned)((m + 7) / 8))), worker);
       return SD_CAS_OK;
     }
+    // streamed: this thread pumps the copies, up to 15 pool threads read (~7 files each for
+    // a 100-file step; the job's share of the host is 16 cores)
+    const unsigned threads = std::max(1u, std::min(15u, (unsigned)((m + 6) / 7)));
     // the pump: metadata first, then each finished prefix of the content (items are taken
     // in staging order, so a prefix of items is a prefix of bytes)
     int prc = SD_CAS_OK;

@@ -271,6 +271,10 @@ def test_from_paths_file_metadata_rules(eng, oracle, tmp_path):
     # caller-given metadata: a length of 0 is NO_CAS (not read), a directory still EISDIR
     k2, s2 = eng.generate_cas_keys_from_paths([paths[5], paths[10], paths[0]], [0, 4096, 700])
     assert list(s2) == [sd.cas.STATUS_NO_CAS, -errno.EISDIR, 0] and k2[0] == 0 and k2[2] == keys[0]
+    # ... also when the caller's metadata puts the directory on the sampled path (its first
+    # read fails: no fstat ahead of a sampled file's reads)
+    k3, s3 = eng.generate_cas_keys_from_paths([paths[10]] * 20, [10_000_000] * 20)
+    assert (s3 == -errno.EISDIR).all() and not k3.any()
     # the job over these rows: decisions and per-step batches vs the literal replay
     for chunk in (3, 100):
         res = sd.identifier_job_step(paths, chunk=chunk, eng=eng)
