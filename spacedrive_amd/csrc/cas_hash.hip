@@ -659,13 +659,13 @@ namespace sdcas {
 // files of one bucket keep their arena order, so a wave's 64 lanes stay close in memory.
 // Measured on 1M ragged files (profiles/r01_k2_order.txt): exact-length global sort 41 ms,
 // per-window exact sort 31.7 ms, chunk buckets 17.4 ms.
-// SD_K2_BLOCK_KEY (default): the key is the message's descending exact 64-B BLOCK count, so
-// the lanes of a wave also share the last chunk's block count — with the chunk count alone
-// they share the trip count of the full chunks but the last chunk's generic loop runs to the
-// longest lane's block count (~half a chunk of idle lane-compressions per file).  One more
-// radix pass (11 key bits).
+// SD_K2_BLOCK_KEY=1 keys on the exact 64-B BLOCK count instead, so a wave's lanes would also
+// share the last chunk's block count — measured 2.5x SLOWER (1M files: 41.2 vs 16.8 ms,
+// profiles/r04_ab_keys.log): 1,664 block buckets of ~600 files spread each wave's 64 lanes over
+// the whole 51 GB arena (the address-translation thrash of a global length sort), where ~104
+// chunk buckets keep them within ~330 MB.  Off.
 #ifndef SD_K2_BLOCK_KEY
-#define SD_K2_BLOCK_KEY 1
+#define SD_K2_BLOCK_KEY 0
 #endif
 constexpr uint32_t CHUNK_KEY_BITS = SD_K2_BLOCK_KEY ? 11 : 7;  // blocks <= 1,664 / chunks <= 104
 
@@ -719,6 +719,26 @@ hipError_t hash_sampled_regions(const uint8_t* content, uint64_t stride, const u
     sd_cas_sampled_group_kernel<<<(uint32_t)blocks, SAMPLED_BLOCK, 0, s>>>(content, stride, sizes, n,
                                                                           keys, ro);
   }
+  return hipGetLastError();
+}
+
+// A copy of pinned host memory into HBM by the shader instead of the SDMA engine (the
+// path gather's streamed pieces of a few hundred KiB: A/B SD_PATHS_PULL): each lane moves
+// 16-B quads, a wave 1 KiB per load instruction over the host link.
+extern "C" __global__ void __launch_bounds__(256)
+sd_pull_host(const uint4* __restrict__ src, uint4* __restrict__ dst, uint64_t quads) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < quads; i += (uint64_t)gridDim.x * 256)
+    dst[i] = src[i];
+}
+
+hipError_t pull_host(void* dst, const void* src, uint64_t bytes, hipStream_t s) {
+  if (bytes == 0) return hipSuccess;
+  if ((bytes & 15) || ((uintptr_t)dst & 15) || ((uintptr_t)src & 15))
+    return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
+  const uint64_t quads = bytes >> 4;
+  uint64_t blocks = (quads + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  sd_pull_host<<<(uint32_t)blocks, 256, 0, s>>>((const uint4*)src, (uint4*)dst, quads);
   return hipGetLastError();
 }
 

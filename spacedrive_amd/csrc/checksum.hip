@@ -562,11 +562,12 @@ constexpr int LANE_BLOCK = 256;
 constexpr size_t LANE_LDS_PAD = (160u << 10) / SD_LANE_WAVES - sizeof(uint32_t) * LANE_LDS_DEPTH * 8 * LANE_BLOCK;
 static_assert((160u << 10) / SD_LANE_WAVES >= sizeof(uint32_t) * LANE_LDS_DEPTH * 8 * LANE_BLOCK,
               "the lane stack fits the workgroup's LDS share");
-// SD_LANE_BLOCK_KEY (default): inside the lane class the visiting key is the exact 64-B
-// block count, so a wave's lanes share the last chunk's block count too (K2's rule); the
-// classes stay contiguous (descending blocks implies descending chunks)
+// SD_LANE_BLOCK_KEY=1: key on the exact 64-B block count inside the lane class (a wave's
+// lanes would share the last chunk's block count too) — 4 % faster on 1M U(0, 16) KiB buffers
+// (3.24 vs 3.37 ms) but 2.4x slower on 262,144 U(1, 128) KiB ones (14.9 vs 6.2 ms): small
+// block buckets scatter a wave over the arena (profiles/r04_ab_keys.log).  Off.
 #ifndef SD_LANE_BLOCK_KEY
-#define SD_LANE_BLOCK_KEY 1
+#define SD_LANE_BLOCK_KEY 0
 #endif
 constexpr int LANE_KEY_BITS = SD_LANE_BLOCK_KEY ? ilog2c(MID_CHUNKS * 16) + 1   // 0..4,096: 13 bits
                                                 : ilog2c(MID_CHUNKS) + 1;       // 0..256: 9 bits

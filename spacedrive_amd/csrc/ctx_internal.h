@@ -83,6 +83,8 @@ struct sd_cas_ctx {
   int device = 0;
   hipStream_t stream = nullptr;  // compute
   hipStream_t copy = nullptr;    // H2D side stream
+  hipStream_t copy2 = nullptr;   // a second H2D stream (the streamed gather's pieces alternate)
+  hipEvent_t copy2_done = nullptr;
   hipEvent_t h2d_done = nullptr;
   DevBuf ws;       // kernel workspace
   DevBuf staging;  // device copy of a host batch

@@ -91,6 +91,8 @@ int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->copy2, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->copy2_done, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->h2d_done, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ws_ev, hipEventDisableTiming) != hipSuccess ||
       hipMalloc((void**)&c->d_scalar, 64) != hipSuccess ||
@@ -168,6 +170,8 @@ void sd_cas_ctx_destroy(sd_cas_ctx* c) {
   if (c->h2d_done) (void)hipEventDestroy(c->h2d_done);
   if (c->ws_ev) (void)hipEventDestroy(c->ws_ev);
   if (c->copy) (void)hipStreamDestroy(c->copy);
+  if (c->copy2) (void)hipStreamDestroy(c->copy2);
+  if (c->copy2_done) (void)hipEventDestroy(c->copy2_done);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -992,6 +996,12 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
 #ifndef SD_PATHS_STREAM_CHUNK_KB
 #define SD_PATHS_STREAM_CHUNK_KB 512
 #endif
+#ifndef SD_PATHS_COPY_STREAMS
+#define SD_PATHS_COPY_STREAMS 1  // 2: the pieces alternate between two copy streams (A/B)
+#endif
+#ifndef SD_PATHS_PULL
+#define SD_PATHS_PULL 0  // 1: the pieces are copied by a kernel, not the SDMA engine (A/B)
+#endif
   constexpr size_t STREAM_CHUNK = (size_t)SD_PATHS_STREAM_CHUNK_KB << 10;
   constexpr size_t STREAM_MIN_FILES = 16;
   char* pin0 = (char*)c->pinned;
@@ -1089,7 +1099,7 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
     // the pump: metadata first, then each finished prefix of the content (items are taken
     // in staging order, so a prefix of items is a prefix of bytes)
     int prc = SD_CAS_OK;
-    size_t ncopies = 0;
+    size_t ncopies = 0, ncopies_all = 0;
     double copy_us = 0, first_us = -1, last_us = 0;
     const auto t_pump = std::chrono::steady_clock::now();
     auto since = [&](std::chrono::steady_clock::time_point a) {
@@ -1111,8 +1121,10 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
         if (hi > sent && (hi - sent >= STREAM_CHUNK || ready == items)) {
           const auto t0 = std::chrono::steady_clock::now();
           if (first_us < 0 && tr.on) first_us = since(t_pump);
+          hipStream_t cs = (SD_PATHS_COPY_STREAMS > 1 && (ncopies_all++ & 1)) ? c->copy2 : c->copy;
           if (prc == SD_CAS_OK &&
-              hipMemcpyAsync(dev + sent, pin + sent, hi - sent, hipMemcpyHostToDevice, c->copy) != hipSuccess)
+              (SD_PATHS_PULL ? pull_host(dev + sent, pin + sent, hi - sent, cs)
+                             : hipMemcpyAsync(dev + sent, pin + sent, hi - sent, hipMemcpyHostToDevice, cs)) != hipSuccess)
             prc = SD_CAS_EHIP;
           if (tr.on) { copy_us += since(t0); last_us = since(t_pump); ++ncopies; }
           sent = hi;
@@ -1126,6 +1138,12 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
       }
     };
     c->pool.run2(threads, worker, pump);
+    if (SD_PATHS_COPY_STREAMS > 1 && ncopies_all > 1 && prc == SD_CAS_OK) {
+      // the copy stream (whose event the hash waits on) also waits for the second one's pieces
+      if (hipEventRecord(c->copy2_done, c->copy2) != hipSuccess ||
+          hipStreamWaitEvent(c->copy, c->copy2_done, 0) != hipSuccess)
+        prc = SD_CAS_EHIP;
+    }
     tr.note("copies", (double)ncopies);
     tr.note("copy_api_us", copy_us);
     tr.note("first_copy_at", first_us);

@@ -37,6 +37,8 @@ hipError_t hash_sampled_regions(const uint8_t* content, uint64_t stride, const u
                                 uint32_t* rfile, uint32_t* cursor, uint64_t cap, uint64_t* spill_keys,
                                 uint32_t* spill_file, uint32_t* overflow, uint64_t* objects,
                                 hipStream_t s, uint32_t cus);
+// pinned host -> device copy by a kernel (16-B aligned; else hipMemcpyAsync)
+hipError_t pull_host(void* dst, const void* src, uint64_t bytes, hipStream_t s);
 hipError_t hash_packed(const uint8_t* arena, const uint64_t* offs, const uint32_t* lens,
                        const uint64_t* sizes, const uint32_t* order, uint64_t n, uint64_t* keys,
                        hipStream_t s);

@@ -14,7 +14,9 @@ import numpy as np  # noqa: E402
 def main():
     import torch  # noqa: F401
     from spacedrive_amd import CasEngine
+    from oracle.pyoracle import Oracle
     eng = CasEngine(0)
+    orc = Oracle()
     rng = np.random.default_rng(3)
     root = "/dev/shm/sdcas_js"
     os.makedirs(root, exist_ok=True)
@@ -28,6 +30,9 @@ def main():
                     fh.write(rng.integers(0, 256, s, dtype=np.uint8).tobytes())
                 paths.append(p)
                 sizes.append(s)
+            keys, st = eng.generate_cas_keys_from_paths(paths, sizes)
+            want = [int(orc.generate_cas_id(p, s), 16) for p, s in zip(paths, sizes)]
+            parity = bool(not st.any() and (keys == np.array(want, dtype=np.uint64)).all())
             for _ in range(20):
                 eng.generate_cas_keys_from_paths(paths, sizes)
             ts = []
@@ -35,7 +40,7 @@ def main():
                 t = time.perf_counter()
                 eng.generate_cas_keys_from_paths(paths, sizes)
                 ts.append(time.perf_counter() - t)
-            print(f"{kind}: median {np.median(ts) * 1e3:.3f} ms  p10 {np.percentile(ts, 10) * 1e3:.3f}  p90 {np.percentile(ts, 90) * 1e3:.3f}", flush=True)
+            print(f"{kind}: median {np.median(ts) * 1e3:.3f} ms  p10 {np.percentile(ts, 10) * 1e3:.3f}  p90 {np.percentile(ts, 90) * 1e3:.3f}  parity {parity}", flush=True)
     finally:
         shutil.rmtree(root, ignore_errors=True)
 
