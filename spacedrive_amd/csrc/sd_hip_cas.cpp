@@ -780,10 +780,23 @@ static void stage_meta(const Plan& pl, const uint64_t* sizes, char* pin) {
   for (size_t k = 0; k < np; k++) h_poffs[k] = pl.poff[k];
 }
 
+// The kernels of a host batch write its keys straight into the pinned staging (at the
+// staging's keys offset) instead of HBM + a D2H copy: a few KiB of posted writes over the
+// host link, and one fewer copy in the call's serial tail (SD_PATHS_KEYS_TO_HOST, A/B)
+#ifndef SD_PATHS_KEYS_TO_HOST
+#define SD_PATHS_KEYS_TO_HOST 1
+#endif
+
+// byte offset of the keys in a staged batch: content | sizes | poffs | plens | keys
+static size_t staged_keys_offset(const Plan& pl) {
+  const size_t ns = pl.sampled.size(), np = pl.packed.size();
+  return pl.sampled_bytes + up256(pl.packed_bytes) + up256((ns + np) * 8) + up256(np * 8) + up256(np * 4);
+}
+
 // Enqueues, for a batch staged in pinned memory at `pin` (stage_meta done): H2D of
 // [h2d_lo, h2d_hi) of the staging to `dev` on the copy stream (the rest is already there),
-// both hash sub-batches on the compute stream after it, and D2H of the keys back to `pin`
-// (the content area is reused).  `done` (optional) is recorded on the compute stream after it.
+// both hash sub-batches on the compute stream after it, their keys into `pin`'s keys area
+// (scatter_keys reads them there).  `done` (optional) is recorded on the compute stream after it.
 static int enqueue_hash(sd_cas_ctx* c, const Plan& pl, size_t n, char* pin, char* dev,
                         hipEvent_t done, size_t h2d_lo, size_t h2d_hi) {
   const size_t ns = pl.sampled.size(), np = pl.packed.size();
@@ -791,7 +804,7 @@ static int enqueue_hash(sd_cas_ctx* c, const Plan& pl, size_t n, char* pin, char
   uint64_t* d_sizes = (uint64_t*)(dev + content_bytes);
   uint64_t* d_poffs = (uint64_t*)((char*)d_sizes + up256((ns + np) * 8));
   uint32_t* d_plens = (uint32_t*)((char*)d_poffs + up256(np * 8));
-  uint64_t* d_keys = (uint64_t*)((char*)d_plens + up256(np * 4));
+  uint64_t* d_keys = (uint64_t*)((SD_PATHS_KEYS_TO_HOST ? pin : dev) + staged_keys_offset(pl));
   (void)n;
   if (h2d_hi > h2d_lo)
     HIP_TRY(c, hipMemcpyAsync(dev + h2d_lo, pin + h2d_lo, h2d_hi - h2d_lo, hipMemcpyHostToDevice, c->copy));
@@ -804,7 +817,9 @@ static int enqueue_hash(sd_cas_ctx* c, const Plan& pl, size_t n, char* pin, char
   if (np && (rc = sd_cas_hash_packed_dev(c, dev + pl.sampled_bytes, d_poffs, d_plens,
                                          d_sizes + ns, np, d_keys + ns, c->stream)))
     return rc;
-  HIP_TRY(c, hipMemcpyAsync(pin, d_keys, (ns + np) * 8, hipMemcpyDeviceToHost, c->stream));
+  if (!SD_PATHS_KEYS_TO_HOST)
+    HIP_TRY(c, hipMemcpyAsync(pin + staged_keys_offset(pl), d_keys, (ns + np) * 8,
+                              hipMemcpyDeviceToHost, c->stream));
   if (done) HIP_TRY(c, hipEventRecord(done, c->stream));
   return SD_CAS_OK;
 }
@@ -822,7 +837,7 @@ static int enqueue_staged(sd_cas_ctx* c, const Plan& pl, const uint64_t* sizes, 
 }
 
 static void scatter_keys(const Plan& pl, const char* pin, uint64_t* out_keys) {
-  const uint64_t* h_keys = (const uint64_t*)pin;
+  const uint64_t* h_keys = (const uint64_t*)(pin + staged_keys_offset(pl));
   const size_t ns = pl.sampled.size(), np = pl.packed.size();
   for (size_t k = 0; k < ns; k++) out_keys[pl.sampled[k]] = h_keys[k];
   for (size_t k = 0; k < np; k++) out_keys[pl.packed[k]] = h_keys[ns + k];
@@ -1000,7 +1015,7 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
 #define SD_PATHS_COPY_STREAMS 1  // 2: the pieces alternate between two copy streams (A/B)
 #endif
 #ifndef SD_PATHS_PULL
-#define SD_PATHS_PULL 0  // 1: the pieces are copied by a kernel, not the SDMA engine (A/B)
+#define SD_PATHS_PULL 1  // the pieces are copied by a kernel (sd_pull_host), not the SDMA engine
 #endif
   constexpr size_t STREAM_CHUNK = (size_t)SD_PATHS_STREAM_CHUNK_KB << 10;
   constexpr size_t STREAM_MIN_FILES = 16;
