@@ -564,6 +564,7 @@ def test_hash_group_fused_overflow_and_fallback(eng, oracle, hot):
         ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
         eng.hash_group_sampled(content, sizes, keys2, rep2, ovf, want_objects=False)
         out = torch.zeros(1, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()  # (its zero fill, on torch's stream, before ours writes it)
         eng._check(eng.L.sd_cas_copy_objects_dev(eng.h, out.data_ptr(), eng.stream), "copy_objects")
         torch.cuda.synchronize()
         assert torch.equal(keys, keys2)
@@ -598,6 +599,9 @@ def test_hash_regions_streams_and_ungrouped(eng):
     keys = [torch.empty(n, dtype=torch.int64, device="cuda") for _ in range(5)]
     reps = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(5)]
     obj = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(5)]
+    late = torch.zeros(1, dtype=torch.int64, device="cuda")
+    # (torch's zero fills run on its own stream: done before our streams write the tensors)
+    torch.cuda.synchronize()
     # batch 0 on s1 (grouped on s3), batch 1 on s2 never grouped, batch 2 on s1 refills set 0,
     # batch 3 on s2 refills batch 1's set while its K1G may still run; batch 4 grouped last
     plan = [(s1, True), (s2, False), (s1, True), (s2, True), (s1, True)]
@@ -614,7 +618,6 @@ def test_hash_regions_streams_and_ungrouped(eng):
     # that set: copy_objects still returns batch 4's count
     eng.hash_regions_sampled(data[0][0], data[0][1], keys[0], reps[0], ovf, stream=s1.cuda_stream)
     eng.hash_regions_sampled(data[1][0], data[1][1], keys[1], reps[1], ovf, stream=s2.cuda_stream)
-    late = torch.zeros(1, dtype=torch.int64, device="cuda")
     eng._check(eng.L.sd_cas_copy_objects_dev(eng.h, late.data_ptr(), s3.cuda_stream), "copy")
     torch.cuda.synchronize()
     assert int(late.item()) == int(obj[4].item())
