@@ -236,6 +236,15 @@ inline int sd_ensure(sd_cas_ctx* c, DevBuf& b, size_t bytes) {
   return SD_CAS_OK;
 }
 
+// The staging's host mapping (A/B SD_PINNED_NONCOHERENT): non-coherent lets the GPU's reads
+// of it (the job step's pull kernel) use cached line fills; host writes are visible at
+// kernel boundaries, which is how every staged batch is ordered. Not adopted: no gain
+// over the coherent mapping in profiles/r04_ab_jobstep_pull.log
+#ifndef SD_PINNED_NONCOHERENT
+#define SD_PINNED_NONCOHERENT 0
+#endif
+#define SD_PINNED_FLAGS (SD_PINNED_NONCOHERENT ? hipHostMallocNonCoherent : hipHostMallocDefault)
+
 inline int sd_ensure_pinned(sd_cas_ctx* c, size_t bytes) {
   if (bytes <= c->pinned_bytes) return SD_CAS_OK;
   if (c->pinned) {
@@ -245,7 +254,7 @@ inline int sd_ensure_pinned(sd_cas_ctx* c, size_t bytes) {
     c->pinned_bytes = 0;
   }
   size_t want = std::max(bytes, (size_t)1 << 22);
-  if (hipHostMalloc(&c->pinned, want, hipHostMallocDefault) != hipSuccess) {
+  if (hipHostMalloc(&c->pinned, want, SD_PINNED_FLAGS) != hipSuccess) {
     (void)hipGetLastError();
     return sd_fail(c, SD_CAS_ENOMEM, "hipHostMalloc(%zu) failed", want);
   }
