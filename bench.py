@@ -28,8 +28,9 @@ Output: ONE JSON line on rank 0 (driver contract), with
                   memory (a pinned ring reused cyclically, every file copied H2D over PCIe)
                   through K1, PCIe-inclusive; never `value` (rank 0, N=1);
   cpu_baseline  — the oracle's AVX-512 16-lane CPU path (oracle/cas_fast.c) on a bounded
-                  sample of the SAME files on the host cores (rank 0, N=1 only); the sample's
-                  keys are also checked against the GPU's.
+                  sample of the SAME files on the host cores (rank 0 at every N, the other
+                  ranks at a barrier; threads: cpu_threads); the sample's keys are also
+                  checked against the GPU's.
 """
 from __future__ import annotations
 
@@ -682,13 +683,32 @@ def e2e_leg(eng, content, sizes, keys, args, world, rank, dev, dist):
                     "strong scaling of the 10.49M-file job over the ranks"}
 
 
+def cpu_threads(world: int) -> int:
+    """Host threads for the CPU baseline: SD_CPU_BASELINE_THREADS, else OMP_NUM_THREADS when
+    it grants more than one (the GPU box sets it to its 16-core share per GPU), else the cores
+    this process may run on, capped at 16 per rank.  torch.distributed.run sets
+    OMP_NUM_THREADS=1 for its workers when the caller left it unset, which would time the
+    node's CPU on one core beside an N-GPU line."""
+    v = int(os.environ.get("SD_CPU_BASELINE_THREADS", "0") or 0)
+    if v > 0:
+        return v
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if omp > 1:
+        return omp
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count() or 1
+    return max(1, min(avail, 16 * max(1, world)))
+
+
 def cpu_baseline(content, sizes, keys, seconds: float):
     """Oracle AVX-512 path on the host cores over a bounded sample of the same files."""
     import numpy as np
 
     from oracle.pyoracle import Oracle
     orc = Oracle()
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    threads = cpu_threads(int(os.environ.get("WORLD_SIZE", "1")))
     m = min(content.shape[0], 16 * 4096)
     host = content[:m].cpu().numpy()
     hs = sizes[:m].cpu().numpy().view(np.uint64)

@@ -53,3 +53,20 @@ def test_visible_gpus_from_kfd_topology(tmp_path, monkeypatch):
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")
     assert bench.visible_gpus(str(tmp_path)) == 1
     assert bench.visible_gpus(str(tmp_path / "none")) == 0
+
+
+def test_cpu_baseline_threads(monkeypatch):
+    """The CPU baseline's thread count: an explicit override, else OMP_NUM_THREADS when it
+    grants more than one, else the process's cores capped at 16 per rank (torchrun's default
+    OMP_NUM_THREADS=1 for its workers must not shrink the baseline to one core)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.delenv("SD_CPU_BASELINE_THREADS", raising=False)
+    monkeypatch.setenv("OMP_NUM_THREADS", "16")
+    assert bench.cpu_threads(1) == 16
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    avail = len(os.sched_getaffinity(0))
+    assert bench.cpu_threads(1) == min(avail, 16)
+    assert bench.cpu_threads(8) == min(avail, 128)
+    monkeypatch.setenv("SD_CPU_BASELINE_THREADS", "3")
+    assert bench.cpu_threads(8) == 3
