@@ -65,6 +65,28 @@ def _np_ptr(a: np.ndarray) -> int:
     return int(a.ctypes.data)
 
 
+def _path_array(paths: Sequence) -> tuple[object, int]:
+    """The `const char* const* paths` argument of the batch path calls: (keep-alive, address).
+    ASCII str paths (the common case) are encoded in one join and their pointers computed
+    by numpy: ~20 us per 100 paths instead of ~90 us for one bytes object and one
+    c_char_p each, which was a third of a 100-file job step's Python overhead.  Anything
+    else (bytes, PathLike, non-ASCII names) takes the per-path encoding."""
+    n = len(paths)
+    if n and all(type(p) is str for p in paths):
+        joined = "\0".join(paths) + "\0"
+        buf = os.fsencode(joined)
+        if len(buf) == len(joined) and joined.count("\0") == n:  # ASCII, no embedded NUL
+            lens = np.fromiter(map(len, paths), dtype=np.uint64, count=n) + np.uint64(1)
+            ptrs = np.empty(n, dtype=np.uint64)
+            ptrs[0] = 0
+            np.cumsum(lens[:-1], out=ptrs[1:])
+            cbuf = ctypes.c_char_p(buf)
+            ptrs += np.uint64(ctypes.cast(cbuf, ctypes.c_void_p).value)
+            return (buf, cbuf, ptrs), _np_ptr(ptrs)
+    parr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
+    return parr, ctypes.cast(parr, ctypes.c_void_p).value
+
+
 class CasEngine:
     """One context on one gfx950 device (one per thread/device, like the C ABI)."""
 
@@ -160,14 +182,18 @@ class CasEngine:
         hashed, STATUS_NO_CAS = length 0 (no cas_id, key 0), -errno = error (EISDIR for a
         directory)."""
         n = len(paths)
-        enc = [os.fsencode(p) for p in paths]
-        parr = (ctypes.c_char_p * n)(*enc)
-        sz = None if sizes is None else np.array([int(s) for s in sizes], dtype=np.uint64)
+        keep, parr = _path_array(paths)
+        sz = None
+        if sizes is not None:
+            sz = (np.ascontiguousarray(sizes, dtype=np.uint64) if isinstance(sizes, np.ndarray)
+                  else np.array([int(s) for s in sizes], dtype=np.uint64))
+            if sz.shape != (n,):
+                raise ValueError(f"sizes has shape {sz.shape}, expected ({n},)")
         keys = np.zeros(n, dtype=np.uint64)
         status = np.zeros(n, dtype=np.int32)
         if n:
             rc = self.L.sd_cas_generate_cas_ids_from_paths(
-                self.h, ctypes.cast(parr, ctypes.c_void_p), None if sz is None else _np_ptr(sz), n,
+                self.h, parr, None if sz is None else _np_ptr(sz), n,
                 _np_ptr(keys), _np_ptr(status))
             self._check(rc, "generate_cas_ids_from_paths")
         return keys, status
@@ -177,14 +203,13 @@ class CasEngine:
         (keys, status, sizes) — sizes = the fs::metadata length each row was decided from
         (sd_cas_file_metadata_from_paths: one stat per path)."""
         n = len(paths)
-        enc = [os.fsencode(p) for p in paths]
-        parr = (ctypes.c_char_p * n)(*enc)
+        keep, parr = _path_array(paths)
         keys = np.zeros(n, dtype=np.uint64)
         status = np.zeros(n, dtype=np.int32)
         sizes = np.zeros(n, dtype=np.uint64)
         if n:
             self._check(self.L.sd_cas_file_metadata_from_paths(
-                self.h, ctypes.cast(parr, ctypes.c_void_p), n, _np_ptr(keys), _np_ptr(status),
+                self.h, parr, n, _np_ptr(keys), _np_ptr(status),
                 _np_ptr(sizes)), "file_metadata_from_paths")
         return keys, status, sizes
 
@@ -236,12 +261,11 @@ class CasEngine:
         per step, hash.rs:11-25) in one call: returns (64-hex digest or None per path, errno
         array — 0, or the errno of the failed open/stat/read)."""
         n = len(paths)
-        enc = [os.fsencode(p) for p in paths]
-        parr = (ctypes.c_char_p * max(n, 1))(*enc)
+        keep, parr = _path_array(paths)
         out = ctypes.create_string_buffer(65 * max(n, 1))
         status = np.zeros(n, dtype=np.int32)
         if n:
-            self._check(self.L.sd_cas_file_checksums(self.h, ctypes.cast(parr, ctypes.c_void_p), n,
+            self._check(self.L.sd_cas_file_checksums(self.h, parr, n,
                                                      out, _np_ptr(status)), "file_checksums")
         raw = out.raw
         digests = [None if status[i] else raw[65 * i:65 * i + 64].decode() for i in range(n)]
