@@ -441,14 +441,25 @@ class Oracle:
         """(keys u64, status -errno) for many paths, files interleaved over `threads`;
         simd=True hashes sampled files 16 at a time with the AVX-512 baseline."""
         n = len(paths)
-        enc = [os.fsencode(p) for p in paths]
-        parr = (ctypes.c_char_p * n)(*enc)
+        # one joined buffer for ASCII str paths (the marshalling cost the product's wrapper
+        # pays too, so per-step timings of the two compare like for like)
+        joined = "\0".join(paths) + "\0" if n and all(type(p) is str for p in paths) else None
+        buf = os.fsencode(joined) if joined is not None else None
+        if buf is not None and len(buf) == len(joined) and joined.count("\0") == n:
+            cbuf = ctypes.c_char_p(buf)
+            lens = np.fromiter(map(len, paths), dtype=np.uint64, count=n) + np.uint64(1)
+            ptrs = np.zeros(n, dtype=np.uint64)
+            np.cumsum(lens[:-1], out=ptrs[1:])
+            ptrs += np.uint64(ctypes.cast(cbuf, ctypes.c_void_p).value)
+            parr_addr = ptrs.ctypes.data
+        else:
+            parr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
+            parr_addr = ctypes.cast(parr, ctypes.c_void_p).value
         sz = np.ascontiguousarray(sizes, dtype=np.uint64)
         keys = np.zeros(n, dtype=np.uint64)
         status = np.zeros(n, dtype=np.int32)
         fn = self.L.orc_fast_generate_cas_keys_paths if simd else self.L.orc_generate_cas_keys_paths
-        fn(ctypes.cast(parr, ctypes.c_void_p), sz.ctypes.data, n, int(threads), keys.ctypes.data,
-           status.ctypes.data)
+        fn(parr_addr, sz.ctypes.data, n, int(threads), keys.ctypes.data, status.ctypes.data)
         return keys, status
 
     def file_checksum(self, path: str) -> str:

@@ -723,22 +723,30 @@ hipError_t hash_sampled_regions(const uint8_t* content, uint64_t stride, const u
 }
 
 // A copy of pinned host memory into HBM by the shader instead of the SDMA engine (the
-// path gather's streamed pieces of a few hundred KiB: A/B SD_PATHS_PULL): each lane moves
-// 16-B quads, a wave 1 KiB per load instruction over the host link.
+// path gather's streamed pieces: A/B SD_PATHS_PULL): each lane moves 16-B quads, a wave
+// 1 KiB per load instruction over the host link, U quads per lane in flight.  Measured one
+// piece at a time (tools/ubench_pull.hip, profiles/r04_ubench_pull.log): a 128 KiB piece
+// 7.8 us with U = 1 (32 workgroups) vs 11.3 with U = 4 (8 workgroups: too few CUs issue);
+// from 1 MiB on U = 4 wins (1 MiB 25.2 vs 29.0 us, 4 MiB 85.7 vs 102.6); SDMA 18 / 34 / 91 us.
+// So pieces under SD_PULL_WIDE_BYTES take U = 1, larger ones SD_PULL_UNROLL.
 #ifndef SD_PULL_UNROLL
-#define SD_PULL_UNROLL 4  // quads per lane in flight (each load stays wave-contiguous); 4 vs 1:
-                          // 100 sampled files 0.29 -> 0.26 ms (profiles/r04_ab_jobstep_pull.log)
+#define SD_PULL_UNROLL 4  // 4 vs 1 for every piece: 100 sampled files 0.29 -> 0.26 ms
+                          // (profiles/r04_ab_jobstep_pull.log)
 #endif
-extern "C" __global__ void __launch_bounds__(256)
+#ifndef SD_PULL_WIDE_BYTES
+#define SD_PULL_WIDE_BYTES (512u << 10)
+#endif
+template <int U>
+__global__ void __launch_bounds__(256)
 sd_pull_host(const uint4* __restrict__ src, uint4* __restrict__ dst, uint64_t quads) {
   const uint64_t step = (uint64_t)gridDim.x * 256;
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < quads; i += step * SD_PULL_UNROLL) {
-    uint4 v[SD_PULL_UNROLL];
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < quads; i += step * U) {
+    uint4 v[U];
 #pragma unroll
-    for (int u = 0; u < SD_PULL_UNROLL; ++u)
+    for (int u = 0; u < U; ++u)
       if (i + u * step < quads) v[u] = src[i + u * step];
 #pragma unroll
-    for (int u = 0; u < SD_PULL_UNROLL; ++u)
+    for (int u = 0; u < U; ++u)
       if (i + u * step < quads) dst[i + u * step] = v[u];
   }
 }
@@ -748,9 +756,13 @@ hipError_t pull_host(void* dst, const void* src, uint64_t bytes, hipStream_t s) 
   if ((bytes & 15) || ((uintptr_t)dst & 15) || ((uintptr_t)src & 15))
     return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
   const uint64_t quads = bytes >> 4;
-  uint64_t blocks = (quads + 256 * SD_PULL_UNROLL - 1) / (256 * SD_PULL_UNROLL);
+  const int u = bytes < SD_PULL_WIDE_BYTES ? 1 : SD_PULL_UNROLL;
+  uint64_t blocks = (quads + 256 * u - 1) / (256 * u);
   if (blocks > 2048) blocks = 2048;
-  sd_pull_host<<<(uint32_t)blocks, 256, 0, s>>>((const uint4*)src, (uint4*)dst, quads);
+  if (u == 1)
+    sd_pull_host<1><<<(uint32_t)blocks, 256, 0, s>>>((const uint4*)src, (uint4*)dst, quads);
+  else
+    sd_pull_host<SD_PULL_UNROLL><<<(uint32_t)blocks, 256, 0, s>>>((const uint4*)src, (uint4*)dst, quads);
   return hipGetLastError();
 }
 

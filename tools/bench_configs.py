@@ -71,19 +71,36 @@ def config1(eng, orc, n_files: int, root: str):
         # the reference's own batch shape: identifier_job_step over CHUNK_SIZE = 100 paths
         # (file_identifier/mod.rs:34), one blocking call per chunk; K1L (default threshold)
         # vs forcing the lane-per-file kernels
-        step = {}
+        step, step_med = {}, {}
         for name, thr in (("k1l", None), ("lane", 0)):
             eng.set_latency_threshold(thr, thr)
-            t = time.perf_counter()
+            ts = []
             for i in range(0, n_files, 100):
+                t = time.perf_counter()
                 k, e = eng.generate_cas_keys_from_paths(paths[i:i + 100], sizes[i:i + 100])
+                ts.append(time.perf_counter() - t)
                 ok = ok and bool((k == keys[i:i + 100]).all())
-            step[name] = (time.perf_counter() - t) / ((n_files + 99) // 100) * 1e3
+            step[name] = float(np.mean(ts)) * 1e3
+            step_med[name] = float(np.median(ts)) * 1e3
         eng.set_latency_threshold()
+        # the CPU oracle at the same step shape: 100 paths per call, gather + AVX-512 hash on
+        # THREADS pthreads (created per call), and on one thread (the reference's job hashes
+        # its step on one task, mod.rs:105-147)
+        cpu_step = {}
+        for name, thr in (("all_cores", THREADS), ("1thread", 1)):
+            ts = []
+            for i in range(0, n_files, 100):
+                t = time.perf_counter()
+                k, _ = orc.generate_cas_keys_paths(paths[i:i + 100], sizes[i:i + 100], thr, simd=True)
+                ts.append(time.perf_counter() - t)
+                ok = ok and bool((k == keys[i:i + 100]).all())
+            cpu_step[name] = {"mean": float(np.mean(ts)) * 1e3, "median": float(np.median(ts)) * 1e3}
         emit({"config": 1, "files": n_files, "bytes_on_disk": total,
               "small_fraction": float((sizes <= 102400).mean()),
               "gpu_dropin_files_per_s": n_files / gpu, "gpu_s": gpu, "gpu_s_first_call": gpu_cold,
               "job_step_100_ms": {k: round(v, 3) for k, v in step.items()},
+              "job_step_100_ms_median": {k: round(v, 3) for k, v in step_med.items()},
+              "cpu_step_100_ms": {k: {a: round(b, 3) for a, b in v.items()} for k, v in cpu_step.items()},
               "cpu_oracle_1thread_files_per_s": n_files / cpu1,
               "cpu_oracle_all_cores_simd_files_per_s": n_files / cpu_mt, "cpu_threads": THREADS,
               "parity": ok,
