@@ -1017,7 +1017,14 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
 #ifndef SD_PATHS_PULL
 #define SD_PATHS_PULL 1  // the pieces are copied by a kernel (sd_pull_host), not the SDMA engine
 #endif
+#ifndef SD_PATHS_FIRST_KB
+#define SD_PATHS_FIRST_KB 128
+#endif
+#ifndef SD_PATHS_RAMP
+#define SD_PATHS_RAMP 0
+#endif
   constexpr size_t STREAM_CHUNK = (size_t)SD_PATHS_STREAM_CHUNK_KB << 10;
+  constexpr size_t STREAM_FIRST = (size_t)SD_PATHS_FIRST_KB << 10;
   constexpr size_t STREAM_MIN_FILES = 16;
   char* pin0 = (char*)c->pinned;
   char* dev0 = (char*)c->staging.p;
@@ -1114,7 +1121,7 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
     // the pump: metadata first, then each finished prefix of the content (items are taken
     // in staging order, so a prefix of items is a prefix of bytes)
     int prc = SD_CAS_OK;
-    size_t ncopies = 0, ncopies_all = 0;
+    size_t ncopies = 0, ncopies_all = 0, npieces = 0;
     double copy_us = 0, first_us = -1, last_us = 0;
     const auto t_pump = std::chrono::steady_clock::now();
     auto since = [&](std::chrono::steady_clock::time_point a) {
@@ -1133,10 +1140,15 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
       while (sent < content_bytes) {
         while (ready < items && fin[ready].load(std::memory_order_acquire)) ++ready;
         const size_t hi = item_end(ready);
-        // (the first piece goes at a quarter of the size: the host link starts sooner)
-        if (hi > sent && (hi - sent >= (sent ? STREAM_CHUNK : STREAM_CHUNK / 4) || ready == items)) {
+        // (the first piece goes at STREAM_FIRST bytes: the host link starts sooner; with
+        // SD_PATHS_RAMP the piece threshold doubles from there up to STREAM_CHUNK)
+        const size_t want = !sent ? STREAM_FIRST
+                            : SD_PATHS_RAMP ? std::min(STREAM_CHUNK, STREAM_FIRST << std::min<size_t>(npieces, 16))
+                                            : STREAM_CHUNK;
+        if (hi > sent && (hi - sent >= want || ready == items)) {
           const auto t0 = std::chrono::steady_clock::now();
           if (first_us < 0 && tr.on) first_us = since(t_pump);
+          ++npieces;
           hipStream_t cs = (SD_PATHS_COPY_STREAMS > 1 && (ncopies_all++ & 1)) ? c->copy2 : c->copy;
           if (prc == SD_CAS_OK &&
               (SD_PATHS_PULL ? pull_host(dev + sent, pin + sent, hi - sent, cs)
