@@ -86,6 +86,8 @@ struct sd_cas_ctx {
   hipStream_t copy2 = nullptr;   // a second H2D stream (the streamed gather's pieces alternate)
   hipEvent_t copy2_done = nullptr;
   hipEvent_t h2d_done = nullptr;
+  hipEvent_t packed_h2d = nullptr;   // the job step's whole-file pieces have landed (early hash)
+  hipEvent_t packed_done = nullptr;  // ... and their hash (on copy2) has run
   DevBuf ws;       // kernel workspace
   DevBuf staging;  // device copy of a host batch
   DevBuf small;    // multi-device exchange buffers (sd_cas_multi_*)

@@ -94,6 +94,8 @@ int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
       hipStreamCreateWithFlags(&c->copy2, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->copy2_done, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->h2d_done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->packed_h2d, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->packed_done, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ws_ev, hipEventDisableTiming) != hipSuccess ||
       hipMalloc((void**)&c->d_scalar, 64) != hipSuccess ||
       hipMalloc((void**)&c->gtotals, GROUP_TOTALS_WORDS * 4) != hipSuccess ||
@@ -168,6 +170,8 @@ void sd_cas_ctx_destroy(sd_cas_ctx* c) {
     if (c->gather_done[b]) (void)hipEventDestroy(c->gather_done[b]);
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->h2d_done) (void)hipEventDestroy(c->h2d_done);
+  if (c->packed_h2d) (void)hipEventDestroy(c->packed_h2d);
+  if (c->packed_done) (void)hipEventDestroy(c->packed_done);
   if (c->ws_ev) (void)hipEventDestroy(c->ws_ev);
   if (c->copy) (void)hipStreamDestroy(c->copy);
   if (c->copy2) (void)hipStreamDestroy(c->copy2);
@@ -797,29 +801,53 @@ static size_t staged_keys_offset(const Plan& pl) {
 // [h2d_lo, h2d_hi) of the staging to `dev` on the copy stream (the rest is already there),
 // both hash sub-batches on the compute stream after it, their keys into `pin`'s keys area
 // (scatter_keys reads them there).  `done` (optional) is recorded on the compute stream after it.
-static int enqueue_hash(sd_cas_ctx* c, const Plan& pl, size_t n, char* pin, char* dev,
-                        hipEvent_t done, size_t h2d_lo, size_t h2d_hi) {
+// The device-side views of a staged batch: content | sizes | poffs | plens, keys in `pin`
+// (SD_PATHS_KEYS_TO_HOST) or on the device.
+struct StagedDev {
+  uint64_t* sizes;
+  uint64_t* poffs;
+  uint32_t* plens;
+  uint64_t* keys;
+};
+static StagedDev staged_dev(const Plan& pl, char* pin, char* dev) {
   const size_t ns = pl.sampled.size(), np = pl.packed.size();
   const size_t content_bytes = pl.sampled_bytes + up256(pl.packed_bytes);
-  uint64_t* d_sizes = (uint64_t*)(dev + content_bytes);
-  uint64_t* d_poffs = (uint64_t*)((char*)d_sizes + up256((ns + np) * 8));
-  uint32_t* d_plens = (uint32_t*)((char*)d_poffs + up256(np * 8));
-  uint64_t* d_keys = (uint64_t*)((SD_PATHS_KEYS_TO_HOST ? pin : dev) + staged_keys_offset(pl));
+  StagedDev d;
+  d.sizes = (uint64_t*)(dev + content_bytes);
+  d.poffs = (uint64_t*)((char*)d.sizes + up256((ns + np) * 8));
+  d.plens = (uint32_t*)((char*)d.poffs + up256(np * 8));
+  d.keys = (uint64_t*)((SD_PATHS_KEYS_TO_HOST ? pin : dev) + staged_keys_offset(pl));
+  return d;
+}
+
+// the whole-file sub-batch's hash on stream s (K1L at job-step sizes)
+static int enqueue_packed(sd_cas_ctx* c, const Plan& pl, char* pin, char* dev, hipStream_t s) {
+  const size_t ns = pl.sampled.size(), np = pl.packed.size();
+  const StagedDev d = staged_dev(pl, pin, dev);
+  return np ? sd_cas_hash_packed_dev(c, dev + pl.sampled_bytes, d.poffs, d.plens, d.sizes + ns, np,
+                                     d.keys + ns, s)
+            : SD_CAS_OK;
+}
+
+static int enqueue_hash(sd_cas_ctx* c, const Plan& pl, size_t n, char* pin, char* dev,
+                        hipEvent_t done, size_t h2d_lo, size_t h2d_hi, bool packed_enqueued = false) {
+  const size_t ns = pl.sampled.size();
+  const StagedDev d = staged_dev(pl, pin, dev);
   (void)n;
   if (h2d_hi > h2d_lo)
     HIP_TRY(c, hipMemcpyAsync(dev + h2d_lo, pin + h2d_lo, h2d_hi - h2d_lo, hipMemcpyHostToDevice, c->copy));
   HIP_TRY(c, hipEventRecord(c->h2d_done, c->copy));
   HIP_TRY(c, hipStreamWaitEvent(c->stream, c->h2d_done, 0));
   int rc;
-  if (ns && (rc = sd_cas_hash_sampled_dev(c, dev, SAMPLED_CONTENT_LEN, d_sizes, ns, d_keys,
+  if (ns && (rc = sd_cas_hash_sampled_dev(c, dev, SAMPLED_CONTENT_LEN, d.sizes, ns, d.keys,
                                           c->stream)))
     return rc;
-  if (np && (rc = sd_cas_hash_packed_dev(c, dev + pl.sampled_bytes, d_poffs, d_plens,
-                                         d_sizes + ns, np, d_keys + ns, c->stream)))
-    return rc;
+  if (!packed_enqueued && (rc = enqueue_packed(c, pl, pin, dev, c->stream))) return rc;
+  // an early whole-file hash ran on copy2, beside the sampled one: join it
+  if (packed_enqueued) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->packed_done, 0));
   if (!SD_PATHS_KEYS_TO_HOST)
-    HIP_TRY(c, hipMemcpyAsync(pin + staged_keys_offset(pl), d_keys, (ns + np) * 8,
-                              hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(pin + staged_keys_offset(pl), d.keys,
+                              (ns + pl.packed.size()) * 8, hipMemcpyDeviceToHost, c->stream));
   if (done) HIP_TRY(c, hipEventRecord(done, c->stream));
   return SD_CAS_OK;
 }
@@ -1023,11 +1051,19 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
 #ifndef SD_PATHS_RAMP
 #define SD_PATHS_RAMP 0
 #endif
+// A streamed batch with both kinds of file reads and sends its whole files FIRST and hashes
+// them as soon as they have landed, while the sampled files' pieces still cross the link:
+// the whole-file K1L (up to 101 chunks: 2 chunks per lane, ~58 us) then overlaps the
+// transfer instead of running after the sampled K1L (~35 us) at the end of the step.
+#ifndef SD_PATHS_PACKED_FIRST
+#define SD_PATHS_PACKED_FIRST 1
+#endif
   constexpr size_t STREAM_CHUNK = (size_t)SD_PATHS_STREAM_CHUNK_KB << 10;
   constexpr size_t STREAM_FIRST = (size_t)SD_PATHS_FIRST_KB << 10;
   constexpr size_t STREAM_MIN_FILES = 16;
   char* pin0 = (char*)c->pinned;
   char* dev0 = (char*)c->staging.p;
+  bool packed_early = false;  // the streamed batch's whole-file hash is already enqueued
   auto gather = [&](size_t w, char* pin, char* dev, bool streamed) {
     const Plan& pl = plans[w];
     const size_t f0 = wstart[w], m = wstart[w + 1] - wstart[w];
@@ -1036,6 +1072,11 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
     uint32_t* h_plens = (uint32_t*)(pin + content_bytes + up256((ns + np) * 8) + up256(np * 8));
     for (size_t k = 0; k < np; k++) h_plens[k] = (uint32_t)lens[f0 + pl.packed[k]];
     const size_t items = ns + np;
+    // visit order (streamed, both kinds present): the whole files, then the sampled ones;
+    // staging item t of visit slot v, and fin[] indexed by v
+    const bool packed_first = streamed && SD_PATHS_PACKED_FIRST && ns > 0 && np > 0;
+    auto vis = [&](size_t v) -> size_t { return !packed_first ? v : v < np ? ns + v : v - np; };
+    packed_early = false;
     std::atomic<size_t> next{0};
     std::unique_ptr<std::atomic<uint8_t>[]> fin;
     if (streamed) {
@@ -1106,9 +1147,9 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
         close(fd);
     };
     auto worker = [&]() {
-      for (size_t t; (t = next.fetch_add(1)) < items;) {
-        item(t);
-        if (streamed) fin[t].store(1, std::memory_order_release);
+      for (size_t v; (v = next.fetch_add(1)) < items;) {
+        item(vis(v));
+        if (streamed) fin[v].store(1, std::memory_order_release);
       }
     };
     if (!streamed) {
@@ -1127,9 +1168,25 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
     auto since = [&](std::chrono::steady_clock::time_point a) {
       return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - a).count();
     };
-    auto item_end = [&](size_t t) -> size_t {  // staging bytes of items [0, t)
-      if (t == items) return content_bytes;  // (incl. the packed area's tail pad)
-      return t <= ns ? t * (size_t)SAMPLED_CONTENT_LEN : pl.sampled_bytes + pl.poff[t - ns];
+    // the pump works in a VIRTUAL byte space laid out in visit order — with packed_first,
+    // [whole-file area (P bytes, incl. its tail pad)][sampled area] — mapped back to the
+    // staging's [sampled][whole-file] layout by phys()
+    const size_t P = content_bytes - pl.sampled_bytes;
+    auto item_end = [&](size_t v) -> size_t {  // virtual bytes of visit slots [0, v)
+      if (v == items) return content_bytes;  // (incl. the packed area's tail pad)
+      if (packed_first) return v < np ? pl.poff[v] : P + (v - np) * (size_t)SAMPLED_CONTENT_LEN;
+      return v <= ns ? v * (size_t)SAMPLED_CONTENT_LEN : pl.sampled_bytes + pl.poff[v - ns];
+    };
+    auto phys = [&](size_t x) -> size_t { return !packed_first ? x : x < P ? pl.sampled_bytes + x : x - P; };
+    auto send = [&](size_t lo, size_t hi, hipStream_t cs) -> hipError_t {  // virtual [lo, hi)
+      const size_t cut = packed_first && lo < P && hi > P ? P : hi;
+      for (size_t a = lo, b = cut; a < hi; a = b, b = hi) {
+        const size_t pa = phys(a);
+        const hipError_t e = SD_PATHS_PULL ? pull_host(dev + pa, pin + pa, b - a, cs)
+                                           : hipMemcpyAsync(dev + pa, pin + pa, b - a, hipMemcpyHostToDevice, cs);
+        if (e != hipSuccess) return e;
+      }
+      return hipSuccess;
     };
     auto pump = [&]() {
       const size_t meta_hi = staged_h2d_bytes(pl);
@@ -1145,21 +1202,36 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
         const size_t want = !sent ? STREAM_FIRST
                             : SD_PATHS_RAMP ? std::min(STREAM_CHUNK, STREAM_FIRST << std::min<size_t>(npieces, 16))
                                             : STREAM_CHUNK;
-        if (hi > sent && (hi - sent >= want || ready == items)) {
+        // (and the whole-file area goes as soon as it is complete, so its hash starts early)
+        if (hi > sent && (hi - sent >= want || ready == items ||
+                          (packed_first && sent < P && hi >= P))) {
           const auto t0 = std::chrono::steady_clock::now();
           if (first_us < 0 && tr.on) first_us = since(t_pump);
           ++npieces;
           hipStream_t cs = (SD_PATHS_COPY_STREAMS > 1 && (ncopies_all++ & 1)) ? c->copy2 : c->copy;
-          if (prc == SD_CAS_OK &&
-              (SD_PATHS_PULL ? pull_host(dev + sent, pin + sent, hi - sent, cs)
-                             : hipMemcpyAsync(dev + sent, pin + sent, hi - sent, hipMemcpyHostToDevice, cs)) != hipSuccess)
-            prc = SD_CAS_EHIP;
+          if (prc == SD_CAS_OK && send(sent, hi, cs) != hipSuccess) prc = SD_CAS_EHIP;
           if (tr.on) { copy_us += since(t0); last_us = since(t_pump); ++ncopies; }
           sent = hi;
-        } else if (size_t t; next.load(std::memory_order_relaxed) < items &&
-                   (t = next.fetch_add(1)) < items) {
-          item(t);  // nothing to copy yet: read a file too (a 16th reader, no extra thread)
-          fin[t].store(1, std::memory_order_release);
+          if (packed_first && !packed_early && sent >= P && prc == SD_CAS_OK) {
+            // every whole file has landed: hash them now, on copy2 (idle with one copy
+            // stream), so the whole-file and sampled hashes run side by side at the end
+            if (SD_PATHS_COPY_STREAMS > 1 &&
+                (hipEventRecord(c->copy2_done, c->copy2) != hipSuccess ||
+                 hipStreamWaitEvent(c->copy, c->copy2_done, 0) != hipSuccess))
+              prc = SD_CAS_EHIP;
+            else if (hipEventRecord(c->packed_h2d, c->copy) != hipSuccess ||
+                     hipStreamWaitEvent(c->copy2, c->packed_h2d, 0) != hipSuccess)
+              prc = SD_CAS_EHIP;
+            else if (enqueue_packed(c, pl, pin, dev, c->copy2) != SD_CAS_OK ||
+                     hipEventRecord(c->packed_done, c->copy2) != hipSuccess)
+              prc = SD_CAS_EHIP;
+            packed_early = prc == SD_CAS_OK;
+            if (tr.on) tr.note("packed_hash_at", since(t_pump));
+          }
+        } else if (size_t v; next.load(std::memory_order_relaxed) < items &&
+                   (v = next.fetch_add(1)) < items) {
+          item(vis(v));  // nothing to copy yet: read a file too (a 16th reader, no extra thread)
+          fin[v].store(1, std::memory_order_release);
         } else {
 #if defined(__x86_64__)
           __builtin_ia32_pause();
@@ -1207,7 +1279,7 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
       if (single) stage_meta(plans[w], psize.data() + f0, pin);
       if ((rc = gather(w, pin, dev, single))) break;
       tr.mark("gather");
-      rc = single ? enqueue_hash(c, plans[w], m, pin, dev, done[b], 0, 0)
+      rc = single ? enqueue_hash(c, plans[w], m, pin, dev, done[b], 0, 0, packed_early)
                   : enqueue_staged(c, plans[w], psize.data() + f0, m, pin, dev, done[b]);
     }
     tr.mark("enqueue");

@@ -224,6 +224,59 @@ def test_from_paths_job_step_shapes(eng, oracle, tmp_path, kind):
                 assert errs[i] == 0 and f"{keys[i]:016x}" == oracle.generate_cas_id(paths[i], sizes[i]), (m, i)
 
 
+@pytest.mark.parametrize("shape", ["default", "seg16", "lane"])
+def test_from_paths_streamed_mixed_edge_rows(eng, oracle, tmp_path, shape):
+    """The streamed single-window path (>= 16 files, whole files read, sent and hashed first,
+    the sampled pieces after them) with every kind of row the gather decides: stale whole
+    files (shrunk, grown within and beyond the whole-file limit: re-read after the window),
+    a stale sampled file (UnexpectedEof -> EIO), a missing file, a directory (EISDIR), a
+    caller size of 0 (NO_CAS, nothing read) — under the default kernel shapes, the sorted
+    four-files-per-wave K1L, and the lane-per-file kernels."""
+    import errno
+
+    import spacedrive_amd as sd
+    rng = np.random.default_rng(41)
+    paths, sizes = [], []
+    for i in range(48):
+        s = int(np.exp(rng.uniform(np.log(10), np.log(2_500_000))))
+        p = tmp_path / f"e{i:02d}"
+        p.write_bytes(rng.integers(0, 256, s, dtype=np.uint8).tobytes())
+        paths.append(str(p))
+        sizes.append(s)
+    for j, (actual, size) in enumerate([(3000, 5000), (90_000, 1000), (300_000, 50)]):
+        p = tmp_path / f"stale{j}"
+        p.write_bytes(rng.integers(0, 256, actual, dtype=np.uint8).tobytes())
+        paths.insert(5 + 7 * j, str(p))
+        sizes.insert(5 + 7 * j, size)
+    short = tmp_path / "short"
+    short.write_bytes(b"z" * 120_000)
+    paths.insert(30, str(short)); sizes.insert(30, 10 ** 7)
+    paths.insert(33, str(tmp_path / "missing")); sizes.insert(33, 5000)
+    os.mkdir(str(tmp_path / "adir"))
+    paths.insert(40, str(tmp_path / "adir")); sizes.insert(40, 4096)
+    sizes[44] = 0
+    if shape == "seg16":
+        eng.set_chunkpar_split(0, 0)
+    elif shape == "lane":
+        eng.set_latency_threshold(0, 0)
+    try:
+        keys, status = eng.generate_cas_keys_from_paths(paths, sizes)
+    finally:
+        eng.set_latency_threshold()
+        eng.set_chunkpar_split()
+    for i, (p, s) in enumerate(zip(paths, sizes)):
+        if i == 30:
+            assert status[i] == -errno.EIO and keys[i] == 0
+        elif i == 33:
+            assert status[i] == -errno.ENOENT and keys[i] == 0
+        elif i == 40:
+            assert status[i] in (-errno.EISDIR,) and keys[i] == 0
+        elif i == 44:
+            assert status[i] == sd.cas.STATUS_NO_CAS and keys[i] == 0
+        else:
+            assert status[i] == 0 and f"{keys[i]:016x}" == oracle.generate_cas_id(p, s), (shape, i, s)
+
+
 def test_from_paths_file_metadata_rules(eng, oracle, tmp_path):
     """FileMetadata::new's rules behind the ABI (file_identifier/mod.rs:55-95): with the
     metadata taken by the library (sizes NULL) a file emptied after it was indexed gets no
