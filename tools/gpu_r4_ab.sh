@@ -8,7 +8,7 @@ OUT=$R/gpurun_out/${1:-r4_ab}
 shift
 mkdir -p $OUT
 cd $R
-for round in 1 2; do
+for round in $(seq 1 ${AB_ROUNDS:-2}); do
   for lib in $R/tools/ablib/*.so current; do
     name=$(basename $lib .so)
     if [ $lib = current ]; then unset SD_HIP_CAS_LIB; else export SD_HIP_CAS_LIB=$lib; fi
