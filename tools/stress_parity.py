@@ -8,7 +8,11 @@ check, every iteration,
   * sd_cas_sort_pairs_dev against numpy's stable argsort,
   * (--validator) sd_cas_checksums_dev over a random batch of ragged buffers of every size
     class against the oracle's BLAKE3; every 8th iteration a batch of 65,536-80,000 buffers
-    (the lane-per-buffer path, mostly <= 128 KiB).
+    (the lane-per-buffer path, mostly <= 128 KiB),
+  * (--fused) the fused hash + group chain (K1G + the region tables, blocking form and the
+    split form over both region sets) on a random batch of synthetic sampled files with
+    random duplication and hot files copied up to 30,000 times: keys against K1, rep against
+    the canonical grouping of those keys.
 Key patterns: uniform 64-bit, few distinct keys (hot keys), small integers (not uniform
 after any mix), bucket-sorted runs.  Prints one JSON line per iteration and a summary.
 """
@@ -64,6 +68,9 @@ def main():
     ap.add_argument("--seed", type=int, default=2026)
     ap.add_argument("--validator", action="store_true",
                     help="also stress sd_cas_checksums_dev: random batches of ragged buffers vs the oracle")
+    ap.add_argument("--fused", action="store_true",
+                    help="also stress the fused K1G + region-table chain (sd_cas_hash_group_sampled_dev)")
+    ap.add_argument("--fused-max", type=int, default=1_310_720)
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -72,6 +79,14 @@ def main():
     eng = CasEngine(0)
     orc = Oracle() if a.validator else None
     rng = np.random.default_rng(a.seed)
+    if a.fused:
+        F = a.fused_max
+        fcontent = torch.empty((F, 57344), dtype=torch.uint8, device="cuda")
+        fsizes = torch.empty(F, dtype=torch.int64, device="cuda")
+        fkeys = torch.empty(F, dtype=torch.int64, device="cuda")
+        fkeys1 = torch.empty(F, dtype=torch.int64, device="cuda")
+        freps = [torch.empty(F, dtype=torch.int32, device="cuda") for _ in range(2)]
+        fovf = torch.zeros(1, dtype=torch.int32, device="cuda")
     t_end = time.time() + a.seconds
     it = fails = 0
     while time.time() < t_end:
@@ -124,7 +139,45 @@ def main():
             res["checksums"] = all(got[i].tobytes() == orc.blake3(host[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes())
                                    for i in range(nb))
             res["buffers"] = nb
-        ok = res["group"] and res["group_min"] and res["sort"] and res.get("checksums", True)
+        if a.fused:
+            q = eng.batch_quantum  # the fused chain takes whole quanta (else: the two calls)
+            fused_shape = it % 2 == 1 or rng.random() < 0.7
+            fn = (q * int(rng.integers(1, F // q + 1)) if fused_shape
+                  else int(rng.integers(1, F + 1)))
+            c, sz = fcontent[:fn], fsizes[:fn]
+            eng.synth_sampled(a.seed + it, 0, fn, c, sz, 57344, dup_permille=int(rng.integers(0, 900)))
+            hot = []
+            if it % 3 == 0 and fn > 64:  # hot files: one file copied many times
+                for h in range(int(rng.integers(1, 4))):
+                    copies = int(rng.integers(2, min(30_000, fn // 2) + 1))
+                    src = int(rng.integers(0, fn))
+                    idx = torch.from_numpy(rng.choice(fn, copies, replace=False)).cuda()
+                    c[idx] = c[src].clone()
+                    sz[idx] = sz[src].clone()
+                    hot.append(copies)
+            torch.cuda.synchronize()
+            eng.hash_sampled(c, sz, fkeys1[:fn])
+            fovf.zero_()
+            torch.cuda.synchronize()
+            if it % 2 == 0 or fn % q:  # blocking form
+                fobj = eng.hash_group_sampled(c, sz, fkeys[:fn], freps[0][:fn], fovf)
+                frep = freps[0][:fn]
+            else:  # split form, two batches in flight over the two region sets
+                eng.hash_regions_sampled(c, sz, fkeys[:fn], freps[0][:fn], fovf)
+                eng.group_regions(fn, freps[0][:fn], want_objects=False)
+                eng.hash_regions_sampled(c, sz, fkeys[:fn], freps[1][:fn], fovf)
+                fobj = eng.group_regions(fn, freps[1][:fn])
+                frep = freps[1][:fn]
+                res["split_sets_equal"] = bool(torch.equal(freps[0][:fn], freps[1][:fn]))
+            torch.cuda.synchronize()
+            kk = fkeys[:fn].cpu().numpy().view(np.uint64)
+            fwant, fwobj = canonical(kk)
+            res["fused"] = bool((fkeys[:fn] == fkeys1[:fn]).all().item() and fobj == fwobj and
+                                (frep.cpu().numpy().astype(np.uint64) == fwant).all() and
+                                res.get("split_sets_equal", True))
+            res.update({"fused_n": fn, "fused_hot": hot, "fused_overflow": int(fovf.item())})
+        ok = (res["group"] and res["group_min"] and res["sort"] and res.get("checksums", True)
+              and res.get("fused", True))
         fails += 0 if ok else 1
         res["ok"] = ok
         print(json.dumps(res), flush=True)
