@@ -8,8 +8,10 @@ drawn from at random every iteration — batch sizes from 1 to 6,000 paths, repe
 inside a batch, caller sizes that are right, stale (shrunk/grown metadata) or 0, or no sizes
 at all, and random kernel shapes (default, four-files-per-wave K1L, lane-per-file) — and each
 result is compared with the C oracle's gather + hash of the same (path, size) list
-(oracle/cas_fast.c, orc_generate_cas_keys_paths: the cas.rs read/seek sequence).  Prints one
-JSON line per iteration and a summary; exit 1 on any mismatch."""
+(oracle/cas_fast.c, orc_generate_cas_keys_paths: the cas.rs read/seek sequence).  With
+--checksums every iteration also runs the validator over a random batch of the same pool
+(sd_cas_file_checksums: hash.rs's full-content BLAKE3) against the oracle's digest of each
+file's bytes.  Prints one JSON line per iteration and a summary; exit 1 on any mismatch."""
 import argparse
 import json
 import os
@@ -26,6 +28,7 @@ def main():
     ap.add_argument("--files", type=int, default=3000)
     ap.add_argument("--seed", type=int, default=2027)
     ap.add_argument("--root", default="/dev/shm/sdcas_stress_paths")
+    ap.add_argument("--checksums", action="store_true")
     a = ap.parse_args()
     import numpy as np
     import torch  # noqa: F401  (loads the HIP runtime first, like the product's users)
@@ -118,8 +121,27 @@ def main():
                                       "key": f"{int(keys[i]):016x}", "want": f"{int(wk[i]):016x}"}),
                           flush=True)
                     break
+            ck = None
+            if a.checksums:
+                cm = int(rng.integers(1, 400))
+                cidx = rng.integers(0, pool, cm)
+                cp = [paths[i] for i in cidx]
+                dig, cerr = eng.file_checksums(cp)
+                ck = True
+                for p, d, e in zip(cp, dig, cerr):
+                    if os.path.isdir(p):
+                        ck &= bool(e == 21 and d is None)
+                    elif not os.path.exists(p):
+                        ck &= bool(e == 2 and d is None)
+                    else:
+                        with open(p, "rb") as fh:
+                            ck &= bool(e == 0 and d == orc.blake3(fh.read()).hex())
+                    if not ck:
+                        print(json.dumps({"it": it, "bad_checksum": p, "errno": int(e), "digest": d}), flush=True)
+                        break
+                ok &= ck
             fails += 0 if ok else 1
-            print(json.dumps({"it": it, "n": m, "mode": mode, "shape": shape,
+            print(json.dumps({"it": it, "n": m, "mode": mode, "shape": shape, "checksums": ck,
                               "errors": int((status < 0).sum()), "no_cas": int((status == STATUS_NO_CAS).sum()),
                               "ok": ok}), flush=True)
             it += 1
