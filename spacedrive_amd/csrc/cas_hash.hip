@@ -667,6 +667,13 @@ namespace sdcas {
 #ifndef SD_K2_BLOCK_KEY
 #define SD_K2_BLOCK_KEY 0
 #endif
+// SD_K2_KEY_SHIFT = s: key on chunks >> s (buckets of 2^s chunk counts: a wave's lanes may
+// differ by up to 2^s - 1 chunks, but a bucket's files lie 2^s times closer in the arena) —
+// measured monotonically slower, 1M files 16.95 / 17.05 / 17.3 / 17.9 ms for s = 0..3
+// (profiles/r04_ab_k2_keyshift.log): the lanes' balance matters, the arena distance does not
+#ifndef SD_K2_KEY_SHIFT
+#define SD_K2_KEY_SHIFT 0
+#endif
 constexpr uint32_t CHUNK_KEY_BITS = SD_K2_BLOCK_KEY ? 11 : 7;  // blocks <= 1,664 / chunks <= 104
 
 extern "C" __global__ void __launch_bounds__(256)
@@ -674,7 +681,7 @@ sd_cas_length_keys(const uint32_t* __restrict__ lens, uint64_t n, uint64_t* __re
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
     const uint64_t units = SD_K2_BLOCK_KEY ? ((uint64_t)lens[i] + 8u + 63u) >> 6
-                                           : ((uint64_t)lens[i] + 8u + 1023u) >> 10;
+                                           : ((uint64_t)lens[i] + 8u + 1023u) >> (10 + SD_K2_KEY_SHIFT);
     out[i] = ((1ull << CHUNK_KEY_BITS) - 1) - units;
   }
 }

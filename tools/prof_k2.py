@@ -34,4 +34,7 @@ for _ in range(a.iters):
     e.record()
     e.synchronize()
     ts.append(s.elapsed_time(e))
-print(f"k2 {n} files: median {float(np.median(ts)):.3f} ms", flush=True)
+kh = keys.cpu().numpy().view(np.uint64)
+digest = int(np.bitwise_xor.reduce(kh * np.uint64(0x9E3779B97F4A7C15) + np.arange(n, dtype=np.uint64)))
+print(f"k2 {n} files: median {float(np.median(ts)):.3f} ms  all {[round(t, 3) for t in ts]}  "
+      f"keys digest {digest:016x}", flush=True)
