@@ -21,7 +21,8 @@ Output: ONE JSON line on rank 0 (driver contract), with
                   lanes x 2.4 GHz = 78.6 T lane-ops/s); secondary views: issue slots (rotates
                   and 3-input adds issue at half rate on gfx950, measured), the measured
                   compute-only ceiling of this instruction stream, the HBM byte view (vs
-                  8 TB/s) and PMC traffic;
+                  8 TB/s) and PMC traffic, VALU busy (PMC) and the power-capped clock
+                  (rocm-smi: K1 on random content runs at the socket power limit);
   sustained     — the same steps back to back for ~--sustain-seconds after the timed region
                   (the DVFS-settled rate, long enough for an outside utilisation sampler);
   e2e           — BASELINE config 3 as worded: sampled files streamed from pinned host
@@ -465,6 +466,29 @@ def main() -> None:
                                  "valu_pipe_busy_mix = the ARX mix's issue cycles (2 full-rate, 4 "
                                  "half-rate per wave64 instruction) over the same SIMD cycles"}
 
+    # the power cap (tools/clock_probe.py -> profiles/r04_clock_probe.jsonl: rocm-smi socket
+    # power and sclk while K1 runs back to back): on random content K1 runs at the board's
+    # power limit and DVFS takes the clock below its maximum; on constant content it stays at
+    # the maximum clock below the limit — so the VALU ceiling that binds is the compute-only
+    # ceiling scaled to the power-capped clock
+    power = None
+    cp = os.path.join(ROOT, "profiles", "r04_clock_probe.jsonl")
+    if os.path.exists(cp):
+        with open(cp) as fh:
+            recs = {r.get("workload"): r for r in map(json.loads, fh) if r.get("workload")}
+        kr, kc = recs.get("k1"), recs.get("k1c")
+        if kr and kc and kr.get("sclk_mhz_median") and kc.get("sclk_mhz_median"):
+            ceil = K1_CEILING_FILES_S * kr["sclk_mhz_median"] / kc["sclk_mhz_median"]
+            power = {"power_w_random": kr["power_w_median"], "sclk_mhz_random": kr["sclk_mhz_median"],
+                     "power_w_constant": kc["power_w_median"], "sclk_mhz_constant": kc["sclk_mhz_median"],
+                     "ceiling_files_per_s_at_capped_clock": ceil,
+                     "frac_of_capped_ceiling": F / (kern_ms / 1e3) / ceil,
+                     "source": "profiles/r04_clock_probe.jsonl (tools/clock_probe.py: rocm-smi while K1 "
+                               "runs back to back on random vs all-zero content)",
+                     "note": "K1 on random content runs at the socket power limit (DVFS lowers sclk); "
+                             "on constant content it runs at the maximum sclk below the limit: the "
+                             "binding roof is the VALU issue ceiling at the power-capped clock"}
+
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(content, sizes, last_keys, args.cpu_seconds)
@@ -534,6 +558,7 @@ def main() -> None:
                 "frac": valu / VALU_PEAK_TOPS,
                 "traffic": traffic,
                 "valu_busy": valu_busy,
+                "power": power,
                 "kernel_ms": kern_ms,
                 "kernel_ms_ranks": {"min": min(k1_ms_ranks), "max": max(k1_ms_ranks),
                                     "per_rank": k1_ms_ranks},
