@@ -1,5 +1,6 @@
 // ctx_internal.h — the sd_cas_ctx object and the host helpers shared by the C-ABI
-// translation units (sd_hip_cas.cpp, sd_multi.cpp).  Not part of the public ABI.
+// translation units (sd_hip_cas.cpp, host_paths.cpp, validator_host.cpp, sd_multi.cpp).  Not
+// part of the public ABI.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
@@ -246,6 +247,11 @@ inline int sd_ensure(sd_cas_ctx* c, DevBuf& b, size_t bytes) {
 #define SD_PINNED_NONCOHERENT 0
 #endif
 #define SD_PINNED_FLAGS (SD_PINNED_NONCOHERENT ? hipHostMallocNonCoherent : hipHostMallocDefault)
+
+// K1 / K1L / K1+K1L by batch size (sd_hip_cas.cpp), shared with the host entry points
+extern "C" hipError_t sd_dispatch_sampled(sd_cas_ctx* c, const uint8_t* content, uint64_t stride,
+                                          const uint64_t* sizes, size_t n, uint64_t* keys,
+                                          hipStream_t s);
 
 inline int sd_ensure_pinned(sd_cas_ctx* c, size_t bytes) {
   if (bytes <= c->pinned_bytes) return SD_CAS_OK;

@@ -1,0 +1,502 @@
+// validator_host.cpp — the validator's entry points of the C ABI (include/sd_hip_cas.h):
+// sd_cas_checksum_dev / sd_cas_file_checksum (file_checksum, core/src/object/validation/
+// hash.rs:9-25: hash.rs's read loop exactly, K3 on the device) and sd_cas_checksums_dev /
+// sd_cas_file_checksums (the validator job over many files, validator_job.rs:107-172: K3b).
+// Split out of sd_hip_cas.cpp; every digest comes from the HIP kernels.
+#include <errno.h>
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "sd_checksum.h"
+#include "sd_group.h"
+#include "sd_kernels.h"
+#include "sd_mix.h"
+
+using namespace sdcas;
+
+#include "sd_debug.h"
+#include "ctx_internal.h"
+
+// short local names for the shared helpers
+#define fail sd_fail
+#define pick sd_pick
+#define ensure sd_ensure
+#define ensure_pinned sd_ensure_pinned
+
+extern "C" {
+
+// ---- file_checksum --------------------------------------------------------------------
+
+int sd_cas_checksum_dev(sd_cas_ctx* c, const void* d_data, uint64_t len, uint8_t out[32],
+                        void* stream) {
+  if (!c || !out) return SD_CAS_EINVAL;
+  if ((len && !d_data) || ((uintptr_t)d_data & 15))
+    return fail(c, SD_CAS_EINVAL, "checksum: bad data pointer");
+  hipStream_t s = pick(c, stream);
+  // up to 64 GiB: the batch chain with one buffer (K3b: its wide static grid and spread
+  // block level ran 2.99 vs K3's 2.88 TB/s on the same 16 GiB, profiles/r02b_validator_batch.log)
+  constexpr uint64_t BATCH_MAX = 64ull << 30;
+  const bool batch = len <= BATCH_MAX;
+  int rc = ensure(c, c->ws, batch ? checksum_batch_workspace_bytes(1, len) : checksum_workspace_bytes(len));
+  if (rc) return rc;
+  uint32_t* d_out = (uint32_t*)c->d_scalar;  // d_scalar[0..3]: digest; [4], [5]: offs, lens
+  HIP_TRY(c, sd_ws_acquire(c, s));
+  if (batch) {
+    uint64_t* d_ol = c->d_scalar + 4;
+    HIP_TRY(c, checksum_single_setup(d_ol, len, (uint32_t*)(c->d_scalar + 6), s));
+    HIP_TRY(c, checksum_batch_device((const uint8_t*)d_data, len, d_ol, d_ol + 1, 1, d_out,
+                                     (uint32_t*)(c->d_scalar + 6), c->ws.p, s));
+  } else {
+    HIP_TRY(c, checksum_device((const uint8_t*)d_data, len, 0, true, d_out, c->ws.p, s));
+  }
+  HIP_TRY(c, hipMemcpyAsync(out, d_out, 32, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, sd_ws_release(c, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  return SD_CAS_OK;
+}
+
+// file_checksum(path) (validation/hash.rs:11-25): the reference issues one read() of
+// BLOCK_LEN = 1 MiB per iteration into one hasher and stops at the FIRST read that returns
+// fewer bytes — the end of a regular file on a local filesystem, but after the first short
+// read on anything that returns short reads before its end (procfs seq_files give about one
+// page per read, FIFOs and FUSE/network mounts whatever is ready).
+// Two read modes, one result:
+//   * parallel (regular files): the file streams through two pinned segment buffers of up
+//     to 64 MiB (a segment = one complete 65,536-chunk subtree, hashed on the GPU while the
+//     pool reads the next one with pread pieces) until a segment comes back short; st_size
+//     only sizes the buffers (a file that outgrows its first buffer is re-read with full-size
+//     segments).  A regular file whose reads show it is not read like a local file — a short
+//     pread followed by more data, or an end before st_size — is redone sequentially;
+//   * sequential (everything else, and those redos): hash.rs's loop literally, 1 MiB read()s
+//     from the start, stopping after the first short one, into the same segment pipeline.
+// The segment CVs are merged on the GPU (pair-and-promote, ROOT on the last parent); a file
+// of one segment is hashed with ROOT inside the segment.
+static int cv_capacity(sd_cas_ctx* c, DevBuf& cvb, size_t need_cvs, hipStream_t s) {
+  if (need_cvs * 32 <= cvb.bytes) return SD_CAS_OK;
+  DevBuf nb;
+  const size_t want = std::max<size_t>(need_cvs * 2 * 32, 1 << 16);
+  HIP_TRY(c, hipStreamSynchronize(s));
+  if (hipMalloc(&nb.p, want) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(c, SD_CAS_ENOMEM, "hipMalloc(%zu) failed", want);
+  }
+  nb.bytes = want;
+  if (cvb.p) {
+    HIP_TRY(c, hipMemcpy(nb.p, cvb.p, cvb.bytes, hipMemcpyDeviceToDevice));
+    HIP_TRY(c, hipFree(cvb.p));
+  }
+  cvb = nb;
+  return SD_CAS_OK;
+}
+
+int sd_cas_file_checksum(sd_cas_ctx* c, const char* path, char out_hex[65], int* err_no) {
+  if (!c || !path || !out_hex) return SD_CAS_EINVAL;
+  if (err_no) *err_no = 0;
+  HIP_TRY(c, hipSetDevice(c->device));
+  int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) {
+    if (err_no) *err_no = errno;
+    return fail(c, SD_CAS_EIO, "open(%s): %s", path, strerror(errno));
+  }
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    if (err_no) *err_no = errno;
+    close(fd);
+    return fail(c, SD_CAS_EIO, "fstat(%s): %s", path, strerror(errno));
+  }
+  const uint64_t SEG = 64ull << 20;  // 65,536 chunks: a complete left subtree
+  constexpr uint64_t PIECE = 4ull << 20;  // pool read unit (one reader tops out near 5-10 GB/s)
+  constexpr uint64_t BLOCK_LEN = 1ull << 20;  // hash.rs:9
+  static_assert((64ull << 20) % BLOCK_LEN == 0, "a segment holds whole hash.rs reads");
+  bool seq = !S_ISREG(st.st_mode);
+  // segment capacity: the whole file plus room to see EOF, capped at one subtree (the
+  // sequential mode reads whole 1 MiB blocks: full segments)
+  uint64_t cap = seq ? SEG : std::min<uint64_t>(SEG, (((uint64_t)st.st_size + 1 + 4095) / 4096) * 4096);
+  hipStream_t s = c->stream;
+  int rc = SD_CAS_OK;
+  hipEvent_t done[2] = {nullptr, nullptr};
+  for (int i = 0; i < 2; i++)
+    if (hipEventCreateWithFlags(&done[i], hipEventDisableTiming) != hipSuccess) {
+      close(fd);
+      for (int k = 0; k < i; k++) (void)hipEventDestroy(done[k]);
+      return fail(c, SD_CAS_EHIP, "file_checksum: event create");
+    }
+  bool irregular = false;  // parallel mode saw reads that a local regular file never gives
+  bool seq_stopped = false;  // sequential mode: the first short read has happened
+  // parallel: read segment `sgi` into dst with pread pieces; its length (< cap at EOF) or -errno
+  auto read_seg_par = [&](uint64_t sgi, char* dst) -> int64_t {
+    const uint64_t off = sgi * cap;
+    const uint64_t npieces = (cap + PIECE - 1) / PIECE;
+    std::atomic<uint64_t> next{0}, eof{cap}, data_end{0};
+    std::atomic<int> rd_err{0};
+    std::atomic<bool> short_then_more{false};
+    c->pool.run((unsigned)std::min<uint64_t>(8, npieces), [&]() {
+      for (uint64_t p; (p = next.fetch_add(1)) < npieces && !rd_err.load();) {
+        const uint64_t p0 = p * PIECE, pn = std::min(PIECE, cap - p0);
+        if (p0 >= eof.load()) break;
+        uint64_t got = 0;
+        bool was_short = false;
+        while (got < pn) {
+          ssize_t r = pread(fd, dst + p0 + got, pn - got, (off_t)(off + p0 + got));
+          if (r < 0 && errno == EINTR) continue;
+          if (r < 0) { rd_err.store(errno); break; }
+          if (r == 0) break;
+          if (was_short) short_then_more.store(true);  // data after a short read
+          if ((uint64_t)r < pn - got) was_short = true;
+          got += (uint64_t)r;
+        }
+        if (got) {
+          uint64_t cur = data_end.load();
+          while (p0 + got > cur && !data_end.compare_exchange_weak(cur, p0 + got)) {}
+        }
+        if (got < pn) {  // eof = min(eof, p0 + got)
+          uint64_t cur = eof.load();
+          while (p0 + got < cur && !eof.compare_exchange_weak(cur, p0 + got)) {}
+        }
+      }
+    });
+    if (int e = rd_err.load()) return -(int64_t)e;
+    // bytes past the first end (a short piece whose successor still had data)
+    if (short_then_more.load() || data_end.load() > eof.load()) irregular = true;
+    return (int64_t)eof.load();
+  };
+  // sequential: hash.rs:15-21 — 1 MiB read()s in order, stop after the first short one
+  auto read_seg_seq = [&](char* dst) -> int64_t {
+    if (seq_stopped) return 0;
+    uint64_t got = 0;
+    while (got < cap) {
+      ssize_t r = read(fd, dst + got, BLOCK_LEN);
+      if (r < 0 && errno == EINTR) continue;
+      if (r < 0) return -(int64_t)errno;
+      got += (uint64_t)r;
+      if ((uint64_t)r != BLOCK_LEN) { seq_stopped = true; break; }
+    }
+    return (int64_t)got;
+  };
+  auto read_seg = [&](uint64_t sgi, char* dst) -> int64_t {
+    return seq ? read_seg_seq(dst) : read_seg_par(sgi, dst);
+  };
+  uint8_t digest[32];
+  for (int attempt = 0; attempt < 3; attempt++) {
+    const size_t sb = up256(cap + 16);
+    if ((rc = ensure_pinned(c, 2 * sb)) || (rc = ensure(c, c->staging, 2 * sb))) break;
+    if ((rc = ensure(c, c->ws, std::max(checksum_workspace_bytes(cap), checksum_workspace_bytes(1 << 20)))))
+      break;
+    char* pin[2] = {(char*)c->pinned, (char*)c->pinned + sb};
+    char* dev[2] = {(char*)c->staging.p, (char*)c->staging.p + sb};
+    if (hipError_t e = sd_ws_acquire(c, s); e != hipSuccess) {
+      rc = fail(c, SD_CAS_EHIP, "file_checksum: %s", hipGetErrorString(e));
+      break;
+    }
+    // segment k is dispatched once it is known whether it is the only one (k == 0 waits for
+    // segment 1's read); ROOT sits inside it only then
+    auto dispatch = [&](uint64_t sgi, uint64_t len, bool only) -> int {
+      const int b = (int)(sgi & 1);
+      int r2 = cv_capacity(c, c->cvbuf, sgi + 1, s);
+      if (r2) return r2;
+      hipError_t e = hipMemcpyAsync(dev[b], pin[b], up16(len), hipMemcpyHostToDevice, s);
+      if (e == hipSuccess)
+        e = checksum_device((const uint8_t*)dev[b], len, (sgi * cap) >> 10, only,
+                            (uint32_t*)c->cvbuf.p + 8 * sgi, c->ws.p, s);
+      if (e == hipSuccess) e = hipEventRecord(done[b], s);
+      if (e != hipSuccess) return fail(c, SD_CAS_EHIP, "checksum segment: %s", hipGetErrorString(e));
+      return SD_CAS_OK;
+    };
+    auto io_fail = [&](int64_t neg) {
+      if (err_no) *err_no = (int)-neg;
+      return fail(c, SD_CAS_EIO, "read(%s): %s", path, strerror((int)-neg));
+    };
+    enum { DONE, GROW, GO_SEQ } next = DONE;
+    uint64_t nseg = 1, total = 0;
+    int64_t len0 = read_seg(0, pin[0]);
+    if (len0 < 0) {
+      rc = io_fail(len0);
+    } else if (irregular) {
+      next = GO_SEQ;
+    } else if ((uint64_t)len0 == cap && cap < SEG) {
+      next = GROW;  // grew past the buffer
+    } else if ((uint64_t)len0 < cap) {
+      total = (uint64_t)len0;
+      rc = dispatch(0, (uint64_t)len0, true);
+    } else {  // a full first segment: more may follow
+      total = (uint64_t)len0;
+      for (uint64_t sgi = 1;; sgi++) {
+        const int b = (int)(sgi & 1);
+        if (sgi >= 2 && hipEventSynchronize(done[b]) != hipSuccess) { rc = fail(c, SD_CAS_EHIP, "checksum: segment sync"); break; }
+        const int64_t ln = read_seg(sgi, pin[b]);
+        if (ln < 0) { rc = io_fail(ln); break; }
+        if (irregular) { next = GO_SEQ; break; }
+        total += (uint64_t)ln;
+        if (sgi == 1) {  // segment 0 is the only one iff nothing follows it
+          if ((rc = dispatch(0, (uint64_t)len0, ln == 0))) break;
+        }
+        if (ln == 0) { nseg = sgi; break; }
+        if ((rc = dispatch(sgi, (uint64_t)ln, false))) break;
+        if ((uint64_t)ln < cap) { nseg = sgi + 1; break; }
+      }
+    }
+    // a regular file that ended before its st_size (it shrank, or a read came back short at
+    // a piece boundary): redo it the way hash.rs reads
+    if (rc == SD_CAS_OK && next == DONE && !seq && total < (uint64_t)st.st_size) next = GO_SEQ;
+    if (rc == SD_CAS_OK && next == DONE) {
+      uint32_t* d_out = (uint32_t*)c->d_scalar;
+      hipError_t e = hipSuccess;
+      // reduce_cvs_device ping-pongs ceil(nseg / 256) CVs per level through ws
+      const size_t red_ws = 2 * up256((nseg + 255) / 256 * 32) + 512;
+      if (nseg > 1) rc = ensure(c, c->ws, red_ws);
+      if (rc == SD_CAS_OK) {
+        if (nseg == 1) e = hipMemcpyAsync(d_out, c->cvbuf.p, 32, hipMemcpyDeviceToDevice, s);
+        else e = reduce_cvs_device((uint32_t*)c->cvbuf.p, nseg, d_out, c->ws.p, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(digest, d_out, 32, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = fail(c, SD_CAS_EHIP, "checksum reduce: %s", hipGetErrorString(e));
+      }
+    }
+    (void)hipStreamSynchronize(s);  // no segment copy may still read the pinned buffers
+    (void)sd_ws_release(c, s);
+    if (rc != SD_CAS_OK || next == DONE) break;
+    if (next == GROW) {
+      cap = SEG;
+    } else {  // GO_SEQ: from the start, hash.rs's reads
+      seq = true;
+      cap = SEG;
+      irregular = false;
+      if (lseek(fd, 0, SEEK_SET) != 0) {
+        if (err_no) *err_no = errno;
+        rc = fail(c, SD_CAS_EIO, "lseek(%s): %s", path, strerror(errno));
+        break;
+      }
+    }
+    if (attempt == 2) rc = fail(c, SD_CAS_EIO, "file_checksum(%s): no stable read", path);
+  }
+  close(fd);
+  (void)hipStreamSynchronize(s);
+  (void)hipEventDestroy(done[0]);
+  (void)hipEventDestroy(done[1]);
+  if (rc) return rc;
+  static const char* hx = "0123456789abcdef";
+  for (int i = 0; i < 32; i++) { out_hex[2 * i] = hx[digest[i] >> 4]; out_hex[2 * i + 1] = hx[digest[i] & 15]; }
+  out_hex[64] = 0;
+  return SD_CAS_OK;
+}
+
+// ---- the validator job over many files -----------------------------------------------
+
+int sd_cas_checksums_dev(sd_cas_ctx* c, const void* d_arena, uint64_t arena_bytes,
+                         const uint64_t* d_offs, const uint64_t* d_lens, size_t n, uint8_t* d_out,
+                         void* stream) {
+  if (!c) return SD_CAS_EINVAL;
+  if (n == 0) return SD_CAS_OK;
+  if (!d_arena || !d_offs || !d_lens || !d_out || ((uintptr_t)d_arena & 15) ||
+      ((uintptr_t)d_out & 3) || n > (1u << 24))
+    return fail(c, SD_CAS_EINVAL, "checksums: bad arguments");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  int rc = ensure(c, c->ws, checksum_batch_workspace_bytes(n, arena_bytes));
+  if (rc) return rc;
+  uint32_t* d_bad = (uint32_t*)(c->d_scalar + 6);
+  uint32_t bad = 0;
+  HIP_TRY(c, sd_ws_acquire(c, s));
+  HIP_TRY(c, hipMemsetAsync(d_bad, 0, 4, s));
+  HIP_TRY(c, checksum_batch_device((const uint8_t*)d_arena, arena_bytes, d_offs, d_lens, n,
+                                   (uint32_t*)d_out, d_bad, c->ws.p, s));
+  HIP_TRY(c, hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, sd_ws_release(c, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  if (bad)
+    return fail(c, SD_CAS_EINVAL, "checksums: %s",
+                (bad & 1) ? "a buffer is longer than 64 GiB"
+                          : (bad & 4) ? "a buffer is misaligned or extends past arena_bytes"
+                                      : "the buffers' subtrees exceed arena_bytes' bound (overlapping buffers?)");
+  return SD_CAS_OK;
+}
+
+// file_checksum over many paths.  Windows of up to CK_WIN bytes / CK_WIN_FILES files in
+// index order, double-buffered: the pool reads window w (one slot of up128(st_size + 1) per
+// file: the spare byte shows EOF, so a file that grew since stat fills its slot and is
+// redone by the streaming path) into one pinned slot while the GPU copies and hashes window
+// w-1 from the other.  Pinned slot layout: offs | lens | digests | data.
+int sd_cas_file_checksums(sd_cas_ctx* c, const char* const* paths, size_t n, char* out_hex,
+                          int32_t* status) {
+  if (!c) return SD_CAS_EINVAL;
+  if (n == 0) return SD_CAS_OK;
+  if (!paths || !out_hex || !status) return fail(c, SD_CAS_EINVAL, "file_checksums: null argument");
+  HIP_TRY(c, hipSetDevice(c->device));
+  constexpr uint64_t CK_WIN = 128ull << 20;  // data bytes per window
+  constexpr uint64_t CK_BIG = CK_WIN / 2;    // larger files stream on their own (64 MiB segments)
+  constexpr size_t CK_WIN_FILES = 32768;
+  constexpr size_t HDR = CK_WIN_FILES * (8 + 8 + 32);
+  constexpr size_t SLOT = HDR + CK_WIN + 256;
+  enum : uint8_t { K_BATCH = 0, K_STREAM = 1, K_ERROR = 2 };
+  std::vector<uint64_t> fsize(n, 0);
+  std::vector<uint8_t> kind(n, K_BATCH);
+  for (size_t i = 0; i < n; i++) { status[i] = 0; out_hex[65 * i] = 0; }
+  {  // stat pass
+    std::atomic<size_t> next{0};
+    c->pool.run(std::max(1u, std::min(16u, (unsigned)((n + 63) / 64))), [&]() {
+      for (size_t i; (i = next.fetch_add(1)) < n;) {
+        struct stat st;
+        if (stat(paths[i], &st) != 0) { status[i] = -errno; kind[i] = K_ERROR; continue; }
+        fsize[i] = (uint64_t)st.st_size;
+        // not a regular file (FIFO, device, ...): hash.rs's sequential reads, streamed
+        if (fsize[i] > CK_BIG || !S_ISREG(st.st_mode)) kind[i] = K_STREAM;
+      }
+    });
+  }
+  // windows: [w0, w1) file ranges in index order
+  std::vector<size_t> wstart{0};
+  {
+    uint64_t bytes = 0;
+    size_t files = 0;
+    for (size_t i = 0; i < n; i++) {
+      if (kind[i] != K_BATCH) continue;
+      const uint64_t need = up128(fsize[i] + 1);
+      if (files && (bytes + need > CK_WIN || files == CK_WIN_FILES)) {
+        wstart.push_back(i);
+        bytes = 0;
+        files = 0;
+      }
+      bytes += need;
+      files++;
+    }
+    wstart.push_back(n);
+  }
+  const size_t nw = wstart.size() - 1;
+  int rc = ensure_pinned(c, 2 * SLOT);
+  if (rc) return rc;
+  if ((rc = ensure(c, c->staging, 2 * SLOT))) return rc;
+  if ((rc = ensure(c, c->ws, checksum_batch_workspace_bytes(CK_WIN_FILES, CK_WIN)))) return rc;
+  hipStream_t s = c->stream;
+  hipEvent_t done[2] = {nullptr, nullptr};
+  for (int b = 0; b < 2; b++)
+    if (hipEventCreateWithFlags(&done[b], hipEventDisableTiming) != hipSuccess) {
+      if (done[0]) (void)hipEventDestroy(done[0]);
+      return fail(c, SD_CAS_EHIP, "file_checksums: event create");
+    }
+  std::vector<size_t> members[2];  // file index of each batch entry of the window in a slot
+  static const char* hx = "0123456789abcdef";
+  auto emit = [&](int b) {  // the window in slot b is complete: digests -> hex
+    const uint8_t* dg = (const uint8_t*)c->pinned + (size_t)b * SLOT + CK_WIN_FILES * 16;
+    for (size_t k = 0; k < members[b].size(); k++) {
+      char* o = out_hex + 65 * members[b][k];
+      for (int j = 0; j < 32; j++) { o[2 * j] = hx[dg[32 * k + j] >> 4]; o[2 * j + 1] = hx[dg[32 * k + j] & 15]; }
+      o[64] = 0;
+    }
+    members[b].clear();
+  };
+  bool pending[2] = {false, false};
+  uint32_t* d_bad = (uint32_t*)(c->d_scalar + 6);
+  {
+    hipError_t e = sd_ws_acquire(c, s);
+    if (e == hipSuccess) e = hipMemsetAsync(d_bad, 0, 4, s);
+    if (e != hipSuccess) rc = fail(c, SD_CAS_EHIP, "file_checksums: %s", hipGetErrorString(e));
+  }
+  for (size_t w = 0; w < nw && rc == SD_CAS_OK; w++) {
+    const int b = (int)(w & 1);
+    if (pending[b]) {  // slot b's previous window: copied, hashed and its digests back
+      if (hipEventSynchronize(done[b]) != hipSuccess) { rc = fail(c, SD_CAS_EHIP, "file_checksums: sync"); break; }
+      emit(b);
+      pending[b] = false;
+    }
+    char* pin = (char*)c->pinned + (size_t)b * SLOT;
+    uint64_t* h_offs = (uint64_t*)pin;
+    uint64_t* h_lens = h_offs + CK_WIN_FILES;
+    char* data = pin + HDR;
+    std::vector<size_t>& mem = members[b];
+    std::vector<uint64_t> cap;
+    uint64_t o = 0;
+    for (size_t i = wstart[w]; i < wstart[w + 1]; i++) {
+      if (kind[i] != K_BATCH) continue;
+      h_offs[mem.size()] = o;
+      cap.push_back(up128(fsize[i] + 1));
+      o += cap.back();
+      mem.push_back(i);
+    }
+    const size_t m = mem.size();
+    if (m == 0) continue;
+    std::atomic<size_t> next{0};
+    c->pool.run(std::max(1u, std::min(16u, (unsigned)((m + 3) / 4))), [&]() {
+      for (size_t k; (k = next.fetch_add(1)) < m;) {
+        const size_t i = mem[k];
+        int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
+        if (fd < 0) { status[i] = -errno; kind[i] = K_ERROR; h_lens[k] = 0; continue; }
+        uint64_t got = 0;
+        bool was_short = false, irregular = false;
+        while (got < cap[k]) {
+          ssize_t r = pread(fd, data + h_offs[k] + got, cap[k] - got, (off_t)got);
+          if (r < 0 && errno == EINTR) continue;
+          if (r < 0) { status[i] = -errno; kind[i] = K_ERROR; break; }
+          if (r == 0) break;  // EOF
+          if (was_short) irregular = true;  // data after a short read: not a local file
+          if ((uint64_t)r < cap[k] - got) was_short = true;
+          got += (uint64_t)r;
+        }
+        close(fd);
+        // grew past its slot, or read unlike a local regular file (a short read before the
+        // end, or an end before st_size): sd_cas_file_checksum afterwards, which reads such
+        // a file exactly as hash.rs:15-21 does (1 MiB reads, stop at the first short one)
+        if (kind[i] == K_BATCH && (got == cap[k] || irregular || got < fsize[i])) kind[i] = K_STREAM;
+        h_lens[k] = kind[i] == K_BATCH ? got : 0;
+      }
+    });
+    // entries that failed or grew are hashed as empty buffers and ignored
+    hipError_t e = hipMemcpyAsync((char*)c->staging.p + (size_t)b * SLOT, pin, CK_WIN_FILES * 16,
+                                  hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync((char*)c->staging.p + (size_t)b * SLOT + HDR, data, o, hipMemcpyHostToDevice, s);
+    char* dbase = (char*)c->staging.p + (size_t)b * SLOT;
+    if (e == hipSuccess)
+      e = checksum_batch_device((const uint8_t*)(dbase + HDR), o, (const uint64_t*)dbase,
+                                (const uint64_t*)dbase + CK_WIN_FILES, m,
+                                (uint32_t*)(dbase + CK_WIN_FILES * 16), d_bad, c->ws.p, s);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(pin + CK_WIN_FILES * 16, dbase + CK_WIN_FILES * 16, m * 32,
+                         hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipEventRecord(done[b], s);
+    if (e != hipSuccess) { rc = fail(c, SD_CAS_EHIP, "file_checksums window: %s", hipGetErrorString(e)); break; }
+    pending[b] = true;
+  }
+  uint32_t bad = 0;
+  if (rc == SD_CAS_OK) {
+    hipError_t e = hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) rc = fail(c, SD_CAS_EHIP, "file_checksums: %s", hipGetErrorString(e));
+    else if (bad) rc = fail(c, SD_CAS_EHIP, "file_checksums: batch work list overflow");
+  }
+  (void)sd_ws_release(c, s);
+  (void)hipStreamSynchronize(s);
+  for (int b = 0; b < 2; b++) {
+    if (rc == SD_CAS_OK && pending[b]) emit(b);
+    (void)hipEventDestroy(done[b]);
+  }
+  if (rc) return rc;
+  // big files and files that grew: the streaming path, one at a time (after the windows:
+  // it reuses the pinned and device staging)
+  for (size_t i = 0; i < n; i++) {
+    if (kind[i] != K_STREAM) continue;
+    char* o = out_hex + 65 * i;
+    int err_no = 0;
+    const int r = sd_cas_file_checksum(c, paths[i], o, &err_no);
+    if (r == SD_CAS_EIO) { status[i] = -(err_no ? err_no : EIO); o[0] = 0; continue; }
+    if (r) return r;
+  }
+  for (size_t i = 0; i < n; i++)
+    if (status[i]) out_hex[65 * i] = 0;
+  return SD_CAS_OK;
+}
+
+}  // extern "C"
