@@ -589,7 +589,14 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
   }
   for (size_t w = nw >= 2 ? nw - 2 : 0; w < nw && rc == 0; w++) rc = finish(w);
   tr.mark("wait");
-  if (rc) (void)hipStreamSynchronize(c->stream);
+  if (rc) {
+    // a failed call leaves nothing in flight: its pulls (copy streams) and an early
+    // whole-file hash (copy2) would otherwise still read the staging, or write keys into it,
+    // while the next call gathers into the same buffers
+    (void)hipStreamSynchronize(c->copy);
+    (void)hipStreamSynchronize(c->copy2);
+    (void)hipStreamSynchronize(c->stream);
+  }
   if (rc) return rc;
   // whole files whose length is not their metadata size: read them as they are now
   // (fs::read, cas.rs:29) and hash the few of them as one host batch
