@@ -13,6 +13,7 @@ result is compared with the C oracle's gather + hash of the same (path, size) li
 (sd_cas_file_checksums: hash.rs's full-content BLAKE3) against the oracle's digest of each
 file's bytes.  Prints one JSON line per iteration and a summary; exit 1 on any mismatch."""
 import argparse
+import errno
 import json
 import os
 import shutil
@@ -97,7 +98,7 @@ def main():
             wk, ws = orc.generate_cas_keys_paths(bp, want_sz, 16, simd=True)
             # the batch oracle's whole-file buffer holds 100 KiB: a file that grew past it
             # under small metadata (cas.rs:29 reads the actual file) takes the one-path oracle
-            for i in np.nonzero(ws == -7)[0]:  # E2BIG
+            for i in np.nonzero(ws == -errno.E2BIG)[0]:
                 try:
                     wk[i], ws[i] = int(orc.generate_cas_id(bp[i], int(want_sz[i])), 16), 0
                 except OSError as e:
@@ -108,9 +109,9 @@ def main():
                 if mode != "none" and want_sz[i] == 0:  # a caller size of 0: no read at all
                     ok &= bool(status[i] == STATUS_NO_CAS and keys[i] == 0)
                 elif os.path.isdir(p):
-                    ok &= bool(status[i] == -21 and keys[i] == 0)  # EISDIR
+                    ok &= bool(status[i] == -errno.EISDIR and keys[i] == 0)
                 elif not os.path.exists(p):
-                    ok &= bool(status[i] == -2 and keys[i] == 0)  # ENOENT
+                    ok &= bool(status[i] == -errno.ENOENT and keys[i] == 0)
                 elif want_sz[i] == 0:
                     ok &= bool(status[i] == STATUS_NO_CAS and keys[i] == 0)
                 else:
@@ -130,9 +131,9 @@ def main():
                 ck = True
                 for p, d, e in zip(cp, dig, cerr):
                     if os.path.isdir(p):
-                        ck &= bool(e == 21 and d is None)
+                        ck &= bool(e == errno.EISDIR and d is None)
                     elif not os.path.exists(p):
-                        ck &= bool(e == 2 and d is None)
+                        ck &= bool(e == errno.ENOENT and d is None)
                     else:
                         with open(p, "rb") as fh:
                             ck &= bool(e == 0 and d == orc.blake3(fh.read()).hex())
