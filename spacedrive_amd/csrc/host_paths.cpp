@@ -463,7 +463,7 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
     // a 100-file step; the job's share of the host is 16 cores)
     const unsigned threads = std::max(1u, std::min(15u, (unsigned)((m + 6) / 7)));
     // the pump: metadata first, then each finished prefix of the content (items are taken
-    // in staging order, so a prefix of items is a prefix of bytes)
+    // in visit order, so a prefix of items is a prefix of the virtual byte space below)
     int prc = SD_CAS_OK;
     size_t ncopies = 0, ncopies_all = 0, npieces = 0;
     double copy_us = 0, first_us = -1, last_us = 0;
