@@ -84,7 +84,7 @@ struct sd_cas_ctx {
   int device = 0;
   hipStream_t stream = nullptr;  // compute
   hipStream_t copy = nullptr;    // H2D side stream
-  hipStream_t copy2 = nullptr;   // a second H2D stream (the streamed gather's pieces alternate)
+  hipStream_t copy2 = nullptr;   // the streamed gather's early whole-file hash (A/B: pieces alternate)
   hipEvent_t copy2_done = nullptr;
   hipEvent_t h2d_done = nullptr;
   hipEvent_t packed_h2d = nullptr;   // the job step's whole-file pieces have landed (early hash)
