@@ -10,6 +10,8 @@ after a 1 s settle, and the kernel's own rate.
   k2     K2 on config 2's 1 M whole-file messages (sizes U(1, 102,400))
   k2c    the same messages with all-zero content
   lane   the validator on 1 M buffers of U(0, 16) KiB (the lane-per-buffer kernel)
+  k1g    the fused chain (K1G + the region tables: the bench's N = 1 step)
+  one    the validator's K3 on one 16 GiB buffer
 """
 import argparse
 import json
@@ -65,6 +67,22 @@ def main():
                 content.zero_()
             units, unit = F, "files"
             launch = lambda: eng.hash_sampled(content, sizes, keys)  # noqa: E731
+        elif w == "k1g":
+            F = 1_310_720
+            content = torch.empty((F, 57344), dtype=torch.uint8, device="cuda")
+            sizes = torch.empty(F, dtype=torch.int64, device="cuda")
+            keys = torch.empty(F, dtype=torch.int64, device="cuda")
+            rep = torch.empty(F, dtype=torch.int32, device="cuda")
+            ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
+            eng.synth_sampled(3, 0, F, content, sizes, 57344, dup_permille=300)
+            units, unit = F, "files"
+            launch = lambda: eng.hash_group_sampled(content, sizes, keys, rep, ovf, want_objects=False)  # noqa: E731
+        elif w == "one":
+            n = 16 << 30
+            arena = torch.empty(n, dtype=torch.uint8, device="cuda")
+            eng.synth_stream(77, 0, 0, n, arena)
+            units, unit = n, "bytes"
+            launch = lambda: eng.checksum_dev(arena)  # noqa: E731  (blocking: returns the hex)
         elif w in ("k2", "k2c"):
             n = 1_000_000
             sizes = torch.empty(n, dtype=torch.int64, device="cuda")
@@ -126,7 +144,7 @@ def main():
                           "sclk_mhz_median": float(np.median(ck)) if ck else None,
                           "samples": len(settled)}), flush=True)
         del launch
-        content = sizes = keys = lens = offs = arena = d_offs = d_lens = out = None  # noqa: F841
+        content = sizes = keys = lens = offs = arena = d_offs = d_lens = out = rep = ovf = None  # noqa: F841
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
 
