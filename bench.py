@@ -15,14 +15,15 @@ are hashed (keys triple-buffered); every step's hash AND grouping complete insid
 timed region (--no-overlap serialises them).
 
 Output: ONE JSON line on rank 0 (driver contract), with
-  roofline      — K1 (sd_cas_sampled_kernel), timed by HIP events on its own stream, priced
-                  as SURVEY.md §8(d) prices it: 953 compressions x 792 spec int32 ops per
-                  file / kernel time vs the guide's int32 VALU peak (256 CUs x 4 SIMDs x 32
-                  lanes x 2.4 GHz = 78.6 T lane-ops/s); secondary views: issue slots (rotates
-                  and 3-input adds issue at half rate on gfx950, measured), the measured
-                  compute-only ceiling of this instruction stream, the HBM byte view (vs
-                  8 TB/s) and PMC traffic, VALU busy (PMC) and the power-capped clock
-                  (rocm-smi: K1 on random content runs at the socket power limit);
+  roofline      — K1 (sd_cas_sampled_kernel; K1G at N=1), timed by HIP events on its own
+                  stream, priced as SURVEY.md §8(d) prices it: 953 compressions x 792 spec
+                  int32 ops per file / kernel time vs the guide's int32 VALU peak (256 CUs x 4
+                  SIMDs x 32 lanes x 2.4 GHz = 78.6 T lane-ops/s); secondary views: the HBM
+                  byte view (vs 8 TB/s) and PMC traffic, and from ONE committed gpurun session
+                  (profiles/r05_valu_power.json, marked measured_in_this_run=false) the
+                  counter-based VALU instruction rate and VALU busy, the compute-only ceiling
+                  of K1's instruction stream per shader cycle and the power-capped clock;
+                  plus rocm-smi power / sclk sampled live during this run's sustained steps;
   sustained     — the same steps back to back for ~--sustain-seconds after the timed region
                   (the DVFS-settled rate, long enough for an outside utilisation sampler);
   e2e           — BASELINE config 3 as worded: sampled files streamed from pinned host
@@ -49,9 +50,6 @@ MSG_BYTES = 57352            # le64(size) || 57,344 sampled bytes
 COMPRESSIONS = 953           # 897 chunk blocks + 56 parents per sampled message
 SPEC_OPS = 792               # int32 ops per compression (7 rounds x 8 G x 14 + 8)
 HW_OPS = 680                 # VALU instructions per compression as compiled (add3/alignbit)
-# Issue slots per wave-compression: 230 v_xor + 112 v_add (full rate, 1 slot) and
-# 224 v_alignbit + 112 v_add3 (half rate on gfx950, 2 slots; profiles/r01_ubench_valu.log)
-SLOTS = 230 + 112 + 2 * (224 + 112)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 # grouping (group_hash.hip): see group_bytes_per_key (the minima of duplicates are the only
 # other stores)
@@ -79,12 +77,7 @@ def eng_region_capacity(n: int) -> int:
         sd += 1
     return int(mean) + 1 + 8 * sd + 64
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # 256 CUs x 4 SIMD32 x 32 lanes x 2.4 GHz = 78.6
-# measured ceiling of K1's own instruction stream (compute-only loop at 2.38 GHz, no loads):
-# profiles/r01_ubench_k1_clock.log
-K1_CEILING_FILES_S = 61.94e6
 PCIE_PEAK_GBS = 64.0         # PCIe Gen5 x16 per direction
-# full-rate wave64 VALU issue: 1024 SIMDs x 2.4 GHz / 2 cycles = 1228.8 G slots/s
-SLOT_PEAK_G = 1024 * 2.4e9 / 2 / 1e9
 
 
 def main() -> None:
@@ -189,6 +182,7 @@ def main() -> None:
           for _ in range(args.steps)]
     results = []      # the last step's ShardResult (sharded runs)
     overflows = []    # per-step overflow flags of the fixed-capacity exchange (device)
+    resolve_in_step = [False]  # read each step's flag inside the step (after an overflow)
     # fixed per-peer capacity: the exchange needs no host sync (spacedrive_amd/shard.py)
     capacity = fixed_capacity(F, world) if sharded else None
     # The exchange path reads part sizes back to the host (all_to_all_single needs host
@@ -210,11 +204,15 @@ def main() -> None:
             else:
                 r = sharded_group(keys[b], file0, ops, capacity=capacity)
                 if r.overflow is not None:
-                    # an overflowed fixed-capacity part is redone with the exact exchange
-                    # inside the step (collective, on this worker thread; the flag read is
-                    # the worker's only host sync), so every timed step's rep is exact
-                    overflows.append(int(r.overflow.item()))
-                    r.resolve()
+                    if resolve_in_step[0]:
+                        # the fallback mode: an overflowed fixed-capacity part is redone with
+                        # the exact exchange inside the step (collective, on this worker
+                        # thread; the flag read is one host sync per step)
+                        overflows.append(int(r.overflow.item()))
+                        r.resolve()
+                    else:
+                        # the flag stays on the device; it is read once after the timed loop
+                        overflows.append(r.overflow.clone())
                 results[:] = [r]
             grouped[b].record(side)
 
@@ -250,22 +248,37 @@ def main() -> None:
         for b in range(NBUF):
             wait_group(b)
 
+    def timed_region() -> float:
+        results.clear()
+        overflows.clear()
+        ovf.zero_()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(args.steps, True)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
     run(args.warmup, False)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    results.clear()
-    overflows.clear()
-    ovf.zero_()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(args.steps, True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    dt = timed_region()
+    # world 1 (--exchange) runs the exact form: its part sizes are read on the host per step
+    host_syncs_per_step = 1 if sharded and world == 1 else 0
+    if sharded and overflows and not resolve_in_step[0]:
+        # the fixed-capacity flags of the timed steps, read after the loop (no host sync
+        # inside a step); any overflow means that step's rep needed the exact redo, so the
+        # timed region is run again with the in-step redo (one flag read per step)
+        fl = torch.stack([f.reshape(()) for f in overflows]).max().reshape(1).to(torch.int64)
+        dist.all_reduce(fl, op=dist.ReduceOp.MAX)
+        if int(fl.item()):
+            resolve_in_step[0] = True
+            host_syncs_per_step = 1
+            dt = timed_region()
     last_keys = keys[(args.steps - 1) % NBUF]
     res = results[-1] if results else None
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -317,9 +330,9 @@ def main() -> None:
                              "launch (sd_bucket_min_regions); tables_ms = that launch alone, "
                              "after K1G, HIP events on its stream"}
     if sharded:
-        # every timed step's fixed-capacity exchange must have fit (else it would have been
-        # redone exactly outside the timed region, and the step time would not stand)
-        n_overflow = sum(overflows)
+        # timed steps whose fixed-capacity exchange overflowed (redone exactly inside the step
+        # in the fallback mode; 0 in the sync-free mode, else the run was repeated)
+        n_overflow = sum(int(f.item()) if torch.is_tensor(f) else f for f in overflows)
         objects = res.objects
     # the grouping alone (after the timed region: inside the steps it overlaps the next K1
     # on a side stream and shares the CUs with it, so its own speed is measured serially)
@@ -403,19 +416,24 @@ def main() -> None:
     # sustained: the same pipelined steps back to back (DVFS-settled; long enough for an
     # outside utilisation sampler to see the GPU busy), after the headline timed region
     sustained = None
+    smi_live = None
     if args.sustain_seconds > 0:
         n_sus = max(1, int(args.sustain_seconds / (dt / args.steps)))
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
+        smi = SmiSampler(torch.cuda.get_device_properties(local)) if rank == 0 else None
         t0 = time.perf_counter()
         run(n_sus, False)
         torch.cuda.synchronize()
+        if smi is not None:
+            smi_live = smi.stop()
         ts = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
         if sharded:
             dist.all_reduce(ts, op=dist.ReduceOp.MAX)
         sus_dt = float(ts.item())
         sustained = {"steps": n_sus, "seconds": sus_dt, "value": world * F * n_sus / sus_dt,
+                     "n_gpus": world,
                      "unit": "cas_ids/s", "ms_per_step": sus_dt / n_sus * 1e3}
 
     e2e = None
@@ -429,7 +447,6 @@ def main() -> None:
     achieved = F * MSG_BYTES / (kern_ms / 1e3) / 1e9  # per-GPU kernel GB/s
     valu = F * COMPRESSIONS * SPEC_OPS / (kern_ms / 1e3) / 1e12
     valu_hw = F * COMPRESSIONS * HW_OPS / (kern_ms / 1e3) / 1e12
-    slots = F * COMPRESSIONS * SLOTS / 64 / (kern_ms / 1e3) / 1e9  # G wave-issue-slots/s
 
     # HBM bytes per launch from PMC (TCC_MISS_sum x 128-B lines, committed summary of the
     # separate rocprofv3 --pmc pass on the same kernel), scaled to this launch's files
@@ -442,52 +459,12 @@ def main() -> None:
             if per_file is not None:
                 traffic = per_file * F
 
-    # the host-CPU baseline beside the line at EVERY world size (the reference path cas.rs:23-62
-    # on the host cores): rank 0 runs it after the timed region, the other ranks wait for it
-    # VALU busy of the headline kernel from the committed PMC pass (tools/pmc_valu.sh ->
-    # profiles/pmc_valu.json; counter conventions in tools/pmc_valu.py)
-    valu_busy = None
-    kname = "sd_cas_sampled_group_kernel" if fused else "sd_cas_sampled_kernel"
-    pv = os.path.join(ROOT, "profiles", "pmc_valu.json")
-    if os.path.exists(pv):
-        with open(pv) as fh:
-            rec = json.load(fh).get(kname)
-        if rec:
-            # issue cycles of K1's measured instruction mix at the PMC pass's own clock:
-            # full-rate v_xor/v_add 2 cycles, half-rate v_alignbit/v_add3 4 (wave64 on SIMD32)
-            mix_cycles = 2 * (230 + 112) + 4 * (224 + 112)
-            wave_comps = rec["counters_mean"]["SQ_WAVES"] * COMPRESSIONS
-            valu_busy = {"valu_busy": rec["valu_busy"], "valu_busy_full_rate": rec["valu_busy_full_rate"],
-                         "valu_pipe_busy_mix": wave_comps * mix_cycles / (1024 * rec["wall_cycles"]),
-                         "clock_ghz": rec.get("clock_ghz"),
-                         "source": "profiles/pmc_valu.json (rocprofv3 --pmc, tools/pmc_valu.sh)",
-                         "note": "valu_busy = SQ_ACTIVE_INST_VALU x 4 / (1,024 SIMDs x GRBM_GUI_ACTIVE/8) "
-                                 "(rocprof VALUBusy, 4 cycles per VALU instruction); "
-                                 "valu_pipe_busy_mix = the ARX mix's issue cycles (2 full-rate, 4 "
-                                 "half-rate per wave64 instruction) over the same SIMD cycles"}
-
-    # the power cap (tools/clock_probe.py -> profiles/r04_clock_probe.jsonl: rocm-smi socket
-    # power and sclk while K1 runs back to back): on random content K1 runs at the board's
-    # power limit and DVFS takes the clock below its maximum; on constant content it stays at
-    # the maximum clock below the limit — so the VALU ceiling that binds is the compute-only
-    # ceiling scaled to the power-capped clock
-    power = None
-    cp = os.path.join(ROOT, "profiles", "r04_clock_probe.jsonl")
-    if os.path.exists(cp):
-        with open(cp) as fh:
-            recs = {r.get("workload"): r for r in map(json.loads, fh) if r.get("workload")}
-        kr, kc = recs.get("k1"), recs.get("k1c")
-        if kr and kc and kr.get("sclk_mhz_median") and kc.get("sclk_mhz_median"):
-            ceil = K1_CEILING_FILES_S * kr["sclk_mhz_median"] / kc["sclk_mhz_median"]
-            power = {"power_w_random": kr["power_w_median"], "sclk_mhz_random": kr["sclk_mhz_median"],
-                     "power_w_constant": kc["power_w_median"], "sclk_mhz_constant": kc["sclk_mhz_median"],
-                     "ceiling_files_per_s_at_capped_clock": ceil,
-                     "frac_of_capped_ceiling": F / (kern_ms / 1e3) / ceil,
-                     "source": "profiles/r04_clock_probe.jsonl (tools/clock_probe.py: rocm-smi while K1 "
-                               "runs back to back on random vs all-zero content)",
-                     "note": "K1 on random content runs at the socket power limit (DVFS lowers sclk); "
-                             "on constant content it runs at the maximum sclk below the limit: the "
-                             "binding roof is the VALU issue ceiling at the power-capped clock"}
+    # VALU evidence of the headline kernel and the power-capped clock: the counters come from
+    # ONE committed gpurun session (tools/gpu_r5_valu_power.sh -> profiles/r05_valu_power.json:
+    # rocprofv3 --pmc pass, compute-only K1 ceiling and rocm-smi probe on the same box); the
+    # live part (power + sclk while the sustained steps run) is measured by this run
+    valu_busy, power = valu_power_evidence("sd_cas_sampled_group_kernel" if fused else "sd_cas_sampled_kernel",
+                                           F, kern_ms, sustained, smi_live)
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
@@ -510,7 +487,10 @@ def main() -> None:
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": None,
+            "vs_baseline": (value / cpu["value"]) if cpu else None,
+            "vs_baseline_basis": ("value / cpu_baseline.value: BASELINE.json's north_star names the "
+                                  "reference CPU path on the same box's host cores as THE baseline "
+                                  "(BASELINE.md publishes no number for this metric)"),
             "dtype": "u32",
             "data": "synthetic (on-device splitmix64 content, 30% duplicates), resident in HBM",
             "config": {
@@ -533,7 +513,12 @@ def main() -> None:
                     "capacity_per_peer": capacity[0], "spill_per_peer": capacity[1],
                     "bytes_sent_per_rank_per_step": exchange_bytes_per_step(world, capacity),
                     "bytes_sent_per_step_all_ranks": world * exchange_bytes_per_step(world, capacity),
-                    "host_syncs_per_step": 0, "timed_steps_overflowed": n_overflow,
+                    "host_syncs_per_step": host_syncs_per_step,
+                    "host_syncs_note": ("0: every step's fixed-capacity overflow flag stays on the "
+                                        "device and is read once after the timed loop; 1: an "
+                                        "overflow was seen, so the steps were re-timed with the "
+                                        "flag read (and the exact redo) inside each step"),
+                    "timed_steps_overflowed": n_overflow,
                     "serial_ms": exchange_ms,
                     "serial_ms_phases": exchange_phases,
                     "serial_ms_note": "one step's exchange + grouping alone (max over ranks, "
@@ -563,16 +548,8 @@ def main() -> None:
                 "kernel_ms_ranks": {"min": min(k1_ms_ranks), "max": max(k1_ms_ranks),
                                     "per_rank": k1_ms_ranks},
                 "work_per_file": {"message_bytes": MSG_BYTES, "compressions": COMPRESSIONS,
-                                  "spec_ops_per_compression": SPEC_OPS,
-                                  "issue_slots_per_wave_compression": SLOTS},
+                                  "spec_ops_per_compression": SPEC_OPS},
                 # secondary views of the same kernel time
-                "issue_slots": {"achieved": slots, "peak": SLOT_PEAK_G, "unit": "G wave-issue-slots/s",
-                                "frac": slots / SLOT_PEAK_G,
-                                "note": "v_alignbit_b32 / v_add3_u32 issue at half rate on gfx950 "
-                                        "(profiles/r01_ubench_valu_v2.log): 1,014 slots per compression"},
-                "measured_ceiling": {"files_per_s": K1_CEILING_FILES_S,
-                                     "frac": F / (kern_ms / 1e3) / K1_CEILING_FILES_S,
-                                     "source": "compute-only K1 loop at 2.38 GHz, profiles/r01_ubench_k1_clock.log"},
                 "hbm": {"achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS,
                         "algorithmic_bytes_per_launch": F * MSG_BYTES,
@@ -612,6 +589,119 @@ def main() -> None:
         worker.shutdown()
     if sharded:
         dist.destroy_process_group()
+
+
+class SmiSampler:
+    """rocm-smi socket power and shader clock of THIS rank's card, sampled every ~0.25 s by a
+    thread (each sample a `rocm-smi -P -g --showbus --json` child process: it reads the SMI,
+    no HIP) until stop(); the card is matched by PCI bus number, and with several cards and
+    no match nothing is reported (never another card's numbers)."""
+
+    def __init__(self, props, settle_s: float = 1.0):
+        import threading
+        self.bus = getattr(props, "pci_bus_id", None)
+        self.settle = settle_s
+        self.samples = []
+        self.t0 = time.perf_counter()
+        self._stop = threading.Event()
+        self._th = threading.Thread(target=self._loop, daemon=True)
+        self._th.start()
+
+    def _sample(self):
+        import re
+        import subprocess
+        try:
+            r = subprocess.run(["rocm-smi", "-P", "-g", "--showbus", "--json"], capture_output=True,
+                               text=True, timeout=10)
+            d = json.loads(r.stdout)
+        except (OSError, ValueError, subprocess.SubprocessError):
+            return None
+        cards = [v for k, v in d.items() if k.startswith("card") and isinstance(v, dict)]
+        pick = None
+        for c in cards:
+            for k, v in c.items():
+                m = re.search(r"[0-9a-fA-F]{4}:([0-9a-fA-F]{2}):", str(v)) if "bus" in k.lower() else None
+                if m and self.bus is not None and int(m.group(1), 16) == self.bus:
+                    pick = c
+        if pick is None and len(cards) == 1:
+            pick = cards[0]
+        if pick is None:
+            return None
+        power = sclk = None
+        for k, v in pick.items():
+            kl = k.lower()
+            if "power" in kl and power is None:
+                m = re.search(r"[\d.]+", str(v))
+                power = float(m.group()) if m else None
+            if "sclk" in kl and sclk is None:
+                m = re.search(r"(\d+)\s*mhz", str(v).lower())
+                sclk = float(m.group(1)) if m else None
+        return power, sclk
+
+    def _loop(self):
+        while not self._stop.is_set():
+            t = time.perf_counter() - self.t0
+            smp = self._sample()
+            if smp is not None:
+                self.samples.append((t, *smp))
+            self._stop.wait(0.25)
+
+    def stop(self):
+        import statistics
+        self._stop.set()
+        self._th.join(timeout=15)
+        settled = [x for x in self.samples if x[0] >= self.settle]
+        pw = [x[1] for x in settled if x[1] is not None]
+        ck = [x[2] for x in settled if x[2] is not None]
+        if not pw and not ck:
+            return None
+        return {"power_w_median": statistics.median(pw) if pw else None,
+                "sclk_mhz_median": statistics.median(ck) if ck else None,
+                "samples": len(settled), "pci_bus": self.bus}
+
+
+def valu_power_evidence(kname: str, F: int, kern_ms: float, sustained, live):
+    """(roofline.valu_busy, roofline.power).  Counter and ceiling figures are read from the
+    committed same-session file profiles/r05_valu_power.json (tools/valu_power.py) and marked
+    measured_in_this_run = false with that session's id; `live` (rocm-smi during this run's
+    sustained steps) is this run's own, and the frac against the compute-only ceiling is
+    given both ways: same-session (probe clock) and live (this run's clock)."""
+    path = os.path.join(ROOT, "profiles", "r05_valu_power.json")
+    if not os.path.exists(path):
+        return None, ({"live": live, "measured_in_this_run": True} if live else None)
+    with open(path) as fh:
+        vp = json.load(fh)
+    prov = {"measured_in_this_run": False, "session": vp.get("session"),
+            "source": "profiles/r05_valu_power.json (tools/gpu_r5_valu_power.sh: rocprofv3 --pmc, "
+                      "tools/ubench_k1 compute-only loop and tools/clock_probe.py in ONE gpurun session)"}
+    valu = None
+    rec = (vp.get("pmc") or {}).get(kname)
+    if rec:
+        valu = {"valu_busy": rec["valu_busy"],
+                "instr_rate_t_per_s": rec["instr_rate_t_per_s"],
+                "instr_rate_frac_of_peak": rec["instr_rate_t_per_s"] / VALU_PEAK_TOPS,
+                "instr_per_wave": rec["valu_instr_per_wave"], "clock_ghz": rec.get("clock_ghz"),
+                "spec_ops_t_per_s_this_run": F * COMPRESSIONS * SPEC_OPS / (kern_ms / 1e3) / 1e12,
+                "note": "instr_rate = SQ_INSTS_VALU x 64 lanes / the PMC pass's mean kernel time "
+                        "(every VALU instruction of the kernel, against the 78.6 T lane-op/s "
+                        "full-rate peak); valu_busy = rocprof VALUBusy = SQ_ACTIVE_INST_VALU x 4 / "
+                        "(1,024 SIMDs x GRBM_GUI_ACTIVE/8).  The ARX mix issues at ~4 cycles per "
+                        "wave64 instruction (DESIGN.md 2.1), which is what VALUBusy charges",
+                **prov}
+    ceil = vp.get("ceiling") or {}
+    power = {"session": {k: vp.get(k) for k in ("clock_probe",)}, **prov}
+    fpc = ceil.get("files_per_cycle")
+    if fpc:
+        power["ceiling_files_per_cycle"] = fpc
+        power["session_frac_of_capped_ceiling"] = ceil.get("k1_frac_of_capped_ceiling")
+    if live:
+        power["live"] = dict(live, measured_in_this_run=True)
+        if fpc and live.get("sclk_mhz_median") and sustained:
+            cap = fpc * live["sclk_mhz_median"] * 1e6
+            power["live"]["ceiling_files_per_s_at_live_clock"] = cap
+            power["live"]["sustained_frac_of_capped_ceiling"] = (
+                sustained["value"] / sustained.get("n_gpus", 1) / cap)
+    return valu, power
 
 
 def fail(msg: str) -> None:
@@ -709,22 +799,34 @@ def e2e_leg(eng, content, sizes, keys, args, world, rank, dev, dist):
 
 
 def cpu_threads(world: int) -> int:
-    """Host threads for the CPU baseline: SD_CPU_BASELINE_THREADS, else OMP_NUM_THREADS when
-    it grants more than one (the GPU box sets it to its 16-core share per GPU), else the cores
-    this process may run on, capped at 16 per rank.  torch.distributed.run sets
-    OMP_NUM_THREADS=1 for its workers when the caller left it unset, which would time the
-    node's CPU on one core beside an N-GPU line."""
+    """Host threads for the CPU baseline beside an N-GPU line: the WHOLE node's share, never
+    one GPU's.  SD_CPU_BASELINE_THREADS if set; else OMP_NUM_THREADS x world when
+    OMP_NUM_THREADS grants more than one (the GPU box sets it to its per-GPU core share, 16),
+    else 16 x world; both capped by the cores this process may run on (its affinity mask).
+    torch.distributed.run sets OMP_NUM_THREADS=1 for its workers when the caller left it
+    unset, which would time the node's CPU on one core beside an N-GPU line."""
     v = int(os.environ.get("SD_CPU_BASELINE_THREADS", "0") or 0)
     if v > 0:
         return v
-    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    if omp > 1:
-        return omp
     try:
         avail = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         avail = os.cpu_count() or 1
-    return max(1, min(avail, 16 * max(1, world)))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    per_gpu = omp if omp > 1 else 16
+    return max(1, min(avail, per_gpu * max(1, world)))
+
+
+def cpu_model() -> str | None:
+    """The host CPU's model name (/proc/cpuinfo), for the baseline's record."""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.lower().startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def cpu_baseline(content, sizes, keys, seconds: float):
@@ -759,6 +861,8 @@ def cpu_baseline(content, sizes, keys, seconds: float):
     one_thread = r1 * m1 / (time.perf_counter() - t0)
     return {"value": files / dt, "unit": "cas_ids/s", "hashed_gb_per_s": files * MSG_BYTES / dt / 1e9,
             "cores": threads, "kind": "port", "value_1thread": one_thread,
+            "cpu_model": cpu_model(), "cpus_online": os.cpu_count(),
+            "threads_rule": "cpu_threads(world): min(affinity, OMP_NUM_THREADS (or 16) x n_gpus)",
             "simd": "avx512 16-lane" if orc.has_simd() else "scalar",
             "sample": f"{reps} passes over the first {m} files of the bench batch (hashing only, "
                       f"messages pre-gathered in DRAM), {dt:.1f}s",

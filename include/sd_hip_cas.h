@@ -24,6 +24,12 @@
  *     sd_cas_ctx_stream(ctx) for the context's own stream); they enqueue and return
  *     without synchronising unless stated.  Host-buffer functions are blocking and run
  *     on the context's streams.
+ *   - Stream ordering is the caller's for its own buffers: a device buffer the caller
+ *     initialises (a zeroed flag or counter, a prefilled output) must be written on the
+ *     stream passed to the *_dev call, or be complete (event / synchronize) before the
+ *     call — the library orders its work on that stream and its internal side streams,
+ *     not against other streams.  E.g. torch.zeros(...) runs on torch's current stream: pass
+ *     that stream, or synchronise after the fill.
  *   - Contexts are not thread-safe; use one per (thread, device).
  */
 #ifndef SD_HIP_CAS_H
@@ -312,7 +318,11 @@ int sd_cas_group_chunked_dev(sd_cas_ctx* ctx, const uint32_t* d_rep, size_t n, u
  *   d_keys[i]  cas key of row i (read for hashed rows only)
  *   rows       the file_paths the job's orphan query returns: object_id or cas_id NULL,
  *              not a directory, and indexed size_in_bytes != 0 (orphan_path_filters,
- *              file_identifier_job.rs:251-277) — a file indexed empty is never a row
+ *              file_identifier_job.rs:251-277) — a file indexed empty is never a row.
+ *              These calls model rows with object_id NULL; rows that already hold an
+ *              Object (object_id set, cas_id NULL) need sd_cas_identifier_links_ex below.
+ *              A stale cas_id on a row without an Object changes nothing (it is rewritten
+ *              before find_many and connects no Object)
  *   d_state[i] SD_CAS_ROW_* (u8; NULL = every row hashed): HASHED = cas_id computed,
  *              NO_CAS = fs::metadata length 0 at identification time (a file emptied
  *              after indexing: no cas_id, mod.rs:78-86), ERROR = FileMetadata::new failed
@@ -371,6 +381,37 @@ int sd_cas_identifier_links_seeded(sd_cas_ctx* ctx, const uint64_t* h_keys, cons
                                    const uint32_t* h_seed_objects, size_t n_seed, uint32_t* h_step,
                                    uint32_t* h_object, uint8_t* h_action, uint64_t* h_step_counts,
                                    size_t max_steps, uint64_t* out_steps);
+/* The same job with rows that ALREADY OWN an Object: the orphan query is `object_id IS NULL OR
+ * cas_id IS NULL` (file_identifier_job.rs:258-261), so a file_path with an Object but no
+ * cas_id is a row — the watcher's sequence for a file created empty (it gets an Object with
+ * no cas_id, watcher/utils.rs:236-293) and then written (the update keeps the old NULL
+ * cas_id, :473-490).  pre_objects[i] = the Object id row i's file_path holds (< 2^31, ids
+ * ascending in the DB's row order like the seeds) or SD_CAS_NO_OBJECT; NULL = none.
+ * Semantics (mod.rs:157-253): the step that processes a HASHED row writes its cas_id X
+ * first, so that step's find_many also returns the row's Object under X: every row of the
+ * step with key X links to the smallest Object id carrying X (seeds, pre-existing Objects of
+ * X rows processed in this or an earlier step, and — only when no pre-job Object carries X —
+ * the Object created for X's first row) and X never creates.  A pre-existing Object can
+ * therefore take over a key that an earlier step created an Object for: rows of later
+ * steps link to it (SD_CAS_LINK_EXISTING).  The row itself is re-linked (counted as linked),
+ * also to a smaller Object than its own.  A NO_CAS row with an Object still creates a new
+ * one (mod.rs:248-253) and an ERROR row keeps its Object, stays orphan and is DROPPED; for
+ * both d_object says what the job did (i / SD_CAS_NO_OBJECT), not the untouched column.
+ * Ids >= 2^31 other than SD_CAS_NO_OBJECT, in seeds or pre_objects, fail with SD_CAS_EINVAL
+ * (the device call checks them on the device).  Costs one stable 64-bit sort of the n keys
+ * plus two linear scans over them when pre_objects != NULL.  n < 2^31. */
+int sd_cas_identifier_links_ex_dev(sd_cas_ctx* ctx, const uint64_t* d_keys, const uint8_t* d_state,
+                                   size_t n, uint32_t chunk, const uint64_t* d_seed_keys,
+                                   const uint32_t* d_seed_objects, size_t n_seed,
+                                   const uint32_t* d_pre_objects, uint32_t* d_step,
+                                   uint32_t* d_object, uint8_t* d_action, uint64_t* h_step_counts,
+                                   size_t max_steps, uint64_t* out_steps, void* stream);
+int sd_cas_identifier_links_ex(sd_cas_ctx* ctx, const uint64_t* h_keys, const uint8_t* h_state,
+                               size_t n, uint32_t chunk, const uint64_t* h_seed_keys,
+                               const uint32_t* h_seed_objects, size_t n_seed,
+                               const uint32_t* h_pre_objects, uint32_t* h_step, uint32_t* h_object,
+                               uint8_t* h_action, uint64_t* h_step_counts, size_t max_steps,
+                               uint64_t* out_steps);
 
 /* Stable LSD radix sort of (u64 key, u32 val) on bits [begin_bit, end_bit).
  * d_vals_in == NULL sorts the identity 0..n-1. */

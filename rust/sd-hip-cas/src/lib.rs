@@ -144,6 +144,20 @@ extern "C" {
                                           h_object: *mut u32, h_action: *mut u8,
                                           h_step_counts: *mut u64, max_steps: usize,
                                           out_steps: *mut u64) -> c_int;
+    pub fn sd_cas_identifier_links_ex_dev(ctx: *mut sd_cas_ctx, d_keys: *const u64, d_state: *const u8,
+                                          n: usize, chunk: u32, d_seed_keys: *const u64,
+                                          d_seed_objects: *const u32, n_seed: usize,
+                                          d_pre_objects: *const u32, d_step: *mut u32,
+                                          d_object: *mut u32, d_action: *mut u8,
+                                          h_step_counts: *mut u64, max_steps: usize,
+                                          out_steps: *mut u64, stream: *mut c_void) -> c_int;
+    pub fn sd_cas_identifier_links_ex(ctx: *mut sd_cas_ctx, h_keys: *const u64, h_state: *const u8,
+                                      n: usize, chunk: u32, h_seed_keys: *const u64,
+                                      h_seed_objects: *const u32, n_seed: usize,
+                                      h_pre_objects: *const u32, h_step: *mut u32,
+                                      h_object: *mut u32, h_action: *mut u8,
+                                      h_step_counts: *mut u64, max_steps: usize,
+                                      out_steps: *mut u64) -> c_int;
     pub fn sd_cas_sort_pairs_dev(ctx: *mut sd_cas_ctx, d_keys_in: *const u64, d_vals_in: *const u32,
                                  n: usize, d_keys_out: *mut u64, d_vals_out: *mut u32, begin_bit: c_int,
                                  end_bit: c_int, stream: *mut c_void) -> c_int;
@@ -224,6 +238,17 @@ pub enum RowState {
     NoCas,
     /// FileMetadata::new failed: logged and dropped from the step (mod.rs:125-141)
     Error,
+}
+
+/// One orphan row with the Object its file_path may already hold: the orphan query is
+/// `object_id IS NULL OR cas_id IS NULL` (file_identifier_job.rs:258-261), so a file the
+/// watcher gave an Object while it was empty and that was written since (object_id set,
+/// cas_id NULL; watcher/utils.rs:236-293, 473-490) is a row too.  `object` = that Object's
+/// id (< 2^31, the DB's row order), `None` for the usual row.
+#[derive(Clone, Copy, Debug, PartialEq, Eq)]
+pub struct OrphanRow {
+    pub state: RowState,
+    pub object: Option<u32>,
 }
 
 /// One job step's DB batches (mod.rs:157-347): `creates` feed `create_many` + the link
@@ -375,16 +400,31 @@ impl HipCas {
     /// (mod.rs:180-253; the query has no location filter).
     pub fn identifier_links_existing(&mut self, rows: &[RowState], chunk: u32,
                                      existing: &[ExistingObject]) -> io::Result<Vec<StepBatch>> {
+        let orphans: Vec<OrphanRow> = rows.iter().map(|&state| OrphanRow { state, object: None }).collect();
+        self.identifier_links_orphans(&orphans, chunk, existing)
+    }
+
+    /// The general job: rows may already own an Object (`OrphanRow::object`).  The step that
+    /// processes such a Hashed row writes its cas_id first, so its find_many (mod.rs:157-198)
+    /// also returns that Object: every row of the step with the cas_id links to the smallest
+    /// Object id carrying it (`links_existing`, the row itself included) and the cas_id never
+    /// creates (mod.rs:202-253) — sd_cas_identifier_links_ex.
+    pub fn identifier_links_orphans(&mut self, rows: &[OrphanRow], chunk: u32,
+                                    existing: &[ExistingObject]) -> io::Result<Vec<StepBatch>> {
         let n = rows.len();
-        let keys: Vec<u64> = rows.iter().map(|r| if let RowState::Hashed(k) = r { k.0 } else { 0 }).collect();
+        let keys: Vec<u64> = rows.iter().map(|r| if let RowState::Hashed(k) = r.state { k.0 } else { 0 }).collect();
         let state: Vec<u8> = rows
             .iter()
-            .map(|r| match r {
+            .map(|r| match r.state {
                 RowState::Hashed(_) => SD_CAS_ROW_HASHED,
                 RowState::NoCas => SD_CAS_ROW_NO_CAS,
                 RowState::Error => SD_CAS_ROW_ERROR,
             })
             .collect();
+        let pre: Option<Vec<u32>> = rows
+            .iter()
+            .any(|r| r.object.is_some())
+            .then(|| rows.iter().map(|r| r.object.unwrap_or(SD_CAS_NO_OBJECT)).collect());
         let max_steps = unsafe { sd_cas_identifier_max_steps(n, chunk) };
         let (mut step, mut object, mut action) = (vec![0u32; n], vec![0u32; n], vec![0u8; n]);
         let mut counts = vec![0u64; 2 * max_steps.max(1)];
@@ -392,10 +432,11 @@ impl HipCas {
         let seed_keys: Vec<u64> = existing.iter().map(|e| e.cas_id.0).collect();
         let seed_ids: Vec<u32> = existing.iter().map(|e| e.id).collect();
         let rc = unsafe {
-            sd_cas_identifier_links_seeded(self.ctx, keys.as_ptr(), state.as_ptr(), n, chunk,
-                                           seed_keys.as_ptr(), seed_ids.as_ptr(), existing.len(),
-                                           step.as_mut_ptr(), object.as_mut_ptr(), action.as_mut_ptr(),
-                                           counts.as_mut_ptr(), max_steps, &mut steps)
+            sd_cas_identifier_links_ex(self.ctx, keys.as_ptr(), state.as_ptr(), n, chunk,
+                                       seed_keys.as_ptr(), seed_ids.as_ptr(), existing.len(),
+                                       pre.as_ref().map_or(ptr::null(), |p| p.as_ptr()),
+                                       step.as_mut_ptr(), object.as_mut_ptr(), action.as_mut_ptr(),
+                                       counts.as_mut_ptr(), max_steps, &mut steps)
         };
         if rc != 0 {
             return Err(self.err(rc));

@@ -69,6 +69,10 @@ SIGNATURES = [
      [_vp, _vp, _vp, _sz, _u32, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _sz, _vp, _vp]),
     ("sd_cas_identifier_links_seeded", _i,
      [_vp, _vp, _vp, _sz, _u32, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _sz, _vp]),
+    ("sd_cas_identifier_links_ex_dev", _i,
+     [_vp, _vp, _vp, _sz, _u32, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp]),
+    ("sd_cas_identifier_links_ex", _i,
+     [_vp, _vp, _vp, _sz, _u32, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     ("sd_cas_sort_pairs_dev", _i, [_vp, _vp, _vp, _sz, _vp, _vp, _i, _i, _vp]),
     ("sd_cas_checksum_dev", _i, [_vp, _vp, _u64, _vp, _vp]),
     ("sd_cas_file_checksum", _i, [_vp, _cp, _cp, ctypes.POINTER(_i)]),

@@ -38,6 +38,7 @@ SAMPLED_CONTENT_LEN = 2 * HEADER_OR_FOOTER_SIZE + SAMPLE_COUNT * SAMPLE_SIZE  # 
 CHUNK_SIZE = 100
 MAX_PACKED_CONTENT_LEN = 104 * 1024 - 8
 THRESHOLD_DEFAULT = (1 << 64) - 1  # SD_CAS_THRESHOLD_DEFAULT
+NO_OBJECT = NO_STEP = 0xFFFFFFFF   # SD_CAS_NO_OBJECT / SD_CAS_NO_STEP
 
 
 def key_to_cas_id(key: int) -> str:
@@ -63,6 +64,32 @@ def _stream(stream: Optional[int]) -> int:
 
 def _np_ptr(a: np.ndarray) -> int:
     return int(a.ctypes.data)
+
+
+def _check_dev(t, dtypes, n: int, what: str) -> None:
+    """A device tensor handed to a *_dev call: one of `dtypes`, n elements, contiguous, on a
+    GPU — checked before the library reads it as raw memory."""
+    if t.dtype not in dtypes or t.numel() != n or not t.is_contiguous() or not t.is_cuda:
+        raise ValueError(f"{what}: expected a contiguous CUDA tensor of {n} x "
+                         f"{'/'.join(str(d) for d in dtypes)}, got {tuple(t.shape)} {t.dtype} "
+                         f"on {t.device}")
+
+
+def _object_ids(ids, what: str, none_ok: bool) -> np.ndarray:
+    """Object ids as the u32 column of the link emission: each in [0, 2^31) (the seeded
+    grouping's row tag is bit 31); none_ok: -1 / None / 0xFFFFFFFF = no Object."""
+    a = np.asarray([NO_OBJECT if x is None else x for x in ids] if not isinstance(ids, np.ndarray)
+                   else ids)
+    if a.size == 0:
+        return np.zeros(0, dtype=np.uint32)
+    if a.dtype.kind not in "iu":
+        raise ValueError(f"{what}: integer Object ids expected, got {a.dtype}")
+    a = a.astype(np.int64)
+    none = (a == -1) | (a == NO_OBJECT)
+    bad = ~none & ((a < 0) | (a >= 1 << 31)) if none_ok else (a < 0) | (a >= 1 << 31)
+    if bad.any():
+        raise ValueError(f"{what}: Object id {int(a[bad][0])} outside [0, 2^31)")
+    return np.ascontiguousarray(np.where(none, NO_OBJECT, a).astype(np.uint32))
 
 
 def _path_array(paths: Sequence) -> tuple[object, int]:
@@ -376,17 +403,23 @@ class CasEngine:
         return int(c.value), int(ln.value)
 
     def identifier_links(self, keys, state=None, chunk: int = CHUNK_SIZE,
-                         stream: Optional[int] = None, existing=None):
+                         stream: Optional[int] = None, existing=None, pre_objects=None):
         """Object-link emission of one file-identifier job over the rows (ascending
-        file_path.id) — sd_cas_identifier_links[_seeded]_dev: returns (step, object, action)
+        file_path.id) — sd_cas_identifier_links_ex_dev: returns (step, object, action)
         device tensors (int32, int32, uint8) and the per-step (created, linked) counts as an
         int64 numpy array [steps, 2].  state: uint8 ROW_* per row (None = all hashed).
-        existing: None (a fresh library) or (seed_keys int64, seed_objects int32) device
-        tensors — the Objects the library holds before the job, as (cas key, Object id)
+        existing: None (a fresh library) or (seed_keys int64/uint64, seed_objects int32)
+        device tensors — the Objects the library holds before the job, as (cas key, Object id)
         pairs (mod.rs:180-198); a row whose key one carries links to the smallest such id
-        (action LINK_EXISTING)."""
+        (action LINK_EXISTING).  pre_objects: None or an int32 device tensor, per row the
+        Object its file_path already holds (object_id set, cas_id NULL:
+        file_identifier_job.rs:258-261) or -1 (= SD_CAS_NO_OBJECT) — see
+        sd_cas_identifier_links_ex_dev.  Ids must be < 2^31 (checked by the library)."""
         import torch
         n = int(keys.numel())
+        _check_dev(keys, (torch.int64, torch.uint64), n, "keys")
+        if state is not None:
+            _check_dev(state, (torch.uint8,), n, "state")
         dev = keys.device
         step = torch.empty(n, dtype=torch.int32, device=dev)
         obj = torch.empty(n, dtype=torch.int32, device=dev)
@@ -396,19 +429,26 @@ class CasEngine:
         steps = ctypes.c_uint64(0)
         sk, so = existing if existing is not None else (None, None)
         ns = 0 if sk is None else int(sk.numel())
-        self._check(self.L.sd_cas_identifier_links_seeded_dev(
+        if ns:
+            _check_dev(sk, (torch.int64, torch.uint64), ns, "existing keys")
+            _check_dev(so, (torch.int32, torch.uint32), ns, "existing Object ids")
+        if pre_objects is not None:
+            _check_dev(pre_objects, (torch.int32, torch.uint32), n, "pre_objects")
+        self._check(self.L.sd_cas_identifier_links_ex_dev(
             self.h, _ptr(keys), _ptr(state) if state is not None else None, n, int(chunk),
             _ptr(sk) if ns else None, _ptr(so) if ns else None, ns,
+            _ptr(pre_objects) if pre_objects is not None else None,
             _ptr(step), _ptr(obj), _ptr(act), _np_ptr(counts), ms, ctypes.byref(steps),
             _stream(stream)), "identifier_links")
         k = int(steps.value)
         return step, obj, act, counts[:2 * k].reshape(k, 2).astype(np.int64)
 
     def identifier_links_host(self, keys: np.ndarray, state: Optional[np.ndarray] = None,
-                              chunk: int = CHUNK_SIZE, existing=None):
-        """sd_cas_identifier_links[_seeded] (host arrays): (step u32, object u32, action u8,
+                              chunk: int = CHUNK_SIZE, existing=None, pre_objects=None):
+        """sd_cas_identifier_links_ex (host arrays): (step u32, object u32, action u8,
         counts int64 [steps, 2]) — the DB layer's view of the same emission.  existing: None
-        or (seed_keys, seed_objects) numpy arrays (see identifier_links)."""
+        or (seed_keys, seed_objects) numpy arrays; pre_objects: None or per-row Object ids
+        (NO_OBJECT / -1 = none) — see identifier_links."""
         n = len(keys)
         k = np.ascontiguousarray(keys, dtype=np.uint64)
         st = None if state is None else np.ascontiguousarray(state, dtype=np.uint8)
@@ -420,15 +460,21 @@ class CasEngine:
         steps = ctypes.c_uint64(0)
         if existing is not None:
             sk = np.ascontiguousarray(existing[0], dtype=np.uint64)
-            so = np.ascontiguousarray(existing[1], dtype=np.uint32)
+            so = _object_ids(existing[1], "existing Object ids", none_ok=False)
             if len(sk) != len(so):
                 raise ValueError("existing: as many Object ids as cas keys")
         else:
             sk = so = np.zeros(0, dtype=np.uint64)
         ns = len(sk)
-        self._check(self.L.sd_cas_identifier_links_seeded(
+        po = None
+        if pre_objects is not None:
+            po = _object_ids(pre_objects, "pre_objects", none_ok=True)
+            if po.shape != (n,):
+                raise ValueError(f"pre_objects has shape {po.shape}, expected ({n},)")
+        self._check(self.L.sd_cas_identifier_links_ex(
             self.h, _np_ptr(k), _np_ptr(st) if st is not None else None, n, int(chunk),
             _np_ptr(sk) if ns else None, _np_ptr(so) if ns else None, ns,
+            _np_ptr(po) if po is not None else None,
             _np_ptr(step), _np_ptr(obj), _np_ptr(act), _np_ptr(counts), ms, ctypes.byref(steps)),
             "identifier_links")
         s = int(steps.value)
@@ -576,7 +622,8 @@ class StepResult:
 
 
 def identifier_job_step(paths: Sequence[str], chunk: int = CHUNK_SIZE,
-                        eng: Optional[CasEngine] = None, existing=None) -> StepResult:
+                        eng: Optional[CasEngine] = None, existing=None,
+                        pre_objects=None) -> StepResult:
     """Run the file identifier over ``paths`` (ascending file_path.id order: the rows the
     job's orphan query returns — object/cas NULL and indexed size != 0, orphan_path_filters,
     file_identifier_job.rs:251-277) as file_identifier_job.rs:180-236 / mod.rs:98-350 would:
@@ -585,8 +632,12 @@ def identifier_job_step(paths: Sequence[str], chunk: int = CHUNK_SIZE,
     GPU link emission (sd_cas_identifier_links: grouping + the cursor walk, a last row that
     stays orphan is queried again by the next step).  existing: None for a fresh library,
     else (cas_ids or keys, Object ids) of the Objects the library already holds
-    (mod.rs:180-238: a row whose cas_id one carries links to the lowest such id).  Returns
-    the per-file decisions, the per-step batches and the summed (created, linked)."""
+    (mod.rs:180-238: a row whose cas_id one carries links to the lowest such id).
+    pre_objects: None, or per row the Object id its file_path already holds (a file the
+    watcher gave an Object while it was empty, then written: object_id set, cas_id NULL,
+    watcher/utils.rs:236-293,473-490) or None / -1 — such rows and the rows of their step
+    with the same cas_id link to the smallest Object carrying it (sd_cas_identifier_links_ex).
+    Returns the per-file decisions, the per-step batches and the summed (created, linked)."""
     eng = eng or engine()
     res = StepResult()
     n = len(paths)
@@ -608,7 +659,8 @@ def identifier_job_step(paths: Sequence[str], chunk: int = CHUNK_SIZE,
         ek, eo = existing
         ek = np.array([cas_id_to_key(x) if isinstance(x, str) else int(x) for x in ek], dtype=np.uint64)
         seed = (ek, np.asarray(eo, dtype=np.uint32))
-    step, obj, act, counts = eng.identifier_links_host(all_keys, state, chunk, existing=seed)
+    step, obj, act, counts = eng.identifier_links_host(all_keys, state, chunk, existing=seed,
+                                                       pre_objects=pre_objects)
     res.steps = [StepBatch(k, total_created=int(c), total_linked=int(ln))
                  for k, (c, ln) in enumerate(counts)]
     for i in range(n):

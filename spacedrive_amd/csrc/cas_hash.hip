@@ -40,33 +40,13 @@ namespace sdcas {
 constexpr uint32_t SAMPLED_PAIRS = SAMPLED_CONTENT_LEN / 128;  // 448
 constexpr uint32_t SAMPLED_CHUNKS = SAMPLED_CONTENT_LEN / 1024;  // 56 full chunks
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-// NT: non-temporal loads — kept for the A/B in tools/ubench_k1.hip only: measured 1.6x
-// SLOWER (33.7 vs 55.0 M files/s), the 8 dwordx4 loads of one 128-B line no longer share
-// the line in L2 and each goes to HBM
-// Layouts of the sampled content in HBM (quad = 16 B; q points at the lane's first quad):
-//   ROW   (0): file f at content + f*stride; quad i of pair P at q[8P + i]
-//   LINE  (1): tiles of 64 files; pair P of lane l at tile + (64P + l)*128 B  -> q[512P + i]
-//   QUAD  (2): tiles of 64 files; quad j of lane l at tile + (64j + l)*16 B    -> q[512P + 64i]
-enum : int { LAYOUT_ROW = 0, LAYOUT_LINE = 1, LAYOUT_QUAD = 2 };
-template <int L> struct LayoutStride;
-template <> struct LayoutStride<LAYOUT_ROW> { static constexpr uint32_t P = 8, I = 1; };
-template <> struct LayoutStride<LAYOUT_LINE> { static constexpr uint32_t P = 512, I = 1; };
-template <> struct LayoutStride<LAYOUT_QUAD> { static constexpr uint32_t P = 512, I = 64; };
-
-template <bool NT = false, int L = LAYOUT_ROW>
+// One 128-B line (block pair P) of the lane's content: 8 x dwordx4 issued back to back.
+// (The A/B variants — non-temporal loads, 1.6x slower; 64-file tiled LINE / QUAD layouts —
+// live in tools/ubench_k1.hip with their measurements.)
 __device__ __forceinline__ void load_pair(const uint4* __restrict__ q, uint32_t P, uint4 (&buf)[8]) {
-  const uint4* p = q + LayoutStride<L>::P * P;
+  const uint4* p = q + 8u * P;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    if (NT) {
-      const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + LayoutStride<L>::I * i));
-      buf[i] = make_uint4(v.x, v.y, v.z, v.w);
-    } else {
-      buf[i] = p[LayoutStride<L>::I * i];
-    }
-  }
+  for (int i = 0; i < 8; ++i) buf[i] = p[i];
 }
 
 // Compress message blocks 2P and 2P+1 of chunk `ctr` from the line in A; the 2-word
@@ -112,21 +92,21 @@ struct LdsStack {
   }
 };
 
-template <bool NT = false, int L = LAYOUT_ROW, int BLK = SAMPLED_BLOCK>
+template <int BLK = SAMPLED_BLOCK>
 __device__ __forceinline__ uint64_t cas_lane_sampled(const uint4* __restrict__ q, uint64_t size,
                                                      LdsStack<BLK>& stk) {
   uint32_t c0 = (uint32_t)size, c1 = (uint32_t)(size >> 32);
   uint4 A[8], B[8];
-  load_pair<NT, L>(q, 0, A);
+  load_pair(q, 0, A);
   uint32_t cv[8];
   for (uint32_t c = 0; c < SAMPLED_CHUNKS; ++c) {
     set_iv(cv);
 #pragma unroll 1
     for (uint32_t pp = 0; pp < 4; ++pp) {  // 4 x (pair A, pair B) = 16 blocks
       const uint32_t P = 8u * c + 2u * pp;
-      load_pair<NT, L>(q, P + 1, B);
+      load_pair(q, P + 1, B);
       compress_pair(cv, A, c0, c1, c, pp == 0 ? (uint32_t)CHUNK_START : 0u, 0u);
-      if (P + 2 < SAMPLED_PAIRS) load_pair<NT, L>(q, P + 2, A);
+      if (P + 2 < SAMPLED_PAIRS) load_pair(q, P + 2, A);
       compress_pair(cv, B, c0, c1, c, 0u, pp == 3 ? (uint32_t)CHUNK_END : 0u);
     }
     // left-balanced tree: merge while the completed-chunk count has trailing zeros
@@ -172,7 +152,7 @@ __device__ __forceinline__ void sampled_kernel_body(const uint8_t* __restrict__ 
   if (f >= n) return;  // no barrier below: each lane only touches its own stack column
   LdsStack<B> stk{stack_lds, threadIdx.x};
   const uint4* q = reinterpret_cast<const uint4*>(content + f * stride);
-  keys[f] = cas_lane_sampled<false, LAYOUT_ROW, B>(q, sizes[f], stk);
+  keys[f] = cas_lane_sampled<B>(q, sizes[f], stk);
 }
 
 extern "C" __global__ void __launch_bounds__(SAMPLED_BLOCK)
@@ -233,7 +213,7 @@ __device__ __forceinline__ void sampled_group_kernel_body(const uint8_t* __restr
   if (live) {  // exactly K1's lane program
     LdsStack<B> stk{stack_lds, threadIdx.x};
     const uint4* q = reinterpret_cast<const uint4*>(content + f * stride);
-    key = cas_lane_sampled<false, LAYOUT_ROW, B>(q, sizes[f], stk);
+    key = cas_lane_sampled<B>(q, sizes[f], stk);
     keys[f] = key;
     ro.rep[f] = (uint32_t)f;
   }

@@ -99,9 +99,10 @@ __device__ __forceinline__ uint32_t step_of(const uint32_t* starts, uint32_t nst
 
 // Per-row decision (mod.rs:202-347 replayed with HashMap order := ascending row):
 //   hashed, key held by an Object that existed before the job (seeded: rep < ROW_FLAG is the
-//           lowest such Object id): EXISTING — the step's find_many returns it (:180-198, no
-//           location filter), find() picks the first Object in id order (:214-224) and the
-//           key never creates (:246-253);
+//           lowest such Object id; premin: the lowest pre-existing Object of a row with the
+//           key in this step or an earlier one, sd_links_pre_*): EXISTING — the step's
+//           find_many returns it (:180-198, no location filter), find() picks the first
+//           Object in id order (:214-224) and the key never creates (:246-253);
 //   hashed: CREATED iff its key's first row (rep) is in the same step — no intra-step dedup,
 //           mod.rs:246-311 — else LINKED to the Object of rep (find() = the lowest Object
 //           id, created for the key's lowest row, :214-224);
@@ -112,7 +113,8 @@ extern "C" __global__ void __launch_bounds__(256)
 sd_links_decide(const uint8_t* __restrict__ state, const uint32_t* __restrict__ rep, uint64_t n,
                 const uint32_t* __restrict__ starts, uint32_t nsteps, uint64_t reached,
                 uint32_t* __restrict__ step_out, uint32_t* __restrict__ object_out,
-                uint8_t* __restrict__ action_out, unsigned int* __restrict__ counts, bool seeded) {
+                uint8_t* __restrict__ action_out, unsigned int* __restrict__ counts, bool seeded,
+                const uint32_t* __restrict__ premin) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t step = SD_LINKS_NO_STEP, object = SD_LINKS_NO_OBJECT;
   uint8_t action = SD_LINKS_NOT_REACHED;
@@ -125,8 +127,9 @@ sd_links_decide(const uint8_t* __restrict__ state, const uint32_t* __restrict__ 
       action = SD_LINKS_CREATED;
       object = (uint32_t)i;
     } else {
-      const uint32_t v = rep[i];
+      uint32_t v = rep[i];
       const uint32_t r = seeded ? v & ~LINKS_ROW_FLAG : v;  // the key's first row
+      if (premin) v = min(v, premin[i]);  // a pre-existing Object its step or an earlier one saw
       if (seeded && v < LINKS_ROW_FLAG) {
         action = SD_LINKS_EXISTING;
         object = v;
@@ -163,6 +166,198 @@ sd_links_decide(const uint8_t* __restrict__ state, const uint32_t* __restrict__ 
   }
 }
 
+// ---- rows that already own an Object (object_id set, cas_id NULL) -----------------------
+// The orphan query takes `object_id IS NULL OR cas_id IS NULL` (file_identifier_job.rs:
+// 258-261), so a file_path the watcher gave an Object while it was still empty and that was
+// written afterwards (watcher/utils.rs:236-293 creates the Object; :473-490 writes the old,
+// NULL cas_id back with the new size) is a row whose Object P exists before the job.  Its
+// step writes its cas_id X first (mod.rs:157-178), so that step's find_many (:180-198) sees P
+// under X: every row of the step with X links to the smallest Object id carrying X and X
+// never creates (:214-224, :246-253).  A later step still sees P when it won (its row stays
+// connected to it); when a smaller Object won, P lost the row — but then the smaller one
+// stays, so what each row needs is the smallest P over the key's rows in its own or an
+// earlier step: a segmented prefix minimum over the rows sorted by (key, row), cut at the
+// end of the row's (key, step) run.  Two linear scans over the sorted rows give it:
+//   forward,  segments = keys:          F[j] = min P over the key's rows up to j;
+//   backward, segments = (key, step) run ends:  G[j] = F[end of j's run].
+// Scan element: bit 63 = segment start, low 32 bits = value (0xFFFFFFFF = no Object).
+constexpr uint64_t SEG_START = 1ull << 63;
+constexpr uint64_t SEG_NONE = 0xFFFFFFFFull;  // the identity: no start, no Object
+__device__ __forceinline__ uint64_t segmin(uint64_t a, uint64_t b) {
+  if (b & SEG_START) return b;
+  const uint32_t va = (uint32_t)a, vb = (uint32_t)b;
+  return (a & SEG_START) | (uint64_t)(va < vb ? va : vb);
+}
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t x, int d) {
+  const uint32_t lo = __shfl_up((uint32_t)x, d, 64), hi = __shfl_up((uint32_t)(x >> 32), d, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Any seeded or pre-existing Object id >= 2^31 (the row tag of the seeded grouping) sets
+// *bad; SD_LINKS_NO_OBJECT is allowed where `none_ok` (a row without an Object).
+extern "C" __global__ void __launch_bounds__(256)
+sd_links_check_ids(const uint32_t* __restrict__ ids, uint64_t n, uint32_t none_ok,
+                   unsigned long long* __restrict__ bad) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool b = false;
+  if (i < n) {
+    const uint32_t v = ids[i];
+    b = v >= LINKS_ROW_FLAG && !(none_ok && v == SD_LINKS_NO_OBJECT);
+  }
+  if (__ballot(b) && (threadIdx.x & 63u) == 0) atomicAdd(bad, 1ull);
+}
+
+// Element j of the sorted rows (skeys ascending, srows ascending inside a key): value = the
+// row's pre-existing Object when it is hashed in a reached step, start = first row of its key.
+extern "C" __global__ void __launch_bounds__(256)
+sd_links_pre_mark(const uint64_t* __restrict__ skeys, const uint32_t* __restrict__ srows,
+                  const uint8_t* __restrict__ state, const uint32_t* __restrict__ pre, uint64_t n,
+                  uint64_t reached, uint64_t* __restrict__ elem) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t r = srows[j];
+  const bool hashed = r < reached && (!state || state[r] == SD_LINKS_HASHED);
+  const uint64_t v = hashed ? (uint64_t)pre[r] : SEG_NONE;  // pre[r] may itself be NO_OBJECT
+  elem[j] = (j == 0 || skeys[j] != skeys[j - 1] ? SEG_START : 0ull) | v;
+}
+
+// F -> the backward scan's input, in place: a (key, step) run's last element carries F as a
+// segment start, every other element the identity.
+extern "C" __global__ void __launch_bounds__(256)
+sd_links_pre_runs(const uint64_t* __restrict__ skeys, const uint32_t* __restrict__ srows,
+                  const uint32_t* __restrict__ starts, uint32_t nsteps, uint64_t n,
+                  uint64_t* __restrict__ elem) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  bool end = j + 1 == n || skeys[j] != skeys[j + 1];
+  if (!end) end = step_of(starts, nsteps, srows[j]) != step_of(starts, nsteps, srows[j + 1]);
+  elem[j] = end ? (SEG_START | (elem[j] & SEG_NONE)) : SEG_NONE;
+}
+
+extern "C" __global__ void __launch_bounds__(256)
+sd_links_pre_scatter(const uint32_t* __restrict__ srows, const uint64_t* __restrict__ elem,
+                     uint64_t n, uint32_t* __restrict__ premin) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < n) premin[srows[j]] = (uint32_t)elem[j];
+}
+
+// Device-wide inclusive segmented-min scan in three launches (reduce-then-scan): each
+// workgroup scans a tile of SCAN_TILE elements and leaves the tile's total; one workgroup
+// scans the totals (exclusive); every tile but the first folds its prefix in.  `reverse`
+// scans from the last element to the first (logical k = physical n-1-k).  Bytes per element:
+// 8 R + 8 W (tiles) + 8 R + 8 W (fix-up) — the rows of one job, a few ms at 10 M rows.
+constexpr int SCAN_THREADS = 256, SCAN_ITEMS = 8;
+constexpr uint64_t SCAN_TILE = (uint64_t)SCAN_THREADS * SCAN_ITEMS;
+
+// inclusive workgroup scan of one value per thread; returns the thread's EXCLUSIVE prefix and
+// (in *total) the workgroup's total
+__device__ __forceinline__ uint64_t block_segmin_excl(uint64_t x, uint64_t* wsum, uint64_t* total) {
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  uint64_t inc = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = shfl_up64(inc, d);
+    if (lane >= (uint32_t)d) inc = segmin(y, inc);
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint64_t excl = SEG_NONE, all = SEG_NONE;
+  for (uint32_t k = 0; k < SCAN_THREADS / 64; ++k) {
+    if (k == w) excl = all;
+    all = segmin(all, wsum[k]);
+  }
+  const uint64_t prev = shfl_up64(inc, 1);
+  if (lane) excl = segmin(excl, prev);
+  *total = all;
+  __syncthreads();  // wsum may be reused by the caller's next round
+  return excl;
+}
+
+extern "C" __global__ void __launch_bounds__(SCAN_THREADS)
+sd_segmin_tiles(uint64_t* __restrict__ data, uint64_t n, int reverse, uint64_t* __restrict__ tiles) {
+  __shared__ uint64_t wsum[SCAN_THREADS / 64];
+  const uint64_t k0 = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+  uint64_t v[SCAN_ITEMS], acc = SEG_NONE;
+#pragma unroll
+  for (int u = 0; u < SCAN_ITEMS; ++u) {
+    const uint64_t k = k0 + u;
+    v[u] = k < n ? data[reverse ? n - 1 - k : k] : SEG_NONE;
+    acc = segmin(acc, v[u]);
+  }
+  uint64_t total;
+  uint64_t run = block_segmin_excl(acc, wsum, &total);
+#pragma unroll
+  for (int u = 0; u < SCAN_ITEMS; ++u) {
+    const uint64_t k = k0 + u;
+    run = segmin(run, v[u]);
+    if (k < n) data[reverse ? n - 1 - k : k] = run;
+  }
+  if (threadIdx.x == 0) tiles[blockIdx.x] = total;
+}
+
+// one workgroup: tiles[t] := the fold of tiles[0..t) (exclusive), in place
+extern "C" __global__ void __launch_bounds__(SCAN_THREADS)
+sd_segmin_tile_prefix(uint64_t* __restrict__ tiles, uint64_t ntiles) {
+  __shared__ uint64_t wsum[SCAN_THREADS / 64];
+  uint64_t carry = SEG_NONE;
+  for (uint64_t b = 0; b < ntiles; b += SCAN_THREADS) {
+    const uint64_t t = b + threadIdx.x;
+    const uint64_t x = t < ntiles ? tiles[t] : SEG_NONE;
+    uint64_t total;
+    const uint64_t excl = block_segmin_excl(x, wsum, &total);
+    if (t < ntiles) tiles[t] = segmin(carry, excl);
+    carry = segmin(carry, total);
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(SCAN_THREADS)
+sd_segmin_fix(uint64_t* __restrict__ data, uint64_t n, int reverse, const uint64_t* __restrict__ tiles) {
+  const uint64_t t = blockIdx.x + 1;  // tile 0 has nothing before it
+  const uint64_t pre = tiles[t];
+  for (uint64_t u = threadIdx.x; u < SCAN_TILE; u += SCAN_THREADS) {
+    const uint64_t k = t * SCAN_TILE + u;
+    if (k >= n) break;
+    const uint64_t p = reverse ? n - 1 - k : k;
+    data[p] = segmin(pre, data[p]);
+  }
+}
+
+hipError_t segmin_scan(uint64_t* data, uint64_t n, bool reverse, uint64_t* tiles, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint64_t nt = (n + SCAN_TILE - 1) / SCAN_TILE;
+  sd_segmin_tiles<<<(uint32_t)nt, SCAN_THREADS, 0, s>>>(data, n, reverse ? 1 : 0, tiles);
+  if (nt > 1) {
+    sd_segmin_tile_prefix<<<1, SCAN_THREADS, 0, s>>>(tiles, nt);
+    sd_segmin_fix<<<(uint32_t)(nt - 1), SCAN_THREADS, 0, s>>>(data, n, reverse ? 1 : 0, tiles);
+  }
+  return hipGetLastError();
+}
+
+size_t segmin_tiles_bytes(uint64_t n) { return ((n + SCAN_TILE - 1) / SCAN_TILE + 1) * 8; }
+
+hipError_t links_check_ids(const uint32_t* ids, uint64_t n, bool none_ok, uint64_t* d_bad,
+                           hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  sd_links_check_ids<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(ids, n, none_ok ? 1u : 0u,
+                                                                (unsigned long long*)d_bad);
+  return hipGetLastError();
+}
+
+hipError_t links_pre_min(const uint64_t* skeys, const uint32_t* srows, const uint8_t* state,
+                         const uint32_t* pre, uint64_t n, uint64_t reached, const uint32_t* starts,
+                         uint32_t nsteps, uint64_t* elem, uint64_t* tiles, uint32_t* premin,
+                         hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint32_t g = (uint32_t)((n + 255) / 256);
+  sd_links_pre_mark<<<g, 256, 0, s>>>(skeys, srows, state, pre, n, reached, elem);
+  hipError_t e = segmin_scan(elem, n, false, tiles, s);
+  if (e != hipSuccess) return e;
+  sd_links_pre_runs<<<g, 256, 0, s>>>(skeys, srows, starts, nsteps, n, elem);
+  if ((e = segmin_scan(elem, n, true, tiles, s)) != hipSuccess) return e;
+  sd_links_pre_scatter<<<g, 256, 0, s>>>(srows, elem, n, premin);
+  return hipGetLastError();
+}
+
 hipError_t links_split(const uint64_t* keys, const uint8_t* state, uint64_t n, uint64_t* hkeys,
                        uint32_t* hrows, uint64_t* d_hcount, uint64_t* orphans, uint64_t* d_ocount,
                        uint32_t row_flag, hipStream_t s) {
@@ -183,10 +378,11 @@ hipError_t links_scatter(const uint32_t* minrow, const uint32_t* hrows, uint64_t
 hipError_t links_decide(const uint8_t* state, const uint32_t* rep, uint64_t n,
                         const uint32_t* starts, uint32_t nsteps, uint64_t reached,
                         uint32_t* step_out, uint32_t* object_out, uint8_t* action_out,
-                        uint32_t* counts, bool seeded, hipStream_t s) {
+                        uint32_t* counts, bool seeded, const uint32_t* premin, hipStream_t s) {
   if (n == 0) return hipSuccess;
   sd_links_decide<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(
-      state, rep, n, starts, nsteps, reached, step_out, object_out, action_out, counts, seeded);
+      state, rep, n, starts, nsteps, reached, step_out, object_out, action_out, counts, seeded,
+      premin);
   return hipGetLastError();
 }
 

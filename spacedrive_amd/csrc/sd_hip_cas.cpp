@@ -564,32 +564,37 @@ size_t sd_cas_identifier_max_steps(size_t n, uint32_t chunk) {
   return chunk ? (n + chunk - 1) / chunk : 0;
 }
 
-int sd_cas_identifier_links_seeded_dev(sd_cas_ctx* c, const uint64_t* d_keys, const uint8_t* d_state,
-                                       size_t n, uint32_t chunk, const uint64_t* d_seed_keys,
-                                       const uint32_t* d_seed_objects, size_t n_seed, uint32_t* d_step,
-                                       uint32_t* d_object, uint8_t* d_action, uint64_t* h_step_counts,
-                                       size_t max_steps, uint64_t* out_steps, void* stream) {
+int sd_cas_identifier_links_ex_dev(sd_cas_ctx* c, const uint64_t* d_keys, const uint8_t* d_state,
+                                   size_t n, uint32_t chunk, const uint64_t* d_seed_keys,
+                                   const uint32_t* d_seed_objects, size_t n_seed,
+                                   const uint32_t* d_pre_objects, uint32_t* d_step,
+                                   uint32_t* d_object, uint8_t* d_action, uint64_t* h_step_counts,
+                                   size_t max_steps, uint64_t* out_steps, void* stream) {
   if (!c) return SD_CAS_EINVAL;
   const size_t steps_total = sd_cas_identifier_max_steps(n, chunk);
   if (chunk == 0 || n >= (1ull << 32) || !out_steps || max_steps < steps_total ||
       (n && (!d_keys || !d_step || !d_object || !d_action || !h_step_counts)) ||
       (n_seed && (!d_seed_keys || !d_seed_objects)))
     return fail(c, SD_CAS_EINVAL, "identifier_links: bad arguments");
-  // a seeded grouping tags rows with LINKS_ROW_FLAG: rows and Object ids below 2^31
-  if (n_seed && (n >= LINKS_ROW_FLAG || n_seed >= LINKS_ROW_FLAG || n + n_seed >= (1ull << 32)))
+  // a seeded grouping tags rows with LINKS_ROW_FLAG: rows and Object ids below 2^31 (rows
+  // that already own an Object run the seeded grouping too)
+  const bool seeded = n_seed > 0 || d_pre_objects;
+  if (seeded && (n >= LINKS_ROW_FLAG || n_seed >= LINKS_ROW_FLAG || n + n_seed >= (1ull << 32)))
     return fail(c, SD_CAS_EINVAL, "identifier_links: %zu rows + %zu existing Objects exceed 2^31",
                 n, n_seed);
   *out_steps = 0;
   for (size_t k = 0; k < 2 * steps_total; k++) h_step_counts[k] = 0;
   if (n == 0) return SD_CAS_OK;
   hipStream_t s = pick(c, stream);
-  const bool seeded = n_seed > 0;
   // staging (this call is blocking): rep | hkeys | hrows | minrow | orphans | starts | counts |
-  // 2 counters; the seeded grouping runs over the hashed rows + the existing Objects' keys
+  // scan tiles | 3 counters; the seeded grouping runs over the hashed rows + the existing
+  // Objects' keys.  Rows with pre-existing Objects reuse hkeys / hrows / orphans / minrow once
+  // the grouping is done: sorted keys / sorted rows / scan elements / per-row minimum
   const size_t m = n + n_seed;
   const size_t b_rep = up256(n * 4), b_hk = up256(m * 8), b_hr = up256(m * 4), b_mr = up256(m * 4),
-               b_or = up256(n * 8), b_st = up256((steps_total + 1) * 4), b_ct = up256(steps_total * 8);
-  int rc = ensure(c, c->staging, b_rep + b_hk + b_hr + b_mr + b_or + b_st + b_ct + 256);
+               b_or = up256(n * 8), b_st = up256((steps_total + 1) * 4), b_ct = up256(steps_total * 8),
+               b_tl = d_pre_objects ? up256(segmin_tiles_bytes(n)) : 0;
+  int rc = ensure(c, c->staging, b_rep + b_hk + b_hr + b_mr + b_or + b_st + b_ct + b_tl + 256);
   if (rc) return rc;
   char* p = (char*)c->staging.p;
   uint32_t* rep = (uint32_t*)p; p += b_rep;
@@ -599,23 +604,28 @@ int sd_cas_identifier_links_seeded_dev(sd_cas_ctx* c, const uint64_t* d_keys, co
   uint64_t* orphans = (uint64_t*)p; p += b_or;
   uint32_t* starts = (uint32_t*)p; p += b_st;
   uint32_t* counts = (uint32_t*)p; p += b_ct;
-  uint64_t* counters = (uint64_t*)p;
+  uint64_t* tiles = (uint64_t*)p; p += b_tl;
+  uint64_t* counters = (uint64_t*)p;  // hashed rows | orphan rows | waves with a bad Object id
   // 1. grouping over the hashed rows (rep = the key's first row; seeded: the lowest existing
   //    Object id when the key has one — mod.rs:180-198 finds Objects by cas over the whole
   //    library), and the rows that stay orphan after being processed (they steer the cursor)
   std::vector<uint64_t> stay;  // row << 8 | state, ascending
   if (d_state || seeded) {
-    uint64_t cnt[2] = {0, 0};
-    HIP_TRY(c, hipMemsetAsync(counters, 0, 16, s));
+    uint64_t cnt[3] = {0, 0, 0};
+    HIP_TRY(c, hipMemsetAsync(counters, 0, 24, s));
+    HIP_TRY(c, links_check_ids(d_seed_objects, n_seed, false, counters + 2, s));
+    if (d_pre_objects) HIP_TRY(c, links_check_ids(d_pre_objects, n, true, counters + 2, s));
     HIP_TRY(c, links_split(d_keys, d_state, n, hkeys, hrows, counters, orphans, counters + 1,
                            seeded ? LINKS_ROW_FLAG : 0u, s));
-    HIP_TRY(c, hipMemcpyAsync(cnt, counters, 16, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(cnt, counters, 24, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
+    if (cnt[2])
+      return fail(c, SD_CAS_EINVAL, "identifier_links: an existing Object id is >= 2^31");
     stay.resize(cnt[1]);
     if (cnt[1]) {
       HIP_TRY(c, hipMemcpyAsync(stay.data(), orphans, cnt[1] * 8, hipMemcpyDeviceToHost, s));
     }
-    if (seeded) {  // the existing Objects' (cas key, id) pairs after the hashed rows
+    if (n_seed) {  // the existing Objects' (cas key, id) pairs after the hashed rows
       HIP_TRY(c, hipMemcpyAsync(hkeys + cnt[0], d_seed_keys, n_seed * 8, hipMemcpyDeviceToDevice, s));
       HIP_TRY(c, hipMemcpyAsync(hrows + cnt[0], d_seed_objects, n_seed * 4, hipMemcpyDeviceToDevice, s));
     }
@@ -659,11 +669,21 @@ int sd_cas_identifier_links_seeded_dev(sd_cas_ctx* c, const uint64_t* d_keys, co
   }
   const size_t nsteps = h_starts.size();
   h_starts.push_back(0xFFFFFFFFu);  // sentinel
-  // 3. per-row decisions + per-step counts (device)
   HIP_TRY(c, hipMemcpyAsync(starts, h_starts.data(), h_starts.size() * 4, hipMemcpyHostToDevice, s));
+  // 3. rows that already own an Object: per row, the smallest such Object of a row with its
+  //    key in its own step or an earlier one (links.hip, sd_links_pre_*) over every row sorted
+  //    by (key, row) — a stable sort of the keys with the identity as values
+  uint32_t* premin = nullptr;
+  if (d_pre_objects) {
+    if ((rc = sd_cas_sort_pairs_dev(c, d_keys, nullptr, n, hkeys, hrows, 0, 64, s))) return rc;
+    premin = minrow;
+    HIP_TRY(c, links_pre_min(hkeys, hrows, d_state, d_pre_objects, n, reached, starts,
+                             (uint32_t)nsteps, orphans, tiles, premin, s));
+  }
+  // 4. per-row decisions + per-step counts (device)
   HIP_TRY(c, hipMemsetAsync(counts, 0, std::max<size_t>(nsteps, 1) * 8, s));
   HIP_TRY(c, links_decide(d_state, rep, n, starts, (uint32_t)nsteps, reached, d_step, d_object,
-                          d_action, counts, seeded, s));
+                          d_action, counts, seeded, premin, s));
   std::vector<uint32_t> hc(2 * std::max<size_t>(nsteps, 1));
   HIP_TRY(c, hipMemcpyAsync(hc.data(), counts, hc.size() * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
@@ -675,6 +695,16 @@ int sd_cas_identifier_links_seeded_dev(sd_cas_ctx* c, const uint64_t* d_keys, co
   return SD_CAS_OK;
 }
 
+int sd_cas_identifier_links_seeded_dev(sd_cas_ctx* c, const uint64_t* d_keys, const uint8_t* d_state,
+                                       size_t n, uint32_t chunk, const uint64_t* d_seed_keys,
+                                       const uint32_t* d_seed_objects, size_t n_seed, uint32_t* d_step,
+                                       uint32_t* d_object, uint8_t* d_action, uint64_t* h_step_counts,
+                                       size_t max_steps, uint64_t* out_steps, void* stream) {
+  return sd_cas_identifier_links_ex_dev(c, d_keys, d_state, n, chunk, d_seed_keys, d_seed_objects,
+                                        n_seed, nullptr, d_step, d_object, d_action, h_step_counts,
+                                        max_steps, out_steps, stream);
+}
+
 int sd_cas_identifier_links_dev(sd_cas_ctx* c, const uint64_t* d_keys, const uint8_t* d_state,
                                 size_t n, uint32_t chunk, uint32_t* d_step, uint32_t* d_object,
                                 uint8_t* d_action, uint64_t* h_step_counts, size_t max_steps,
@@ -684,11 +714,12 @@ int sd_cas_identifier_links_dev(sd_cas_ctx* c, const uint64_t* d_keys, const uin
                                             stream);
 }
 
-int sd_cas_identifier_links_seeded(sd_cas_ctx* c, const uint64_t* h_keys, const uint8_t* h_state,
-                                   size_t n, uint32_t chunk, const uint64_t* h_seed_keys,
-                                   const uint32_t* h_seed_objects, size_t n_seed, uint32_t* h_step,
-                                   uint32_t* h_object, uint8_t* h_action, uint64_t* h_step_counts,
-                                   size_t max_steps, uint64_t* out_steps) {
+int sd_cas_identifier_links_ex(sd_cas_ctx* c, const uint64_t* h_keys, const uint8_t* h_state,
+                               size_t n, uint32_t chunk, const uint64_t* h_seed_keys,
+                               const uint32_t* h_seed_objects, size_t n_seed,
+                               const uint32_t* h_pre_objects, uint32_t* h_step, uint32_t* h_object,
+                               uint8_t* h_action, uint64_t* h_step_counts, size_t max_steps,
+                               uint64_t* out_steps) {
   if (!c) return SD_CAS_EINVAL;
   if ((n && (!h_keys || !h_step || !h_object || !h_action)) ||
       (n_seed && (!h_seed_keys || !h_seed_objects)))
@@ -696,14 +727,20 @@ int sd_cas_identifier_links_seeded(sd_cas_ctx* c, const uint64_t* h_keys, const 
   for (size_t j = 0; j < n_seed; j++)
     if (h_seed_objects[j] >= LINKS_ROW_FLAG)
       return fail(c, SD_CAS_EINVAL, "identifier_links: existing Object id %u >= 2^31", h_seed_objects[j]);
+  if (h_pre_objects)
+    for (size_t i = 0; i < n; i++)
+      if (h_pre_objects[i] >= LINKS_ROW_FLAG && h_pre_objects[i] != SD_CAS_NO_OBJECT)
+        return fail(c, SD_CAS_EINVAL, "identifier_links: row %zu's Object id %u >= 2^31", i,
+                    h_pre_objects[i]);
   if (n == 0 || n >= (1ull << 32))
     return sd_cas_identifier_links_dev(c, nullptr, nullptr, n, chunk, nullptr, nullptr, nullptr,
                                        h_step_counts, max_steps, out_steps, c->stream);
   HIP_TRY(c, hipSetDevice(c->device));
-  // device copies (c->io): keys | state | step | object | action | seed keys | seed ids
+  // device copies (c->io): keys | state | step | object | action | seed keys | seed ids |
+  // pre-existing Objects
   const size_t bk = up256(n * 8), bs = up256(n), b4 = up256(n * 4);
-  const size_t bsk = up256(n_seed * 8), bso = up256(n_seed * 4);
-  int rc = ensure(c, c->io, bk + 2 * bs + 2 * b4 + bsk + bso);
+  const size_t bsk = up256(n_seed * 8), bso = up256(n_seed * 4), bpo = h_pre_objects ? b4 : 0;
+  int rc = ensure(c, c->io, bk + 2 * bs + 2 * b4 + bsk + bso + bpo);
   if (rc) return rc;
   char* p = (char*)c->io.p;
   uint64_t* d_keys = (uint64_t*)p; p += bk;
@@ -712,7 +749,8 @@ int sd_cas_identifier_links_seeded(sd_cas_ctx* c, const uint64_t* h_keys, const 
   uint32_t* d_object = (uint32_t*)p; p += b4;
   uint8_t* d_action = (uint8_t*)p; p += bs;
   uint64_t* d_seed_keys = (uint64_t*)p; p += bsk;
-  uint32_t* d_seed_objects = (uint32_t*)p;
+  uint32_t* d_seed_objects = (uint32_t*)p; p += bso;
+  uint32_t* d_pre = h_pre_objects ? (uint32_t*)p : nullptr;
   hipStream_t s = c->stream;
   HIP_TRY(c, hipMemcpyAsync(d_keys, h_keys, n * 8, hipMemcpyHostToDevice, s));
   if (h_state) HIP_TRY(c, hipMemcpyAsync(d_state, h_state, n, hipMemcpyHostToDevice, s));
@@ -720,15 +758,26 @@ int sd_cas_identifier_links_seeded(sd_cas_ctx* c, const uint64_t* h_keys, const 
     HIP_TRY(c, hipMemcpyAsync(d_seed_keys, h_seed_keys, n_seed * 8, hipMemcpyHostToDevice, s));
     HIP_TRY(c, hipMemcpyAsync(d_seed_objects, h_seed_objects, n_seed * 4, hipMemcpyHostToDevice, s));
   }
-  rc = sd_cas_identifier_links_seeded_dev(c, d_keys, d_state, n, chunk, d_seed_keys, d_seed_objects,
-                                          n_seed, d_step, d_object, d_action, h_step_counts,
-                                          max_steps, out_steps, s);
+  if (d_pre) HIP_TRY(c, hipMemcpyAsync(d_pre, h_pre_objects, n * 4, hipMemcpyHostToDevice, s));
+  rc = sd_cas_identifier_links_ex_dev(c, d_keys, d_state, n, chunk, d_seed_keys, d_seed_objects,
+                                      n_seed, d_pre, d_step, d_object, d_action, h_step_counts,
+                                      max_steps, out_steps, s);
   if (rc) return rc;
   HIP_TRY(c, hipMemcpyAsync(h_step, d_step, n * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipMemcpyAsync(h_object, d_object, n * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipMemcpyAsync(h_action, d_action, n, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
   return SD_CAS_OK;
+}
+
+int sd_cas_identifier_links_seeded(sd_cas_ctx* c, const uint64_t* h_keys, const uint8_t* h_state,
+                                   size_t n, uint32_t chunk, const uint64_t* h_seed_keys,
+                                   const uint32_t* h_seed_objects, size_t n_seed, uint32_t* h_step,
+                                   uint32_t* h_object, uint8_t* h_action, uint64_t* h_step_counts,
+                                   size_t max_steps, uint64_t* out_steps) {
+  return sd_cas_identifier_links_ex(c, h_keys, h_state, n, chunk, h_seed_keys, h_seed_objects, n_seed,
+                                    nullptr, h_step, h_object, h_action, h_step_counts, max_steps,
+                                    out_steps);
 }
 
 int sd_cas_identifier_links(sd_cas_ctx* c, const uint64_t* h_keys, const uint8_t* h_state,

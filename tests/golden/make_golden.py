@@ -96,37 +96,58 @@ NO_STEP = NO_OBJECT = 0xFFFFFFFF
 
 
 def replay_identifier_job(keys, states, chunk: int = 100, with_creates: bool = False,
-                          existing=None):
+                          existing=None, pre_objects=None):
     """Literal replay of one file-identifier job, DB state included:
     file_identifier_job.rs:86-178 (init: orphan count, ceil(n/chunk) steps, cursor = first
-    orphan id), :180-236 (execute_step: get_orphan_file_paths = orphan rows with id >=
-    cursor, ascending, LIMIT chunk (:251-319); an empty query ends the job), mod.rs:98-350
-    (identifier_job_step: FileMetadata per row, errors dropped; cas_id written; Objects
-    found by cas; links to the first; one new Object per remaining row, HashMap order :=
-    ascending row) and mod.rs:401-405 (the next cursor = the chunk's last row).
-    Rows: file_path ids 0..n-1, all orphan at init (object_id and cas_id NULL).
+    orphan id), :180-236 (execute_step: get_orphan_file_paths = orphan rows — object_id NULL
+    OR cas_id NULL, :258-261 — with id >= cursor, ascending, LIMIT chunk (:251-319); an empty
+    query ends the job), mod.rs:98-350 (identifier_job_step: FileMetadata per row, errors
+    dropped; cas_id written; find_many = every Object connected to a file_path whose cas_id
+    is one of the step's, in id order; each row links to the first that carries its cas_id;
+    one new Object per remaining row, HashMap order := ascending row) and mod.rs:401-405 (the
+    next cursor = the chunk's last row).
+    Rows: file_path ids 0..n-1 with cas_id NULL at init; object_id NULL unless pre_objects.
     existing: None (a fresh library) or (cas key, Object id) pairs — Objects the library
     holds before the job, each connected to a file_path (outside the job's rows) with that
-    cas.  They take the Object table's first rows in id order, so a later find_many returns
-    them ahead of the job's own Objects (:181-188; the query has no location filter).
+    cas.  pre_objects: None or per row the Object its file_path already holds (None / -1 /
+    NO_OBJECT: none) — the watcher's "created empty, then written" rows
+    (watcher/utils.rs:236-293, 473-490).  Pre-job Objects take the Object table's first rows
+    in id order, so find_many returns them ahead of the job's own Objects (:181-188; the
+    query has no location filter).  Which Objects a cas_id finds is recomputed from the
+    file_path table at every step (a row re-linked away from its Object disconnects it).
     Returns (step[], object[], action[], [(created, linked)] per step) where object[i] is
     the row that created the Object row i is connected to, or (LINK_EXISTING) the id of the
     pre-job Object; with_creates: also the rows that created an Object in each step (a
     re-queried empty row appears in every step it was processed in)."""
     n = len(keys)
-    cas_col = [None] * n         # file_path.cas_id
-    obj_col = [None] * n         # file_path.object_id
-    creator = []                 # Object table: id -> creating row (None: a pre-job Object)
-    cas_objects = {}             # cas -> Object ids having a file_path with that cas, in id order
-    pre_id = []                  # pre-job Objects' own ids, by Object-table row
-    for oid in sorted({int(o) for _, o in existing or ()}):
-        pre_id.append(oid)
-        creator.append(None)
-    pos = {oid: t for t, oid in enumerate(pre_id)}
-    for c, o in sorted(existing or (), key=lambda e: int(e[1])):
-        lst = cas_objects.setdefault(int(c), [])
-        if pos[int(o)] not in lst:
-            lst.append(pos[int(o)])
+    none = (None, -1, NO_OBJECT)
+    pre = [None if p in none else int(p) for p in pre_objects] if pre_objects is not None else [None] * n
+    assert len(pre) == n
+    pre_id = sorted({int(o) for _, o in existing or ()} | {p for p in pre if p is not None})
+    pos = {oid: t for t, oid in enumerate(pre_id)}   # Object-table row of a pre-job Object
+    creator = [None] * len(pre_id)  # Object table: position -> creating row (None: pre-job)
+    cas_col = [None] * n            # file_path.cas_id
+    obj_col = [None if p is None else pos[p] for p in pre]  # file_path.object_id (table row)
+    conn = {}                       # cas -> {Object position: file_paths connecting them}
+
+    def connect(cas, o, d):
+        if cas is None or o is None:
+            return
+        m = conn.setdefault(cas, {})
+        m[o] = m.get(o, 0) + d
+        if m[o] == 0:
+            del m[o]
+
+    def update(r, cas=..., obj=...):  # one file_path UPDATE: keeps `conn` in step with the table
+        connect(cas_col[r], obj_col[r], -1)
+        if cas is not ...:
+            cas_col[r] = cas
+        if obj is not ...:
+            obj_col[r] = obj
+        connect(cas_col[r], obj_col[r], +1)
+
+    for c, o in existing or ():     # the seeds' own file_paths (never job rows)
+        connect(int(c), pos[int(o)], +1)
     step = [NO_STEP] * n
     processed_ok = [False] * n   # last processing of the row succeeded
     processed = [False] * n
@@ -151,25 +172,22 @@ def replay_identifier_job(keys, states, chunk: int = 100, with_creates: bool = F
                 continue
             meta[r] = None if states[r] == ROW_NO_CAS else keys[r]
         for r, c in meta.items():                    # cas_id write (mod.rs:157-178)
-            cas_col[r] = c
+            update(r, cas=c)
         unique = {c for c in meta.values() if c is not None}
-        found = {c: cas_objects[c] for c in unique if c in cas_objects}  # :181-198
+        found = {c: sorted(conn[c]) for c in unique if conn.get(c)}  # :181-198, id order
         linked = 0
         for r in sorted(meta):                       # :202-238 link to the FIRST Object
             c = meta[r]
             if c is not None and c in found:
-                obj_col[r] = found[c][0]
+                update(r, obj=found[c][0])
                 linked += 1
         created = 0
         step_creates.append([])
         for r in sorted(meta):                       # :246-347 one new Object per remaining row
             c = meta[r]
             if c is None or c not in found:
-                oid = len(creator)
                 creator.append(r)
-                obj_col[r] = oid
-                if c is not None:
-                    cas_objects.setdefault(c, []).append(oid)
+                update(r, obj=len(creator) - 1)
                 created += 1
                 step_creates[-1].append(r)
         counts.append((created, linked))

@@ -56,17 +56,23 @@ def test_visible_gpus_from_kfd_topology(tmp_path, monkeypatch):
 
 
 def test_cpu_baseline_threads(monkeypatch):
-    """The CPU baseline's thread count: an explicit override, else OMP_NUM_THREADS when it
-    grants more than one, else the process's cores capped at 16 per rank (torchrun's default
-    OMP_NUM_THREADS=1 for its workers must not shrink the baseline to one core)."""
+    """The CPU baseline's thread count is the whole node's share: an explicit
+    override, else OMP_NUM_THREADS (the box's per-GPU share) x n_gpus — or 16 x n_gpus when
+    OMP_NUM_THREADS is 1 or unset (torchrun's default for its workers must not shrink the
+    baseline to one core) — capped by the process's affinity mask."""
     sys.path.insert(0, ROOT)
     import bench
     monkeypatch.delenv("SD_CPU_BASELINE_THREADS", raising=False)
-    monkeypatch.setenv("OMP_NUM_THREADS", "16")
-    assert bench.cpu_threads(1) == 16
-    monkeypatch.setenv("OMP_NUM_THREADS", "1")
-    avail = len(os.sched_getaffinity(0))
-    assert bench.cpu_threads(1) == min(avail, 16)
-    assert bench.cpu_threads(8) == min(avail, 128)
+    for cores in (200, 96, 8):
+        monkeypatch.setattr(os, "sched_getaffinity", lambda pid, c=cores: set(range(c)))
+        monkeypatch.setenv("OMP_NUM_THREADS", "16")
+        assert bench.cpu_threads(1) == min(cores, 16)
+        assert bench.cpu_threads(8) == min(cores, 128)   # never one GPU's 16-core share
+        monkeypatch.setenv("OMP_NUM_THREADS", "1")
+        assert bench.cpu_threads(1) == min(cores, 16)
+        assert bench.cpu_threads(8) == min(cores, 128)
+        monkeypatch.delenv("OMP_NUM_THREADS")
+        assert bench.cpu_threads(4) == min(cores, 64)
     monkeypatch.setenv("SD_CPU_BASELINE_THREADS", "3")
     assert bench.cpu_threads(8) == 3
+    assert bench.cpu_model() is None or isinstance(bench.cpu_model(), str)

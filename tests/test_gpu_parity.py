@@ -1519,8 +1519,126 @@ def test_identifier_links_existing_vs_replay(eng, chunk):
     b = eng.identifier_links_host(keys, states, chunk)
     assert all((x == y).all() for x, y in zip(a, b))
     from spacedrive_amd import CasError
-    with pytest.raises(CasError):
+    with pytest.raises(ValueError):  # the Python wrapper refuses it before the call ...
         eng.identifier_links_host(keys, states, chunk, existing=(sk[:1], np.array([2 ** 31], np.uint32)))
+    # ... the device entry point checks the ids on the device (an id >= 2^31 would
+    # read as a row tag), a negative int32 included
+    with pytest.raises(CasError):
+        eng.identifier_links(dev64(keys), torch.from_numpy(states).cuda(), chunk,
+                             existing=(dev64(sk[:2]), torch.tensor([5, -7], dtype=torch.int32).cuda()))
+
+
+@pytest.mark.parametrize("chunk", [100, 7, 1])
+def test_identifier_links_pre_objects_vs_replay(eng, chunk):
+    """sd_cas_identifier_links_ex[_dev] vs the literal replay with rows that ALREADY OWN an
+    Object (object_id set, cas_id NULL: orphan by file_identifier_job.rs:258-261; VERDICT r4
+    #1): ~10 % of rows carry a pre-existing Object, a key with one repeats inside its chunk
+    and across chunks (a pre-job Object taking over a key an earlier step created), combined
+    with seeded Objects (ids interleaved), NO_CAS / ERROR rows with Objects, stay-orphan rows
+    at chunk ends.  Device and host entry points; an id >= 2^31 is refused on both."""
+    rng = np.random.default_rng(280 + chunk)
+    n = 12_000 if chunk > 2 else 2_500
+    pool = rng.integers(1, 2 ** 64, n // 4, dtype=np.uint64)
+    keys = pool[rng.integers(0, len(pool), n)]
+    keys[20:26] = keys[20]           # one key six times inside one chunk, with an Object at 23
+    keys[[150, 420, 900]] = keys[20]  # ... and in later chunks
+    states = rng.choice(np.array([0, 1, 2], dtype=np.uint8), n, p=[0.9, 0.05, 0.05])
+    last_rows = np.arange(chunk - 1, n, chunk)
+    states[last_rows[rng.random(len(last_rows)) < 0.3]] = 2
+    states[last_rows[rng.random(len(last_rows)) < 0.2]] = 1
+    if chunk == 1:
+        states[:] = 0
+        states[-3:] = [1, 0, 2]
+    states[20:26] = 0
+    ids = rng.permutation(4 * n).astype(np.uint32)
+    pre = np.where(rng.random(n) < 0.1, ids[:n], 0xFFFFFFFF).astype(np.uint32)
+    pre[23] = 5
+    pre[420] = 3  # smaller: takes the key over from row 23's Object in a later chunk
+    seeded_keys = pool[rng.random(len(pool)) < 0.2]
+    sk = seeded_keys.astype(np.uint64)
+    so = ids[n:n + len(sk)].astype(np.uint32)
+    pre_list = [None if int(p) == 0xFFFFFFFF else int(p) for p in pre]
+    for existing in ((sk, so), None):
+        ex = None if existing is None else list(zip((int(k) for k in sk), (int(o) for o in so)))
+        want_step, want_obj, want_act, want_counts = replay_identifier_job(
+            [int(k) for k in keys], [int(s) for s in states], chunk, existing=ex, pre_objects=pre_list)
+        assert 4 in want_act and 0 in want_act
+        step, obj, act, counts = eng.identifier_links(
+            dev64(keys), torch.from_numpy(states).cuda(), chunk,
+            existing=None if existing is None else (dev64(sk), torch.from_numpy(so.view(np.int32)).cuda()),
+            pre_objects=torch.from_numpy(pre.view(np.int32)).cuda())
+        assert [tuple(c) for c in counts.tolist()] == want_counts
+        assert (step.cpu().numpy().view(np.uint32) == np.array(want_step, dtype=np.uint32)).all()
+        assert (obj.cpu().numpy().view(np.uint32) == np.array(want_obj, dtype=np.uint32)).all()
+        assert (act.cpu().numpy() == np.array(want_act, dtype=np.uint8)).all()
+        hstep, hobj, hact, hcounts = eng.identifier_links_host(keys, states, chunk, existing=existing,
+                                                               pre_objects=pre_list)
+        assert [tuple(c) for c in hcounts.tolist()] == want_counts
+        assert (hobj == np.array(want_obj, dtype=np.uint32)).all()
+        assert (hact == np.array(want_act, dtype=np.uint8)).all()
+    if chunk == 100:
+        assert want_act[23] == 4 and want_obj[23] == 5 and want_obj[420] == 3 and want_obj[900] == 3
+    # no row owning an Object = the seeded / fresh call
+    none = np.full(n, 0xFFFFFFFF, np.uint32)
+    a = eng.identifier_links_host(keys, states, chunk, existing=(sk, so), pre_objects=none)
+    b = eng.identifier_links_host(keys, states, chunk, existing=(sk, so))
+    assert all((x == y).all() for x, y in zip(a, b))
+    from spacedrive_amd import CasError
+    bad = pre.copy()
+    bad[7] = 2 ** 31
+    with pytest.raises(ValueError):
+        eng.identifier_links_host(keys, states, chunk, pre_objects=bad)
+    with pytest.raises(CasError):
+        eng.identifier_links(dev64(keys), torch.from_numpy(states).cuda(), chunk,
+                             pre_objects=torch.from_numpy(bad.view(np.int32)).cuda())
+
+
+def test_identifier_links_pre_objects_hot_key_1m(eng):
+    """The two scans at scale: 1M rows, one hot key over every chunk with pre-existing
+    Objects whose ids decrease step by step (each step's minimum takes over), plus random
+    keys; every row hashed (chunk 100) vs the closed form of the replay."""
+    rng = np.random.default_rng(281)
+    n = 1 << 20
+    keys = rng.integers(1, 2 ** 64, 700_000, dtype=np.uint64)[rng.integers(0, 700_000, n)]
+    hot = np.arange(0, n, 37)
+    keys[hot] = np.uint64(0xABCDEF)
+    pre = np.full(n, 0xFFFFFFFF, np.uint32)
+    owners = hot[::5]
+    pre[owners] = (2 ** 30 - owners).astype(np.uint32)  # later rows, smaller ids
+    some = rng.choice(n, n // 50, replace=False)
+    pre[some] = rng.integers(0, 2 ** 31 - 1, len(some)).astype(np.uint32)
+    step, obj, act, counts = eng.identifier_links(dev64(keys), None, 100,
+                                                  pre_objects=torch.from_numpy(pre.view(np.int32)).cuda())
+    st = np.arange(n) // 100
+    assert (step.cpu().numpy() == st).all()
+    # closed form: per key, the minimum pre-existing Object over rows in steps <= the row's
+    order = np.lexsort((np.arange(n), keys))
+    sk, sr = keys[order], order
+    want = np.full(n, 0xFFFFFFFF, np.uint64)
+    first = np.empty(n, np.int64)
+    p = pre[sr].astype(np.uint64)
+    starts = np.flatnonzero(np.r_[True, sk[1:] != sk[:-1]])
+    for a, b in zip(starts, np.r_[starts[1:], n]):
+        first[sr[a:b]] = sr[a]
+        if b - a == 1:
+            want[sr[a]] = p[a]
+            continue
+        pm = np.minimum.accumulate(p[a:b])
+        s = st[sr[a:b]]
+        last = np.r_[np.flatnonzero(s[1:] != s[:-1]), b - a - 1]   # end of each step's run
+        want[sr[a:b]] = pm[last[np.searchsorted(last, np.arange(b - a))]]
+    o = obj.cpu().numpy().view(np.uint32).astype(np.int64)
+    a_ = act.cpu().numpy()
+    ex = want != 0xFFFFFFFF
+    assert (a_[ex] == 4).all() and (o[ex] == want[ex].astype(np.int64)).all()
+    created = ~ex & (st[first] == st)
+    assert (a_[created] == 0).all() and (o[created] == np.arange(n)[created]).all()
+    linked = ~ex & ~created
+    assert (a_[linked] == 1).all() and (o[linked] == first[linked]).all()
+    assert ex[hot].sum() > len(hot) // 2 and linked.any() and created.any()
+    # the hot key's target falls step by step: every owner row takes it over
+    assert (o[owners] <= pre[owners]).all()
+    assert int(counts[:, 0].sum()) + int(counts[:, 1].sum()) == n
 
 
 def test_identifier_job_step_existing(eng, oracle, tmp_path):
@@ -1548,6 +1666,43 @@ def test_identifier_job_step_existing(eng, oracle, tmp_path):
             assert i in res.object_of
     assert sum(len(b.links_existing) for b in res.steps) == len(res.existing_of) > 0
     assert res.total_linked == sum(len(b.links) + len(b.links_existing) for b in res.steps)
+
+
+def test_identifier_job_step_watcher_sequence(eng, oracle, tmp_path):
+    """The watcher's create-then-write sequence end to end: files created empty got an
+    Object with no cas_id (watcher/utils.rs:236-293), then were written — the update keeps
+    the old NULL cas_id with the new size (:473-490) — so the job's orphan query returns them
+    with their Object (file_identifier_job.rs:258-261).  identifier_job_step(pre_objects=)
+    hashes them and links them, and every file of their step with the same content, to the
+    smallest such Object; one file still empty at identification time gets a new Object;
+    decisions and per-step counts equal the literal replay on the oracle's cas_ids."""
+    import spacedrive_amd as sd
+    rng = np.random.default_rng(12)
+    blobs = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in [4_000, 180_000, 33]]
+    paths, pre = [], []
+    for i in range(230):
+        p = tmp_path / f"w{i:03d}"
+        p.write_bytes(b"")                       # the watcher's create: empty, Object made
+        pre.append(1000 + 3 * i if i % 9 == 4 else None)
+        paths.append(str(p))
+    for i, p in enumerate(paths):                # ... then written
+        if i == 121:
+            continue                             # still empty: NO_CAS, a new Object
+        open(p, "wb").write(blobs[i % 3] if i % 4 == 0 else
+                            rng.integers(0, 256, int(rng.integers(1, 150_000)), dtype=np.uint8).tobytes())
+    pre[121] = 7
+    pre[8] = 2                                   # row 8 (blob 2) owns the smallest Object
+    res = sd.identifier_job_step(paths, eng=eng, pre_objects=pre)
+    keys = [0 if os.path.getsize(p) == 0 else int(oracle.generate_cas_id(p, os.path.getsize(p)), 16)
+            for p in paths]
+    states = [1 if k == 0 else 0 for k in keys]
+    step, obj, act, counts = replay_identifier_job(keys, states, 100, pre_objects=pre)
+    assert [(b.total_created, b.total_linked) for b in res.steps] == counts
+    assert {i: o for i, (o, a) in enumerate(zip(obj, act)) if a == 4} == res.existing_of
+    assert {i: o for i, (o, a) in enumerate(zip(obj, act)) if a in (0, 1)} == res.object_of
+    assert res.existing_of[8] == 2 and 121 in res.object_of and res.object_of[121] == 121
+    assert all(res.existing_of[i] == 2 for i in range(8, 100, 4) if i % 3 == 2)  # blob 2 in step 0
+    assert res.metadata[4].cas_id == f"{keys[4]:016x}" and res.existing_of[4] <= 1000 + 12
 
 
 def test_identifier_links_all_hashed_1m(eng, oracle):

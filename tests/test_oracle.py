@@ -275,6 +275,97 @@ def test_job_replay_existing_objects():
     assert act0[0] == 0 and obj0[6] == 0 and act0[2] == 0
 
 
+def test_job_replay_rows_owning_objects():
+    """Rows that already own an Object (object_id set, cas_id NULL — orphan by
+    file_identifier_job.rs:258-261; the watcher's "created empty, then written" file,
+    watcher/utils.rs:236-293,473-490): the step writes the row's cas_id before find_many
+    (mod.rs:157-198), so the row's Object joins its key's Objects in that step; every row of
+    the step with the key links to the smallest such id and the key never creates there; a
+    pre-job Object takes over a key an earlier step created an Object for; a NO_CAS row with
+    an Object still creates, an ERROR row keeps it (dropped)."""
+    from tests.golden.make_golden import LINK_DROPPED, LINK_EXISTING, replay_identifier_job
+    A, B, C, D, E = 0xA0, 0xB0, 0xC0, 0xD0, 0xE0
+    keys = [A, B, A, C, A, B, D, A, C, A, E, B, A, 0, 0, A]
+    states = [0] * 12 + [0, 1, 2, 0]
+    pre = [None, None, None, 50, None, 20, None, None, None, 10, None, None, 60, 70, 80, None]
+    step, obj, act, counts = replay_identifier_job(keys, states, 4, pre_objects=pre)
+    assert step == [k // 4 for k in range(16)]
+    assert act[:3] == [0, 0, 0] and (act[3], obj[3]) == (LINK_EXISTING, 50)  # C: its own Object
+    assert (act[4], obj[4]) == (1, 0) and (act[7], obj[7]) == (1, 0)          # A: row 0's
+    assert (act[5], obj[5]) == (LINK_EXISTING, 20)  # B: 20 is older than row 1's Object
+    assert (act[8], obj[8]) == (LINK_EXISTING, 50)
+    assert (act[9], obj[9]) == (LINK_EXISTING, 10)  # A taken over by the pre-job Object 10
+    assert (act[11], obj[11]) == (LINK_EXISTING, 20) and act[10] == 0
+    assert (act[12], obj[12]) == (LINK_EXISTING, 10)  # its own 60 loses to 10
+    assert (act[13], obj[13]) == (0, 13) and act[14] == LINK_DROPPED
+    assert (act[15], obj[15]) == (LINK_EXISTING, 10)
+    assert counts == [(3, 1), (1, 3), (1, 3), (1, 2)]
+    # without the pre-existing Objects: the fresh-library answer
+    _, obj0, act0, _ = replay_identifier_job(keys, states, 4)
+    assert act0[3] == 0 and (act0[9], obj0[9]) == (1, 0)
+
+
+def closed_form_links(keys, states, step, chunk, existing=(), pre=None):
+    """The per-row formula the GPU emission evaluates (links.hip), from the rows' steps:
+    a hashed row's Object is the smallest pre-job Object carrying its key that the step
+    sees — seeds, or pre-existing Objects of rows with the key in this or an earlier step —
+    else the Object created for the key's first row (CREATED in that row's step)."""
+    n = len(keys)
+    NONE = 0xFFFFFFFF
+    seedmin, first, ev = {}, {}, {}
+    for c, o in existing:
+        seedmin[c] = min(seedmin.get(c, NONE), o)
+    for i in range(n):
+        if step[i] != NONE and states[i] == 0:
+            first.setdefault(keys[i], i)
+            if pre is not None and pre[i] is not None:
+                ev.setdefault(keys[i], []).append((step[i], pre[i]))
+    obj, act = [NONE] * n, [3] * n
+    for i in range(n):
+        if step[i] == NONE:
+            continue
+        if states[i] == 2:
+            act[i] = 2
+        elif states[i] == 1:
+            act[i], obj[i] = 0, i
+        else:
+            k = keys[i]
+            v = min([seedmin.get(k, NONE)] + [p for s, p in ev.get(k, ()) if s <= step[i]])
+            if v != NONE:
+                act[i], obj[i] = 4, v
+            elif step[first[k]] == step[i]:
+                act[i], obj[i] = 0, i
+            else:
+                act[i], obj[i] = 1, first[k]
+    return obj, act
+
+
+@pytest.mark.parametrize("chunk", [100, 7, 3, 1])
+def test_pre_object_closed_form_vs_replay(chunk):
+    """The closed form behind sd_cas_identifier_links_ex (per-key prefix minimum over steps)
+    equals the literal DB replay: random keys with repeats inside and across chunks, ~10 %
+    of rows owning an Object (ids interleaved with the seeds'), seeds, NO_CAS / ERROR rows
+    at chunk ends (the cursor re-queries them)."""
+    from tests.golden.make_golden import replay_identifier_job
+    rng = np.random.default_rng(400 + chunk)
+    for trial in range(4):
+        n = 700 if chunk > 2 else 300
+        pool = [int(x) for x in rng.integers(1, 2 ** 63, max(4, n // (3 + trial)))]
+        keys = [pool[int(j)] for j in rng.integers(0, len(pool), n)]
+        states = [int(s) for s in rng.choice([0, 1, 2], n, p=[0.88, 0.06, 0.06])]
+        if chunk == 1:  # a row that stays orphan is re-queried until the step budget ends
+            states = [0] * (n - 3) + [1, 0, 2]
+        ids = rng.permutation(4 * n)
+        pre = [int(ids[i]) if rng.random() < 0.1 else None for i in range(n)]
+        existing = [(pool[int(j)], int(ids[2 * n + t])) for t, j in
+                    enumerate(rng.integers(0, len(pool), len(pool) // 4 * (trial % 2)))]
+        step, obj, act, _ = replay_identifier_job(keys, states, chunk, existing=existing,
+                                                  pre_objects=pre)
+        cobj, cact = closed_form_links(keys, states, step, chunk, existing, pre)
+        assert cact == act and cobj == obj, (chunk, trial)
+        assert 4 in act
+
+
 def test_simd_baseline_matches_scalar(oracle):
     rng = np.random.default_rng(2)
     n = 48

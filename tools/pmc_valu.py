@@ -11,6 +11,8 @@ the chip has 256 CUs x 4 SIMDs = 1,024 SIMDs.
   valu_busy_full_rate  = SQ_INSTS_VALU x 2 / (1,024 x GRBM_GUI_ACTIVE / 8) — the same with
                          every wave64 instruction at the full SIMD32 rate (2 cycles): a floor
   clock_ghz            = GRBM_GUI_ACTIVE / 8 / the kernel's mean duration (kernel trace)
+  instr_rate_t_per_s   = SQ_INSTS_VALU x 64 lanes / the kernel's mean duration (T lane-instr/s:
+                         the achieved integer instruction rate, vs the 78.6 T full-rate peak)
 Prints one JSON object {kernel: {...}} (per-dispatch means)."""
 import csv
 import glob
@@ -22,10 +24,10 @@ from collections import defaultdict
 SIMDS = 256 * 4
 
 
-def main():
+def summarize(dirs):
     acc = defaultdict(lambda: defaultdict(list))
     dur = defaultdict(list)
-    for d in sys.argv[1:]:
+    for d in dirs:
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
                 acc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
@@ -47,8 +49,13 @@ def main():
             t = sum(dur[k]) / len(dur[k])
             rec["mean_s"] = t
             rec["clock_ghz"] = wall / t / 1e9
+            rec["instr_rate_t_per_s"] = m["SQ_INSTS_VALU"] * 64 / t / 1e12
         out[k] = rec
-    print(json.dumps(out, indent=1))
+    return out
+
+
+def main():
+    print(json.dumps(summarize(sys.argv[1:]), indent=1))
 
 
 if __name__ == "__main__":

@@ -9,6 +9,78 @@
 
 #include "../spacedrive_amd/csrc/cas_hash.hip"
 
+// ---- the A/B-only variants of K1's lane program (moved out of the product, round 5) ------
+// NT: non-temporal loads — measured 1.6x SLOWER (33.7 vs 55.0 M files/s): the 8 dwordx4
+// loads of one 128-B line no longer share the line in L2 and each goes to HBM.
+// Layouts of the sampled content in HBM (quad = 16 B; q points at the lane's first quad):
+//   ROW   (0): file f at content + f*stride; quad i of pair P at q[8P + i]  (the product's)
+//   LINE  (1): tiles of 64 files; pair P of lane l at tile + (64P + l)*128 B  -> q[512P + i]
+//   QUAD  (2): tiles of 64 files; quad j of lane l at tile + (64j + l)*16 B    -> q[512P + 64i]
+namespace ab {
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+enum : int { LAYOUT_ROW = 0, LAYOUT_LINE = 1, LAYOUT_QUAD = 2 };
+template <int L> struct LayoutStride;
+template <> struct LayoutStride<LAYOUT_ROW> { static constexpr uint32_t P = 8, I = 1; };
+template <> struct LayoutStride<LAYOUT_LINE> { static constexpr uint32_t P = 512, I = 1; };
+template <> struct LayoutStride<LAYOUT_QUAD> { static constexpr uint32_t P = 512, I = 64; };
+
+template <bool NT, int L>
+__device__ __forceinline__ void load_pair(const uint4* __restrict__ q, uint32_t P, uint4 (&buf)[8]) {
+  const uint4* p = q + LayoutStride<L>::P * P;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (NT) {
+      const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + LayoutStride<L>::I * i));
+      buf[i] = make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+      buf[i] = p[LayoutStride<L>::I * i];
+    }
+  }
+}
+
+// the product's sdcas::cas_lane_sampled with the loader swapped
+template <bool NT = false, int L = LAYOUT_ROW>
+__device__ __forceinline__ uint64_t cas_lane_sampled(const uint4* __restrict__ q, uint64_t size,
+                                                     sdcas::LdsStack<>& stk) {
+  using namespace sdcas;
+  uint32_t c0 = (uint32_t)size, c1 = (uint32_t)(size >> 32);
+  uint4 A[8], B[8];
+  load_pair<NT, L>(q, 0, A);
+  uint32_t cv[8];
+  for (uint32_t c = 0; c < SAMPLED_CHUNKS; ++c) {
+    set_iv(cv);
+#pragma unroll 1
+    for (uint32_t pp = 0; pp < 4; ++pp) {
+      const uint32_t P = 8u * c + 2u * pp;
+      load_pair<NT, L>(q, P + 1, B);
+      compress_pair(cv, A, c0, c1, c, pp == 0 ? (uint32_t)CHUNK_START : 0u, 0u);
+      if (P + 2 < SAMPLED_PAIRS) load_pair<NT, L>(q, P + 2, A);
+      compress_pair(cv, B, c0, c1, c, 0u, pp == 3 ? (uint32_t)CHUNK_END : 0u);
+    }
+    uint32_t total = c + 1;
+    while ((total & 1u) == 0u) {
+      uint32_t left[8];
+      stk.pop(left);
+      parent(cv, left, cv, 0u);
+      total >>= 1;
+    }
+    stk.push(cv);
+  }
+  {
+    const uint32_t m[16] = {c0, c1, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    set_iv(cv);
+    compress(cv, m, SAMPLED_CHUNKS, 0u, 8u, CHUNK_START | CHUNK_END);
+  }
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    uint32_t left[8];
+    stk.pop(left);
+    parent(cv, left, cv, d == 2 ? (uint32_t)ROOT : 0u);
+  }
+  return key_of(cv);
+}
+}  // namespace ab
+
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
 
 // mode 0: real (file f), 1: window of 32 files (L2), 2: broadcast (file 0 for every lane),
@@ -27,11 +99,11 @@ __global__ void __launch_bounds__(256) k1_variant(const uint8_t* __restrict__ co
     if (MODE == 5 || MODE == 6) {
       const uint4* q = reinterpret_cast<const uint4*>(content + (f >> 6) * 64 * stride) +
                        (MODE == 5 ? (f & 63) * 8 : (f & 63));
-      keys[f] = MODE == 5 ? sdcas::cas_lane_sampled<false, sdcas::LAYOUT_LINE>(q, sizes[f], stk)
-                          : sdcas::cas_lane_sampled<false, sdcas::LAYOUT_QUAD>(q, sizes[f], stk);
+      keys[f] = MODE == 5 ? ab::cas_lane_sampled<false, ab::LAYOUT_LINE>(q, sizes[f], stk)
+                          : ab::cas_lane_sampled<false, ab::LAYOUT_QUAD>(q, sizes[f], stk);
     } else {
       const uint4* q = reinterpret_cast<const uint4*>(content + g * stride);
-      keys[f] = sdcas::cas_lane_sampled<MODE == 4>(q, sizes[f], stk);
+      keys[f] = ab::cas_lane_sampled<MODE == 4>(q, sizes[f], stk);
     }
   }
   uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
