@@ -39,9 +39,9 @@ __device__ __forceinline__ void load_pair(const uint4* __restrict__ q, uint32_t 
 }
 
 // the product's sdcas::cas_lane_sampled with the loader swapped
-template <bool NT = false, int L = LAYOUT_ROW>
+template <bool NT = false, int L = LAYOUT_ROW, int BLK = 256>
 __device__ __forceinline__ uint64_t cas_lane_sampled(const uint4* __restrict__ q, uint64_t size,
-                                                     sdcas::LdsStack<>& stk) {
+                                                     sdcas::LdsStack<BLK>& stk) {
   using namespace sdcas;
   uint32_t c0 = (uint32_t)size, c1 = (uint32_t)(size >> 32);
   uint4 A[8], B[8];
@@ -90,12 +90,16 @@ template <int MODE>
 __global__ void __launch_bounds__(256) k1_variant(const uint8_t* __restrict__ content, uint64_t stride,
                                                   const uint64_t* __restrict__ sizes, uint64_t n,
                                                   uint64_t* __restrict__ keys, uint64_t* clk) {
-  __shared__ uint32_t stack_lds[sdcas::SAMPLED_DEPTH][8][sdcas::SAMPLED_BLOCK];
+  // 256-lane workgroups (the launch below): the stack is sized and the file indexed by the
+  // workgroup's own width (indexing by the product's 512-lane SAMPLED_BLOCK skipped half the
+  // files: the K1 rows of profiles/r05/valu_power/ubench_k1_halfgrid_bug.txt are 2x too fast;
+  // its compute-only row, a separate kernel, is valid)
+  __shared__ uint32_t stack_lds[sdcas::SAMPLED_DEPTH][8][256];
   uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-  const uint64_t f = (uint64_t)blockIdx.x * sdcas::SAMPLED_BLOCK + threadIdx.x;
+  const uint64_t f = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (f < n) {
     const uint64_t g = (MODE == 0 || MODE == 4) ? f : (MODE == 1 ? (f & 31) : 0);
-    sdcas::LdsStack<> stk{stack_lds, threadIdx.x};
+    sdcas::LdsStack<256> stk{stack_lds, threadIdx.x};
     if (MODE == 5 || MODE == 6) {
       const uint4* q = reinterpret_cast<const uint4*>(content + (f >> 6) * 64 * stride) +
                        (MODE == 5 ? (f & 63) * 8 : (f & 63));
