@@ -863,6 +863,7 @@ def cpu_baseline(content, sizes, keys, seconds: float):
             "cores": threads, "kind": "port", "value_1thread": one_thread,
             "cpu_model": cpu_model(), "cpus_online": os.cpu_count(),
             "threads_rule": "cpu_threads(world): min(affinity, OMP_NUM_THREADS (or 16) x n_gpus)",
+            "threads_override": os.environ.get("SD_CPU_BASELINE_THREADS") or None,
             "simd": "avx512 16-lane" if orc.has_simd() else "scalar",
             "sample": f"{reps} passes over the first {m} files of the bench batch (hashing only, "
                       f"messages pre-gathered in DRAM), {dt:.1f}s",

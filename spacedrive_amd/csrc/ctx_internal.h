@@ -239,14 +239,18 @@ inline int sd_ensure(sd_cas_ctx* c, DevBuf& b, size_t bytes) {
   return SD_CAS_OK;
 }
 
-// The staging's host mapping (A/B SD_PINNED_NONCOHERENT): non-coherent lets the GPU's reads
-// of it (the job step's pull kernel) use cached line fills; host writes are visible at
-// kernel boundaries, which is how every staged batch is ordered. Not adopted: no gain
-// over the coherent mapping in profiles/r04_ab_jobstep_pull.log
-#ifndef SD_PINNED_NONCOHERENT
-#define SD_PINNED_NONCOHERENT 0
+// The staging's host mapping.  SD_PINNED_MODE 0 = hipHostMallocDefault (the product), whose
+// coherence follows HIP_HOST_COHERENT (unset = 0 = NON-coherent on ROCm); 1 = explicitly
+// hipHostMallocNonCoherent; 2 = explicitly hipHostMallocCoherent.  Round 4's "coherent vs
+// non-coherent" A/B compared modes 0 and 1 — with HIP_HOST_COHERENT unset both are the same
+// non-coherent mapping, so it showed nothing; the three-arm A/B of round 5 with
+// an explicit coherent arm is profiles/r05/ab_pinned_mode/ (DESIGN.md §2.2, f1).
+#ifndef SD_PINNED_MODE
+#define SD_PINNED_MODE 0
 #endif
-#define SD_PINNED_FLAGS (SD_PINNED_NONCOHERENT ? hipHostMallocNonCoherent : hipHostMallocDefault)
+#define SD_PINNED_FLAGS                                                              \
+  (SD_PINNED_MODE == 1 ? hipHostMallocNonCoherent                                    \
+                       : SD_PINNED_MODE == 2 ? hipHostMallocCoherent : hipHostMallocDefault)
 
 // K1 / K1L / K1+K1L by batch size (sd_hip_cas.cpp), shared with the host entry points
 extern "C" hipError_t sd_dispatch_sampled(sd_cas_ctx* c, const uint8_t* content, uint64_t stride,

@@ -2,7 +2,10 @@
 """Object grouping on one GPU: K4h/K5h (bucket partition + LDS hash min, sd_cas_group_dev)
 vs the LSD radix sort + run heads (sd_cas_sort_pairs_dev + sd_cas_group_sorted_dev), at
 the bench's per-GPU batch (1.31M keys) and config 4's rank share (12.5M keys), 30 % dups.
-Both results are checked against each other; one JSON line per size."""
+Both results are checked against each other; one JSON line per size.
+--only hash|lsd: run ONE method only (chain_calls of it, incl. the warm-up call) and no
+cross-check — the PMC passes of tools/gpu_r5_pmc_sort.sh attribute every sd_* dispatch of
+the process to that method."""
 import json
 import os
 import sys
@@ -27,9 +30,15 @@ def timed(fn, reps=5):
 
 
 def main():
+    args = sys.argv[1:]
+    only = None
+    if "--only" in args:
+        i = args.index("--only")
+        only = args[i + 1]
+        del args[i:i + 2]
     eng = CasEngine(0)
     rng = np.random.default_rng(1)
-    for n in [int(x) for x in (sys.argv[1:] or ["1310720", "12500000"])]:
+    for n in [int(x) for x in (args or ["1310720", "12500000"])]:
         uniq = rng.integers(0, 2 ** 64, int(n * 0.7), dtype=np.uint64)
         keys_h = np.concatenate([uniq, uniq[rng.integers(0, len(uniq), n - len(uniq))]])
         rng.shuffle(keys_h)
@@ -38,12 +47,21 @@ def main():
         rep2 = torch.empty(n, dtype=torch.int32, device="cuda")
         ko = torch.empty_like(keys)
         vo = torch.empty(n, dtype=torch.int32, device="cuda")
-        obj = eng.group(keys, rep)  # warm + workspace
-        t_hash = timed(lambda: eng.group(keys, rep, want_objects=False))
-
         def legacy():
             eng.sort_pairs(keys, None, ko, vo)
             eng.group_sorted(ko, vo, rep2)
+        if only == "hash":
+            obj = eng.group(keys, rep)
+            t = timed(lambda: eng.group(keys, rep, want_objects=False))
+            print(json.dumps({"keys": n, "method": "hash", "objects": obj, "ms": t, "chain_calls": 6}), flush=True)
+            continue
+        if only == "lsd":
+            legacy()
+            t = timed(legacy)
+            print(json.dumps({"keys": n, "method": "lsd", "ms": t, "chain_calls": 6}), flush=True)
+            continue
+        obj = eng.group(keys, rep)  # warm + workspace
+        t_hash = timed(lambda: eng.group(keys, rep, want_objects=False))
         legacy()
         t_lsd = timed(legacy)
         same = bool(torch.equal(rep, rep2))
