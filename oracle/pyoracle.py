@@ -275,6 +275,15 @@ def build_oracle(quiet: bool = True) -> str:
     return LIB_PATH
 
 
+def _sizes_u64(sizes) -> np.ndarray:
+    """Sizes as u64; a negative entry of a signed array is refused instead of wrapping to
+    2^64 - 1 (the same check as the product wrapper's, spacedrive_amd/cas.py)."""
+    a = np.asarray(sizes)
+    if a.size and a.dtype.kind == "i" and int(a.min()) < 0:
+        raise ValueError(f"negative size {int(a.min())}")
+    return np.ascontiguousarray(a, dtype=np.uint64)
+
+
 class Oracle:
     def __init__(self, path: str = LIB_PATH):
         if not os.path.exists(path):
@@ -394,7 +403,7 @@ class Oracle:
         out = np.zeros(n, dtype=np.uint64)
         offs = np.ascontiguousarray(offs, dtype=np.uint64)
         lens = np.ascontiguousarray(lens, dtype=np.uint64)
-        sizes = np.ascontiguousarray(sizes, dtype=np.uint64)
+        sizes = _sizes_u64(sizes)
         self.L.orc_cas_keys(arena.ctypes.data, _p64(offs), _p64(lens), _p64(sizes), n,
                             _p64(out), threads)
         return out
@@ -403,7 +412,7 @@ class Oracle:
                          threads: int = 1) -> np.ndarray:
         n = len(sizes)
         out = np.zeros(n, dtype=np.uint64)
-        sizes = np.ascontiguousarray(sizes, dtype=np.uint64)
+        sizes = _sizes_u64(sizes)
         self.L.orc_cas_keys_strided(arena.ctypes.data, stride, clen, _p64(sizes), n, _p64(out),
                                     threads)
         return out
@@ -412,7 +421,7 @@ class Oracle:
                               sizes: np.ndarray, threads: int = 1) -> np.ndarray:
         n = len(sizes)
         out = np.zeros(n, dtype=np.uint64)
-        sizes = np.ascontiguousarray(sizes, dtype=np.uint64)
+        sizes = _sizes_u64(sizes)
         self.L.orc_fast_cas_keys(arena.ctypes.data, None, None, stride, clen, _p64(sizes), n,
                                  _p64(out), threads)
         return out
@@ -422,7 +431,7 @@ class Oracle:
         out = np.zeros(n, dtype=np.uint64)
         offs = np.ascontiguousarray(offs, dtype=np.uint64)
         lens = np.ascontiguousarray(lens, dtype=np.uint64)
-        sizes = np.ascontiguousarray(sizes, dtype=np.uint64)
+        sizes = _sizes_u64(sizes)
         self.L.orc_fast_cas_keys(arena.ctypes.data, offs.ctypes.data, lens.ctypes.data, 0, 0,
                                  _p64(sizes), n, _p64(out), threads)
         return out
@@ -455,7 +464,7 @@ class Oracle:
         else:
             parr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
             parr_addr = ctypes.cast(parr, ctypes.c_void_p).value
-        sz = np.ascontiguousarray(sizes, dtype=np.uint64)
+        sz = _sizes_u64(sizes)
         keys = np.zeros(n, dtype=np.uint64)
         status = np.zeros(n, dtype=np.int32)
         fn = self.L.orc_fast_generate_cas_keys_paths if simd else self.L.orc_generate_cas_keys_paths

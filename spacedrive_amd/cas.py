@@ -66,6 +66,18 @@ def _np_ptr(a: np.ndarray) -> int:
     return int(a.ctypes.data)
 
 
+def _sizes_u64(sizes, what: str = "sizes") -> np.ndarray:
+    """File sizes (fs::metadata lengths) as the u64 column of the ABI.  A signed array is
+    checked first: a negative size (e.g. a -1 'stat failed' marker) would otherwise wrap to
+    2^64 - 1 and be hashed as a huge sampled file."""
+    a = np.asarray(sizes) if isinstance(sizes, np.ndarray) else np.array([int(x) for x in sizes])
+    if a.size and a.dtype.kind == "i" and int(a.min()) < 0:
+        raise ValueError(f"{what}: negative size {int(a.min())}")
+    if a.size and a.dtype.kind not in "iu":
+        raise ValueError(f"{what}: integer sizes expected, got {a.dtype}")
+    return np.ascontiguousarray(a, dtype=np.uint64)
+
+
 def _check_dev(t, dtypes, n: int, what: str) -> None:
     """A device tensor handed to a *_dev call: one of `dtypes`, n elements, contiguous, on a
     GPU — checked before the library reads it as raw memory."""
@@ -212,8 +224,7 @@ class CasEngine:
         keep, parr = _path_array(paths)
         sz = None
         if sizes is not None:
-            sz = (np.ascontiguousarray(sizes, dtype=np.uint64) if isinstance(sizes, np.ndarray)
-                  else np.array([int(s) for s in sizes], dtype=np.uint64))
+            sz = _sizes_u64(sizes)
             if sz.shape != (n,):
                 raise ValueError(f"sizes has shape {sz.shape}, expected ({n},)")
         keys = np.zeros(n, dtype=np.uint64)
@@ -254,7 +265,7 @@ class CasEngine:
                           batch_files: int = 0) -> np.ndarray:
         """End-to-end K1 from host memory (H2D pipelined with hashing)."""
         n = len(sizes)
-        sz = np.ascontiguousarray(sizes, dtype=np.uint64)
+        sz = _sizes_u64(sizes)
         keys = np.zeros(n, dtype=np.uint64)
         self._check(self.L.sd_cas_hash_sampled_host(self.h, int(content.ctypes.data), int(stride),
                                                     _np_ptr(sz), n, _np_ptr(keys), int(batch_files)),
@@ -266,7 +277,7 @@ class CasEngine:
         """End-to-end K1 over len(sizes) files whose contents cycle through a host ring of
         ring_files x stride bytes at ring_ptr (every file is copied host -> device)."""
         n = len(sizes)
-        sz = np.ascontiguousarray(sizes, dtype=np.uint64)
+        sz = _sizes_u64(sizes)
         keys = np.zeros(n, dtype=np.uint64)
         self._check(self.L.sd_cas_hash_sampled_host_ring(self.h, int(ring_ptr), int(stride),
                                                          int(ring_files), _np_ptr(sz), n,

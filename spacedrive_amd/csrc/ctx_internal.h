@@ -143,6 +143,7 @@ struct sd_cas_ctx {
   // 100-file job step ~10 us)
   hipEvent_t gather_done[2] = {nullptr, nullptr};
   bool trace = false;  // SD_CAS_TRACE=1: per-phase host timestamps of host-buffer calls on stderr
+  uint32_t test_table_fill = 0;  // SD_CAS_TEST_TABLE_FILL (tests): region tables' overflow bound
   std::string err;
 };
 

@@ -708,9 +708,13 @@ __device__ __forceinline__ void bucket_min(uint32_t bucket, uint32_t* __restrict
                                            uint32_t count_stride = 1,
                                            const uint64_t* __restrict__ spill_keys = nullptr,
                                            const uint32_t* __restrict__ spill_pos = nullptr,
-                                           uint32_t* __restrict__ spill_cnt = nullptr) {
+                                           uint32_t* __restrict__ spill_cnt = nullptr,
+                                           uint32_t fill_limit = 0) {
   constexpr uint32_t TILE = THREADS * NI;
-  constexpr uint32_t FILL = TBL / 8 * 7;  // above this the bucket goes to global memory
+  // above FILL distinct keys the bucket goes to global memory; fill_limit (tests only, the
+  // context's SD_CAS_TEST_TABLE_FILL) lowers it so the overflow and whole-input paths run on
+  // keys K1G cannot be made to produce
+  const uint32_t FILL = fill_limit && fill_limit < TBL / 8 * 7 ? fill_limit : TBL / 8 * 7;
   static_assert(TILE < TBL, "one-trip buckets must leave an empty slot (lds_claim's unbounded probe)");
   __shared__ uint64_t tk[TBL];
   __shared__ uint32_t tv[TBL];
@@ -952,12 +956,13 @@ sd_bucket_min_regions(const uint64_t* __restrict__ rkeys, const uint32_t* __rest
                       uint32_t* __restrict__ cursor, uint64_t cap, uint32_t* __restrict__ out,
                       unsigned long long* __restrict__ objects, uint64_t* __restrict__ gkeys,
                       uint32_t* __restrict__ gvals, const uint64_t* __restrict__ keys, uint64_t n,
-                      const uint64_t* __restrict__ spill_keys, const uint32_t* __restrict__ spill_file) {
+                      const uint64_t* __restrict__ spill_keys, const uint32_t* __restrict__ spill_file,
+                      uint32_t fill_limit) {
   bucket_min<REG_TABLE, REG_THREADS, REG_ITEMS, true>(blockIdx.x, nullptr, 0, rkeys, rfile, nullptr,
                                                       nullptr, REGIONS, REGION_BITS, 0, out, objects,
                                                       gkeys, gvals, cursor, cap, keys, n, objects + 1,
                                                       1, spill_keys, spill_file,
-                                                      cursor + REGION_SPILL_WORD);
+                                                      cursor + REGION_SPILL_WORD, fill_limit);
 }
 
 // The standalone chain for small batches (<= BIG_MAX_KEYS keys, default plan): the keys
@@ -1280,10 +1285,11 @@ void region_group_layout(void* ws, uint64_t n, uint64_t** rkeys, uint32_t** rfil
 hipError_t region_group_min(const uint64_t* rkeys, const uint32_t* rfile, uint32_t* cursor,
                             uint64_t cap, uint32_t* out, uint64_t* d_objects, uint64_t* gkeys,
                             uint32_t* gvals, const uint64_t* keys, uint64_t n,
-                            const uint64_t* spill_keys, const uint32_t* spill_file, hipStream_t s) {
+                            const uint64_t* spill_keys, const uint32_t* spill_file,
+                            uint32_t fill_limit, hipStream_t s) {
   sd_bucket_min_regions<<<REGIONS, REG_THREADS, 0, s>>>(rkeys, rfile, cursor, cap, out,
                                                         (unsigned long long*)d_objects, gkeys, gvals,
-                                                        keys, n, spill_keys, spill_file);
+                                                        keys, n, spill_keys, spill_file, fill_limit);
   return hipGetLastError();
 }
 

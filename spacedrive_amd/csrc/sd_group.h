@@ -62,11 +62,13 @@ void region_group_layout(void* ws, uint64_t n, uint64_t** rkeys, uint32_t** rfil
 // cursor: the set's REGION_SET_WORDS counters (sd_mix.h); d_objects: 2 u64 (count, overflow
 // carve cursor; K1G zeroed both); spill_keys/spill_file: the rows K1G could not store in
 // their region; keys/n: the batch's key array, read only if a full region's distinct keys
-// overflow its LDS table
+// overflow its LDS table; fill_limit: 0, or (tests) a lower distinct-key bound for the LDS
+// tables so their overflow paths run
 hipError_t region_group_min(const uint64_t* rkeys, const uint32_t* rfile, uint32_t* cursor,
                             uint64_t cap, uint32_t* out, uint64_t* d_objects, uint64_t* gkeys,
                             uint32_t* gvals, const uint64_t* keys, uint64_t n,
-                            const uint64_t* spill_keys, const uint32_t* spill_file, hipStream_t stream);
+                            const uint64_t* spill_keys, const uint32_t* spill_file,
+                            uint32_t fill_limit, hipStream_t stream);
 // Key-range partition: part(k) = floor(k * parts / 2^64); out_keys/out_pos hold the keys and
 // their input positions part-contiguous (order inside a part unspecified), d_counts[p] the
 // part sizes.  ws: partition_workspace_bytes(n, parts).

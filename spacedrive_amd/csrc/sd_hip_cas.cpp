@@ -118,6 +118,11 @@ int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
   {
     const char* t = getenv("SD_CAS_TRACE");
     c->trace = t && *t && strcmp(t, "0") != 0;
+    // test knob: a lower distinct-key bound for the fused chain's region tables, so that the
+    // tables' overflow paths (a region's own global table, and a full region's regroup from
+    // the whole key array) run on K1G output — uniform BLAKE3 keys never reach the real bound
+    const char* f = getenv("SD_CAS_TEST_TABLE_FILL");
+    c->test_table_fill = f && *f ? (uint32_t)strtoul(f, nullptr, 10) : 0u;
   }
   sd_cas_set_latency_threshold(c, SD_CAS_THRESHOLD_DEFAULT, SD_CAS_THRESHOLD_DEFAULT);
   sd_cas_set_chunkpar_split(c, SD_CAS_THRESHOLD_DEFAULT, SD_CAS_THRESHOLD_DEFAULT);
@@ -430,7 +435,7 @@ int sd_cas_group_regions_dev(sd_cas_ctx* c, size_t n, uint32_t* d_rep, uint64_t*
   uint32_t* cur = c->gcursor + REGION_SET_WORDS * k;
   HIP_TRY(c, hipStreamWaitEvent(s, c->region_hashed[k], 0));  // after its K1G, whatever stream
   hipError_t e = region_group_min(rkeys, rfile, cur, region_capacity(n), d_rep, obj, gkeys, gvals,
-                                  c->region_keys[k], n, skeys, sfile, s);
+                                  c->region_keys[k], n, skeys, sfile, c->test_table_fill, s);
   if (e != hipSuccess) {
     (void)hipMemsetAsync(cur, 0, REGION_SET_WORDS * 4, s);
     return fail(c, SD_CAS_EHIP, "group_regions: %s", hipGetErrorString(e));

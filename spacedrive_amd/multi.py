@@ -11,6 +11,7 @@ import numpy as np
 
 from . import _native
 from ._native import CasError
+from .cas import _sizes_u64
 
 
 class MultiEngine:
@@ -60,7 +61,7 @@ class MultiEngine:
 
     def hash_group_sampled_host(self, content: np.ndarray, sizes: np.ndarray, stride: int = 57344):
         n = len(sizes)
-        sz = np.ascontiguousarray(sizes, dtype=np.uint64)
+        sz = _sizes_u64(sizes)
         keys = np.zeros(n, dtype=np.uint64)
         rep = np.zeros(n, dtype=np.uint64)
         obj = ctypes.c_uint64(0)

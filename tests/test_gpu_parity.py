@@ -591,8 +591,9 @@ def test_hash_group_fused_overflow_and_fallback(eng, oracle, hot):
     """Coarse buckets outgrowing their fixed regions (files copied thousands of times in a
     batch of one quantum: region capacity ~450 rows): the flag is raised and the grouping is
     still exact — the async call's rep and Object count (copy_objects) equal the standalone
-    grouping's with no caller regroup (each overflowed region is regrouped from the whole key
-    array by its table workgroup; several hot keys carve several global tables).  A batch that
+    grouping's with no caller regroup (each full region's table workgroup reads the region's
+    rows and then its rows on the set's spill list into the same LDS table; the whole-key-array
+    regroup behind it is forced in test_hash_group_fused_table_overflow_paths).  A batch that
     is not a multiple of the quantum runs K1 + the standalone chain (flag untouched)."""
     q = eng.batch_quantum
     for n in ([q, q + 1000] if not hot else [q]):
@@ -633,6 +634,50 @@ def test_hash_group_fused_overflow_and_fallback(eng, oracle, hot):
         torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("hot", [[20_000], [9_000, 7_000, 5_000], []])
+def test_hash_group_fused_table_overflow_paths(eng, oracle, monkeypatch, hot):
+    """the fused chain's table overflow paths, which uniform BLAKE3 keys never
+    reach (a region holds ~5,100 distinct keys at 1.31 M files against a 10,752 bound, and K1G
+    keys cannot be crafted): a context created with SD_CAS_TEST_TABLE_FILL=200 sends every
+    region with more than 200 distinct keys to its own global table, and a FULL region (hot
+    files copied thousands of times: its rows + spill list) to the regroup from the whole key
+    array in a global table carved from the set's overflow slots — several hot files carve
+    several tables, and K1G's keys must stay alive until the tables finish.  rep and Objects
+    == the standalone grouping and the oracle, over both region sets."""
+    from spacedrive_amd import CasEngine
+    monkeypatch.setenv("SD_CAS_TEST_TABLE_FILL", "200")
+    e2 = CasEngine(0)
+    q = eng.batch_quantum
+    n = q
+    content = torch.empty((n, SAMPLED_CONTENT_LEN), dtype=torch.uint8, device="cuda")
+    sizes = torch.empty(n, dtype=torch.int64, device="cuda")
+    eng.synth_sampled(72, 0, n, content, sizes, SAMPLED_CONTENT_LEN, dup_permille=100)
+    for h, copies in enumerate(hot):
+        idx = torch.from_numpy(np.random.default_rng(10 + h).choice(
+            np.setdiff1d(np.arange(n), [40_000 + j for j in range(len(hot))]), copies,
+            replace=False)).cuda()
+        content[idx] = content[40_000 + h].clone()
+        sizes[idx] = sizes[40_000 + h].clone()
+    keys = torch.empty(n, dtype=torch.int64, device="cuda")
+    rep = torch.empty(n, dtype=torch.int32, device="cuda")
+    eng.hash_sampled(content, sizes, keys)
+    objects = eng.group(keys, rep)
+    orep, oobj = oracle.group_canonical(keys.cpu().numpy().view(np.uint64))
+    assert oobj == objects and (rep.cpu().numpy().astype(np.uint32) == orep).all()
+    for rnd in range(3):  # the two region sets alternate
+        keys2 = torch.empty(n, dtype=torch.int64, device="cuda")
+        rep2 = torch.empty(n, dtype=torch.int32, device="cuda")
+        ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        got = e2.hash_group_sampled(content, sizes, keys2, rep2, ovf)
+        assert torch.equal(keys, keys2), rnd
+        assert got == objects and torch.equal(rep, rep2), rnd
+        assert int(ovf.item()) == (1 if hot else 0)
+    e2.close()
+    del content
+    torch.cuda.empty_cache()
+
+
 def test_hash_regions_streams_and_ungrouped(eng):
     """K1G batches on two streams with one batch hashed but never grouped — the
     next hash_regions into its set waits for that K1G (no cursor or row corruption), tables on
@@ -653,7 +698,10 @@ def test_hash_regions_streams_and_ungrouped(eng):
     reps = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(5)]
     obj = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(5)]
     late = torch.zeros(1, dtype=torch.int64, device="cuda")
-    # (torch's zero fills run on its own stream: done before our streams write the tensors)
+    # torch's zero fills run on its current stream, not on s1/s2/s3: they must be complete
+    # before the library writes these tensors on those streams — the caller-side ordering rule
+    # of include/sd_hip_cas.h's conventions and INTEGRATION.md §1 (round 4's failure of this
+    # test was exactly a missing synchronize here)
     torch.cuda.synchronize()
     # batch 0 on s1 (grouped on s3), batch 1 on s2 never grouped, batch 2 on s1 refills set 0,
     # batch 3 on s2 refills batch 1's set while its K1G may still run; batch 4 grouped last
