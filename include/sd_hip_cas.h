@@ -398,8 +398,10 @@ int sd_cas_identifier_links_seeded(sd_cas_ctx* ctx, const uint64_t* h_keys, cons
  * one (mod.rs:248-253) and an ERROR row keeps its Object, stays orphan and is DROPPED; for
  * both d_object says what the job did (i / SD_CAS_NO_OBJECT), not the untouched column.
  * Ids >= 2^31 other than SD_CAS_NO_OBJECT, in seeds or pre_objects, fail with SD_CAS_EINVAL
- * (the device call checks them on the device).  Costs one stable 64-bit sort of the n keys
- * plus two linear scans over them when pre_objects != NULL.  n < 2^31. */
+ * (the device call checks them on the device).  pre_objects != NULL costs one pass over the
+ * rows' states and Objects, then work on the EVENTS only — the hashed rows holding an Object:
+ * a stable sort of their keys, two segmented-min scans, and per hashed row a lookup of its
+ * key (a 1 MiB key bitmap, then a binary search).  n < 2^31. */
 int sd_cas_identifier_links_ex_dev(sd_cas_ctx* ctx, const uint64_t* d_keys, const uint8_t* d_state,
                                    size_t n, uint32_t chunk, const uint64_t* d_seed_keys,
                                    const uint32_t* d_seed_objects, size_t n_seed,

@@ -97,15 +97,55 @@ __device__ __forceinline__ uint32_t step_of(const uint32_t* starts, uint32_t nst
   return lo;
 }
 
+// The same for a wave of consecutive rows: one binary search for the wave's first row
+// (wave-uniform: scalar loads), then each lane walks forward over the few step starts inside
+// its 64-row span.  A search per lane — 17 dependent loads at 100 K steps — was most of the
+// decision kernel's time at 10 M rows.
+__device__ __forceinline__ uint32_t wave_step_of(const uint32_t* starts, uint32_t nsteps,
+                                                 uint32_t i0, uint32_t i) {
+  uint32_t k = step_of(starts, nsteps, __builtin_amdgcn_readfirstlane(i0));
+  while (starts[k + 1] <= i) ++k;  // starts[nsteps] = sentinel
+  return k;
+}
+
+// Rows that already own an Object (sd_links_pre_*, below): the event list sorted by (key,
+// row) — ekeys / erows — and T[j] = the smallest pre-existing Object over the key's events in
+// steps up to event j's; a row's own value is T at its key's last event with row < bound
+// (the first row of the next step), found by one binary search over (key, row) order.
+struct PreEvents {
+  const uint64_t* ekeys;
+  const uint32_t* erows;
+  const uint64_t* T;       // scan elements: low 32 bits
+  const uint32_t* filter;  // bitmap of mix(key) over the events' keys (FILTER_BITS bits)
+  uint64_t m;
+};
+constexpr uint32_t FILTER_BITS = 23;  // 1 MiB: ~1 % false positives at 100 K events
+__device__ __forceinline__ uint32_t filter_bit(uint64_t key) {
+  uint64_t z = key * 0x9E3779B97F4A7C15ull;
+  return (uint32_t)(z >> (64 - FILTER_BITS));
+}
+__device__ __forceinline__ uint32_t pre_min_of(const PreEvents& ev, uint64_t key, uint32_t bound) {
+  const uint32_t bit = filter_bit(key);
+  if (!((ev.filter[bit >> 5] >> (bit & 31u)) & 1u)) return 0xFFFFFFFFu;
+  uint64_t lo = 0, hi = ev.m;  // first element not < (key, bound)
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    const uint64_t k = ev.ekeys[mid];
+    if (k < key || (k == key && ev.erows[mid] < bound)) lo = mid + 1; else hi = mid;
+  }
+  return lo > 0 && ev.ekeys[lo - 1] == key ? (uint32_t)ev.T[lo - 1] : 0xFFFFFFFFu;
+}
+
 // Per-row decision (mod.rs:202-347 replayed with HashMap order := ascending row):
 //   hashed, key held by an Object that existed before the job (seeded: rep < ROW_FLAG is the
-//           lowest such Object id; premin: the lowest pre-existing Object of a row with the
-//           key in this step or an earlier one, sd_links_pre_*): EXISTING — the step's
-//           find_many returns it (:180-198, no location filter), find() picks the first
-//           Object in id order (:214-224) and the key never creates (:246-253);
+//           lowest such Object id; ev: the lowest pre-existing Object of a row with the key in
+//           this step or an earlier one, sd_links_pre_*): EXISTING — the step's find_many
+//           returns it (:180-198, no location filter), find() picks the first Object in id
+//           order (:214-224) and the key never creates (:246-253);
 //   hashed: CREATED iff its key's first row (rep) is in the same step — no intra-step dedup,
 //           mod.rs:246-311 — else LINKED to the Object of rep (find() = the lowest Object
-//           id, created for the key's lowest row, :214-224);
+//           id, created for the key's lowest row, :214-224).  The first row r <= i is a hashed
+//           row, never a re-queried one, so it shares i's step iff r >= starts[step];
 //   no cas_id (empty): CREATED, its own Object (:248-253);
 //   error: DROPPED (:125-141);  rows past the last step: NOT_REACHED.
 // counts[2k] / counts[2k+1] += created / linked rows whose final step is k.
@@ -114,13 +154,18 @@ sd_links_decide(const uint8_t* __restrict__ state, const uint32_t* __restrict__ 
                 const uint32_t* __restrict__ starts, uint32_t nsteps, uint64_t reached,
                 uint32_t* __restrict__ step_out, uint32_t* __restrict__ object_out,
                 uint8_t* __restrict__ action_out, unsigned int* __restrict__ counts, bool seeded,
-                const uint32_t* __restrict__ premin) {
+                const uint64_t* __restrict__ keys, PreEvents ev) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i0 = i - (threadIdx.x & 63u);  // the wave's first row
   uint32_t step = SD_LINKS_NO_STEP, object = SD_LINKS_NO_OBJECT;
   uint8_t action = SD_LINKS_NOT_REACHED;
-  if (i < n && i < reached) {
+  if (i0 < n && i0 < reached) {  // (uniform) rows of a wave straddling `reached` search too
+    const uint32_t k = wave_step_of(starts, nsteps, (uint32_t)i0,
+                                    (uint32_t)(i < reached ? i : reached - 1));
+    if (i < n && i < reached) step = k;
+  }
+  if (step != SD_LINKS_NO_STEP) {
     const uint8_t st = state ? state[i] : (uint8_t)SD_LINKS_HASHED;
-    step = step_of(starts, nsteps, (uint32_t)i);
     if (st == SD_LINKS_ERROR) {
       action = SD_LINKS_DROPPED;
     } else if (st == SD_LINKS_NO_CAS) {
@@ -129,11 +174,14 @@ sd_links_decide(const uint8_t* __restrict__ state, const uint32_t* __restrict__ 
     } else {
       uint32_t v = rep[i];
       const uint32_t r = seeded ? v & ~LINKS_ROW_FLAG : v;  // the key's first row
-      if (premin) v = min(v, premin[i]);  // a pre-existing Object its step or an earlier one saw
+      if (ev.m) {  // a pre-existing Object its step or an earlier one saw
+        const uint32_t bound = step + 1 < nsteps ? starts[step + 1] : 0xFFFFFFFFu;
+        v = min(v, pre_min_of(ev, keys[i], bound));
+      }
       if (seeded && v < LINKS_ROW_FLAG) {
         action = SD_LINKS_EXISTING;
         object = v;
-      } else if (r == (uint32_t)i || step_of(starts, nsteps, r) == step) {
+      } else if (r == (uint32_t)i || r >= starts[step]) {
         action = SD_LINKS_CREATED;
         object = (uint32_t)i;
       } else {
@@ -176,11 +224,16 @@ sd_links_decide(const uint8_t* __restrict__ state, const uint32_t* __restrict__ 
 // never creates (:214-224, :246-253).  A later step still sees P when it won (its row stays
 // connected to it); when a smaller Object won, P lost the row — but then the smaller one
 // stays, so what each row needs is the smallest P over the key's rows in its own or an
-// earlier step: a segmented prefix minimum over the rows sorted by (key, row), cut at the
-// end of the row's (key, step) run.  Two linear scans over the sorted rows give it:
-//   forward,  segments = keys:          F[j] = min P over the key's rows up to j;
-//   backward, segments = (key, step) run ends:  G[j] = F[end of j's run].
-// Scan element: bit 63 = segment start, low 32 bits = value (0xFFFFFFFF = no Object).
+// earlier step.  Only those rows' events matter, and they are few (a create-then-write is
+// the exception, not the rule), so the work is on the EVENT list (hashed, reached rows with
+// an Object), not on every row:
+//   1. ordered compaction of the events: (key, row), row order kept (count / scan / emit);
+//   2. a stable sort of the events by key (sd_cas_sort_pairs_dev): (key, row) order;
+//   3. forward segmented min over the events, segments = keys:   F[j] = min P up to j;
+//      backward, segments = (key, step) run ends:  T[j] = F[end of j's run]
+//      (scan element: bit 63 = segment start, low 32 bits = value, 0xFFFFFFFF = none);
+//   4. each hashed row looks its key up (a 1 MiB bitmap of the events' keys first, then one
+//      binary search over (key, row) order) in the decision kernel above.
 constexpr uint64_t SEG_START = 1ull << 63;
 constexpr uint64_t SEG_NONE = 0xFFFFFFFFull;  // the identity: no start, no Object
 __device__ __forceinline__ uint64_t segmin(uint64_t a, uint64_t b) {
@@ -207,50 +260,135 @@ sd_links_check_ids(const uint32_t* __restrict__ ids, uint64_t n, uint32_t none_o
   if (__ballot(b) && (threadIdx.x & 63u) == 0) atomicAdd(bad, 1ull);
 }
 
-// Element j of the sorted rows (skeys ascending, srows ascending inside a key): value = the
-// row's pre-existing Object when it is hashed in a reached step, start = first row of its key.
+// 1. ordered compaction of the events.  A workgroup takes EV_ROWS rows; count: its events
+// (ballots); the block counts' exclusive scan (one workgroup); emit: the events in row order
+// at the block's offset, and each event key's bit in the filter.
+constexpr int EV_THREADS = 1024, EV_ITEMS = 16;
+constexpr uint64_t EV_ROWS = (uint64_t)EV_THREADS * EV_ITEMS;
+__device__ __forceinline__ bool is_event(const uint8_t* state, const uint32_t* pre, uint64_t i,
+                                         uint64_t reached) {
+  return i < reached && (!state || state[i] == SD_LINKS_HASHED) && pre[i] != SD_LINKS_NO_OBJECT;
+}
+
+extern "C" __global__ void __launch_bounds__(EV_THREADS)
+sd_links_pre_count(const uint8_t* __restrict__ state, const uint32_t* __restrict__ pre,
+                   uint64_t reached, uint32_t* __restrict__ bcount) {
+  __shared__ uint32_t wsum[EV_THREADS / 64];
+  uint32_t c = 0;
+  for (int u = 0; u < EV_ITEMS; ++u) {
+    const uint64_t i = blockIdx.x * EV_ROWS + (uint64_t)u * EV_THREADS + threadIdx.x;
+    c += (uint32_t)__popcll(__ballot(is_event(state, pre, i, reached)));
+  }
+  if ((threadIdx.x & 63u) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < EV_THREADS / 64; ++w) t += wsum[w];
+    bcount[blockIdx.x] = t;
+  }
+}
+
+// one workgroup: bcount[b] := sum of bcount[0..b) in place, total -> *total
+extern "C" __global__ void __launch_bounds__(256)
+sd_links_pre_bscan(uint32_t* __restrict__ bcount, uint64_t nb, unsigned long long* __restrict__ total) {
+  __shared__ uint32_t wsum[4];
+  uint64_t carry = 0;
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  for (uint64_t base = 0; base < nb; base += 256) {
+    const uint64_t b = base + threadIdx.x;
+    const uint32_t x = b < nb ? bcount[b] : 0u;
+    uint32_t inc = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(inc, d, 64);
+      if (lane >= (uint32_t)d) inc += y;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+    for (uint32_t k = 0; k < 4; ++k) {
+      if (k < w) before += wsum[k];
+      all += wsum[k];
+    }
+    if (b < nb) bcount[b] = (uint32_t)(carry + before + inc - x);
+    carry += all;
+    __syncthreads();  // wsum is rewritten by the next round
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+
+extern "C" __global__ void __launch_bounds__(EV_THREADS)
+sd_links_pre_emit(const uint64_t* __restrict__ keys, const uint8_t* __restrict__ state,
+                  const uint32_t* __restrict__ pre, uint64_t reached,
+                  const uint32_t* __restrict__ boff, uint64_t* __restrict__ ekeys,
+                  uint32_t* __restrict__ erows, uint32_t* __restrict__ filter) {
+  __shared__ uint32_t wbase[EV_ITEMS][EV_THREADS / 64];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint64_t below = (1ull << lane) - 1ull;
+  uint64_t m[EV_ITEMS];
+  for (int u = 0; u < EV_ITEMS; ++u) {
+    const uint64_t i = blockIdx.x * EV_ROWS + (uint64_t)u * EV_THREADS + threadIdx.x;
+    m[u] = __ballot(is_event(state, pre, i, reached));
+    if (lane == 0) wbase[u][w] = (uint32_t)__popcll(m[u]);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // row order = (u, wave) order: exclusive prefix in place
+    uint32_t t = boff[blockIdx.x];
+    for (int u = 0; u < EV_ITEMS; ++u)
+      for (int k = 0; k < EV_THREADS / 64; ++k) {
+        const uint32_t c = wbase[u][k];
+        wbase[u][k] = t;
+        t += c;
+      }
+  }
+  __syncthreads();
+  for (int u = 0; u < EV_ITEMS; ++u) {
+    if (!((m[u] >> lane) & 1ull)) continue;
+    const uint64_t i = blockIdx.x * EV_ROWS + (uint64_t)u * EV_THREADS + threadIdx.x;
+    const uint32_t d = wbase[u][w] + (uint32_t)__popcll(m[u] & below);
+    const uint64_t k = keys[i];
+    ekeys[d] = k;
+    erows[d] = (uint32_t)i;
+    const uint32_t bit = filter_bit(k);
+    atomicOr(&filter[bit >> 5], 1u << (bit & 31u));
+  }
+}
+
+// 3. over the m sorted events (skeys, srows): value = the row's Object, start = first event
+// of its key
 extern "C" __global__ void __launch_bounds__(256)
 sd_links_pre_mark(const uint64_t* __restrict__ skeys, const uint32_t* __restrict__ srows,
-                  const uint8_t* __restrict__ state, const uint32_t* __restrict__ pre, uint64_t n,
-                  uint64_t reached, uint64_t* __restrict__ elem) {
+                  const uint32_t* __restrict__ pre, uint64_t m, uint64_t* __restrict__ elem) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
-  const uint32_t r = srows[j];
-  const bool hashed = r < reached && (!state || state[r] == SD_LINKS_HASHED);
-  const uint64_t v = hashed ? (uint64_t)pre[r] : SEG_NONE;  // pre[r] may itself be NO_OBJECT
-  elem[j] = (j == 0 || skeys[j] != skeys[j - 1] ? SEG_START : 0ull) | v;
+  if (j >= m) return;
+  elem[j] = (j == 0 || skeys[j] != skeys[j - 1] ? SEG_START : 0ull) | (uint64_t)pre[srows[j]];
 }
 
 // F -> the backward scan's input, in place: a (key, step) run's last element carries F as a
-// segment start, every other element the identity.
+// segment start, every other element the identity
 extern "C" __global__ void __launch_bounds__(256)
 sd_links_pre_runs(const uint64_t* __restrict__ skeys, const uint32_t* __restrict__ srows,
-                  const uint32_t* __restrict__ starts, uint32_t nsteps, uint64_t n,
+                  const uint32_t* __restrict__ starts, uint32_t nsteps, uint64_t m,
                   uint64_t* __restrict__ elem) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
-  bool end = j + 1 == n || skeys[j] != skeys[j + 1];
-  if (!end) end = step_of(starts, nsteps, srows[j]) != step_of(starts, nsteps, srows[j + 1]);
+  if (j >= m) return;
+  bool end = j + 1 == m || skeys[j] != skeys[j + 1];
+  if (!end) {  // the next event of the key is in a later step iff it is past this step's end
+    const uint32_t k = step_of(starts, nsteps, srows[j]);
+    end = k + 1 < nsteps && srows[j + 1] >= starts[k + 1];
+  }
   elem[j] = end ? (SEG_START | (elem[j] & SEG_NONE)) : SEG_NONE;
-}
-
-extern "C" __global__ void __launch_bounds__(256)
-sd_links_pre_scatter(const uint32_t* __restrict__ srows, const uint64_t* __restrict__ elem,
-                     uint64_t n, uint32_t* __restrict__ premin) {
-  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j < n) premin[srows[j]] = (uint32_t)elem[j];
 }
 
 // Device-wide inclusive segmented-min scan in three launches (reduce-then-scan): each
 // workgroup scans a tile of SCAN_TILE elements and leaves the tile's total; one workgroup
 // scans the totals (exclusive); every tile but the first folds its prefix in.  `reverse`
-// scans from the last element to the first (logical k = physical n-1-k).  Bytes per element:
-// 8 R + 8 W (tiles) + 8 R + 8 W (fix-up) — the rows of one job, a few ms at 10 M rows.
+// scans from the last element to the first (logical k = physical n-1-k).
 constexpr int SCAN_THREADS = 256, SCAN_ITEMS = 8;
 constexpr uint64_t SCAN_TILE = (uint64_t)SCAN_THREADS * SCAN_ITEMS;
 
-// inclusive workgroup scan of one value per thread; returns the thread's EXCLUSIVE prefix and
-// (in *total) the workgroup's total
+// workgroup scan of one value per thread: returns the thread's EXCLUSIVE prefix and (in
+// *total) the workgroup's total; the closing barrier lets the caller reuse wsum
 __device__ __forceinline__ uint64_t block_segmin_excl(uint64_t x, uint64_t* wsum, uint64_t* total) {
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   uint64_t inc = x;
@@ -269,7 +407,7 @@ __device__ __forceinline__ uint64_t block_segmin_excl(uint64_t x, uint64_t* wsum
   const uint64_t prev = shfl_up64(inc, 1);
   if (lane) excl = segmin(excl, prev);
   *total = all;
-  __syncthreads();  // wsum may be reused by the caller's next round
+  __syncthreads();
   return excl;
 }
 
@@ -334,6 +472,8 @@ hipError_t segmin_scan(uint64_t* data, uint64_t n, bool reverse, uint64_t* tiles
 }
 
 size_t segmin_tiles_bytes(uint64_t n) { return ((n + SCAN_TILE - 1) / SCAN_TILE + 1) * 8; }
+size_t pre_blocks(uint64_t n) { return (n + EV_ROWS - 1) / EV_ROWS; }
+size_t pre_filter_bytes() { return ((size_t)1 << FILTER_BITS) / 8; }
 
 hipError_t links_check_ids(const uint32_t* ids, uint64_t n, bool none_ok, uint64_t* d_bad,
                            hipStream_t s) {
@@ -343,19 +483,35 @@ hipError_t links_check_ids(const uint32_t* ids, uint64_t n, bool none_ok, uint64
   return hipGetLastError();
 }
 
-hipError_t links_pre_min(const uint64_t* skeys, const uint32_t* srows, const uint8_t* state,
-                         const uint32_t* pre, uint64_t n, uint64_t reached, const uint32_t* starts,
-                         uint32_t nsteps, uint64_t* elem, uint64_t* tiles, uint32_t* premin,
-                         hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  const uint32_t g = (uint32_t)((n + 255) / 256);
-  sd_links_pre_mark<<<g, 256, 0, s>>>(skeys, srows, state, pre, n, reached, elem);
-  hipError_t e = segmin_scan(elem, n, false, tiles, s);
-  if (e != hipSuccess) return e;
-  sd_links_pre_runs<<<g, 256, 0, s>>>(skeys, srows, starts, nsteps, n, elem);
-  if ((e = segmin_scan(elem, n, true, tiles, s)) != hipSuccess) return e;
-  sd_links_pre_scatter<<<g, 256, 0, s>>>(srows, elem, n, premin);
+hipError_t links_pre_count(const uint8_t* state, const uint32_t* pre, uint64_t reached,
+                           uint32_t* bcount, uint64_t* d_total, hipStream_t s) {
+  const uint64_t nb = pre_blocks(reached);
+  if (nb == 0) return hipMemsetAsync(d_total, 0, 8, s);
+  sd_links_pre_count<<<(uint32_t)nb, EV_THREADS, 0, s>>>(state, pre, reached, bcount);
+  sd_links_pre_bscan<<<1, 256, 0, s>>>(bcount, nb, (unsigned long long*)d_total);
   return hipGetLastError();
+}
+
+hipError_t links_pre_emit(const uint64_t* keys, const uint8_t* state, const uint32_t* pre,
+                          uint64_t reached, const uint32_t* boff, uint64_t* ekeys,
+                          uint32_t* erows, uint32_t* filter, hipStream_t s) {
+  const uint64_t nb = pre_blocks(reached);
+  if (nb == 0) return hipSuccess;
+  sd_links_pre_emit<<<(uint32_t)nb, EV_THREADS, 0, s>>>(keys, state, pre, reached, boff, ekeys,
+                                                        erows, filter);
+  return hipGetLastError();
+}
+
+hipError_t links_pre_scan(const uint64_t* skeys, const uint32_t* srows, const uint32_t* pre,
+                          uint64_t m, const uint32_t* starts, uint32_t nsteps, uint64_t* elem,
+                          uint64_t* tiles, hipStream_t s) {
+  if (m == 0) return hipSuccess;
+  const uint32_t g = (uint32_t)((m + 255) / 256);
+  sd_links_pre_mark<<<g, 256, 0, s>>>(skeys, srows, pre, m, elem);
+  hipError_t e = segmin_scan(elem, m, false, tiles, s);
+  if (e != hipSuccess) return e;
+  sd_links_pre_runs<<<g, 256, 0, s>>>(skeys, srows, starts, nsteps, m, elem);
+  return segmin_scan(elem, m, true, tiles, s);
 }
 
 hipError_t links_split(const uint64_t* keys, const uint8_t* state, uint64_t n, uint64_t* hkeys,
@@ -378,11 +534,14 @@ hipError_t links_scatter(const uint32_t* minrow, const uint32_t* hrows, uint64_t
 hipError_t links_decide(const uint8_t* state, const uint32_t* rep, uint64_t n,
                         const uint32_t* starts, uint32_t nsteps, uint64_t reached,
                         uint32_t* step_out, uint32_t* object_out, uint8_t* action_out,
-                        uint32_t* counts, bool seeded, const uint32_t* premin, hipStream_t s) {
+                        uint32_t* counts, bool seeded, const uint64_t* keys,
+                        const uint64_t* ekeys, const uint32_t* erows, const uint64_t* T,
+                        const uint32_t* filter, uint64_t m, hipStream_t s) {
   if (n == 0) return hipSuccess;
+  PreEvents ev{ekeys, erows, T, filter, m};
   sd_links_decide<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(
       state, rep, n, starts, nsteps, reached, step_out, object_out, action_out, counts, seeded,
-      premin);
+      keys, ev);
   return hipGetLastError();
 }
 

@@ -592,14 +592,18 @@ int sd_cas_identifier_links_ex_dev(sd_cas_ctx* c, const uint64_t* d_keys, const 
   if (n == 0) return SD_CAS_OK;
   hipStream_t s = pick(c, stream);
   // staging (this call is blocking): rep | hkeys | hrows | minrow | orphans | starts | counts |
-  // scan tiles | 3 counters; the seeded grouping runs over the hashed rows + the existing
-  // Objects' keys.  Rows with pre-existing Objects reuse hkeys / hrows / orphans / minrow once
-  // the grouping is done: sorted keys / sorted rows / scan elements / per-row minimum
+  // [event block offsets | scan tiles | key filter] | 4 counters; the seeded grouping runs over
+  // the hashed rows + the existing Objects' keys.  Rows with pre-existing Objects reuse the
+  // grouping's buffers once it is done: events (hkeys / hrows), sorted events (orphans /
+  // minrow), scan elements (hkeys)
   const size_t m = n + n_seed;
   const size_t b_rep = up256(n * 4), b_hk = up256(m * 8), b_hr = up256(m * 4), b_mr = up256(m * 4),
                b_or = up256(n * 8), b_st = up256((steps_total + 1) * 4), b_ct = up256(steps_total * 8),
-               b_tl = d_pre_objects ? up256(segmin_tiles_bytes(n)) : 0;
-  int rc = ensure(c, c->staging, b_rep + b_hk + b_hr + b_mr + b_or + b_st + b_ct + b_tl + 256);
+               b_bo = d_pre_objects ? up256(pre_blocks(n) * 4) : 0,
+               b_tl = d_pre_objects ? up256(segmin_tiles_bytes(n)) : 0,
+               b_fl = d_pre_objects ? up256(pre_filter_bytes()) : 0;
+  int rc = ensure(c, c->staging,
+                  b_rep + b_hk + b_hr + b_mr + b_or + b_st + b_ct + b_bo + b_tl + b_fl + 256);
   if (rc) return rc;
   char* p = (char*)c->staging.p;
   uint32_t* rep = (uint32_t*)p; p += b_rep;
@@ -609,15 +613,18 @@ int sd_cas_identifier_links_ex_dev(sd_cas_ctx* c, const uint64_t* d_keys, const 
   uint64_t* orphans = (uint64_t*)p; p += b_or;
   uint32_t* starts = (uint32_t*)p; p += b_st;
   uint32_t* counts = (uint32_t*)p; p += b_ct;
+  uint32_t* boff = (uint32_t*)p; p += b_bo;
   uint64_t* tiles = (uint64_t*)p; p += b_tl;
-  uint64_t* counters = (uint64_t*)p;  // hashed rows | orphan rows | waves with a bad Object id
+  uint32_t* filter = (uint32_t*)p; p += b_fl;
+  // hashed rows | orphan rows | waves with a bad Object id | events
+  uint64_t* counters = (uint64_t*)p;
   // 1. grouping over the hashed rows (rep = the key's first row; seeded: the lowest existing
   //    Object id when the key has one — mod.rs:180-198 finds Objects by cas over the whole
   //    library), and the rows that stay orphan after being processed (they steer the cursor)
   std::vector<uint64_t> stay;  // row << 8 | state, ascending
   if (d_state || seeded) {
     uint64_t cnt[3] = {0, 0, 0};
-    HIP_TRY(c, hipMemsetAsync(counters, 0, 24, s));
+    HIP_TRY(c, hipMemsetAsync(counters, 0, 32, s));
     HIP_TRY(c, links_check_ids(d_seed_objects, n_seed, false, counters + 2, s));
     if (d_pre_objects) HIP_TRY(c, links_check_ids(d_pre_objects, n, true, counters + 2, s));
     HIP_TRY(c, links_split(d_keys, d_state, n, hkeys, hrows, counters, orphans, counters + 1,
@@ -675,20 +682,29 @@ int sd_cas_identifier_links_ex_dev(sd_cas_ctx* c, const uint64_t* d_keys, const 
   const size_t nsteps = h_starts.size();
   h_starts.push_back(0xFFFFFFFFu);  // sentinel
   HIP_TRY(c, hipMemcpyAsync(starts, h_starts.data(), h_starts.size() * 4, hipMemcpyHostToDevice, s));
-  // 3. rows that already own an Object: per row, the smallest such Object of a row with its
-  //    key in its own step or an earlier one (links.hip, sd_links_pre_*) over every row sorted
-  //    by (key, row) — a stable sort of the keys with the identity as values
-  uint32_t* premin = nullptr;
+  // 3. rows that already own an Object (links.hip, sd_links_pre_*): the events — hashed rows
+  //    of the reached steps that hold an Object — compacted in row order, sorted stably by key,
+  //    and scanned; each hashed row then looks its key up in the decision kernel
+  uint64_t n_ev = 0;
   if (d_pre_objects) {
-    if ((rc = sd_cas_sort_pairs_dev(c, d_keys, nullptr, n, hkeys, hrows, 0, 64, s))) return rc;
-    premin = minrow;
-    HIP_TRY(c, links_pre_min(hkeys, hrows, d_state, d_pre_objects, n, reached, starts,
-                             (uint32_t)nsteps, orphans, tiles, premin, s));
+    HIP_TRY(c, links_pre_count(d_state, d_pre_objects, reached, boff, counters + 3, s));
+    HIP_TRY(c, hipMemcpyAsync(&n_ev, counters + 3, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+  }
+  if (n_ev) {
+    HIP_TRY(c, hipMemsetAsync(filter, 0, pre_filter_bytes(), s));
+    HIP_TRY(c, links_pre_emit(d_keys, d_state, d_pre_objects, reached, boff, hkeys, hrows, filter, s));
+    uint64_t* skeys = orphans;
+    uint32_t* srows = minrow;
+    if ((rc = sd_cas_sort_pairs_dev(c, hkeys, hrows, n_ev, skeys, srows, 0, 64, s))) return rc;
+    HIP_TRY(c, links_pre_scan(skeys, srows, d_pre_objects, n_ev, starts, (uint32_t)nsteps, hkeys,
+                              tiles, s));
   }
   // 4. per-row decisions + per-step counts (device)
   HIP_TRY(c, hipMemsetAsync(counts, 0, std::max<size_t>(nsteps, 1) * 8, s));
   HIP_TRY(c, links_decide(d_state, rep, n, starts, (uint32_t)nsteps, reached, d_step, d_object,
-                          d_action, counts, seeded, premin, s));
+                          d_action, counts, seeded, d_keys, orphans, minrow, hkeys, filter, n_ev,
+                          s));
   std::vector<uint32_t> hc(2 * std::max<size_t>(nsteps, 1));
   HIP_TRY(c, hipMemcpyAsync(hc.data(), counts, hc.size() * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));

@@ -33,23 +33,35 @@ hipError_t links_scatter(const uint32_t* minrow, const uint32_t* hrows, uint64_t
                          uint32_t row_flag, hipStream_t s);
 // per-row decisions; counts[2k], counts[2k+1] (u32, zeroed by the caller) += created, linked.
 // seeded: rep[i] < LINKS_ROW_FLAG is an existing Object's id, else LINKS_ROW_FLAG | first row;
-// premin (NULL: none; needs seeded) = links_pre_min's output
+// m > 0 (needs seeded): rows already owning an Object — the sorted event list of
+// links_pre_* (ekeys / erows, scan elements T, key filter) and every row's key (keys)
 hipError_t links_decide(const uint8_t* state, const uint32_t* rep, uint64_t n,
                         const uint32_t* starts, uint32_t nsteps, uint64_t reached,
                         uint32_t* step_out, uint32_t* object_out, uint8_t* action_out,
-                        uint32_t* counts, bool seeded, const uint32_t* premin, hipStream_t s);
+                        uint32_t* counts, bool seeded, const uint64_t* keys,
+                        const uint64_t* ekeys, const uint32_t* erows, const uint64_t* T,
+                        const uint32_t* filter, uint64_t m, hipStream_t s);
 // *d_bad (u64, zeroed by the caller) += 1 per wave holding an id >= LINKS_ROW_FLAG (none_ok:
 // SD_LINKS_NO_OBJECT allowed)
 hipError_t links_check_ids(const uint32_t* ids, uint64_t n, bool none_ok, uint64_t* d_bad,
                            hipStream_t s);
-// Rows that already own an Object (pre[r], SD_LINKS_NO_OBJECT = none): over the n rows sorted
-// by (key, row) (skeys / srows, the stable sort of every row's key), premin[r] = the smallest
-// pre[r'] over the hashed reached rows r' with r's key whose step is <= r's step (0xFFFFFFFF:
-// none).  elem: n u64 of scratch; tiles: segmin_tiles_bytes(n).
-hipError_t links_pre_min(const uint64_t* skeys, const uint32_t* srows, const uint8_t* state,
-                         const uint32_t* pre, uint64_t n, uint64_t reached, const uint32_t* starts,
-                         uint32_t nsteps, uint64_t* elem, uint64_t* tiles, uint32_t* premin,
-                         hipStream_t s);
+// Rows that already own an Object (pre[r], SD_LINKS_NO_OBJECT = none).  The events (hashed
+// rows r < reached with an Object): count -> bcount[pre_blocks(reached)] = the blocks' event
+// offsets, *d_total = the number of events (u64, device); emit -> ekeys / erows in row order
+// and their keys' bits in `filter` (pre_filter_bytes(), zeroed by the caller); after the
+// caller's stable sort of the events by key (skeys / srows), scan -> elem[j] (low 32 bits) =
+// the smallest Object over the key's events in steps up to event j's.  tiles:
+// segmin_tiles_bytes(m).
+size_t pre_blocks(uint64_t n);
+size_t pre_filter_bytes();
 size_t segmin_tiles_bytes(uint64_t n);
+hipError_t links_pre_count(const uint8_t* state, const uint32_t* pre, uint64_t reached,
+                           uint32_t* bcount, uint64_t* d_total, hipStream_t s);
+hipError_t links_pre_emit(const uint64_t* keys, const uint8_t* state, const uint32_t* pre,
+                          uint64_t reached, const uint32_t* boff, uint64_t* ekeys,
+                          uint32_t* erows, uint32_t* filter, hipStream_t s);
+hipError_t links_pre_scan(const uint64_t* skeys, const uint32_t* srows, const uint32_t* pre,
+                          uint64_t m, const uint32_t* starts, uint32_t nsteps, uint64_t* elem,
+                          uint64_t* tiles, hipStream_t s);
 
 }  // namespace sdcas
