@@ -49,6 +49,13 @@ void orc_stream_blake3_mt(uint64_t seed, uint64_t file, uint64_t len, int thread
 void orc_blake3_pieces(const uint8_t* const* pieces, const size_t* lens, size_t n,
                        uint8_t out[32]);
 
+/* Balloon hashing over BLAKE3 (balloon_ref.c): the reference's password-hash KATs,
+ * crates/crypto/src/keys/hashing.rs:180-208 — the multi-block streamed inputs that pin BLAKE3
+ * inside a chunk.  secret_len 0 = no secret.  Returns 0, or -1 on bad sizes / no memory. */
+int orc_balloon_blake3(const uint8_t* pwd, size_t pwd_len, const uint8_t* salt, size_t salt_len,
+                       const uint8_t* secret, size_t secret_len, uint64_t s_cost, uint64_t t_cost,
+                       uint8_t out[32]);
+
 /* ---- cas_id (core/src/object/cas.rs) ------------------------------------ */
 #define ORC_SAMPLE_COUNT 4ull
 #define ORC_SAMPLE_SIZE (1024ull * 10)

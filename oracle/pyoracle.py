@@ -333,6 +333,9 @@ class Oracle:
         L.orc_synth_root.restype = ctypes.c_uint64
         L.orc_synth_size.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]
         L.orc_synth_size.restype = ctypes.c_uint64
+        L.orc_balloon_blake3.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz, ctypes.c_char_p,
+                                         sz, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_char_p]
+        L.orc_balloon_blake3.restype = ctypes.c_int
         self.L = L
         _ = u8p
 
@@ -382,6 +385,17 @@ class Oracle:
     def derive_key(self, context: str, material: bytes) -> bytes:
         out = ctypes.create_string_buffer(32)
         self.L.orc_blake3_derive_key(context.encode(), material, len(material), out)
+        return out.raw
+
+    def balloon_blake3(self, password: bytes, salt: bytes, secret: bytes | None, s_cost: int,
+                       t_cost: int) -> bytes:
+        """Balloon::<blake3::Hasher> (balloon_ref.c), the reference's password hash
+        (crates/crypto/src/keys/hashing.rs:95-114): its KATs pin multi-block BLAKE3."""
+        out = ctypes.create_string_buffer(32)
+        rc = self.L.orc_balloon_blake3(password, len(password), salt, len(salt), secret,
+                                       len(secret or b""), s_cost, t_cost, out)
+        if rc:
+            raise ValueError("balloon: bad sizes")
         return out.raw
 
     # -- cas -----------------------------------------------------------------

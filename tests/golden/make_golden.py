@@ -230,6 +230,29 @@ def main() -> None:
     assert o.derive_key(ctx, material) == expected == py_derive_key(ctx, material)
     out["derive_key_kat"] = {"context": ctx, "material_hex": material.hex(), "expected_hex": expected.hex(),
                              "source": "crates/crypto/src/keys/hashing.rs:210-213,323-328"}
+    # the reference's Balloon-BLAKE3 password-hash KATs (hashing.rs:58-65 params, :130
+    # password, :138-141 salt, :143-146 secret, :180-208 expected; tests :269-321): reproduced
+    # by oracle/balloon_ref.c, they pin BLAKE3 on streamed multi-block inputs
+    balloon = {"password_hex": b"password".hex(), "salt_hex": "ff" * 16, "secret_hex": "55" * 18,
+               "t_cost": 2, "p_cost": 1, "source": "crates/crypto/src/keys/hashing.rs:58-65,130-146,180-208",
+               "vectors": []}
+    b3b = [bytes([105, 36, 165, 219, 22, 136, 156, 19, 32, 143, 237, 150, 236, 194, 70, 113, 73, 137,
+                  243, 106, 80, 31, 43, 73, 207, 210, 29, 251, 88, 6, 132, 77]),
+           bytes([179, 71, 60, 122, 54, 72, 132, 209, 146, 96, 15, 115, 41, 95, 5, 75, 214, 135, 6, 122,
+                  82, 42, 158, 9, 117, 19, 19, 40, 48, 233, 207, 237]),
+           bytes([233, 60, 62, 184, 29, 152, 111, 46, 239, 126, 98, 90, 211, 255, 151, 0, 10, 189, 61,
+                  84, 229, 11, 245, 228, 47, 114, 87, 74, 227, 67, 24, 141])]
+    b3bs = [bytes([188, 0, 43, 39, 137, 199, 91, 142, 97, 31, 98, 6, 130, 75, 251, 71, 150, 109, 29, 62,
+                   237, 171, 210, 22, 139, 108, 94, 190, 91, 74, 134, 47]),
+            bytes([19, 247, 102, 192, 129, 184, 29, 147, 68, 215, 234, 146, 153, 221, 65, 134, 68, 120,
+                   207, 209, 184, 246, 127, 131, 9, 245, 91, 250, 220, 61, 76, 248]),
+            bytes([165, 240, 162, 25, 172, 3, 232, 2, 43, 230, 226, 128, 174, 28, 211, 61, 139, 136, 221,
+                   197, 16, 83, 221, 18, 212, 190, 138, 79, 239, 148, 89, 215])]
+    for k, s_cost in enumerate((131_072, 262_144, 524_288)):
+        for sec, want in ((None, b3b[k]), (b"\x55" * 18, b3bs[k])):
+            assert o.balloon_blake3(b"password", b"\xff" * 16, sec, s_cost, 2) == want, (s_cost, sec)
+            balloon["vectors"].append({"s_cost": s_cost, "secret": sec is not None, "expected_hex": want.hex()})
+    out["balloon_b3_kat"] = balloon
     pub = {"": "af1349b9f5f9a1a6a0404dea36dcc9499bcb25c9adc112b7cc9a93cae41f3262",
            "abc": "6437b3ac38465133ffb63b75273a8db548c558465d79db03fd359c6cd5bd9d85"}
     for s, h in pub.items():

@@ -852,6 +852,46 @@ CHECKSUM_LENS = [0, 1, 63, 64, 65, 1023, 1024, 1025, 2048, 4097, 255 * 1024, 256
                  256 * 1024 + 1, 257 * 1024 + 3, 512 * 1024, 65536 * 1024 + 5, 3 * 256 * 1024 * 256 + 777]
 
 
+def test_device_blake3_runs_the_reference_balloon(eng, oracle):
+    """The device BLAKE3 (sd_cas_checksum_dev, K3) driven through the reference's password
+    hash — Balloon::<blake3::Hasher> (crates/crypto/src/keys/hashing.rs:95-114; every block
+    hash a streamed 40-106-B, one- or two-block input) — at s_cost 256, t_cost 2, with and
+    without the KAT's secret, equals the oracle's Balloon, whose full-size runs reproduce the
+    reference's six HASH_B3BALLOON KATs (tests/test_oracle.py): the GPU's compression,
+    flags and block chaining sit on the same reference vectors as the oracle's.  Sequential
+    by construction: 5,376 dependent device hashes per run."""
+    buf = torch.zeros(256, dtype=torch.uint8, device="cuda")
+
+    def H(*parts):
+        m = b"".join(parts)
+        buf[:len(m)].copy_(torch.frombuffer(bytearray(m), dtype=torch.uint8))
+        return bytes.fromhex(eng.checksum_dev(buf, len(m)))
+
+    def le(v):
+        return int(v).to_bytes(8, "little")
+
+    pwd, salt = b"password", b"\xff" * 16
+    for secret in (None, b"\x55" * 18):
+        sec = secret or b""
+        s_cost, t_cost, cnt = 256, 2, 0
+        blk = [H(le(cnt), pwd, salt, sec)]
+        cnt += 1
+        for m in range(1, s_cost):
+            blk.append(H(le(cnt), blk[m - 1]))
+            cnt += 1
+        for t in range(t_cost):
+            for m in range(s_cost):
+                blk[m] = H(le(cnt), blk[m - 1], blk[m])  # blk[-1] is the last block for m == 0
+                cnt += 1
+                for i in range(3):
+                    idx = H(le(t), le(m), le(i))
+                    other = int.from_bytes(H(le(cnt), salt, sec, idx), "little") % s_cost
+                    cnt += 1
+                    blk[m] = H(le(cnt), blk[m], blk[other])
+                    cnt += 1
+        assert blk[-1] == oracle.balloon_blake3(pwd, salt, secret, s_cost, t_cost), secret is not None
+
+
 def test_checksum_device_vs_oracle(eng, oracle):
     rng = np.random.default_rng(7)
     for L in CHECKSUM_LENS:

@@ -33,6 +33,23 @@ def test_derive_key_kat_from_reference(oracle, golden):
     assert py_derive_key(kat["context"], mat).hex() == kat["expected_hex"]
 
 
+def test_balloon_b3_kats_from_reference(oracle, golden):
+    """The reference's other BLAKE3 known answers: Balloon::<blake3::Hasher> password hashes
+    (crates/crypto/src/keys/hashing.rs:180-208, tests :269-321) — millions of streamed
+    multi-piece BLAKE3 inputs of one and two 64-B blocks, so they pin the chunk-internal block
+    chaining that the one-block derive_key vector does not.  The standard-params vectors run
+    here (~1 s each); all six were reproduced by tests/golden/make_golden.py."""
+    g = golden["balloon_b3_kat"]
+    pwd, salt, sec = (bytes.fromhex(g[k]) for k in ("password_hex", "salt_hex", "secret_hex"))
+    assert pwd == b"password" and salt == b"\xff" * 16 and sec == b"\x55" * 18
+    assert len(g["vectors"]) == 6
+    for v in g["vectors"]:
+        if v["s_cost"] != 131_072:
+            continue
+        got = oracle.balloon_blake3(pwd, salt, sec if v["secret"] else None, v["s_cost"], g["t_cost"])
+        assert got.hex() == v["expected_hex"], v
+
+
 def test_public_vectors(oracle, golden):
     for s, h in golden["blake3_public"].items():
         assert oracle.blake3(s.encode()).hex() == h
