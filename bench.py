@@ -616,7 +616,9 @@ class SmiSampler:
             d = json.loads(r.stdout)
         except (OSError, ValueError, subprocess.SubprocessError):
             return None
-        cards = [v for k, v in d.items() if k.startswith("card") and isinstance(v, dict)]
+        if not isinstance(d, dict):
+            return None
+        cards = [v for k, v in d.items() if str(k).startswith("card") and isinstance(v, dict)]
         pick = None
         for c in cards:
             for k, v in c.items():

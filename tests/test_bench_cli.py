@@ -76,3 +76,46 @@ def test_cpu_baseline_threads(monkeypatch):
     monkeypatch.setenv("SD_CPU_BASELINE_THREADS", "3")
     assert bench.cpu_threads(8) == 3
     assert bench.cpu_model() is None or isinstance(bench.cpu_model(), str)
+
+
+def test_smi_sampler_and_session_evidence(monkeypatch):
+    """bench.py's live power sampling picks THIS rank's card by PCI bus (never another card's
+    numbers when several are listed and none matches) and tolerates a missing or garbled
+    rocm-smi; the VALU / power evidence read from the committed same-session file is marked
+    as not measured in the run."""
+    import json as _json
+    import subprocess
+    import time as _time
+    import types
+    sys.path.insert(0, ROOT)
+    import bench
+    smi = {"card0": {"PCI Bus": "0000:05:00.0", "Current Socket Graphic Package Power (W)": "1000.0",
+                     "sclk clock speed:": "(1900Mhz)"},
+           "card1": {"PCI Bus": "0000:f1:00.0", "Current Socket Graphic Package Power (W)": "1361.0",
+                     "sclk clock speed:": "(2212Mhz)"}}
+    out = {"stdout": _json.dumps(smi)}
+
+    def fake_run(cmd, **kw):
+        if out["stdout"] is None:
+            raise OSError("no rocm-smi")
+        return types.SimpleNamespace(stdout=out["stdout"], returncode=0)
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    s = bench.SmiSampler(types.SimpleNamespace(pci_bus_id=0xF1), settle_s=0.0)
+    _time.sleep(0.6)
+    live = s.stop()
+    assert live["power_w_median"] == 1361.0 and live["sclk_mhz_median"] == 2212.0 and live["pci_bus"] == 0xF1
+    s = bench.SmiSampler(types.SimpleNamespace(pci_bus_id=0x33), settle_s=0.0)  # no such card
+    _time.sleep(0.3)
+    assert s.stop() is None
+    for bad in (None, "not json", "[1, 2]"):
+        out["stdout"] = bad
+        s = bench.SmiSampler(types.SimpleNamespace(pci_bus_id=0xF1), settle_s=0.0)
+        _time.sleep(0.3)
+        assert s.stop() is None
+    valu, power = bench.valu_power_evidence("sd_cas_sampled_group_kernel", 1310720, 24.0,
+                                            {"value": 54e6, "n_gpus": 1}, live)
+    assert valu["measured_in_this_run"] is False and valu["session"]
+    assert 0.3 < valu["instr_rate_frac_of_peak"] < 0.6 and valu["valu_busy"] > 0.9
+    assert power["measured_in_this_run"] is False and power["live"]["measured_in_this_run"] is True
+    assert 0.8 < power["live"]["sustained_frac_of_capped_ceiling"] < 1.0
+    assert 0.8 < power["session_frac_of_capped_ceiling"] < 1.0
