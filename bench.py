@@ -336,7 +336,7 @@ def main() -> None:
         objects = res.objects
     # the grouping alone (after the timed region: inside the steps it overlaps the next K1
     # on a side stream and shares the CUs with it, so its own speed is measured serially)
-    group_ms = group_ms_sync = group12_ms = group12_objects = None
+    group_ms = group_ms_sync = group12_ms = group12_objects = lsd12 = None
     if not sharded:
         # (a) each call synchronised: includes the host's enqueue latency of its 2-4 launches
         # (the GPU idles ~4 us between the first two: profiles/r02b_group_chain_trace.txt);
@@ -382,6 +382,7 @@ def main() -> None:
             gb.append(a.elapsed_time(b) / 5)
         group12_ms = float(np.median(gb))
         group12_objects = eng.group(big, rep_big)
+        lsd12 = lsd_sort_leg(eng, big, rep_big, group12_objects, main)
         del big, base, rep_big
 
     # the N > 1 exchange alone (partition + fixed-capacity all-to-all + grouping of the
@@ -580,7 +581,8 @@ def main() -> None:
                     "objects_expected": 12_500_000 - 3_750_000,
                     "ms": group12_ms, "algorithmic_bytes_per_key": group_bytes_per_key(12_500_000),
                     "hbm_frac": 12_500_000 * group_bytes_per_key(12_500_000) / (group12_ms / 1e3)
-                                / 1e9 / HBM_PEAK_GBS},
+                                / 1e9 / HBM_PEAK_GBS,
+                    "lsd_sort": lsd12},
             },
             "cpu_baseline": cpu,
         }
@@ -589,6 +591,52 @@ def main() -> None:
         worker.shutdown()
     if sharded:
         dist.destroy_process_group()
+
+
+def lsd_sort_leg(eng, keys, rep, objects, stream):
+    """The north star's dedup primitive on config 4's rank share: the stable LSD radix sort of
+    the 12.5 M keys (K4, 8 x 8-bit passes) and the sort + run heads (K4 + K5), HIP events on
+    the stream they run on — "HBM GB/s for the sort": algorithmic bytes (as implemented: 8 x
+    (8 B upsweep read + 24 B key/idx read + write) = 256 B/key for the sort, + run heads 8 and
+    emit 16 = 280 with the runs) and the PMC bytes per key of the committed pass
+    (profiles/r05/pmc_sort_12p5m.json) over this run's times.  The Object count must equal
+    the hash grouping's."""
+    import numpy as np
+    import torch
+    n = int(keys.numel())
+    ko = torch.empty_like(keys)
+    vo = torch.empty(n, dtype=torch.int32, device=keys.device)
+    eng.sort_pairs(keys, None, ko, vo)
+    objs = eng.group_sorted(ko, vo, rep)
+    t_sort, t_runs = [], []
+    for _ in range(3):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        eng.sort_pairs(keys, None, ko, vo)
+        b.record(stream)
+        b.synchronize()
+        t_sort.append(a.elapsed_time(b))
+        a.record(stream)
+        eng.sort_pairs(keys, None, ko, vo)
+        eng.group_sorted(ko, vo, rep)
+        b.record(stream)
+        b.synchronize()
+        t_runs.append(a.elapsed_time(b))
+    ms_sort, ms_runs = float(np.median(t_sort)), float(np.median(t_runs))
+    rec = {"keys": n, "ms_sort": ms_sort, "ms_sort_runs": ms_runs, "objects": objs,
+           "objects_equal_hash_grouping": objs == objects,
+           "algorithmic_bytes_per_key_sort": 256, "algorithmic_bytes_per_key_sort_runs": 280,
+           "achieved_gb_s_sort": n * 256 / (ms_sort / 1e3) / 1e9,
+           "hbm_frac_sort": n * 256 / (ms_sort / 1e3) / 1e9 / HBM_PEAK_GBS,
+           "hbm_frac_sort_runs": n * 280 / (ms_runs / 1e3) / 1e9 / HBM_PEAK_GBS}
+    path = os.path.join(ROOT, "profiles", "r05", "pmc_sort_12p5m.json")
+    if os.path.exists(path):
+        with open(path) as fh:
+            pm = json.load(fh)["lsd"]
+        rec["pmc_bytes_per_key_sort_runs"] = pm["measured_b_per_key"]
+        rec["pmc_gb_s_sort_runs"] = n * pm["measured_b_per_key"] / (ms_runs / 1e3) / 1e9
+        rec["pmc_source"] = "profiles/r05/pmc_sort_12p5m.json (measured_in_this_run: false)"
+    return rec
 
 
 class SmiSampler:

@@ -6,6 +6,7 @@ the host drop-ins (buffers and paths, with per-file I/O errors), grouping (canon
 the chunk-of-100 replay), the radix sort, the validator checksum (device buffer and
 streamed file), and — at BASELINE sizes — size-independent properties.
 """
+import ctypes
 import os
 
 import numpy as np
@@ -890,6 +891,32 @@ def test_device_blake3_runs_the_reference_balloon(eng, oracle):
                     blk[m] = H(le(cnt), blk[m], blk[other])
                     cnt += 1
         assert blk[-1] == oracle.balloon_blake3(pwd, salt, secret, s_cost, t_cost), secret is not None
+
+
+def test_device_blake3_reproduces_reference_balloon_kats(eng, golden):
+    """The reference's own Balloon-BLAKE3 known answers, computed on the GPU: the product's
+    device BLAKE3 compression (spacedrive_amd/csrc/blake3_device.hpp) driven through
+    Balloon::<blake3::Hasher> (tests/native/balloon_dev.hip, the construction of
+    oracle/balloon_ref.c) reproduces HASH_B3BALLOON_EXPECTED[0] and
+    HASH_B3BALLOON_WITH_SECRET_EXPECTED[0] (crates/crypto/src/keys/hashing.rs:180-208,
+    s_cost 131,072, t_cost 2): ~2.75 M dependent one- and two-block hashes per chain, the
+    two chains side by side.  The GPU thereby sits on the reference's vectors directly, not
+    only on the oracle's outputs."""
+    lib_path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native", "libballoon_dev.so")
+    assert os.path.exists(lib_path), "build() builds tests/native/libballoon_dev.so"
+    L = ctypes.CDLL(lib_path)
+    L.balloon_dev_run.restype = ctypes.c_int
+    g = golden["balloon_b3_kat"]
+    pwd, salt, sec = (bytes.fromhex(g[k]) for k in ("password_hex", "salt_hex", "secret_hex"))
+    secrets = (ctypes.c_char_p * 2)(b"", sec)
+    lens = (ctypes.c_uint32 * 2)(0, len(sec))
+    out = ctypes.create_string_buffer(64)
+    rc = L.balloon_dev_run(pwd, ctypes.c_uint32(len(pwd)), salt, ctypes.c_uint32(len(salt)), secrets,
+                           lens, ctypes.c_int(2), ctypes.c_uint64(131_072), ctypes.c_uint64(2), out)
+    assert rc == 0
+    want = {v["secret"]: v["expected_hex"] for v in g["vectors"] if v["s_cost"] == 131_072}
+    assert out.raw[:32].hex() == want[False]
+    assert out.raw[32:].hex() == want[True]
 
 
 def test_checksum_device_vs_oracle(eng, oracle):
