@@ -5,6 +5,8 @@ from .cas import (  # noqa: F401
     CHUNK_SIZE,
     HEADER_OR_FOOTER_SIZE,
     MINIMUM_FILE_SIZE,
+    NO_OBJECT,
+    NO_STEP,
     SAMPLE_COUNT,
     SAMPLE_SIZE,
     SAMPLED_CONTENT_LEN,

@@ -1708,6 +1708,46 @@ def test_identifier_links_pre_objects_vs_replay(eng, chunk):
                              pre_objects=torch.from_numpy(bad.view(np.int32)).cuda())
 
 
+def test_identifier_links_pre_objects_edges(eng):
+    """Edge shapes of sd_cas_identifier_links_ex against the replay: no rows; one row owning
+    an Object; every row owning the same Object; Objects only on ERROR / NO_CAS rows (no
+    event: the fresh answer); Objects on rows past the job's last step (not reached, so not
+    seen); an Object id of 0 and of 2^31 - 1; chunk larger than the job."""
+    from spacedrive_amd import NO_OBJECT  # noqa: F401  (re-exported constant)
+    cases = []
+    k = np.array([5, 5, 7, 5, 9, 7, 5], np.uint64)
+    cases.append((k, np.zeros(7, np.uint8), [None, None, None, 0, None, 2 ** 31 - 1, None], 3, None))
+    cases.append((k[:1], np.zeros(1, np.uint8), [42], 100, None))
+    cases.append((k, np.zeros(7, np.uint8), [11] * 7, 2, None))
+    st = np.array([2, 1, 0, 2, 1, 0, 0], np.uint8)
+    cases.append((k, st, [3, 4, None, 5, 6, None, None], 3, None))
+    # chunk 1 with a stay-orphan row in front: the job re-queries it until its steps run out,
+    # so the later rows (with Objects) are never reached
+    cases.append((k, np.array([2, 0, 0, 0, 0, 0, 0], np.uint8), [None, 8, 9, 1, 2, 3, 4], 1, None))
+    cases.append((k, np.zeros(7, np.uint8), [None, 50, None, None, 40, None, 30], 2,
+                  [(5, 60), (9, 35), (7, 70)]))
+    for keys, states, pre, chunk, seeds in cases:
+        want_step, want_obj, want_act, want_counts = replay_identifier_job(
+            [int(x) for x in keys], [int(x) for x in states], chunk, existing=seeds, pre_objects=pre)
+        po = np.array([0xFFFFFFFF if p is None else p for p in pre], np.uint32)
+        ex = None
+        if seeds:
+            ex = (np.array([a for a, _ in seeds], np.uint64), np.array([b for _, b in seeds], np.uint32))
+        step, obj, act, counts = eng.identifier_links(
+            dev64(keys), torch.from_numpy(states).cuda(), chunk,
+            existing=None if ex is None else (dev64(ex[0]), torch.from_numpy(ex[1].view(np.int32)).cuda()),
+            pre_objects=torch.from_numpy(po.view(np.int32)).cuda())
+        assert [tuple(c) for c in counts.tolist()] == want_counts, (pre, chunk)
+        assert (step.cpu().numpy().view(np.uint32) == np.array(want_step, np.uint32)).all()
+        assert (obj.cpu().numpy().view(np.uint32) == np.array(want_obj, np.uint32)).all(), (pre, chunk)
+        assert (act.cpu().numpy() == np.array(want_act, np.uint8)).all(), (pre, chunk)
+    # no rows at all
+    e = torch.empty(0, dtype=torch.int64, device="cuda")
+    step, obj, act, counts = eng.identifier_links(e, None, 100,
+                                                  pre_objects=torch.empty(0, dtype=torch.int32, device="cuda"))
+    assert step.numel() == 0 and counts.shape == (0, 2)
+
+
 def test_identifier_links_pre_objects_hot_key_1m(eng):
     """The two scans at scale: 1M rows, one hot key over every chunk with pre-existing
     Objects whose ids decrease step by step (each step's minimum takes over), plus random
