@@ -155,6 +155,16 @@ void orc_blake3(const uint8_t* in, size_t len, uint8_t* out, size_t out_len) {
   hash_stack(IV, 0, in, len, out, out_len);
 }
 
+/* blake3::keyed_hash(key, in) (KEYED_HASH mode: the key replaces IV in every chunk and
+ * parent compression, flag 16 on all of them).  The tree is formulation 1's; this mode is
+ * how an independent BLAKE3 in the image (hf_xet's, tests/golden/make_xet_vectors.py) pins
+ * that tree on messages of up to 128 chunks. */
+void orc_blake3_keyed(const uint8_t key[32], const uint8_t* in, size_t len, uint8_t out[32]) {
+  uint32_t k[8];
+  for (int i = 0; i < 8; i++) k[i] = ld32(key + 4 * i);
+  hash_stack(k, B3_KEYED, in, len, out, 32);
+}
+
 /* ---- formulation 2: recursive left-balanced split ------------------------ */
 static uint64_t largest_pow2_below(uint64_t n) { /* largest power of two strictly < n, n >= 2 */
   uint64_t p = 1;

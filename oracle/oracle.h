@@ -11,9 +11,11 @@
  *     core/src/object/validation/hash.rs:13-22).  The crate is not vendored in the
  *     reference, so this is a restatement of the published BLAKE3 spec, pinned by the
  *     reference's only in-repo BLAKE3 known answer (derive_key KAT,
- *     crates/crypto/src/keys/hashing.rs:210-213, 323-328) and by two independent
- *     tree formulations that must agree (recursive left-balanced vs incremental
- *     CV stack).
+ *     crates/crypto/src/keys/hashing.rs:210-213, 323-328), its six Balloon-BLAKE3
+ *     KATs (hashing.rs:180-208), multi-chunk trees of 1-128 chunks against an
+ *     independent BLAKE3 in the image (hf_xet's Rust crate, keyed mode:
+ *     tests/golden/make_xet_vectors.py) and by independent tree formulations that must
+ *     agree (incremental CV stack, recursive left-balanced, level-wise, threaded).
  *   - generate_cas_id message layout (core/src/object/cas.rs:10-61).
  *   - file_checksum (core/src/object/validation/hash.rs:11-25).
  *   - Object grouping (core/src/object/file_identifier/mod.rs:98-350), canonical form
@@ -39,6 +41,8 @@ void orc_blake3_levelwise(const uint8_t* in, size_t len, uint8_t out[32]);
 /* blake3::derive_key(context, material) -> 32 bytes. */
 void orc_blake3_derive_key(const char* context, const uint8_t* material, size_t len,
                            uint8_t out[32]);
+/* blake3::keyed_hash(key, in) -> 32 bytes (formulation 1's tree in KEYED_HASH mode). */
+void orc_blake3_keyed(const uint8_t key[32], const uint8_t* in, size_t len, uint8_t out[32]);
 /* Same hash, tree-parallel over `threads` pthreads (16 MiB subtrees, then pair-and-promote;
  * SURVEY §8d's "multithreaded tree" CPU mode). */
 void orc_blake3_mt(const uint8_t* in, size_t len, int threads, uint8_t out[32]);

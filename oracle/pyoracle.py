@@ -43,6 +43,7 @@ _PERM = (2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8)
 _M32 = 0xFFFFFFFF
 CHUNK_START, CHUNK_END, PARENT, ROOT = 1, 2, 4, 8
 DERIVE_KEY_CONTEXT, DERIVE_KEY_MATERIAL = 32, 64
+KEYED_HASH = 16
 
 
 def _rotr(x: int, n: int) -> int:
@@ -117,6 +118,12 @@ def py_derive_key(context: str, material: bytes) -> bytes:
     ck = _root_bytes(_subtree(_IV, context.encode(), 0, DERIVE_KEY_CONTEXT))
     key = [int.from_bytes(ck[4 * i:4 * i + 4], "little") for i in range(8)]
     return _root_bytes(_subtree(key, bytes(material), 0, DERIVE_KEY_MATERIAL))
+
+
+def py_keyed_hash(key: bytes, data: bytes) -> bytes:
+    """blake3::keyed_hash: the 32-byte key replaces IV, KEYED_HASH on every compression."""
+    k = [int.from_bytes(key[4 * i:4 * i + 4], "little") for i in range(8)]
+    return _root_bytes(_subtree(k, bytes(data), 0, KEYED_HASH))
 
 
 def py_sample_plan(size: int):
@@ -297,6 +304,7 @@ class Oracle:
         L.orc_blake3_recursive.argtypes = [ctypes.c_void_p, sz, ctypes.c_void_p]
         L.orc_blake3_levelwise.argtypes = [ctypes.c_void_p, sz, ctypes.c_void_p]
         L.orc_blake3_derive_key.argtypes = [ctypes.c_char_p, ctypes.c_void_p, sz, ctypes.c_void_p]
+        L.orc_blake3_keyed.argtypes = [ctypes.c_char_p, ctypes.c_void_p, sz, ctypes.c_void_p]
         L.orc_sample_plan.argtypes = [ctypes.c_uint64, u64p, u64p]
         L.orc_cas_key.argtypes = [ctypes.c_void_p, sz, ctypes.c_uint64]
         L.orc_cas_key.restype = ctypes.c_uint64
@@ -381,6 +389,12 @@ class Oracle:
         if rc != 0:
             raise OSError(-rc, os.strerror(-rc), path)
         return out.value.decode()
+
+    def keyed_hash(self, key: bytes, data: bytes) -> bytes:
+        assert len(key) == 32
+        out = ctypes.create_string_buffer(32)
+        self.L.orc_blake3_keyed(key, data, len(data), out)
+        return out.raw
 
     def derive_key(self, context: str, material: bytes) -> bytes:
         out = ctypes.create_string_buffer(32)

@@ -893,6 +893,39 @@ def test_device_blake3_runs_the_reference_balloon(eng, oracle):
         assert blk[-1] == oracle.balloon_blake3(pwd, salt, secret, s_cost, t_cost), secret is not None
 
 
+def test_device_trees_on_the_independently_pinned_lengths(eng, oracle):
+    """The lengths whose trees hf_xet's BLAKE3 pins in the oracle (tests/golden/xet_blake3.json,
+    1-128 chunks): the same contents through the product's three whole-message kernels — the
+    validator batch (K3b), the single-buffer tree (K3) and the whole-file cas_id (K2, message
+    le64(size) || content) — bit-exact against the oracle."""
+    import json
+    import torch
+    from tests.golden.make_xet_vectors import content
+    with open(os.path.join(os.path.dirname(__file__), "golden", "xet_blake3.json")) as f:
+        vecs = json.load(f)["vectors"]
+    datas = [content(v["len"], v["seed"]) for v in vecs]
+    offs = np.zeros(len(datas), np.int64)
+    pos = 0
+    for i, d in enumerate(datas):
+        offs[i] = pos
+        pos += (len(d) + 15) // 16 * 16
+    arena = np.zeros(pos, np.uint8)
+    for o, d in zip(offs, datas):
+        arena[o:o + len(d)] = np.frombuffer(d, np.uint8)
+    lens = np.array([len(d) for d in datas], np.int64)
+    out = torch.zeros((len(datas), 32), dtype=torch.uint8, device="cuda")
+    eng.checksums_dev(torch.from_numpy(arena).cuda(), torch.from_numpy(offs).cuda(),
+                      torch.from_numpy(lens).cuda(), out)
+    got = out.cpu().numpy()
+    for i, d in enumerate(datas):
+        want = oracle.blake3(d)
+        assert got[i].tobytes() == want, len(d)
+        if i % 7 == 0:
+            assert eng.checksum_dev(torch.from_numpy(np.frombuffer(d, np.uint8).copy()).cuda()) == want.hex()
+    small = [(d, len(d)) for d in datas if len(d) <= 102_400]
+    assert eng.generate_cas_ids(small) == [oracle.cas_id(d, n) for d, n in small]
+
+
 def test_device_blake3_reproduces_reference_balloon_kats(eng, golden):
     """The reference's own Balloon-BLAKE3 known answers, computed on the GPU: the product's
     device BLAKE3 compression (spacedrive_amd/csrc/blake3_device.hpp) driven through

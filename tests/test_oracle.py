@@ -5,6 +5,8 @@ parity claim rests on it, it is pinned here:
   * derive_key KAT from crates/crypto/src/keys/hashing.rs:210-213 (the reference's only
     in-repo BLAKE3 known answer),
   * public BLAKE3("") / BLAKE3("abc"),
+  * multi-chunk trees (1-128 chunks, every chunk count) against an independent BLAKE3 in the
+    image (hf_xet's Rust crate; tests/golden/make_xet_vectors.py),
   * three independent tree formulations + a pure-Python restatement agreeing,
   * cas.rs:35-58 offsets simulated literally,
   * grouping against a literal replay of identifier_job_step (mod.rs:98-350).
@@ -48,6 +50,52 @@ def test_balloon_b3_kats_from_reference(oracle, golden):
             continue
         got = oracle.balloon_blake3(pwd, salt, sec if v["secret"] else None, v["s_cost"], g["t_cost"])
         assert got.hex() == v["expected_hex"], v
+
+
+def _xet_vectors():
+    import json
+    with open(os.path.join(os.path.dirname(__file__), "golden", "xet_blake3.json")) as f:
+        return json.load(f)
+
+
+def test_blake3_trees_pinned_by_independent_blake3(oracle):
+    """Multi-chunk trees: every chunk count 1..128 with a ragged last chunk, plus the sampled
+    cas message (57,352 B) and the largest whole-file one (102,408 B), each reproduced from
+    digests hf_xet 1.5.2's Rust BLAKE3 computed on single-Xet-chunk files
+    (tests/golden/make_xet_vectors.py has the relation).  The C oracle's keyed mode runs
+    formulation 1's tree, the pure-Python restatement its own recursive tree."""
+    import zlib
+
+    from oracle.pyoracle import py_keyed_hash
+    from tests.golden.make_xet_vectors import DATA_KEY, content, xet_display
+    doc = _xet_vectors()
+    assert doc["data_key"] == DATA_KEY.hex() and doc["unpinned"] == []
+    lens = [v["len"] for v in doc["vectors"]]
+    chunks = {-(-n // 1024) for n in lens}
+    assert chunks == set(range(1, 129)) and {57_352, 102_408} <= set(lens)
+    for i, v in enumerate(doc["vectors"]):
+        d = content(v["len"], v["seed"])
+        assert zlib.crc32(d) == v["crc32"], v
+        inner = oracle.keyed_hash(DATA_KEY, d)
+        assert xet_display(oracle.keyed_hash(bytes(32), inner)) == v["xet_hash"], v
+        if i % 9 == 0:  # the pure-Python tree on a spread of lengths
+            assert py_keyed_hash(DATA_KEY, d) == inner, v
+
+
+def test_blake3_live_against_hf_xet(oracle, tmp_path):
+    """Fresh draws (lengths 1..8 KiB, below Xet's minimum chunk, so always one Xet chunk)
+    hashed live by hf_xet and by the oracle."""
+    hf_xet = pytest.importorskip("hf_xet")
+    from tests.golden.make_xet_vectors import DATA_KEY, xet_display
+    rng = np.random.default_rng(int.from_bytes(os.urandom(4), "little"))
+    draws = []
+    for i in range(24):
+        d = rng.integers(0, 256, int(rng.integers(1, 8192)), dtype=np.uint8).tobytes()
+        p = tmp_path / f"{i}.bin"
+        p.write_bytes(d)
+        draws.append((str(p), d))
+    for (p, d), r in zip(draws, hf_xet.hash_files([p for p, _ in draws])):
+        assert r.hash == xet_display(oracle.keyed_hash(bytes(32), oracle.keyed_hash(DATA_KEY, d))), len(d)
 
 
 def test_public_vectors(oracle, golden):
