@@ -8,12 +8,13 @@
 // objects = #distinct keys.  LSD radix sort is stable and the values enter in ascending
 // idx order, so the head of every equal-key run carries the minimum idx.
 //
-// Sort pass = upsweep (per-tile digit histogram in LDS) -> exclusive scan over the
-// digit-major [digit][tile] table -> downsweep (stable wave-level ranking with 8 ballots
-// per item, tile-local digit offsets in LDS, scatter).  All integer/byte work bound by
-// HBM; nothing here is reshaped into a GEMM.
+// Sort pass = upsweep (per-tile digit histogram in LDS) -> row scan of the digit-major
+// [digit][tile] table (one workgroup per digit) -> scatter (stable wave-private ranking with
+// 8 ballots per item, the tile staged in LDS in digit order, runs written out coalesced).
+// All integer/byte work bound by HBM; nothing here is reshaped into a GEMM.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "sd_debug.h"
 #include "sd_group.h"
@@ -29,58 +30,124 @@ __device__ __forceinline__ uint32_t digit_of(uint64_t k, uint32_t shift, uint32_
   return (uint32_t)(k >> shift) & mask;
 }
 
-// hist[d * ntiles + tile] = #keys of `tile` with digit d
+// hist[d * ntiles + tile] = #keys of `tile` with digit d.  Every key of the tile is loaded
+// before the first count (16 loads in flight per lane); each wave counts into its own LDS
+// row (a quarter of the same-address LDS atomics of one shared row).
 extern "C" __global__ void __launch_bounds__(SORT_THREADS)
 sd_radix_upsweep(const uint64_t* __restrict__ keys, uint64_t n, uint32_t shift, uint32_t mask,
                  uint32_t* __restrict__ hist, uint32_t ntiles) {
-  __shared__ uint32_t cnt[RADIX];
-  const uint32_t t = threadIdx.x;
-  cnt[t] = 0;
-  __syncthreads();
+  constexpr int WAVES = SORT_THREADS / 64;
+  __shared__ uint32_t cnt[WAVES][RADIX];
+  const uint32_t t = threadIdx.x, w = t >> 6;
+#pragma unroll
+  for (int v = 0; v < WAVES; ++v) cnt[v][t] = 0;
   const uint64_t base = (uint64_t)blockIdx.x * TILE;
-#pragma unroll 4
+  uint64_t kr[SORT_ROUNDS];
+#pragma unroll
   for (int r = 0; r < SORT_ROUNDS; ++r) {
     const uint64_t i = base + (uint64_t)r * SORT_THREADS + t;
-    if (i < n) atomicAdd(&cnt[digit_of(keys[i], shift, mask)], 1u);
+    kr[r] = i < n ? keys[i] : 0ull;
   }
   __syncthreads();
-  hist[(uint64_t)t * ntiles + blockIdx.x] = cnt[t];
+#pragma unroll
+  for (int r = 0; r < SORT_ROUNDS; ++r) {
+    const uint64_t i = base + (uint64_t)r * SORT_THREADS + t;
+    if (i < n) atomicAdd(&cnt[w][digit_of(kr[r], shift, mask)], 1u);
+  }
+  __syncthreads();
+  hist[(uint64_t)t * ntiles + blockIdx.x] = cnt[0][t] + cnt[1][t] + cnt[2][t] + cnt[3][t];
 }
 
-// Stable scatter of one tile.  offs = exclusive-scanned hist (same layout).  The tile is
-// first ranked into LDS in digit order (stable: round, then wave, then lane order within a
-// digit), then written out so that consecutive lanes store consecutive slots of one digit's
-// run: coalesced runs of ~16 keys per digit instead of ~1 key per digit per store
-// instruction (PMC: 41.5 B/key written per pass for 12 algorithmic, profiles/r02_pmc_group.txt).
-template <bool HAS_VALS>
-__device__ __forceinline__ void downsweep_body(const uint64_t* __restrict__ keys_in,
-                                               const uint32_t* __restrict__ vals_in,
-                                               uint64_t* __restrict__ keys_out,
-                                               uint32_t* __restrict__ vals_out, uint64_t n,
-                                               uint32_t shift, uint32_t mask,
-                                               const uint32_t* __restrict__ offs,
-                                               uint32_t ntiles) {
-  __shared__ uint32_t run[RADIX];        // per-digit running count within this tile
-  // per-wave digit counts, double-buffered by round parity: a wave that runs ahead into
-  // round r+1 writes the other buffer while thread d may still be folding round r's counts
-  // of digit d into run[d] and zeroing them (one buffer raced there: rare lost counts)
-  __shared__ uint32_t wcnt[2][4][RADIX];
-  __shared__ uint32_t gbase[RADIX];      // global offset of this tile's digit d
-  __shared__ uint32_t tstart[RADIX];     // first LDS slot of digit d in this tile
+// Row-local exclusive scan of the digit-major table, one workgroup per digit:
+// offs[d * ntiles + t] = sum of hist[d * ntiles + t'] for t' < t, rowtot[d] = the row's sum.
+// (The digit bases, the exclusive scan of rowtot over 256 digits, are taken by each scatter
+// workgroup itself: one launch per pass instead of three.)
+extern "C" __global__ void __launch_bounds__(SORT_THREADS)
+sd_radix_rowscan(const uint32_t* __restrict__ hist, uint32_t ntiles, uint32_t* __restrict__ offs,
+                 uint32_t* __restrict__ rowtot) {
   __shared__ uint32_t wsum[SORT_THREADS / 64];
+  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+  const uint64_t row = (uint64_t)blockIdx.x * ntiles;
+  constexpr uint32_t PER = 8;  // elements per thread per chunk
+  uint32_t carry = 0;
+  for (uint32_t c0 = 0; c0 < ntiles; c0 += SORT_THREADS * PER) {
+    uint32_t v[PER], s = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) {
+      const uint32_t j = c0 + t * PER + k;
+      v[k] = j < ntiles ? hist[row + j] : 0u;
+      s += v[k];
+    }
+    uint32_t inc = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= (uint32_t)o) inc += y;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t pre = carry, tot = carry;
+#pragma unroll
+    for (int i = 0; i < SORT_THREADS / 64; ++i) {
+      if ((uint32_t)i < w) pre += wsum[i];
+      tot += wsum[i];
+    }
+    __syncthreads();
+    uint32_t run = pre + inc - s;
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) {
+      const uint32_t j = c0 + t * PER + k;
+      if (j < ntiles) offs[row + j] = run;
+      run += v[k];
+    }
+    carry = tot;
+  }
+  if (t == 0) rowtot[blockIdx.x] = carry;
+}
+
+// Stable scatter of one tile, wave-private ranking (round 5).  Wave w owns the contiguous
+// quarter [w*1024, (w+1)*1024) of the tile, round r its 64 items from w*1024 + r*64, so the
+// tile order (w, r, lane) is the input order and a wave can rank its own items across its
+// 16 rounds with no workgroup barrier: wrun[w][d] counts digit d among the wave's earlier
+// rounds (only wave w touches row w; one wave's LDS operations complete in program order).
+// One barrier then turns the four rows into tile slots: slot = tstart[d] + (digit d in
+// earlier waves) + the item's wave-local rank.  3 barriers per tile instead of 33, and 50 KB
+// of LDS instead of 59 (3 workgroups per CU instead of 2).
+template <bool HAS_VALS>
+__device__ __forceinline__ void scatter_body(const uint64_t* __restrict__ keys_in,
+                                             const uint32_t* __restrict__ vals_in,
+                                             uint64_t* __restrict__ keys_out,
+                                             uint32_t* __restrict__ vals_out, uint64_t n,
+                                             uint32_t shift, uint32_t mask,
+                                             const uint32_t* __restrict__ offs,
+                                             const uint32_t* __restrict__ rowtot,
+                                             uint32_t ntiles) {
+  constexpr int WAVES = SORT_THREADS / 64;
+  constexpr int WAVE_ITEMS = 64 * SORT_ROUNDS;
   __shared__ uint64_t skey[TILE];
   __shared__ uint32_t sval[TILE];
+  __shared__ uint16_t wrun[WAVES][RADIX];  // wave-local digit counts, then wave slot bases
+  __shared__ uint32_t gbase[RADIX];
+  __shared__ uint16_t tstart[RADIX];
+  __shared__ uint32_t wsum[WAVES];
   const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
   const uint64_t idx = (uint64_t)t * ntiles + blockIdx.x;
-  const uint32_t mine = offs[idx];
-  // this tile's count of digit t: the next entry of the digit-major scan minus this one
-  const uint32_t cnt = (idx + 1 < (uint64_t)RADIX * ntiles ? offs[idx + 1] : (uint32_t)n) - mine;
-  run[t] = 0;
+  const uint32_t mine = offs[idx];  // row-local: digit t's keys in earlier tiles
+  const uint32_t rtot = rowtot[t];
+  const uint64_t base = (uint64_t)blockIdx.x * TILE;
+  const uint64_t wbase = base + (uint64_t)w * WAVE_ITEMS;
+  uint64_t kr[SORT_ROUNDS];
+  uint32_t vr[SORT_ROUNDS];
 #pragma unroll
-  for (int b = 0; b < 8; ++b) wcnt[b >> 2][b & 3][t] = 0;
-  gbase[t] = mine;
-  {  // tstart = exclusive scan of the tile's digit counts (256 threads, one digit each)
-    uint32_t inc = cnt;
+  for (int r = 0; r < SORT_ROUNDS; ++r) {
+    const uint64_t i = wbase + (uint64_t)r * 64 + lane;
+    kr[r] = i < n ? keys_in[i] : 0ull;
+    vr[r] = (HAS_VALS && i < n) ? vals_in[i] : (uint32_t)i;
+  }
+#pragma unroll
+  for (int j = 0; j < RADIX / 64; ++j) wrun[w][lane + 64 * j] = 0;
+  {  // digit base = exclusive scan of the row totals over the 256 digits
+    uint32_t inc = rtot;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t y = __shfl_up(inc, o, 64);
@@ -90,58 +157,61 @@ __device__ __forceinline__ void downsweep_body(const uint64_t* __restrict__ keys
     __syncthreads();
     uint32_t pre = 0;
     for (uint32_t i = 0; i < w; ++i) pre += wsum[i];
-    tstart[t] = pre + inc - cnt;
+    gbase[t] = pre + inc - rtot + mine;
   }
-  __syncthreads();
-  const uint64_t base = (uint64_t)blockIdx.x * TILE;
-  const uint32_t tile_n = (uint32_t)(n - base < (uint64_t)TILE ? n - base : (uint64_t)TILE);
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  // every round's key (and value) is loaded up front: one memory latency per tile, not one
-  // per round (the rounds are separated by barriers)
-  uint64_t kr[SORT_ROUNDS];
-  uint32_t vr[SORT_ROUNDS];
+  uint32_t dr[SORT_ROUNDS];  // digit << 16 | wave-local rank
 #pragma unroll
   for (int r = 0; r < SORT_ROUNDS; ++r) {
-    const uint64_t i = base + (uint64_t)r * SORT_THREADS + t;
-    kr[r] = i < n ? keys_in[i] : 0ull;
-    vr[r] = (HAS_VALS && i < n) ? vals_in[i] : (uint32_t)i;
-  }
-#pragma unroll
-  for (int r = 0; r < SORT_ROUNDS; ++r) {
-    const uint64_t i = base + (uint64_t)r * SORT_THREADS + t;
+    const uint64_t i = wbase + (uint64_t)r * 64 + lane;
     const bool valid = i < n;
-    const uint64_t k = kr[r];
-    const uint32_t v = vr[r];
-    const uint32_t d = digit_of(k, shift, mask);
-    // lanes of this wave holding the same digit
+    const uint32_t d = digit_of(kr[r], shift, mask);
     uint64_t peers = __ballot(valid);
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
       const uint64_t bal = __ballot((d >> b) & 1u);
       peers &= ((d >> b) & 1u) ? bal : ~bal;
     }
-    const uint32_t rank_in_wave = __popcll(peers & lt_mask);
-    uint32_t (&wc)[4][RADIX] = wcnt[r & 1];
-    if (valid && rank_in_wave == 0) wc[w][d] = (uint32_t)__popcll(peers);
-    __syncthreads();
-    if (valid) {
-      uint32_t before = run[d];
-      for (uint32_t ww = 0; ww < w; ++ww) before += wc[ww][d];
-      const uint32_t slot = tstart[d] + before + rank_in_wave;
-      skey[slot] = k;
-      sval[slot] = v;
-    }
-    __syncthreads();
-    // round r+1 writes the other buffer; round r+2 (this buffer again) is behind round
-    // r+1's barriers, which this thread reaches only after the lines below
-    run[t] += wc[0][t] + wc[1][t] + wc[2][t] + wc[3][t];
-    wc[0][t] = 0; wc[1][t] = 0; wc[2][t] = 0; wc[3][t] = 0;
+    const uint32_t before = valid ? (uint32_t)wrun[w][d] : 0u;
+    const uint32_t rank = __popcll(peers & lt_mask);
+    dr[r] = (d << 16) | (before + rank);
+    if (valid && rank == 0) wrun[w][d] = (uint16_t)(before + __popcll(peers));
   }
   __syncthreads();
-  // conservation: the per-wave digit counts of every round add up to the tile's count of
-  // digit t from the upsweep (the round-2 race lost exactly such a count)
-  SD_DBG_CHECK(run[t] == cnt, "downsweep tile %u digit %u: ranked %u, counted %u", blockIdx.x, t,
-               run[t], cnt);
+  // digit t: tile count, tile start (block exclusive scan), wave slot bases
+  uint32_t c[WAVES], cnt = 0;
+#pragma unroll
+  for (int v = 0; v < WAVES; ++v) { c[v] = wrun[v][t]; cnt += c[v]; }
+  uint32_t inc = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= (uint32_t)o) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  // conservation: the wave counts of digit t add up to the upsweep's count of it
+  SD_DBG_CHECK(cnt == (blockIdx.x + 1 < ntiles ? offs[idx + 1] : rtot) - mine,
+               "scatter tile %u digit %u: ranked %u", blockIdx.x, t, cnt);
+  __syncthreads();
+  uint32_t pre = 0;
+  for (uint32_t i = 0; i < w; ++i) pre += wsum[i];
+  const uint32_t ts = pre + inc - cnt;
+  tstart[t] = (uint16_t)ts;
+  uint32_t run = ts;
+#pragma unroll
+  for (int v = 0; v < WAVES; ++v) { wrun[v][t] = (uint16_t)run; run += c[v]; }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < SORT_ROUNDS; ++r) {
+    const uint64_t i = wbase + (uint64_t)r * 64 + lane;
+    if (i < n) {
+      const uint32_t slot = (uint32_t)wrun[w][dr[r] >> 16] + (dr[r] & 0xFFFFu);
+      skey[slot] = kr[r];
+      sval[slot] = vr[r];
+    }
+  }
+  __syncthreads();
+  const uint32_t tile_n = (uint32_t)(n - base < (uint64_t)TILE ? n - base : (uint64_t)TILE);
   for (uint32_t s = t; s < tile_n; s += SORT_THREADS) {
     const uint64_t k = skey[s];
     const uint32_t d = digit_of(k, shift, mask);
@@ -152,19 +222,19 @@ __device__ __forceinline__ void downsweep_body(const uint64_t* __restrict__ keys
 }
 
 extern "C" __global__ void __launch_bounds__(SORT_THREADS)
-sd_radix_downsweep(const uint64_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
-                   uint64_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out, uint64_t n,
-                   uint32_t shift, uint32_t mask, const uint32_t* __restrict__ offs,
-                   uint32_t ntiles) {
-  downsweep_body<true>(keys_in, vals_in, keys_out, vals_out, n, shift, mask, offs, ntiles);
+sd_radix_scatter(const uint64_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
+                 uint64_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out, uint64_t n,
+                 uint32_t shift, uint32_t mask, const uint32_t* __restrict__ offs,
+                 const uint32_t* __restrict__ rowtot, uint32_t ntiles) {
+  scatter_body<true>(keys_in, vals_in, keys_out, vals_out, n, shift, mask, offs, rowtot, ntiles);
 }
 
-// first pass: values are the identity (file idx) — no value read
 extern "C" __global__ void __launch_bounds__(SORT_THREADS)
-sd_radix_downsweep_iota(const uint64_t* __restrict__ keys_in, uint64_t* __restrict__ keys_out,
-                        uint32_t* __restrict__ vals_out, uint64_t n, uint32_t shift,
-                        uint32_t mask, const uint32_t* __restrict__ offs, uint32_t ntiles) {
-  downsweep_body<false>(keys_in, nullptr, keys_out, vals_out, n, shift, mask, offs, ntiles);
+sd_radix_scatter_iota(const uint64_t* __restrict__ keys_in, uint64_t* __restrict__ keys_out,
+                      uint32_t* __restrict__ vals_out, uint64_t n, uint32_t shift, uint32_t mask,
+                      const uint32_t* __restrict__ offs, const uint32_t* __restrict__ rowtot,
+                      uint32_t ntiles) {
+  scatter_body<false>(keys_in, nullptr, keys_out, vals_out, n, shift, mask, offs, rowtot, ntiles);
 }
 
 // ---- device-wide exclusive scan (u32, sum) over m <= SCAN_TILE^2 elements ----------
@@ -443,7 +513,7 @@ size_t sort_workspace_bytes(uint64_t n) {
   const uint64_t nt = tiles_of(n ? n : 1, TILE);
   const uint64_t m = (uint64_t)RADIX * nt;
   return align_up(n * 8, 256) + align_up(n * 4, 256) + 2 * align_up(m * 4, 256) +
-         align_up(tiles_of(m, SCAN_TILE) * 4 + 4, 256) + 256;
+         align_up(RADIX * 4, 256) + 256;
 }
 
 size_t group_workspace_bytes(uint64_t n) {
@@ -482,7 +552,7 @@ hipError_t radix_sort_pairs(const uint64_t* keys_in, const uint32_t* vals_in, ui
   uint32_t* valt = (uint32_t*)p; p += align_up(n * 4, 256);
   uint32_t* hist = (uint32_t*)p; p += align_up(m * 4, 256);
   uint32_t* offs = (uint32_t*)p; p += align_up(m * 4, 256);
-  uint32_t* partial = (uint32_t*)p;
+  uint32_t* rowtot = (uint32_t*)p;
   const int passes = (end_bit - begin_bit + 7) / 8;
   const uint64_t* ksrc = keys_in;
   const uint32_t* vsrc = vals_in;
@@ -494,12 +564,11 @@ hipError_t radix_sort_pairs(const uint64_t* keys_in, const uint32_t* vals_in, ui
     uint64_t* kdst = to_out ? keys_out : kalt;
     uint32_t* vdst = to_out ? vals_out : valt;
     sd_radix_upsweep<<<nt, SORT_THREADS, 0, s>>>(ksrc, n, shift, mask, hist, nt);
-    hipError_t e = exclusive_scan_u32(hist, offs, m, partial, s);
-    if (e != hipSuccess) return e;
+    sd_radix_rowscan<<<RADIX, SORT_THREADS, 0, s>>>(hist, nt, offs, rowtot);
     if (vsrc)
-      sd_radix_downsweep<<<nt, SORT_THREADS, 0, s>>>(ksrc, vsrc, kdst, vdst, n, shift, mask, offs, nt);
+      sd_radix_scatter<<<nt, SORT_THREADS, 0, s>>>(ksrc, vsrc, kdst, vdst, n, shift, mask, offs, rowtot, nt);
     else
-      sd_radix_downsweep_iota<<<nt, SORT_THREADS, 0, s>>>(ksrc, kdst, vdst, n, shift, mask, offs, nt);
+      sd_radix_scatter_iota<<<nt, SORT_THREADS, 0, s>>>(ksrc, kdst, vdst, n, shift, mask, offs, rowtot, nt);
     ksrc = kdst;
     vsrc = vdst;
   }

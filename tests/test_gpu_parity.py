@@ -358,6 +358,11 @@ def test_sort_pairs_vs_numpy(eng):
         eng.sort_pairs(dev64(k), None, ko, vo, 56, 64)
         order = np.argsort(k >> np.uint64(56), kind="stable")
         assert (vo.cpu().numpy() == order).all()
+        # caller values and a bit range whose last digit is narrower than 8 bits
+        v = rng.permutation(n).astype(np.int32)
+        eng.sort_pairs(dev64(k), torch.from_numpy(v).cuda(), ko, vo, 3, 23)
+        order = np.argsort((k >> np.uint64(3)) & np.uint64((1 << 20) - 1), kind="stable")
+        assert (vo.cpu().numpy() == v[order]).all() and (host64(ko) == k[order]).all()
 
 
 def test_sort_pairs_repeated_large(eng):

@@ -6,7 +6,7 @@ WRITE_SIZE of every sd_* dispatch summed and divided by chain_calls x keys.  gfx
 correction (MI355X_MICROARCH.md, HBM/rocprofv3): FETCH_SIZE reports half the bytes of a wide
 coalesced read, so it is doubled; both are in KiB.  Algorithmic bytes per key: hash chain
 68 B (bench.group_bytes_per_key, two-level region chain); LSD sort as implemented (group.hip):
-8 passes x (upsweep reads the 8-B key + downsweep reads and writes key + 4-B idx = 32 B) +
+8 passes x (upsweep reads the 8-B key + scatter reads and writes key + 4-B idx = 32 B) +
 run heads (read 8) + emit (read 12, write the 4-B rep) = 280 B; SURVEY §8(d)'s model of a
 sort without a separate histogram read (8 x 24 + 16 = 208 B) is reported beside it.
 Usage: pmc_sort.py <out dir>   (expects <out>/{hash,lsd}_{fetch,write,hit}/ and *.log)"""
