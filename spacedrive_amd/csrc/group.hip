@@ -8,8 +8,8 @@
 // objects = #distinct keys.  LSD radix sort is stable and the values enter in ascending
 // idx order, so the head of every equal-key run carries the minimum idx.
 //
-// Sort pass = upsweep (per-tile digit histogram in LDS) -> row scan of the digit-major
-// [digit][tile] table (one workgroup per digit) -> scatter (stable wave-private ranking with
+// Sort pass = upsweep (per-tile digit counts in LDS, tile-major, plus per-block sums) ->
+// per-digit scan of the block sums -> scatter (stable wave-private ranking with
 // 8 ballots per item, the tile staged in LDS in digit order, runs written out coalesced).
 // All integer/byte work bound by HBM; nothing here is reshaped into a GEMM.
 #include <hip/hip_runtime.h>
@@ -30,79 +30,94 @@ __device__ __forceinline__ uint32_t digit_of(uint64_t k, uint32_t shift, uint32_
   return (uint32_t)(k >> shift) & mask;
 }
 
-// hist[d * ntiles + tile] = #keys of `tile` with digit d.  Every key of the tile is loaded
-// before the first count (16 loads in flight per lane); each wave counts into its own LDS
-// row (a quarter of the same-address LDS atomics of one shared row).
-extern "C" __global__ void __launch_bounds__(SORT_THREADS)
+// Digit counts, tile-major: hist[tile * RADIX + d] = #keys of `tile` with digit d (one
+// coalesced 1-KB row per tile; a digit-major store was 256 sectors per tile), and per BLOCK of
+// UP_TILES tiles bsum[blk * RADIX + d] = the block's count.  One 256-thread group per tile (a
+// block's tiles are counted side by side: as many waves in flight as one workgroup per tile);
+// each tile's keys are loaded before its first count (16 loads in flight per lane); each wave
+// counts into its own LDS row.
+constexpr int UP_TILES = 4;
+constexpr int UP_THREADS = UP_TILES * SORT_THREADS;
+extern "C" __global__ void __launch_bounds__(UP_THREADS)
 sd_radix_upsweep(const uint64_t* __restrict__ keys, uint64_t n, uint32_t shift, uint32_t mask,
-                 uint32_t* __restrict__ hist, uint32_t ntiles) {
-  constexpr int WAVES = SORT_THREADS / 64;
+                 uint32_t* __restrict__ hist, uint32_t* __restrict__ bsum, uint32_t ntiles) {
+  constexpr int WAVES = UP_THREADS / 64;
   __shared__ uint32_t cnt[WAVES][RADIX];
-  const uint32_t t = threadIdx.x, w = t >> 6;
-#pragma unroll
-  for (int v = 0; v < WAVES; ++v) cnt[v][t] = 0;
-  const uint64_t base = (uint64_t)blockIdx.x * TILE;
+  __shared__ uint32_t tcount[UP_TILES][RADIX];
+  const uint32_t t = threadIdx.x, w = t >> 6, g = t / SORT_THREADS, d = t % SORT_THREADS;
+  const uint32_t tile = blockIdx.x * UP_TILES + g;
+  const uint64_t base = (uint64_t)tile * TILE;
   uint64_t kr[SORT_ROUNDS];
 #pragma unroll
   for (int r = 0; r < SORT_ROUNDS; ++r) {
-    const uint64_t i = base + (uint64_t)r * SORT_THREADS + t;
+    const uint64_t i = base + (uint64_t)r * SORT_THREADS + d;
     kr[r] = i < n ? keys[i] : 0ull;
   }
+#pragma unroll
+  for (int v = 0; v < SORT_THREADS / 64; ++v) cnt[g * (SORT_THREADS / 64) + v][d] = 0;
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < SORT_ROUNDS; ++r) {
-    const uint64_t i = base + (uint64_t)r * SORT_THREADS + t;
+    const uint64_t i = base + (uint64_t)r * SORT_THREADS + d;
     if (i < n) atomicAdd(&cnt[w][digit_of(kr[r], shift, mask)], 1u);
   }
   __syncthreads();
-  hist[(uint64_t)t * ntiles + blockIdx.x] = cnt[0][t] + cnt[1][t] + cnt[2][t] + cnt[3][t];
+  uint32_t x = 0;
+#pragma unroll
+  for (int v = 0; v < SORT_THREADS / 64; ++v) x += cnt[g * (SORT_THREADS / 64) + v][d];
+  if (tile < ntiles) hist[(uint64_t)tile * RADIX + d] = x;
+  tcount[g][d] = x;
+  __syncthreads();
+  if (g == 0) {
+    uint32_t tot = 0;
+#pragma unroll
+    for (int k = 0; k < UP_TILES; ++k) tot += tcount[k][d];
+    bsum[(uint64_t)blockIdx.x * RADIX + d] = tot;
+  }
 }
 
-// Row-local exclusive scan of the digit-major table, one workgroup per digit:
-// offs[d * ntiles + t] = sum of hist[d * ntiles + t'] for t' < t, rowtot[d] = the row's sum.
-// (The digit bases, the exclusive scan of rowtot over 256 digits, are taken by each scatter
-// workgroup itself: one launch per pass instead of three.)
-extern "C" __global__ void __launch_bounds__(SORT_THREADS)
-sd_radix_rowscan(const uint32_t* __restrict__ hist, uint32_t ntiles, uint32_t* __restrict__ offs,
-                 uint32_t* __restrict__ rowtot) {
-  __shared__ uint32_t wsum[SORT_THREADS / 64];
-  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-  const uint64_t row = (uint64_t)blockIdx.x * ntiles;
-  constexpr uint32_t PER = 8;  // elements per thread per chunk
-  uint32_t carry = 0;
-  for (uint32_t c0 = 0; c0 < ntiles; c0 += SORT_THREADS * PER) {
-    uint32_t v[PER], s = 0;
+// Exclusive scan of the block counts per digit, in place: bsum[b * RADIX + d] = digit d's
+// keys in blocks before b; rowtot[d] = digit d's total.  Workgroup g owns digits
+// [32g, 32g + 32), thread (seg, d) the seg-th of 32 contiguous block ranges of digit d: it sums
+// its range (loads independent, 128 B per row per wave), one LDS scan over the 32 ranges,
+// then it rewrites its range as running prefixes.  (The digit bases, the exclusive scan of
+// rowtot over 256 digits, are taken by each scatter workgroup itself.)
+constexpr int BSCAN_DIGITS = 32, BSCAN_SEGS = 32;
+extern "C" __global__ void __launch_bounds__(BSCAN_DIGITS * BSCAN_SEGS)
+sd_radix_blockscan(uint32_t* __restrict__ bsum, uint32_t nblk, uint32_t* __restrict__ rowtot) {
+  __shared__ uint32_t part[BSCAN_SEGS][BSCAN_DIGITS + 1];
+  const uint32_t dsub = threadIdx.x % BSCAN_DIGITS, seg = threadIdx.x / BSCAN_DIGITS;
+  const uint32_t d = blockIdx.x * BSCAN_DIGITS + dsub;
+  const uint32_t per = (nblk + BSCAN_SEGS - 1) / BSCAN_SEGS;
+  const uint32_t b0 = seg * per, b1 = min(nblk, b0 + per);
+  uint32_t s = 0;
+  for (uint32_t b = b0; b < b1; b += 8) {
+    uint32_t x[8];
 #pragma unroll
-    for (uint32_t k = 0; k < PER; ++k) {
-      const uint32_t j = c0 + t * PER + k;
-      v[k] = j < ntiles ? hist[row + j] : 0u;
-      s += v[k];
-    }
-    uint32_t inc = s;
+    for (int k = 0; k < 8; ++k) x[k] = b + k < b1 ? bsum[(uint64_t)(b + k) * RADIX + d] : 0u;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(inc, o, 64);
-      if (lane >= (uint32_t)o) inc += y;
-    }
-    if (lane == 63) wsum[w] = inc;
-    __syncthreads();
-    uint32_t pre = carry, tot = carry;
-#pragma unroll
-    for (int i = 0; i < SORT_THREADS / 64; ++i) {
-      if ((uint32_t)i < w) pre += wsum[i];
-      tot += wsum[i];
-    }
-    __syncthreads();
-    uint32_t run = pre + inc - s;
-#pragma unroll
-    for (uint32_t k = 0; k < PER; ++k) {
-      const uint32_t j = c0 + t * PER + k;
-      if (j < ntiles) offs[row + j] = run;
-      run += v[k];
-    }
-    carry = tot;
+    for (int k = 0; k < 8; ++k) s += x[k];
   }
-  if (t == 0) rowtot[blockIdx.x] = carry;
+  part[seg][dsub] = s;
+  __syncthreads();
+  uint32_t run = 0, tot = 0;
+  for (uint32_t k = 0; k < (uint32_t)BSCAN_SEGS; ++k) {
+    const uint32_t x = part[k][dsub];
+    if (k < seg) run += x;
+    tot += x;
+  }
+  // rewrite in batches: 8 independent loads, then their 8 stores
+  for (uint32_t b = b0; b < b1; b += 8) {
+    uint32_t x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = b + k < b1 ? bsum[(uint64_t)(b + k) * RADIX + d] : 0u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (b + k < b1) bsum[(uint64_t)(b + k) * RADIX + d] = run;
+      run += x[k];
+    }
+  }
+  if (seg == 0) rowtot[d] = tot;
 }
 
 // Stable scatter of one tile, wave-private ranking (round 5).  Wave w owns the contiguous
@@ -119,7 +134,8 @@ __device__ __forceinline__ void scatter_body(const uint64_t* __restrict__ keys_i
                                              uint64_t* __restrict__ keys_out,
                                              uint32_t* __restrict__ vals_out, uint64_t n,
                                              uint32_t shift, uint32_t mask,
-                                             const uint32_t* __restrict__ offs,
+                                             const uint32_t* __restrict__ hist,
+                                             const uint32_t* __restrict__ bsum,
                                              const uint32_t* __restrict__ rowtot,
                                              uint32_t ntiles) {
   constexpr int WAVES = SORT_THREADS / 64;
@@ -131,8 +147,10 @@ __device__ __forceinline__ void scatter_body(const uint64_t* __restrict__ keys_i
   __shared__ uint16_t tstart[RADIX];
   __shared__ uint32_t wsum[WAVES];
   const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-  const uint64_t idx = (uint64_t)t * ntiles + blockIdx.x;
-  const uint32_t mine = offs[idx];  // row-local: digit t's keys in earlier tiles
+  // digit t's keys in earlier tiles: earlier blocks (scanned) + this block's earlier tiles
+  const uint32_t blk = blockIdx.x / UP_TILES;
+  uint32_t mine = bsum[(uint64_t)blk * RADIX + t];
+  for (uint32_t tt = blk * UP_TILES; tt < blockIdx.x; ++tt) mine += hist[(uint64_t)tt * RADIX + t];
   const uint32_t rtot = rowtot[t];
   const uint64_t base = (uint64_t)blockIdx.x * TILE;
   const uint64_t wbase = base + (uint64_t)w * WAVE_ITEMS;
@@ -190,8 +208,8 @@ __device__ __forceinline__ void scatter_body(const uint64_t* __restrict__ keys_i
   }
   if (lane == 63) wsum[w] = inc;
   // conservation: the wave counts of digit t add up to the upsweep's count of it
-  SD_DBG_CHECK(cnt == (blockIdx.x + 1 < ntiles ? offs[idx + 1] : rtot) - mine,
-               "scatter tile %u digit %u: ranked %u", blockIdx.x, t, cnt);
+  SD_DBG_CHECK(cnt == hist[(uint64_t)blockIdx.x * RADIX + t], "scatter tile %u digit %u: ranked %u",
+               blockIdx.x, t, cnt);
   __syncthreads();
   uint32_t pre = 0;
   for (uint32_t i = 0; i < w; ++i) pre += wsum[i];
@@ -224,17 +242,20 @@ __device__ __forceinline__ void scatter_body(const uint64_t* __restrict__ keys_i
 extern "C" __global__ void __launch_bounds__(SORT_THREADS)
 sd_radix_scatter(const uint64_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
                  uint64_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out, uint64_t n,
-                 uint32_t shift, uint32_t mask, const uint32_t* __restrict__ offs,
-                 const uint32_t* __restrict__ rowtot, uint32_t ntiles) {
-  scatter_body<true>(keys_in, vals_in, keys_out, vals_out, n, shift, mask, offs, rowtot, ntiles);
+                 uint32_t shift, uint32_t mask, const uint32_t* __restrict__ hist,
+                 const uint32_t* __restrict__ bsum, const uint32_t* __restrict__ rowtot,
+                 uint32_t ntiles) {
+  scatter_body<true>(keys_in, vals_in, keys_out, vals_out, n, shift, mask, hist, bsum, rowtot,
+                     ntiles);
 }
 
 extern "C" __global__ void __launch_bounds__(SORT_THREADS)
 sd_radix_scatter_iota(const uint64_t* __restrict__ keys_in, uint64_t* __restrict__ keys_out,
                       uint32_t* __restrict__ vals_out, uint64_t n, uint32_t shift, uint32_t mask,
-                      const uint32_t* __restrict__ offs, const uint32_t* __restrict__ rowtot,
-                      uint32_t ntiles) {
-  scatter_body<false>(keys_in, nullptr, keys_out, vals_out, n, shift, mask, offs, rowtot, ntiles);
+                      const uint32_t* __restrict__ hist, const uint32_t* __restrict__ bsum,
+                      const uint32_t* __restrict__ rowtot, uint32_t ntiles) {
+  scatter_body<false>(keys_in, nullptr, keys_out, vals_out, n, shift, mask, hist, bsum, rowtot,
+                      ntiles);
 }
 
 // ---- device-wide exclusive scan (u32, sum) over m <= SCAN_TILE^2 elements ----------
@@ -511,9 +532,9 @@ static inline uint32_t tiles_of(uint64_t n, uint64_t tile) { return (uint32_t)((
 
 size_t sort_workspace_bytes(uint64_t n) {
   const uint64_t nt = tiles_of(n ? n : 1, TILE);
-  const uint64_t m = (uint64_t)RADIX * nt;
-  return align_up(n * 8, 256) + align_up(n * 4, 256) + 2 * align_up(m * 4, 256) +
-         align_up(RADIX * 4, 256) + 256;
+  const uint64_t nb = tiles_of(nt, UP_TILES);
+  return align_up(n * 8, 256) + align_up(n * 4, 256) + align_up(RADIX * nt * 4, 256) +
+         align_up(RADIX * nb * 4, 256) + align_up(RADIX * 4, 256) + 256;
 }
 
 size_t group_workspace_bytes(uint64_t n) {
@@ -546,12 +567,12 @@ hipError_t radix_sort_pairs(const uint64_t* keys_in, const uint32_t* vals_in, ui
   if (n >= (1ull << 32) || begin_bit < 0 || end_bit > 64 || end_bit <= begin_bit)
     return hipErrorInvalidValue;
   const uint32_t nt = tiles_of(n, TILE);
-  const uint64_t m = (uint64_t)RADIX * nt;
+  const uint32_t nb = tiles_of(nt, UP_TILES);
   char* p = (char*)ws;
   uint64_t* kalt = (uint64_t*)p; p += align_up(n * 8, 256);
   uint32_t* valt = (uint32_t*)p; p += align_up(n * 4, 256);
-  uint32_t* hist = (uint32_t*)p; p += align_up(m * 4, 256);
-  uint32_t* offs = (uint32_t*)p; p += align_up(m * 4, 256);
+  uint32_t* hist = (uint32_t*)p; p += align_up((uint64_t)RADIX * nt * 4, 256);
+  uint32_t* bsum = (uint32_t*)p; p += align_up((uint64_t)RADIX * nb * 4, 256);
   uint32_t* rowtot = (uint32_t*)p;
   const int passes = (end_bit - begin_bit + 7) / 8;
   const uint64_t* ksrc = keys_in;
@@ -563,12 +584,14 @@ hipError_t radix_sort_pairs(const uint64_t* keys_in, const uint32_t* vals_in, ui
     const bool to_out = ((passes - 1 - i) % 2) == 0;
     uint64_t* kdst = to_out ? keys_out : kalt;
     uint32_t* vdst = to_out ? vals_out : valt;
-    sd_radix_upsweep<<<nt, SORT_THREADS, 0, s>>>(ksrc, n, shift, mask, hist, nt);
-    sd_radix_rowscan<<<RADIX, SORT_THREADS, 0, s>>>(hist, nt, offs, rowtot);
+    sd_radix_upsweep<<<nb, UP_THREADS, 0, s>>>(ksrc, n, shift, mask, hist, bsum, nt);
+    sd_radix_blockscan<<<RADIX / BSCAN_DIGITS, BSCAN_DIGITS * BSCAN_SEGS, 0, s>>>(bsum, nb, rowtot);
     if (vsrc)
-      sd_radix_scatter<<<nt, SORT_THREADS, 0, s>>>(ksrc, vsrc, kdst, vdst, n, shift, mask, offs, rowtot, nt);
+      sd_radix_scatter<<<nt, SORT_THREADS, 0, s>>>(ksrc, vsrc, kdst, vdst, n, shift, mask, hist, bsum,
+                                                   rowtot, nt);
     else
-      sd_radix_scatter_iota<<<nt, SORT_THREADS, 0, s>>>(ksrc, kdst, vdst, n, shift, mask, offs, rowtot, nt);
+      sd_radix_scatter_iota<<<nt, SORT_THREADS, 0, s>>>(ksrc, kdst, vdst, n, shift, mask, hist, bsum,
+                                                        rowtot, nt);
     ksrc = kdst;
     vsrc = vdst;
   }
