@@ -2,19 +2,22 @@
 # Round-5 evidence pass: GPU suite (release, then the debug build's invariant checks), smoke,
 # headline bench (fused chain at N=1, live rocm-smi power in the line), the --gpus 8 one-GPU
 # rehearsal, BASELINE configs 1-4, the validator shapes, the link emission forms, rocprofv3
-# kernel stats of the bench and PMC passes on K1G (HBM bytes).  Usage: <tag> [skip-suite]
+# kernel stats of the bench and PMC passes on K1G (HBM bytes).
+# Usage: <tag> [skip-suite | suite]   (suite: the suites and smoke only; two calls fit gpurun)
 # Each GPU step has its own time limit; stop at the first failure.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/${1:-r5_final}
 mkdir -p $OUT
 cd $R
-if [ -z "$2" ]; then
+if [ "$2" != "skip-suite" ]; then
   timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -30 $OUT/pytest_gpu.log; exit 1; }
   tail -1 $OUT/pytest_gpu.log
   SD_HIP_CAS_LIB=$R/spacedrive_amd/libsd_hip_cas_debug.so SD_CAS_DEBUG_INVARIANTS=1 timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 600 --timeout-method thread > $OUT/pytest_gpu_debug.log 2>&1 || { echo DEBUG_FAIL; tail -30 $OUT/pytest_gpu_debug.log; exit 1; }
   tail -1 $OUT/pytest_gpu_debug.log
   timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo SMOKE_FAIL; exit 1; }
+  tail -1 $OUT/smoke.log
+  [ "$2" = "suite" ] && { echo SUITE_OK; exit 0; }
 fi
 timeout -k 10 400 python3 -u bench.py --steps 20 --warmup 3 > $OUT/bench.log 2>&1 || { echo BENCH_FAIL; tail -20 $OUT/bench.log; exit 1; }
 tail -1 $OUT/bench.log | cut -c1-300
