@@ -344,8 +344,10 @@ def test_from_paths_file_metadata_rules(eng, oracle, tmp_path):
 
 
 def test_sort_pairs_vs_numpy(eng):
+    """Tile (4,096 keys) and count-block (4 tiles) boundaries included: a block's last tile
+    partial, a lone tile in the last block, several scan batches per block range."""
     rng = np.random.default_rng(5)
-    for n in [1, 255, 4096, 4097, 100_003]:
+    for n in [1, 255, 4096, 4097, 16_383, 16_384, 16_385, 20_481, 100_003, 1_000_003]:
         k = rng.integers(0, 2 ** 64, n, dtype=np.uint64)
         k[: n // 3] = k[n // 2] if n > 2 else k[0]  # ties: stability matters
         ko = torch.empty(n, dtype=torch.int64, device="cuda")
