@@ -12,9 +12,10 @@
  *     reference, so this is a restatement of the published BLAKE3 spec, pinned by the
  *     reference's only in-repo BLAKE3 known answer (derive_key KAT,
  *     crates/crypto/src/keys/hashing.rs:210-213, 323-328), its six Balloon-BLAKE3
- *     KATs (hashing.rs:180-208), multi-chunk trees of 1-128 chunks against an
- *     independent BLAKE3 in the image (hf_xet's Rust crate, keyed mode:
- *     tests/golden/make_xet_vectors.py) and by independent tree formulations that must
+ *     KATs (hashing.rs:180-208), by the BLAKE3 team's C implementation (1.8.2, exported
+ *     by ROCm's libclang-cpp.so: tests/ext_blake3.py) at every tree shape up to 1 GiB, by
+ *     hf_xet's Rust BLAKE3 on trees of 1-128 chunks (keyed mode:
+ *     tests/golden/make_xet_vectors.py), and by independent tree formulations that must
  *     agree (incremental CV stack, recursive left-balanced, level-wise, threaded).
  *   - generate_cas_id message layout (core/src/object/cas.rs:10-61).
  *   - file_checksum (core/src/object/validation/hash.rs:11-25).

@@ -900,6 +900,68 @@ def test_device_blake3_runs_the_reference_balloon(eng, oracle):
         assert blk[-1] == oracle.balloon_blake3(pwd, salt, secret, s_cost, t_cost), secret is not None
 
 
+def test_device_kernels_vs_independent_c_blake3(eng, tmp_path):
+    """The product's kernels against the BLAKE3 team's C implementation (1.8.2, exported by
+    ROCm's libclang-cpp.so; tests/ext_blake3.py) with no oracle in between: K1 (8,192 sampled
+    files), K2 (140,000 ragged whole-file messages: above the two-quanta crossover), the
+    latency path (3,000 whole files through the host entry), K3 (one 1 GiB + 7 device
+    buffer), K3b (a validator batch of small, mid and multi-MiB buffers) and the streamed
+    file path (a 300 MB file, one call and the batch call)."""
+    from tests import ext_blake3 as ext
+    if not ext.available():
+        pytest.skip("no libclang-cpp.so with the BLAKE3 C API in this image")
+    rng = np.random.default_rng(91)
+    # K1
+    n = 8192
+    content = rng.integers(0, 256, (n, SAMPLED_CONTENT_LEN), dtype=np.uint8)
+    sizes = rng.integers(MINIMUM_FILE_SIZE + 1, 2 ** 40, n, dtype=np.uint64)
+    keys = torch.zeros(n, dtype=torch.int64, device="cuda")
+    eng.hash_sampled(torch.from_numpy(content).cuda(), dev64(sizes), keys)
+    want = np.array([ext.cas_key(content[i], int(sizes[i])) for i in range(n)], dtype=np.uint64)
+    assert (host64(keys) == want).all()
+    # K2
+    lens = rng.integers(1, 8193, 140_000)
+    lens[:64] = [1, 63, 64, 65, 1016, 1017, 1024, 1025] * 8
+    arena = rng.integers(0, 256, int(((lens + 15) // 16 * 16).sum()) + 128, dtype=np.uint8)
+    offs = np.zeros(len(lens), dtype=np.uint64)
+    offs[1:] = np.cumsum((lens[:-1] + 15) // 16 * 16)
+    keys = torch.zeros(len(lens), dtype=torch.int64, device="cuda")
+    eng.hash_packed(torch.from_numpy(arena).cuda(), dev64(offs),
+                    torch.from_numpy(lens.astype(np.int32)).cuda(), dev64(lens.astype(np.uint64)), keys)
+    want = np.array([ext.cas_key(arena[int(o):int(o) + int(L)], int(L)) for o, L in zip(offs, lens)],
+                    dtype=np.uint64)
+    assert (host64(keys) == want).all()
+    # latency path, host entry
+    items = [(rng.integers(0, 256, int(L), dtype=np.uint8).tobytes(), int(L))
+             for L in rng.integers(1, MINIMUM_FILE_SIZE + 1, 3000)]
+    got = eng.generate_cas_keys(items)
+    assert [int(x) for x in got] == [ext.cas_key(c, L) for c, L in items]
+    # K3: one device buffer
+    big = torch.randint(0, 256, ((1 << 30) + 7,), dtype=torch.uint8, device="cuda")
+    assert eng.checksum_dev(big) == ext.blake3(big.cpu().numpy()).hex()
+    del big
+    # K3b: a validator batch
+    blens = np.concatenate([rng.integers(0, 16_385, 200), rng.integers(16_385, 2 << 20, 80),
+                            rng.integers(2 << 20, 40 << 20, 12)])
+    boffs = np.zeros(len(blens), dtype=np.int64)
+    boffs[1:] = np.cumsum((blens[:-1] + 15) // 16 * 16)
+    barena = torch.randint(0, 256, (int(boffs[-1] + blens[-1]) + 16,), dtype=torch.uint8, device="cuda")
+    out = torch.zeros((len(blens), 32), dtype=torch.uint8, device="cuda")
+    eng.checksums_dev(barena, torch.from_numpy(boffs).cuda(), torch.from_numpy(blens.astype(np.int64)).cuda(), out)
+    h = barena.cpu().numpy()
+    got = out.cpu().numpy()
+    for i, (o, L) in enumerate(zip(boffs, blens)):
+        assert got[i].tobytes() == ext.blake3(h[int(o):int(o) + int(L)]), (i, int(L))
+    # streamed file path
+    f = tmp_path / "big.bin"
+    data = rng.integers(0, 256, 300_000_123, dtype=np.uint8)
+    data.tofile(f)
+    want = ext.blake3(data).hex()
+    assert eng.file_checksum(str(f)) == want
+    digests, errs = eng.file_checksums([str(f)])
+    assert digests == [want] and int(errs[0]) == 0
+
+
 def test_device_trees_on_the_independently_pinned_lengths(eng, oracle):
     """The lengths whose trees hf_xet's BLAKE3 pins in the oracle (tests/golden/xet_blake3.json,
     1-128 chunks): the same contents through the product's three whole-message kernels — the

@@ -7,6 +7,9 @@ parity claim rests on it, it is pinned here:
   * public BLAKE3("") / BLAKE3("abc"),
   * multi-chunk trees (1-128 chunks, every chunk count) against an independent BLAKE3 in the
     image (hf_xet's Rust crate; tests/golden/make_xet_vectors.py),
+  * every tree shape up to 1 GiB, the cas messages, keyed/derive_key modes and file_checksum
+    against the BLAKE3 team's C implementation (1.8.2, exported by ROCm's libclang-cpp.so;
+    tests/ext_blake3.py),
   * three independent tree formulations + a pure-Python restatement agreeing,
   * cas.rs:35-58 offsets simulated literally,
   * grouping against a literal replay of identifier_job_step (mod.rs:98-350).
@@ -96,6 +99,69 @@ def test_blake3_live_against_hf_xet(oracle, tmp_path):
         draws.append((str(p), d))
     for (p, d), r in zip(draws, hf_xet.hash_files([p for p, _ in draws])):
         assert r.hash == xet_display(oracle.keyed_hash(bytes(32), oracle.keyed_hash(DATA_KEY, d))), len(d)
+
+
+needs_ext = pytest.mark.skipif(not __import__("tests.ext_blake3").ext_blake3.available(),
+                               reason="no libclang-cpp.so with the BLAKE3 C API in this image")
+
+
+@needs_ext
+def test_independent_c_blake3_binding(golden):
+    """The binding itself: public vectors and the reference's derive_key KAT
+    (crates/crypto/src/keys/hashing.rs:210-213) through the BLAKE3 team's C code."""
+    from tests import ext_blake3 as ext
+    assert ext.version().count(".") == 2
+    for s_, h in golden["blake3_public"].items():
+        assert ext.blake3(s_.encode()).hex() == h
+    kat = golden["derive_key_kat"]
+    assert ext.derive_key(kat["context"], bytes.fromhex(kat["material_hex"])).hex() == kat["expected_hex"]
+
+
+@needs_ext
+def test_oracle_trees_vs_independent_c_blake3(oracle, golden):
+    """Every tree shape the product builds, oracle vs the BLAKE3 team's C implementation:
+    the committed boundary lengths, every chunk count 1..300 with a ragged last chunk, 2^k
+    chunks and one byte either side up to 64 MiB (all four formulations where they are
+    fast), and a 1 GiB + 12,345-byte buffer through the threaded tree."""
+    from tests import ext_blake3 as ext
+    rng = np.random.default_rng(77)
+    buf = rng.integers(0, 256, (1 << 26) + 2, dtype=np.uint8)
+    lens = {r["len"] for r in golden["blake3_lengths"]["vectors"]}
+    lens |= {(c - 1) * 1024 + int(rng.integers(1, 1025)) for c in range(1, 301)}
+    for k in range(0, 17):
+        lens |= {1024 * 2 ** k - 1, 1024 * 2 ** k, 1024 * 2 ** k + 1}
+    for n in sorted(lens):
+        d = buf[:n].tobytes()
+        want = ext.blake3(d)
+        assert oracle.blake3(d) == want, n
+        if n <= 1 << 20:
+            assert oracle.blake3_recursive(d) == want and oracle.blake3_levelwise(d) == want, n
+        if n >= 1 << 22:
+            assert oracle.blake3_mt(buf[:n], 8) == want, n
+    big = rng.integers(0, 256, (1 << 30) + 12_345, dtype=np.uint8)
+    assert oracle.blake3_mt(big, 8) == ext.blake3(big)
+
+
+@needs_ext
+def test_oracle_cas_keyed_and_checksum_vs_independent_c_blake3(oracle, tmp_path):
+    """cas.rs's message (le64(size) || content) for both paths, the keyed mode the Xet
+    vectors use, and file_checksum (hash.rs's 1 MiB read loop) against the C implementation."""
+    from tests import ext_blake3 as ext
+    rng = np.random.default_rng(78)
+    for _ in range(200):
+        size = int(rng.integers(1, 2 ** 40)) if rng.random() < 0.5 else int(rng.integers(1, 102_401))
+        clen = SAMPLED_CONTENT_LEN if size > MINIMUM_FILE_SIZE else size
+        c = rng.integers(0, 256, clen, dtype=np.uint8).tobytes()
+        assert oracle.cas_key(c, size) == ext.cas_key(c, size), size
+    for n in [1, 1024, 1025, 65_537, 131_072]:
+        key = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert oracle.keyed_hash(key, d) == ext.keyed_hash(key, d), n
+    for n in [0, 1, (1 << 20) - 1, 1 << 20, (1 << 20) + 1, 5 * (1 << 20) + 3]:
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        p = tmp_path / f"f{n}"
+        p.write_bytes(d)
+        assert oracle.file_checksum(str(p)) == ext.blake3(d).hex(), n
 
 
 def test_public_vectors(oracle, golden):
