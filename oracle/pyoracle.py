@@ -282,6 +282,45 @@ def build_oracle(quiet: bool = True) -> str:
     return LIB_PATH
 
 
+EXT_PATH = os.path.join(HERE, "libext_b3.so")
+
+
+class ExtBlake3:
+    """The BLAKE3 team's C implementation (1.8.2, dlopened from ROCm's libclang-cpp.so by
+    oracle/ext_b3.c) run through cas.rs's per-file call sequence — bench.py's second CPU
+    baseline leg and a parity check; never the product."""
+
+    def __init__(self, path: str = EXT_PATH):
+        if not os.path.exists(path):
+            build_oracle()
+        L = ctypes.CDLL(path)
+        L.ext_b3_load.restype = ctypes.c_int
+        L.ext_b3_version.restype = ctypes.c_char_p
+        L.ext_b3_cas_keys_strided.restype = ctypes.c_int
+        L.ext_b3_cas_keys_strided.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                              ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                              ctypes.c_int]
+        if L.ext_b3_load() != 0:
+            raise OSError("libclang-cpp.so with the BLAKE3 C API not found")
+        self.L = L
+
+    def version(self) -> str:
+        return self.L.ext_b3_version().decode()
+
+    def cas_keys_strided(self, arena: np.ndarray, stride: int, clen: int, sizes,
+                         threads: int = 1) -> np.ndarray:
+        sz = _sizes_u64(sizes)
+        n = len(sz)
+        a = np.ascontiguousarray(arena, dtype=np.uint8)
+        assert n == 0 or a.size >= (n - 1) * stride + clen
+        out = np.zeros(n, dtype=np.uint64)
+        rc = self.L.ext_b3_cas_keys_strided(a.ctypes.data, stride, clen, sz.ctypes.data, n,
+                                            out.ctypes.data, threads)
+        if rc != 0:
+            raise OSError("ext_b3_cas_keys_strided failed")
+        return out
+
+
 def _sizes_u64(sizes) -> np.ndarray:
     """Sizes as u64; a negative entry of a signed array is refused instead of wrapping to
     2^64 - 1 (the same check as the product wrapper's, spacedrive_amd/cas.py)."""

@@ -78,6 +78,29 @@ def test_cpu_baseline_threads(monkeypatch):
     assert bench.cpu_model() is None or isinstance(bench.cpu_model(), str)
 
 
+def test_official_c_leg():
+    """The CPU baseline's second leg: cas.rs's per-file sequence through the BLAKE3 team's C
+    library (oracle/ext_b3.c) — its keys equal the oracle's and it reports its library."""
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    import bench
+    from oracle.pyoracle import ExtBlake3, Oracle
+    try:
+        ExtBlake3()
+    except OSError:
+        import pytest
+        pytest.skip("no libclang-cpp.so with the BLAKE3 C API in this image")
+    rng = np.random.default_rng(3)
+    host = rng.integers(0, 256, (64, 57344), dtype=np.uint8)
+    hs = rng.integers(102_401, 2 ** 40, 64, dtype=np.uint64)
+    gk = Oracle().fast_cas_keys_strided(host.reshape(-1), 57344, 57344, hs, 2)
+    leg = bench.official_c_leg(host, hs, gk, 2, 0.1)
+    assert leg["parity_vs_gpu"] and leg["value"] > 0 and leg["value_1thread"] > 0
+    assert "libclang-cpp.so" in leg["library"] and leg["threads"] == 2
+    leg = bench.official_c_leg(host, hs, gk ^ np.uint64(1), 2, 0.05)
+    assert not leg["parity_vs_gpu"]
+
+
 def test_smi_sampler_and_session_evidence(monkeypatch):
     """bench.py's live power sampling picks THIS rank's card by PCI bus (never another card's
     numbers when several are listed and none matches) and tolerates a missing or garbled

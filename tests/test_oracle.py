@@ -164,6 +164,23 @@ def test_oracle_cas_keyed_and_checksum_vs_independent_c_blake3(oracle, tmp_path)
         assert oracle.file_checksum(str(p)) == ext.blake3(d).hex(), n
 
 
+@needs_ext
+def test_ext_b3_harness_matches_oracle(oracle):
+    """bench.py's second CPU leg (oracle/ext_b3.c: the C implementation run through cas.rs's
+    per-file sequence on pthreads) computes the same keys as the oracle's AVX-512 port."""
+    from oracle.pyoracle import ExtBlake3
+    ext = ExtBlake3()
+    rng = np.random.default_rng(79)
+    n = 300
+    arena = rng.integers(0, 256, n * SAMPLED_CONTENT_LEN, dtype=np.uint8)
+    sizes = rng.integers(MINIMUM_FILE_SIZE + 1, 2 ** 40, n, dtype=np.uint64)
+    want = oracle.fast_cas_keys_strided(arena, SAMPLED_CONTENT_LEN, SAMPLED_CONTENT_LEN, sizes, 4)
+    for threads in (1, 3, 8):
+        got = ext.cas_keys_strided(arena, SAMPLED_CONTENT_LEN, SAMPLED_CONTENT_LEN, sizes, threads)
+        assert (got == want).all(), threads
+    assert ext.version().count(".") == 2
+
+
 def test_public_vectors(oracle, golden):
     for s, h in golden["blake3_public"].items():
         assert oracle.blake3(s.encode()).hex() == h
