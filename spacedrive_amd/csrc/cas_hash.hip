@@ -12,8 +12,8 @@
 // cross-lane traffic.  For the whole-file path files are pre-sorted by message length
 // (on-device key sort) so the lanes of a wave finish together.
 //
-// Memory: each lane streams its message one 128-B line (a block pair, 8 x
-// global_load_dwordx4) at a time, prefetched one pair ahead.  The le64(size) prefix
+// Memory: each lane streams its message in 128-B lines (a block pair, 8 x
+// global_load_dwordx4), two lines per loop iteration.  The le64(size) prefix
 // shifts the content by exactly two 32-bit words, which becomes register renaming (a
 // 2-word carry), not byte shuffling.
 //
@@ -34,11 +34,12 @@ namespace sdcas {
 // tail chunk.  A lane fetches one whole 128-B line (a block pair, 8 x dwordx4 issued back
 // to back) per batch, so each line is consumed while it is still in L2 (fetching 64 B per
 // block let the other half be evicted between blocks and doubled the HBM traffic), and
-// the next pair is already in flight while the current one is compressed.  The two pair
-// buffers ping-pong in registers (A, B) — no moves, no early waits.
+// both lines of an iteration are in flight together (16 x dwordx4); the other waves of the
+// SIMD cover their latency.
 
 constexpr uint32_t SAMPLED_PAIRS = SAMPLED_CONTENT_LEN / 128;  // 448
 constexpr uint32_t SAMPLED_CHUNKS = SAMPLED_CONTENT_LEN / 1024;  // 56 full chunks
+static_assert(SAMPLED_PAIRS == 8 * SAMPLED_CHUNKS, "the sampled content is whole chunks of 8 lines");
 
 // One 128-B line (block pair P) of the lane's content: 8 x dwordx4 issued back to back.
 // (The A/B variants — non-temporal loads, 1.6x slower; 64-file tiled LINE / QUAD layouts —
@@ -97,16 +98,19 @@ __device__ __forceinline__ uint64_t cas_lane_sampled(const uint4* __restrict__ q
                                                      LdsStack<BLK>& stk) {
   uint32_t c0 = (uint32_t)size, c1 = (uint32_t)(size >> 32);
   uint4 A[8], B[8];
-  load_pair(q, 0, A);
   uint32_t cv[8];
   for (uint32_t c = 0; c < SAMPLED_CHUNKS; ++c) {
     set_iv(cv);
 #pragma unroll 1
     for (uint32_t pp = 0; pp < 4; ++pp) {  // 4 x (pair A, pair B) = 16 blocks
+      // both lines at the iteration start: a pair prefetched across the back edge was
+      // renamed and copied back (32 v_mov_b64 per iteration, 687.5 VALU instructions per
+      // compression); the load latency is covered by the SIMD's other three waves
+      // (681.5 per compression, +0.3-0.5 %: profiles/r05/ab_k1_prefetch/)
       const uint32_t P = 8u * c + 2u * pp;
+      load_pair(q, P, A);
       load_pair(q, P + 1, B);
       compress_pair(cv, A, c0, c1, c, pp == 0 ? (uint32_t)CHUNK_START : 0u, 0u);
-      if (P + 2 < SAMPLED_PAIRS) load_pair(q, P + 2, A);
       compress_pair(cv, B, c0, c1, c, 0u, pp == 3 ? (uint32_t)CHUNK_END : 0u);
     }
     // left-balanced tree: merge while the completed-chunk count has trailing zeros
