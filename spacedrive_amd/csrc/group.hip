@@ -126,7 +126,7 @@ sd_radix_blockscan(uint32_t* __restrict__ bsum, uint32_t nblk, uint32_t* __restr
 // 16 rounds with no workgroup barrier: wrun[w][d] counts digit d among the wave's earlier
 // rounds (only wave w touches row w; one wave's LDS operations complete in program order).
 // One barrier then turns the four rows into tile slots: slot = tstart[d] + (digit d in
-// earlier waves) + the item's wave-local rank.  3 barriers per tile instead of 33, and 50 KB
+// earlier waves) + the item's wave-local rank.  3 barriers per tile instead of 33, and 52.7 KB
 // of LDS instead of 59 (3 workgroups per CU instead of 2).
 template <bool HAS_VALS>
 __device__ __forceinline__ void scatter_body(const uint64_t* __restrict__ keys_in,
