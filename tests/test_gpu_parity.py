@@ -1055,7 +1055,11 @@ def test_checksum_device_over_4gib(eng, oracle):
         # the device generator is the oracle's stream, at the start and past 2^32
         for off in (0, (L - 4096) & ~7):  # the last window lies past 2^32
             assert (buf[off:off + 4096].cpu().numpy() == oracle.fill_content_range(55, 3, off, 4096)).all()
-        assert eng.checksum_dev(buf, L) == oracle.stream_blake3_mt(55, 3, L, ORC_THREADS).hex(), L
+        got = eng.checksum_dev(buf, L)
+        assert got == oracle.stream_blake3_mt(55, 3, L, ORC_THREADS).hex(), L
+        from tests import ext_blake3 as ext
+        if ext.available():  # and the BLAKE3 team's C implementation on the same bytes
+            assert got == ext.blake3(buf[:L].cpu().numpy()).hex(), L
         del buf
         torch.cuda.empty_cache()
 
@@ -1075,6 +1079,9 @@ def test_file_checksum_streamed_multi_gib(eng, oracle, tmp_path):
         want = oracle.stream_blake3_mt(56, 4, L, ORC_THREADS).hex()
         assert eng.file_checksum(path) == want
         assert oracle.file_checksum_mt(path, ORC_THREADS) == want
+        from tests import ext_blake3 as ext
+        if ext.available():  # the file's bytes through the BLAKE3 team's C implementation
+            assert ext.blake3(np.memmap(path, dtype=np.uint8, mode="r")).hex() == want
     finally:
         if os.path.exists(path):
             os.unlink(path)
