@@ -13,10 +13,15 @@
  */
 #define _GNU_SOURCE
 #include <dlfcn.h>
+#include <errno.h>
+#include <fcntl.h>
 #include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
+
+#include "oracle.h" /* orc_gather_path: cas.rs's reads (liboracle_cas.so) */
 
 #define EXT_B3_LIB "/opt/rocm/lib/llvm/lib/libclang-cpp.so"
 #define HASHER_BYTES 4096 /* sizeof(llvm_blake3_hasher) is 1,912 */
@@ -96,4 +101,94 @@ int ext_b3_cas_keys_strided(const uint8_t* arena, uint64_t stride, uint64_t clen
   free(th);
   free(js);
   return 0;
+}
+
+/* ---- the paths forms: the reference's reads, the C library's hashing ------------------ */
+
+/* hash.rs:11-25 streamed: one hasher, read(1 MiB) and update with what was read, stop at
+ * the first read shorter than 1 MiB.  out: 64 hex + NUL.  0 ok, -errno, -1000 no library. */
+int ext_b3_file_checksum(const char* path, char out[65]) {
+  enum { BLOCK_LEN = 1 << 20 };
+  if (ext_b3_load()) return -1000;
+  int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return -errno;
+  uint8_t* buf = malloc(BLOCK_LEN);
+  _Alignas(64) uint8_t hasher[HASHER_BYTES];
+  b3_init(hasher);
+  for (;;) {
+    ssize_t r;
+    do { r = read(fd, buf, BLOCK_LEN); } while (r < 0 && errno == EINTR);
+    if (r < 0) { int e = -errno; free(buf); close(fd); return e; }
+    b3_update(hasher, buf, (size_t)r);
+    if (r != BLOCK_LEN) break;
+  }
+  close(fd);
+  free(buf);
+  uint8_t h[32];
+  b3_finalize(hasher, h, 32);
+  static const char* hx = "0123456789abcdef";
+  for (int i = 0; i < 32; i++) { out[2 * i] = hx[h[i] >> 4]; out[2 * i + 1] = hx[h[i] & 15]; }
+  out[64] = 0;
+  return 0;
+}
+
+typedef struct {
+  const char* const* paths; const uint64_t* sizes; size_t n; int t, threads;
+  char* hex; uint64_t* keys; int32_t* status;
+} pjob;
+
+static void* sums_worker(void* p) {
+  pjob* j = (pjob*)p;
+  for (size_t i = (size_t)j->t; i < j->n; i += (size_t)j->threads)
+    j->status[i] = ext_b3_file_checksum(j->paths[i], j->hex + 65 * i);
+  return NULL;
+}
+
+static void* keys_worker(void* p) {
+  pjob* j = (pjob*)p;
+  const size_t cap = ORC_MINIMUM_FILE_SIZE + 1 > ORC_SAMPLED_CONTENT_LEN ? ORC_MINIMUM_FILE_SIZE + 1
+                                                                         : ORC_SAMPLED_CONTENT_LEN;
+  uint8_t* buf = malloc(cap);
+  for (size_t i = (size_t)j->t; i < j->n; i += (size_t)j->threads) {
+    const int64_t got = orc_gather_path(j->paths[i], j->sizes[i], buf, cap);
+    if (got < 0) { j->keys[i] = 0; j->status[i] = (int32_t)got; continue; }
+    j->keys[i] = cas_key(buf, (size_t)got, j->sizes[i]);
+    j->status[i] = 0;
+  }
+  free(buf);
+  return NULL;
+}
+
+static int run_paths(pjob proto, void* (*fn)(void*)) {
+  if (ext_b3_load()) return -1;
+  int threads = proto.threads < 1 ? 1 : proto.threads;
+  pthread_t* th = calloc((size_t)threads, sizeof *th);
+  pjob* js = calloc((size_t)threads, sizeof *js);
+  for (int t = 0; t < threads; t++) {
+    js[t] = proto;
+    js[t].t = t;
+    js[t].threads = threads;
+    if (t) pthread_create(&th[t], NULL, fn, &js[t]);
+  }
+  fn(&js[0]);
+  for (int t = 1; t < threads; t++) pthread_join(th[t], NULL);
+  free(th);
+  free(js);
+  return 0;
+}
+
+/* The validator over many files, files interleaved over `threads` pthreads (each file one
+ * hash.rs call).  hex: n x 65 bytes; status[i] 0 or -errno. */
+int ext_b3_file_checksums(const char* const* paths, size_t n, int threads, char* hex, int32_t* status) {
+  pjob proto = {paths, NULL, n, 0, threads, hex, NULL, status};
+  return run_paths(proto, sums_worker);
+}
+
+/* cas.rs:23-62 per path: the reference's reads (orc_gather_path: whole file at or below
+ * 100 KiB, else header / 4 samples / footer at the cas.rs offsets), then Hasher::new,
+ * update(le64(size)), update(content), finalize through the C library. */
+int ext_b3_cas_keys_paths(const char* const* paths, const uint64_t* sizes, size_t n, int threads,
+                          uint64_t* keys, int32_t* status) {
+  pjob proto = {paths, sizes, n, 0, threads, NULL, keys, status};
+  return run_paths(proto, keys_worker);
 }

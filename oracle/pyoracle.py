@@ -300,12 +300,54 @@ class ExtBlake3:
         L.ext_b3_cas_keys_strided.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                               ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                                               ctypes.c_int]
+        L.ext_b3_file_checksum.restype = ctypes.c_int
+        L.ext_b3_file_checksum.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        L.ext_b3_file_checksums.restype = ctypes.c_int
+        L.ext_b3_file_checksums.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                            ctypes.c_void_p, ctypes.c_void_p]
+        L.ext_b3_cas_keys_paths.restype = ctypes.c_int
+        L.ext_b3_cas_keys_paths.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                            ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         if L.ext_b3_load() != 0:
             raise OSError("libclang-cpp.so with the BLAKE3 C API not found")
         self.L = L
 
     def version(self) -> str:
         return self.L.ext_b3_version().decode()
+
+    def file_checksum(self, path: str) -> str:
+        """hash.rs:11-25 streamed (1 MiB reads, one hasher) through the C library."""
+        out = ctypes.create_string_buffer(65)
+        rc = self.L.ext_b3_file_checksum(os.fsencode(path), out)
+        if rc != 0:
+            raise OSError(-rc, os.strerror(-rc) if rc > -1000 else "no library", path)
+        return out.value.decode()
+
+    def file_checksums(self, paths, threads: int = 1):
+        """(hex digest or None, -errno) per path, files interleaved over `threads`."""
+        n = len(paths)
+        keep = [os.fsencode(p) for p in paths]
+        parr = (ctypes.c_char_p * max(n, 1))(*keep)
+        hexbuf = ctypes.create_string_buffer(65 * max(n, 1))
+        status = np.zeros(n, dtype=np.int32)
+        if self.L.ext_b3_file_checksums(ctypes.cast(parr, ctypes.c_void_p), n, int(threads), hexbuf,
+                                        status.ctypes.data) != 0:
+            raise OSError("ext_b3_file_checksums failed")
+        raw = hexbuf.raw
+        return [None if status[i] else raw[65 * i:65 * i + 64].decode() for i in range(n)], -status
+
+    def cas_keys_paths(self, paths, sizes, threads: int = 1):
+        """(keys u64, status -errno): cas.rs's reads, then the C library's hashing."""
+        n = len(paths)
+        keep = [os.fsencode(p) for p in paths]
+        parr = (ctypes.c_char_p * max(n, 1))(*keep)
+        sz = _sizes_u64(sizes)
+        keys = np.zeros(n, dtype=np.uint64)
+        status = np.zeros(n, dtype=np.int32)
+        if self.L.ext_b3_cas_keys_paths(ctypes.cast(parr, ctypes.c_void_p), sz.ctypes.data, n,
+                                        int(threads), keys.ctypes.data, status.ctypes.data) != 0:
+            raise OSError("ext_b3_cas_keys_paths failed")
+        return keys, status
 
     def cas_keys_strided(self, arena: np.ndarray, stride: int, clen: int, sizes,
                          threads: int = 1) -> np.ndarray:

@@ -181,6 +181,34 @@ def test_ext_b3_harness_matches_oracle(oracle):
     assert ext.version().count(".") == 2
 
 
+@needs_ext
+def test_ext_b3_path_forms_match_oracle(oracle, tmp_path):
+    """The paths legs of the CPU baselines (oracle/ext_b3.c): hash.rs's streamed loop and
+    cas.rs's reads + the C library's hashing agree with the oracle file by file."""
+    from oracle.pyoracle import ExtBlake3
+    ext = ExtBlake3()
+    rng = np.random.default_rng(80)
+    paths, sizes = [], []
+    for i, n in enumerate([0, 1, 1000, 102_400, 102_401, (1 << 20) - 1, 1 << 20, (1 << 20) + 1,
+                           3 * (1 << 20) + 5]):
+        p = tmp_path / f"f{i}"
+        p.write_bytes(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+        paths.append(str(p))
+        sizes.append(n)
+    paths.append(str(tmp_path / "missing"))
+    sizes.append(5)
+    for threads in (1, 4):
+        hexes, errs = ext.file_checksums(paths, threads)
+        for p, h, e in zip(paths, hexes, errs):
+            if p.endswith("missing"):
+                assert h is None and e == 2
+            else:
+                assert h == oracle.file_checksum(p) == ext.file_checksum(p), p
+        keys, st = ext.cas_keys_paths(paths, sizes, threads)
+        want, wst = oracle.generate_cas_keys_paths(paths, sizes, 2)
+        assert (keys[:-1] == want[:-1]).all() and st[-1] == wst[-1] != 0
+
+
 def test_public_vectors(oracle, golden):
     for s, h in golden["blake3_public"].items():
         assert oracle.blake3(s.encode()).hex() == h

@@ -95,7 +95,30 @@ def config1(eng, orc, n_files: int, root: str):
                 ts.append(time.perf_counter() - t)
                 ok = ok and bool((k == keys[i:i + 100]).all())
             cpu_step[name] = {"mean": float(np.mean(ts)) * 1e3, "median": float(np.median(ts)) * 1e3}
-        emit({"config": 1, "files": n_files, "bytes_on_disk": total,
+        # the BLAKE3 team's C library after cas.rs's reads (what the crate's SIMD does per
+        # file): one thread, all cores, and the 100-path step on all cores
+        official = None
+        try:
+            from oracle.pyoracle import ExtBlake3
+            ext = ExtBlake3()
+            t = time.perf_counter()
+            ko1, _ = ext.cas_keys_paths(paths, sizes, 1)
+            o1 = time.perf_counter() - t
+            t = time.perf_counter()
+            kon, _ = ext.cas_keys_paths(paths, sizes, THREADS)
+            on = time.perf_counter() - t
+            ts = []
+            for i in range(0, n_files, 100):
+                t = time.perf_counter()
+                ext.cas_keys_paths(paths[i:i + 100], sizes[i:i + 100], THREADS)
+                ts.append(time.perf_counter() - t)
+            official = {"library": f"BLAKE3 C {ext.version()} (libclang-cpp.so)",
+                        "files_per_s_1thread": n_files / o1, "files_per_s_all_cores": n_files / on,
+                        "step_100_ms_all_cores_median": round(float(np.median(ts)) * 1e3, 3),
+                        "parity": bool((ko1 == keys).all() and (kon == keys).all())}
+        except OSError:
+            pass
+        emit({"config": 1, "files": n_files, "bytes_on_disk": total, "cpu_official_c": official,
               "small_fraction": float((sizes <= 102400).mean()),
               "gpu_dropin_files_per_s": n_files / gpu, "gpu_s": gpu, "gpu_s_first_call": gpu_cold,
               "job_step_100_ms": {k: round(v, 3) for k, v in step.items()},
@@ -342,10 +365,20 @@ def config5(eng, orc, gib: float, file_mb: int):
         t = time.perf_counter()
         wm = orc.file_checksum_mt(path, THREADS)
         cpum = time.perf_counter() - t
+        official = None
+        try:  # hash.rs's loop with the BLAKE3 team's C library (the crate's speed, 1 thread)
+            from oracle.pyoracle import ExtBlake3
+            ext = ExtBlake3()
+            t = time.perf_counter()
+            wo = ext.file_checksum(path)
+            official = {"library": f"BLAKE3 C {ext.version()} (libclang-cpp.so)",
+                        "cpu_1thread_gb_per_s": L / (time.perf_counter() - t) / 1e9, "parity": wo == h}
+        except OSError:
+            pass
         emit({"config": "5-file", "bytes": L, "gpu_seconds": dt, "gpu_gb_per_s": L / dt / 1e9,
               "cpu_oracle_1thread_gb_per_s": L / cpu1 / 1e9,
               "cpu_oracle_tree_parallel_gb_per_s": L / cpum / 1e9, "cpu_threads": THREADS,
-              "parity_full": h == w1 == wm})
+              "cpu_official_c": official, "parity_full": h == w1 == wm})
     finally:
         if os.path.exists(path):
             os.unlink(path)

@@ -127,12 +127,29 @@ def paths_run(eng, orc, n, root):
         allc = list(ex.map(orc.file_checksum, paths))
     cpun_s = time.perf_counter() - t
     parity = got == allc and got[:m1] == one and not any(errs)
+    # the same hash.rs loop with the BLAKE3 team's C library (SIMD, what the crate does)
+    official = None
+    try:
+        from oracle.pyoracle import ExtBlake3
+        ext = ExtBlake3()
+        t = time.perf_counter()
+        o1, _ = ext.file_checksums(paths[:m1], 1)
+        e1 = (time.perf_counter() - t) * n / m1
+        t = time.perf_counter()
+        on, _ = ext.file_checksums(paths, threads)
+        en = time.perf_counter() - t
+        official = {"library": f"BLAKE3 C {ext.version()} (libclang-cpp.so)",
+                    "cpu_1thread_gb_per_s": total / e1 / 1e9,
+                    "cpu_all_gb_per_s": total / en / 1e9, "parity": on == got and o1 == got[:m1]}
+    except OSError:
+        pass
     for p in paths:
         os.unlink(p)
     return {"files": n, "bytes": total, "gpu_s": gpu_s, "gpu_gb_per_s": total / gpu_s / 1e9,
             "gpu_files_per_s": n / gpu_s, "cpu_1thread_gb_per_s": total / cpu1_s / 1e9,
             "cpu_threads": threads, "cpu_all_gb_per_s": total / cpun_s / 1e9,
-            "parity": bool(parity)}
+            "cpu_note": "cpu_* = the oracle's portable C (scalar); official_c = the C library",
+            "official_c": official, "parity": bool(parity)}
 
 
 def main():
