@@ -934,7 +934,7 @@ def official_c_leg(host, hs, gk, threads: int, seconds: float):
     try:
         from oracle.pyoracle import ExtBlake3
         ext = ExtBlake3()
-    except OSError:
+    except Exception:  # no libclang-cpp.so, or the harness could not be built: no leg
         return None
     m = host.shape[0]
     t0 = time.perf_counter()
