@@ -211,6 +211,84 @@ def replay_identifier_job(keys, states, chunk: int = 100, with_creates: bool = F
     return step, obj, act, counts
 
 
+# ---- the link emission's closed form, vectorised (large jobs; sd_cas_identifier_links_ex):
+# a hashed row's Object = min(seeds of its key, Objects of its key's rows in steps <= its own);
+# else CREATED in its key's first step, LINKED to that first row after.  Equal to the literal
+# replay above (tests/test_oracle.py::test_pre_object_closed_form_vs_replay pins the scalar
+# form; tools/stress_links.py checks this one against the replay on small jobs).
+_NONE = 0xFFFFFFFF
+
+
+def cursor_walk(states, n, chunk):
+    """Per-row final step (_NONE if unreached) and the job's step starts (the reference's
+    `id >= cursor` query; a chunk's last row that stays orphan is queried again)."""
+    steps_total = -(-n // chunk)
+    starts = []
+    start, reached = 0, 0
+    for _ in range(steps_total):
+        if start >= n:
+            break
+        starts.append(start)
+        end = min(start + chunk, n)
+        reached = end
+        start = end - 1 if states[end - 1] != 0 else end
+    step = np.full(n, _NONE, np.int64)
+    for k, s in enumerate(starts):
+        e = starts[k + 1] if k + 1 < len(starts) else reached
+        step[s:e] = k
+    return step, starts, reached
+
+
+def closed_form(keys, states, pre, seeds, step, starts=None):
+    """Vectorised: per hashed row, min(seeds of its key, the Objects of its key's rows in
+    steps <= its step); else CREATED in its key's first step, LINKED to the first row after."""
+    n = len(keys)
+    obj = np.full(n, _NONE, np.int64)
+    act = np.full(n, 3, np.int64)
+    act[(step != _NONE) & (states == 2)] = 2
+    nc = (step != _NONE) & (states == 1)
+    act[nc] = 0
+    obj[nc] = np.flatnonzero(nc)
+    rows = np.flatnonzero((states == 0) & (step != _NONE))
+    if len(rows) == 0:
+        return obj, act
+    rows = rows[np.lexsort((rows, keys[rows]))]          # (key, row) order
+    k = keys[rows]
+    st = step[rows]
+    m = len(rows)
+    head = np.r_[True, k[1:] != k[:-1]]
+    seg = np.cumsum(head) - 1
+    first = rows[np.flatnonzero(head)][seg]
+    # segmented running minimum of the rows' Objects (max-accumulate of seg * 2^33 + ~v)
+    BIG = np.int64(1) << 33
+    v = pre[rows].astype(np.int64)
+    w = np.maximum.accumulate(seg.astype(np.int64) * BIG + (BIG - 1 - v))
+    pm = BIG - 1 - (w - seg.astype(np.int64) * BIG)
+    # value at the end of each (key, step) run
+    end = np.flatnonzero(np.r_[(k[1:] != k[:-1]) | (st[1:] != st[:-1]), True])
+    target = pm[end[np.searchsorted(end, np.arange(m))]]
+    if seeds:
+        sk = np.array([x for x, _ in seeds], np.uint64)
+        so = np.array([o for _, o in seeds], np.int64)
+        o2 = np.lexsort((so, sk))
+        sk, so = sk[o2], so[o2]
+        sh = np.r_[True, sk[1:] != sk[:-1]]
+        uk, umin = sk[sh], so[sh]
+        pos = np.searchsorted(uk, k)
+        hit = (pos < len(uk)) & (uk[np.minimum(pos, len(uk) - 1)] == k)
+        target = np.where(hit, np.minimum(target, umin[np.minimum(pos, len(uk) - 1)]), target)
+    ex = target != _NONE
+    obj[rows[ex]] = target[ex]
+    act[rows[ex]] = 4
+    cr = ~ex & (st == step[first])
+    obj[rows[cr]] = rows[cr]
+    act[rows[cr]] = 0
+    ln = ~ex & ~cr
+    obj[rows[ln]] = first[ln]
+    act[rows[ln]] = 1
+    return obj, act
+
+
 def canonical(keys: list[int]):
     first = {}
     rep = []

@@ -1857,6 +1857,43 @@ def test_identifier_links_pre_objects_edges(eng):
     assert step.numel() == 0 and counts.shape == (0, 2)
 
 
+def test_identifier_links_job_at_library_scale(eng):
+    """One identifier job over 50 M rows (half of config 4's 100 M-file library as ONE job):
+    30 % duplicate keys, 2 % NO_CAS / ERROR rows (some at chunk ends: the cursor re-queries
+    them), 5 % of rows owning an Object, seeds for 1 % of keys; chunk 100 (500 k steps) — every
+    row's step, decision and owner vs the vectorised closed form of the replay
+    (tests/golden/make_golden.py::closed_form, pinned against the replay by a CPU test)."""
+    from tests.golden.make_golden import closed_form, cursor_walk
+    rng = np.random.default_rng(505)
+    n, chunk = 50_000_000, 100
+    uniq = rng.integers(1, 2 ** 64, int(n * 0.7), dtype=np.uint64)
+    keys = np.concatenate([uniq, uniq[rng.integers(0, len(uniq), n - len(uniq))]])
+    rng.shuffle(keys)
+    states = np.zeros(n, np.uint8)
+    bad = rng.random(n) < 0.02
+    states[bad] = rng.choice(np.array([1, 2], np.uint8), int(bad.sum()))
+    pre = np.full(n, 0xFFFFFFFF, np.uint32)
+    own = rng.random(n) < 0.05
+    ids = rng.permutation(1 << 30)[: int(own.sum()) + len(uniq) // 100]
+    pre[own] = ids[: int(own.sum())].astype(np.uint32)
+    sk = uniq[: len(uniq) // 100]
+    so = ids[int(own.sum()):int(own.sum()) + len(sk)].astype(np.uint32)
+    step, obj, act, counts = eng.identifier_links(
+        dev64(keys), torch.from_numpy(states).cuda(), chunk,
+        existing=(dev64(sk), torch.from_numpy(so.view(np.int32)).cuda()),
+        pre_objects=torch.from_numpy(pre.view(np.int32)).cuda())
+    wstep, starts, _ = cursor_walk(states, n, chunk)
+    assert (step.cpu().numpy().view(np.uint32).astype(np.int64) == wstep).all()
+    wo, wa = closed_form(keys, states, pre, list(zip(sk.tolist(), so.tolist())), wstep, starts)
+    assert (obj.cpu().numpy().view(np.uint32).astype(np.int64) == wo).all()
+    assert (act.cpu().numpy().astype(np.int64) == wa).all()
+    # per-step counts: every decided row once, plus a NO_CAS row a step re-queries (the
+    # cursor's last row stays orphan) created again — at most one per step
+    done = int(((wa == 0) | (wa == 1) | (wa == 4)).sum())
+    total = int(counts[:, 0].sum()) + int(counts[:, 1].sum())
+    assert done <= total <= done + len(starts) and len(counts) == len(starts)
+
+
 def test_identifier_links_pre_objects_hot_key_1m(eng):
     """The two scans at scale: 1M rows, one hot key over every chunk with pre-existing
     Objects whose ids decrease step by step (each step's minimum takes over), plus random

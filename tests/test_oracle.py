@@ -516,6 +516,30 @@ def closed_form_links(keys, states, step, chunk, existing=(), pre=None):
     return obj, act
 
 
+def test_vectorised_closed_form_vs_replay():
+    """The vectorised closed form the large GPU link tests check against
+    (tests/golden/make_golden.py::closed_form, cursor_walk) equals the literal replay on 150
+    random jobs: chunk 1..19, NO_CAS / ERROR rows, rows owning Objects, seeds."""
+    from tests.golden.make_golden import closed_form, cursor_walk, replay_identifier_job
+    rng = np.random.default_rng(33)
+    for it in range(150):
+        n = int(rng.integers(1, 300))
+        chunk = int(rng.integers(1, 20))
+        keys = rng.integers(1, max(2, n // 3), n).astype(np.uint64)
+        states = rng.choice(np.array([0, 1, 2], np.uint8), n, p=[0.9, 0.05, 0.05])
+        pre = np.full(n, 0xFFFFFFFF, np.uint32)
+        m = rng.random(n) < 0.2
+        pre[m] = rng.permutation(10 * n + 40)[:int(m.sum())]
+        uk = np.unique(keys)
+        seeds = [(int(k), int(10 * n + 100 + j)) for j, k in enumerate(uk[rng.random(len(uk)) < 0.2])]
+        step, starts, _ = cursor_walk(states, n, chunk)
+        o, a = closed_form(keys, states, pre, seeds, step, starts)
+        ws, wo, wa, _ = replay_identifier_job([int(k) for k in keys], [int(x) for x in states], chunk,
+                                              existing=seeds,
+                                              pre_objects=[None if x == 0xFFFFFFFF else int(x) for x in pre])
+        assert (np.array(ws) == step).all() and (np.array(wo) == o).all() and (np.array(wa) == a).all(), it
+
+
 @pytest.mark.parametrize("chunk", [100, 7, 3, 1])
 def test_pre_object_closed_form_vs_replay(chunk):
     """The closed form behind sd_cas_identifier_links_ex (per-key prefix minimum over steps)
