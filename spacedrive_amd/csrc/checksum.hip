@@ -562,15 +562,15 @@ constexpr int LANE_BLOCK = 256;
 constexpr size_t LANE_LDS_PAD = (160u << 10) / SD_LANE_WAVES - sizeof(uint32_t) * LANE_LDS_DEPTH * 8 * LANE_BLOCK;
 static_assert((160u << 10) / SD_LANE_WAVES >= sizeof(uint32_t) * LANE_LDS_DEPTH * 8 * LANE_BLOCK,
               "the lane stack fits the workgroup's LDS share");
-// SD_LANE_BLOCK_KEY=1: key on the exact 64-B block count inside the lane class (a wave's
-// lanes would share the last chunk's block count too) — 4 % faster on 1M U(0, 16) KiB buffers
-// (3.24 vs 3.37 ms) but 2.4x slower on 262,144 U(1, 128) KiB ones (14.9 vs 6.2 ms): small
-// block buckets scatter a wave over the arena (profiles/r04_ab_keys.log).  Off.
-#ifndef SD_LANE_BLOCK_KEY
-#define SD_LANE_BLOCK_KEY 0
-#endif
-constexpr int LANE_KEY_BITS = SD_LANE_BLOCK_KEY ? ilog2c(MID_CHUNKS * 16) + 1   // 0..4,096: 13 bits
-                                                : ilog2c(MID_CHUNKS) + 1;       // 0..256: 9 bits
+// The lane class's visiting key: the chunk count, or (block_key) the exact 64-B block count,
+// so a wave's lanes share the last chunk's length too.  The block key ran 4 % faster on 1M
+// U(0, 16) KiB buffers (3.24 vs 3.37 ms) but 2.4x slower on 262,144 U(1, 128) KiB ones (14.9
+// vs 6.2 ms): small block buckets scatter a wave over the arena (profiles/r04_ab_keys.log).
+// checksum_batch_device takes it when the arena averages <= LANE_BLOCK_KEY_MEAN bytes per
+// buffer (round 5).
+constexpr uint64_t LANE_BLOCK_KEY_MEAN = 16384;
+constexpr int LANE_KEY_BITS_BLOCKS = ilog2c(MID_CHUNKS * 16) + 1;  // 0..4,096: 13 bits
+constexpr int LANE_KEY_BITS_CHUNKS = ilog2c(MID_CHUNKS) + 1;       // 0..256: 9 bits
 
 struct LaneStack {
   uint32_t (*s)[8][LANE_BLOCK];
@@ -711,7 +711,8 @@ __device__ __forceinline__ void lane_digest(const uint4* __restrict__ q, uint32_
 // class sizes (wave sums, one atomic each per wave)
 extern "C" __global__ void __launch_bounds__(256)
 sd_b3_lane_keys(const uint64_t* __restrict__ offs, const uint64_t* __restrict__ lens, uint64_t n,
-                uint64_t arena_bytes, uint64_t* __restrict__ keys, uint32_t* __restrict__ info) {
+                uint64_t arena_bytes, int block_key, uint64_t* __restrict__ keys,
+                uint32_t* __restrict__ info) {
   __shared__ uint32_t part[4][4];
   uint32_t v[4] = {0u, 0u, 0u, 0u};  // <= 2^24 buffers x 128 chunks: fits u32
   for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < n;
@@ -719,7 +720,7 @@ sd_b3_lane_keys(const uint64_t* __restrict__ offs, const uint64_t* __restrict__ 
     const uint64_t len = lens[f];
     const uint64_t nch = chunks_of(len);
     const bool ok = nch <= MID_CHUNKS && buffer_ok(offs[f], len, arena_bytes);
-    if (SD_LANE_BLOCK_KEY) {
+    if (block_key) {
       const uint64_t blocks = len == 0 ? 1u : (len + 63u) >> 6;  // a 0-byte buffer: one block
       keys[f] = ok ? MID_CHUNKS * 16 - blocks : MID_CHUNKS * 16;
     } else {
@@ -944,9 +945,11 @@ hipError_t checksum_batch_device(const uint8_t* arena, uint64_t arena_bytes, con
     uint64_t* lkeys = (uint64_t*)p; p += al256c(n * 8);
     uint64_t* skeys = (uint64_t*)p; p += al256c(n * 8);
     order = (uint32_t*)p; p += al256c(n * 4);
-    sd_b3_lane_keys<<<std::min<uint32_t>(nb, 1024), 256, 0, s>>>(offs, lens, n, arena_bytes, lkeys,
-                                                               lane_info);
-    e = radix_sort_pairs(lkeys, nullptr, skeys, order, n, 0, LANE_KEY_BITS, p, s);
+    const bool block_key = arena_bytes <= n * LANE_BLOCK_KEY_MEAN;
+    sd_b3_lane_keys<<<std::min<uint32_t>(nb, 1024), 256, 0, s>>>(offs, lens, n, arena_bytes,
+                                                               block_key ? 1 : 0, lkeys, lane_info);
+    e = radix_sort_pairs(lkeys, nullptr, skeys, order, n, 0,
+                         block_key ? LANE_KEY_BITS_BLOCKS : LANE_KEY_BITS_CHUNKS, p, s);
     if (e != hipSuccess) return e;
     sd_b3_batch_lane<<<(uint32_t)((n + LANE_BLOCK - 1) / LANE_BLOCK), LANE_BLOCK, LANE_LDS_PAD, s>>>(
         arena, arena_bytes, offs, lens, order, n, lane_info, d_digests);
