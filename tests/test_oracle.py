@@ -90,7 +90,7 @@ def test_blake3_live_against_hf_xet(oracle, tmp_path):
     hashed live by hf_xet and by the oracle."""
     hf_xet = pytest.importorskip("hf_xet")
     from tests.golden.make_xet_vectors import DATA_KEY, xet_display
-    rng = np.random.default_rng(int.from_bytes(os.urandom(4), "little"))
+    rng = np.random.default_rng(2718)  # fixed: deterministic, still hashed live by hf_xet
     draws = []
     for i in range(24):
         d = rng.integers(0, 256, int(rng.integers(1, 8192)), dtype=np.uint8).tobytes()
