@@ -83,7 +83,7 @@ static void* worker(void* p) {
 }
 
 /* keys[i] = cas key of file i: content arena[i*stride, +clen), size sizes[i]; 0 ok, -1 no
- * library. */
+ * library, -ENOMEM. */
 int ext_b3_cas_keys_strided(const uint8_t* arena, uint64_t stride, uint64_t clen,
                             const uint64_t* sizes, size_t n, uint64_t* keys, int threads) {
   if (ext_b3_load()) return -1;
@@ -91,13 +91,18 @@ int ext_b3_cas_keys_strided(const uint8_t* arena, uint64_t stride, uint64_t clen
   if ((size_t)threads > n) threads = n ? (int)n : 1;
   pthread_t* th = malloc(sizeof(pthread_t) * (size_t)threads);
   job* js = malloc(sizeof(job) * (size_t)threads);
+  if (!th || !js) { free(th); free(js); return -ENOMEM; }
+  int started[threads];
   for (int t = 0; t < threads; t++) {
     js[t] = (job){arena, stride, clen, sizes, keys, n * (size_t)t / (size_t)threads,
                   n * (size_t)(t + 1) / (size_t)threads};
-    if (t) pthread_create(&th[t], NULL, worker, &js[t]);
+    started[t] = t && pthread_create(&th[t], NULL, worker, &js[t]) == 0;
   }
   worker(&js[0]);
-  for (int t = 1; t < threads; t++) pthread_join(th[t], NULL);
+  for (int t = 1; t < threads; t++) {
+    if (started[t]) pthread_join(th[t], NULL);
+    else worker(&js[t]);  /* a thread that could not start: its share on this thread */
+  }
   free(th);
   free(js);
   return 0;
@@ -113,6 +118,7 @@ int ext_b3_file_checksum(const char* path, char out[65]) {
   int fd = open(path, O_RDONLY | O_CLOEXEC);
   if (fd < 0) return -errno;
   uint8_t* buf = malloc(BLOCK_LEN);
+  if (!buf) { close(fd); return -ENOMEM; }
   _Alignas(64) uint8_t hasher[HASHER_BYTES];
   b3_init(hasher);
   for (;;) {
@@ -150,6 +156,7 @@ static void* keys_worker(void* p) {
                                                                          : ORC_SAMPLED_CONTENT_LEN;
   uint8_t* buf = malloc(cap);
   for (size_t i = (size_t)j->t; i < j->n; i += (size_t)j->threads) {
+    if (!buf) { j->keys[i] = 0; j->status[i] = -ENOMEM; continue; }
     const int64_t got = orc_gather_path(j->paths[i], j->sizes[i], buf, cap);
     if (got < 0) { j->keys[i] = 0; j->status[i] = (int32_t)got; continue; }
     j->keys[i] = cas_key(buf, (size_t)got, j->sizes[i]);
@@ -164,14 +171,19 @@ static int run_paths(pjob proto, void* (*fn)(void*)) {
   int threads = proto.threads < 1 ? 1 : proto.threads;
   pthread_t* th = calloc((size_t)threads, sizeof *th);
   pjob* js = calloc((size_t)threads, sizeof *js);
+  if (!th || !js) { free(th); free(js); return -ENOMEM; }
+  int started[threads > 0 ? threads : 1];
   for (int t = 0; t < threads; t++) {
     js[t] = proto;
     js[t].t = t;
     js[t].threads = threads;
-    if (t) pthread_create(&th[t], NULL, fn, &js[t]);
+    started[t] = t && pthread_create(&th[t], NULL, fn, &js[t]) == 0;
   }
   fn(&js[0]);
-  for (int t = 1; t < threads; t++) pthread_join(th[t], NULL);
+  for (int t = 1; t < threads; t++) {
+    if (started[t]) pthread_join(th[t], NULL);
+    else fn(&js[t]);  /* a thread that could not start: its share on this thread */
+  }
   free(th);
   free(js);
   return 0;

@@ -128,6 +128,19 @@ sd_radix_blockscan(uint32_t* __restrict__ bsum, uint32_t nblk, uint32_t* __restr
 // One barrier then turns the four rows into tile slots: slot = tstart[d] + (digit d in
 // earlier waves) + the item's wave-local rank.  3 barriers per tile instead of 33, and 52.7 KB
 // of LDS instead of 59 (3 workgroups per CU instead of 2).
+// Workgroups are dispatched to the 8 XCDs round-robin (workgroup b on XCD b % 8), and each
+// XCD has its own L2.  Tile t's digit-d run ends where tile t+1's begins, so when consecutive
+// tiles run on different XCDs the partial 32-B sectors at every run end are written back from
+// two L2s (PMC round 5: 219 B/key of scatter traffic for 192).  Round 6: workgroup b takes
+// tile xcd_tile(b) — XCD x holds the contiguous tile range [x*q + min(x, r), ...) — so the
+// neighbouring runs of the tiles an XCD runs side by side meet in ONE L2.  A permutation of
+// the tiles: the result does not depend on it.
+constexpr uint32_t XCDS = 8;
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nt) {
+  const uint32_t q = nt / XCDS, r = nt % XCDS, x = b % XCDS;
+  return x * q + min(x, r) + b / XCDS;
+}
+
 template <bool HAS_VALS>
 __device__ __forceinline__ void scatter_body(const uint64_t* __restrict__ keys_in,
                                              const uint32_t* __restrict__ vals_in,
@@ -137,7 +150,7 @@ __device__ __forceinline__ void scatter_body(const uint64_t* __restrict__ keys_i
                                              const uint32_t* __restrict__ hist,
                                              const uint32_t* __restrict__ bsum,
                                              const uint32_t* __restrict__ rowtot,
-                                             uint32_t ntiles) {
+                                             uint32_t ntiles, uint32_t* __restrict__ iota_out) {
   constexpr int WAVES = SORT_THREADS / 64;
   constexpr int WAVE_ITEMS = 64 * SORT_ROUNDS;
   __shared__ uint64_t skey[TILE];
@@ -147,12 +160,13 @@ __device__ __forceinline__ void scatter_body(const uint64_t* __restrict__ keys_i
   __shared__ uint16_t tstart[RADIX];
   __shared__ uint32_t wsum[WAVES];
   const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+  const uint32_t tile = xcd_tile(blockIdx.x, ntiles);
   // digit t's keys in earlier tiles: earlier blocks (scanned) + this block's earlier tiles
-  const uint32_t blk = blockIdx.x / UP_TILES;
+  const uint32_t blk = tile / UP_TILES;
   uint32_t mine = bsum[(uint64_t)blk * RADIX + t];
-  for (uint32_t tt = blk * UP_TILES; tt < blockIdx.x; ++tt) mine += hist[(uint64_t)tt * RADIX + t];
+  for (uint32_t tt = blk * UP_TILES; tt < tile; ++tt) mine += hist[(uint64_t)tt * RADIX + t];
   const uint32_t rtot = rowtot[t];
-  const uint64_t base = (uint64_t)blockIdx.x * TILE;
+  const uint64_t base = (uint64_t)tile * TILE;
   const uint64_t wbase = base + (uint64_t)w * WAVE_ITEMS;
   uint64_t kr[SORT_ROUNDS];
   uint32_t vr[SORT_ROUNDS];
@@ -161,6 +175,8 @@ __device__ __forceinline__ void scatter_body(const uint64_t* __restrict__ keys_i
     const uint64_t i = wbase + (uint64_t)r * 64 + lane;
     kr[r] = i < n ? keys_in[i] : 0ull;
     vr[r] = (HAS_VALS && i < n) ? vals_in[i] : (uint32_t)i;
+    // (the first pass of an iota sort can also lay down rep[i] = i for the runs kernel)
+    if (!HAS_VALS && iota_out && i < n) iota_out[i] = (uint32_t)i;
   }
 #pragma unroll
   for (int j = 0; j < RADIX / 64; ++j) wrun[w][lane + 64 * j] = 0;
@@ -208,8 +224,8 @@ __device__ __forceinline__ void scatter_body(const uint64_t* __restrict__ keys_i
   }
   if (lane == 63) wsum[w] = inc;
   // conservation: the wave counts of digit t add up to the upsweep's count of it
-  SD_DBG_CHECK(cnt == hist[(uint64_t)blockIdx.x * RADIX + t], "scatter tile %u digit %u: ranked %u",
-               blockIdx.x, t, cnt);
+  SD_DBG_CHECK(cnt == hist[(uint64_t)tile * RADIX + t], "scatter tile %u digit %u: ranked %u",
+               tile, t, cnt);
   __syncthreads();
   uint32_t pre = 0;
   for (uint32_t i = 0; i < w; ++i) pre += wsum[i];
@@ -246,16 +262,17 @@ sd_radix_scatter(const uint64_t* __restrict__ keys_in, const uint32_t* __restric
                  const uint32_t* __restrict__ bsum, const uint32_t* __restrict__ rowtot,
                  uint32_t ntiles) {
   scatter_body<true>(keys_in, vals_in, keys_out, vals_out, n, shift, mask, hist, bsum, rowtot,
-                     ntiles);
+                     ntiles, nullptr);
 }
 
 extern "C" __global__ void __launch_bounds__(SORT_THREADS)
 sd_radix_scatter_iota(const uint64_t* __restrict__ keys_in, uint64_t* __restrict__ keys_out,
                       uint32_t* __restrict__ vals_out, uint64_t n, uint32_t shift, uint32_t mask,
                       const uint32_t* __restrict__ hist, const uint32_t* __restrict__ bsum,
-                      const uint32_t* __restrict__ rowtot, uint32_t ntiles) {
+                      const uint32_t* __restrict__ rowtot, uint32_t ntiles,
+                      uint32_t* __restrict__ iota_out) {
   scatter_body<false>(keys_in, nullptr, keys_out, vals_out, n, shift, mask, hist, bsum, rowtot,
-                      ntiles);
+                      ntiles, iota_out);
 }
 
 // ---- device-wide exclusive scan (u32, sum) over m <= SCAN_TILE^2 elements ----------
@@ -317,139 +334,130 @@ sd_scan_tiles(const uint32_t* __restrict__ in, uint64_t m, uint32_t* __restrict_
 }
 
 // ---- grouping over the sorted pairs -------------------------------------------------
-// head position scan: hp[i] = max{ j <= i : key[j] != key[j-1] or j == 0 }.
-// Done per tile with a block max-scan, then the cross-tile carry is resolved by the
-// tiny per-tile "last head" array (sd_group_carry), then applied in sd_group_emit.
-__device__ __forceinline__ uint32_t block_inclusive_max(uint32_t x, uint32_t* total) {
-  __shared__ uint32_t wmax[SCAN_THREADS / 64];
+// Run heads + rep in ONE pass over the sorted pairs (round 6; round 5 ran tile heads -> a
+// single-workgroup carry scan -> emit, reading the keys twice and staging 52 KB of LDS per
+// workgroup).  Workgroup = one SCAN_TILE of sorted positions, wave w the contiguous quarter
+// [w*1024, (w+1)*1024) as 16 rounds of 64 consecutive positions (coalesced loads, all issued
+// up front).  A position is a head iff its key differs from its predecessor's (the previous
+// lane's by a shuffle, the previous round's last lane, or one load before the wave); a lane's
+// run head is the highest head lane at or below it (one ballot + clz), else the last head of
+// the wave's earlier rounds (a wave-uniform carry).  No LDS staging and no barrier in the
+// rounds; the positions of a wave before its first head (a run entering the wave, usually
+// none) are resolved after ONE barrier from the last head of an earlier wave, else from the
+// run entering the tile: its head is the key's FIRST position, a lower bound found by wave 0
+// galloping back from tile0 - 1 and bisecting (a few dependent loads for the short runs of
+// real libraries, ~2 log2(n) for one hot key, one if the key starts at position 0).
+// rep[v] = the head's val for every run member; PREFILLED: rep[v] == v already holds for
+// every val (the iota sort's first pass wrote it), so only members that are not heads store —
+// a library without duplicates writes nothing here.  The tile's head count goes to
+// tile_heads[] (the Object total, summed by sd_sum_u32_block).
+
+// first position of key K in the sorted keys, given skeys[hi] == K (hi < 2^32)
+__device__ uint32_t run_first(const uint64_t* __restrict__ skeys, uint64_t K, int64_t hi) {
+  if (skeys[0] == K) return 0;  // (one key everywhere: one load)
+  int64_t lo = 0, step = 1;     // invariant: skeys[lo] < K == skeys[hi]
+  for (;;) {
+    const int64_t j = hi - step;
+    if (j <= 0) break;
+    if (skeys[j] != K) { lo = j; break; }
+    hi = j;
+    step <<= 1;
+  }
+  while (hi - lo > 1) {
+    const int64_t mid = lo + (hi - lo) / 2;
+    if (skeys[mid] == K) hi = mid; else lo = mid;
+  }
+  return (uint32_t)hi;
+}
+
+constexpr uint32_t RUN_WAVES = SCAN_THREADS / 64;
+constexpr uint32_t RUN_ROUNDS = SCAN_TILE / SCAN_THREADS;  // 16 rounds of 64 per wave
+
+template <bool PREFILLED>
+__device__ __forceinline__ void group_runs_body(const uint64_t* __restrict__ skeys,
+                                                const uint32_t* __restrict__ svals, uint64_t n,
+                                                uint32_t* __restrict__ rep,
+                                                uint32_t* __restrict__ tile_heads) {
+  __shared__ uint32_t w_val[RUN_WAVES];    // the val of the wave's last head
+  __shared__ uint32_t w_has[RUN_WAVES];    // the wave holds a head
+  __shared__ uint32_t w_heads[RUN_WAVES];  // heads in the wave
+  __shared__ uint32_t tile_carry;          // the val of the head of the run entering the tile
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-  uint32_t inc = x;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(inc, o, 64);
-    if (lane >= (uint32_t)o) inc = max(inc, y);
-  }
-  if (lane == 63) wmax[w] = inc;
-  __syncthreads();
-  uint32_t pre = 0, tot = 0;
-#pragma unroll
-  for (int i = 0; i < SCAN_THREADS / 64; ++i) {
-    const uint32_t s = wmax[i];
-    if ((uint32_t)i < w) pre = max(pre, s);
-    tot = max(tot, s);
-  }
-  __syncthreads();
-  *total = tot;
-  return max(pre, inc);
-}
-
-// Run heads of one SCAN_TILE of sorted keys, in blocked order (thread t owns items
-// t*SCAN_ITEMS ..): bit k of the result = item k starts a run.  The keys are loaded striped
-// (coalesced) into LDS, one padding slot per SCAN_ITEMS so the blocked reads hit distinct
-// banks; a blocked global load made every load instruction touch 64 cache lines and read
-// 107-150 B/key from HBM for 8 (PMC, profiles/r01_pmc_group.json).
-constexpr uint32_t PADDED_TILE = SCAN_TILE + SCAN_TILE / SCAN_ITEMS + 1;
-__device__ __forceinline__ uint32_t padded(uint32_t i) { return i + i / SCAN_ITEMS; }
-
-__device__ __forceinline__ uint32_t tile_head_bits(const uint64_t* __restrict__ skeys, uint64_t n,
-                                                   uint64_t tile0, uint64_t* sk) {
-  // sk[padded(i) + 1] = key tile0 + i; sk[0] = the previous tile's last key
-#pragma unroll
-  for (int k = 0; k < SCAN_ITEMS; ++k) {
-    const uint32_t i = (uint32_t)k * SCAN_THREADS + threadIdx.x;
-    const uint64_t g = tile0 + i;
-    sk[padded(i) + 1] = g < n ? skeys[g] : 0;
-  }
-  if (threadIdx.x == 0) sk[0] = tile0 ? skeys[tile0 - 1] : 0;
-  __syncthreads();
-  uint32_t bits = 0;
-#pragma unroll
-  for (int k = 0; k < SCAN_ITEMS; ++k) {
-    const uint32_t i = threadIdx.x * SCAN_ITEMS + k;
-    const uint64_t g = tile0 + i;
-    const uint64_t prev = i ? sk[padded(i - 1) + 1] : sk[0];
-    if (g < n && (g == 0 || sk[padded(i) + 1] != prev)) bits |= 1u << k;
-  }
-  return bits;
-}
-
-// +1-encoded head positions (0 = no head seen in this prefix of the tile)
-extern "C" __global__ void __launch_bounds__(SCAN_THREADS)
-sd_group_tile_heads(const uint64_t* __restrict__ skeys, uint64_t n,
-                    uint32_t* __restrict__ tile_last_head, uint32_t* __restrict__ tile_heads) {
-  __shared__ uint64_t sk[PADDED_TILE];
   const uint64_t tile0 = (uint64_t)blockIdx.x * SCAN_TILE;
-  const uint32_t bits = tile_head_bits(skeys, n, tile0, sk);
-  const uint32_t hmax = bits ? (uint32_t)(tile0 + threadIdx.x * SCAN_ITEMS + 31 - __clz(bits)) + 1u : 0u;
-  const uint32_t hcnt = (uint32_t)__popc(bits);
-  uint32_t tmax, tsum;
-  (void)block_inclusive_max(hmax, &tmax);
-  (void)block_exclusive_sum(hcnt, &tsum);
-  if (threadIdx.x == 0) { tile_last_head[blockIdx.x] = tmax; tile_heads[blockIdx.x] = tsum; }
-}
-
-// carry[t] = max(tile_last_head[0..t-1]) (single block, sequential over <= ~64k tiles)
-extern "C" __global__ void __launch_bounds__(SCAN_THREADS)
-sd_group_carry(const uint32_t* __restrict__ tile_last_head, uint32_t ntiles,
-               uint32_t* __restrict__ carry, const uint32_t* __restrict__ tile_heads,
-               uint64_t* __restrict__ objects) {
-  // chunked sequential scan: each thread owns a contiguous slice
-  const uint32_t per = (ntiles + SCAN_THREADS - 1) / SCAN_THREADS;
-  const uint32_t lo = threadIdx.x * per, hi = min(ntiles, lo + per);
-  uint32_t m = 0, s = 0;
-  for (uint32_t t = lo; t < hi; ++t) { m = max(m, tile_last_head[t]); s += tile_heads[t]; }
-  uint32_t tot;
-  const uint32_t pre = block_inclusive_max(m, &tot);
-  // exclusive max for my slice start: inclusive of previous threads
-  __shared__ uint32_t incl[SCAN_THREADS];
-  incl[threadIdx.x] = pre;
-  __syncthreads();
-  uint32_t run = threadIdx.x ? incl[threadIdx.x - 1] : 0u;
-  for (uint32_t t = lo; t < hi; ++t) { carry[t] = run; run = max(run, tile_last_head[t]); }
-  uint32_t stot;
-  (void)block_exclusive_sum(s, &stot);
-  if (threadIdx.x == 0) *objects = stot;
-}
-
-// rep[vals[i]] = vals[head(i)]; keys and vals staged through LDS like sd_group_tile_heads
-extern "C" __global__ void __launch_bounds__(SCAN_THREADS)
-sd_group_emit(const uint64_t* __restrict__ skeys, const uint32_t* __restrict__ svals,
-              uint64_t n, const uint32_t* __restrict__ carry, uint32_t* __restrict__ rep) {
-  __shared__ uint64_t sk[PADDED_TILE];
-  __shared__ uint32_t sv[PADDED_TILE];
-  const uint64_t tile0 = (uint64_t)blockIdx.x * SCAN_TILE;
+  const uint64_t wbase = tile0 + (uint64_t)w * (64 * RUN_ROUNDS);
+  uint64_t kr[RUN_ROUNDS];
+  uint32_t vr[RUN_ROUNDS];
 #pragma unroll
-  for (int k = 0; k < SCAN_ITEMS; ++k) {
-    const uint32_t i = (uint32_t)k * SCAN_THREADS + threadIdx.x;
-    const uint64_t g = tile0 + i;
-    sv[padded(i)] = g < n ? svals[g] : 0u;
+  for (int r = 0; r < (int)RUN_ROUNDS; ++r) {
+    const uint64_t i = wbase + (uint64_t)r * 64 + lane;
+    kr[r] = i < n ? skeys[i] : 0ull;
+    vr[r] = i < n ? svals[i] : 0u;
   }
-  const uint32_t bits = tile_head_bits(skeys, n, tile0, sk);  // (its barrier publishes sv)
-  const uint64_t base = tile0 + (uint64_t)threadIdx.x * SCAN_ITEMS;
-  uint32_t hm[SCAN_ITEMS];
-  uint32_t run = 0;
+  // the key before the wave (wave-uniform)
+  uint64_t prevk = (wbase > 0 && wbase <= n) ? skeys[wbase - 1] : 0ull;
+  uint32_t carry_val = 0, heads = 0, npend = 0;
+  bool carry = false;  // a head seen in this wave's earlier rounds
+  const uint64_t le_mask = ~0ull >> (63u - lane);  // lanes <= this lane
 #pragma unroll
-  for (int k = 0; k < SCAN_ITEMS; ++k) {
-    if ((bits >> k) & 1u) run = (uint32_t)(base + k) + 1u;
-    hm[k] = run;
-  }
-  uint32_t tot;
-  const uint32_t incl = block_inclusive_max(run, &tot);
-  // exclusive prefix max from earlier threads of this block, and from earlier tiles
-  __shared__ uint32_t inc_s[SCAN_THREADS];
-  inc_s[threadIdx.x] = incl;
-  __syncthreads();
-  uint32_t prev = threadIdx.x ? inc_s[threadIdx.x - 1] : 0u;
-  prev = max(prev, carry[blockIdx.x]);
-#pragma unroll
-  for (int k = 0; k < SCAN_ITEMS; ++k) {
-    const uint64_t i = base + k;
-    if (i < n) {
-      const uint32_t h = max(prev, hm[k]) - 1u;  // always >= 1 because i==0 is a head
-      const uint32_t hv = h >= tile0 ? sv[padded((uint32_t)(h - tile0))] : svals[h];
-      rep[sv[padded(threadIdx.x * SCAN_ITEMS + k)]] = hv;
+  for (int r = 0; r < (int)RUN_ROUNDS; ++r) {
+    const uint64_t i = wbase + (uint64_t)r * 64 + lane;
+    const bool valid = i < n;
+    uint64_t kp = __shfl_up(kr[r], 1, 64);
+    if (lane == 0) kp = prevk;
+    const bool head = valid && (i == 0 || kr[r] != kp);
+    const uint64_t hmask = __ballot(head);
+    const uint64_t mine = hmask & le_mask;
+    // the val of this lane's run head: a head lane of this round, else the carried one
+    const uint32_t hl = mine ? 63u - (uint32_t)__clzll(mine) : 0u;
+    const uint32_t hv = __shfl(vr[r], (int)hl, 64);
+    if (valid) {
+      if (head) {
+        if (!PREFILLED) rep[vr[r]] = vr[r];
+      } else if (mine) {
+        rep[vr[r]] = hv;
+      } else if (carry) {
+        rep[vr[r]] = carry_val;
+      }  // else: before the wave's first head, resolved below
     }
+    if (!carry) npend += (uint32_t)__popcll(__ballot(valid && !mine));
+    if (hmask) {
+      carry = true;
+      carry_val = __shfl(vr[r], 63 - __clzll(hmask), 64);
+    }
+    heads += (uint32_t)__popcll(hmask);
+    prevk = __shfl(kr[r], 63, 64);
   }
+  if (lane == 0) {
+    w_val[w] = carry_val;
+    w_has[w] = carry ? 1u : 0u;
+    w_heads[w] = heads;
+    // wave 0 before a head: the run entering the tile (its head is before tile0)
+    if (w == 0) tile_carry = (npend && tile0 < n) ? svals[run_first(skeys, skeys[tile0], (int64_t)tile0 - 1)] : 0u;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < RUN_WAVES; ++k) t += w_heads[k];
+    tile_heads[blockIdx.x] = t;
+  }
+  if (npend) {  // (wave-uniform) positions [wbase, wbase + npend) continue an earlier run
+    uint32_t hv = tile_carry;
+    for (int k = (int)w - 1; k >= 0; --k)
+      if (w_has[k]) { hv = w_val[k]; break; }
+    for (uint32_t j = lane; j < npend; j += 64) rep[svals[wbase + j]] = hv;
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(SCAN_THREADS)
+sd_group_runs(const uint64_t* __restrict__ skeys, const uint32_t* __restrict__ svals, uint64_t n,
+              uint32_t* __restrict__ rep, uint32_t* __restrict__ tile_heads) {
+  group_runs_body<false>(skeys, svals, n, rep, tile_heads);
+}
+extern "C" __global__ void __launch_bounds__(SCAN_THREADS)
+sd_group_runs_prefilled(const uint64_t* __restrict__ skeys, const uint32_t* __restrict__ svals,
+                        uint64_t n, uint32_t* __restrict__ rep, uint32_t* __restrict__ tile_heads) {
+  group_runs_body<true>(skeys, svals, n, rep, tile_heads);
 }
 
 // *total = sum of v[0..m) in u64 (one workgroup; m <= SCAN_TILE tile sums, or one tile):
@@ -562,7 +570,7 @@ hipError_t exclusive_scan_u32(const uint32_t* in, uint32_t* out, uint64_t m, uin
 
 hipError_t radix_sort_pairs(const uint64_t* keys_in, const uint32_t* vals_in, uint64_t* keys_out,
                             uint32_t* vals_out, uint64_t n, int begin_bit, int end_bit, void* ws,
-                            hipStream_t s) {
+                            hipStream_t s, uint32_t* iota_out) {
   if (n == 0) return hipSuccess;
   if (n >= (1ull << 32) || begin_bit < 0 || end_bit > 64 || end_bit <= begin_bit)
     return hipErrorInvalidValue;
@@ -591,7 +599,7 @@ hipError_t radix_sort_pairs(const uint64_t* keys_in, const uint32_t* vals_in, ui
                                                    rowtot, nt);
     else
       sd_radix_scatter_iota<<<nt, SORT_THREADS, 0, s>>>(ksrc, kdst, vdst, n, shift, mask, hist, bsum,
-                                                        rowtot, nt);
+                                                        rowtot, nt, iota_out);
     ksrc = kdst;
     vsrc = vdst;
   }
@@ -599,16 +607,15 @@ hipError_t radix_sort_pairs(const uint64_t* keys_in, const uint32_t* vals_in, ui
 }
 
 hipError_t group_sorted(const uint64_t* skeys, const uint32_t* svals, uint64_t n, uint32_t* rep,
-                        uint64_t* d_objects, void* ws, hipStream_t s) {
+                        uint64_t* d_objects, void* ws, hipStream_t s, bool rep_prefilled) {
   if (n == 0) return hipMemsetAsync(d_objects, 0, 8, s);
   const uint32_t ng = tiles_of(n, SCAN_TILE);
-  char* p = (char*)ws;
-  uint32_t* last_head = (uint32_t*)p; p += align_up(ng * 4, 256);
-  uint32_t* heads = (uint32_t*)p; p += align_up(ng * 4, 256);
-  uint32_t* carry = (uint32_t*)p;
-  sd_group_tile_heads<<<ng, SCAN_THREADS, 0, s>>>(skeys, n, last_head, heads);
-  sd_group_carry<<<1, SCAN_THREADS, 0, s>>>(last_head, ng, carry, heads, d_objects);
-  sd_group_emit<<<ng, SCAN_THREADS, 0, s>>>(skeys, svals, n, carry, rep);
+  uint32_t* heads = (uint32_t*)ws;
+  if (rep_prefilled)
+    sd_group_runs_prefilled<<<ng, SCAN_THREADS, 0, s>>>(skeys, svals, n, rep, heads);
+  else
+    sd_group_runs<<<ng, SCAN_THREADS, 0, s>>>(skeys, svals, n, rep, heads);
+  sd_sum_u32_block<<<1, SCAN_THREADS, 0, s>>>(heads, ng, (unsigned long long*)d_objects);
   return hipGetLastError();
 }
 
@@ -619,9 +626,10 @@ hipError_t group_keys(const uint64_t* keys, uint64_t n, uint32_t* rep, uint64_t*
   char* sort_ws = p; p += sort_workspace_bytes(n);
   uint64_t* skeys = (uint64_t*)p; p += align_up(n * 8, 256);
   uint32_t* svals = (uint32_t*)p; p += align_up(n * 4, 256);
-  hipError_t e = radix_sort_pairs(keys, nullptr, skeys, svals, n, 0, 64, sort_ws, s);
+  // (the first pass also writes rep[i] = i: the runs kernel then stores only duplicates)
+  hipError_t e = radix_sort_pairs(keys, nullptr, skeys, svals, n, 0, 64, sort_ws, s, rep);
   if (e != hipSuccess) return e;
-  return group_sorted(skeys, svals, n, rep, d_objects, p, s);
+  return group_sorted(skeys, svals, n, rep, d_objects, p, s, true);
 }
 
 size_t group_min_sorted_workspace_bytes(uint64_t n) {
@@ -645,12 +653,13 @@ hipError_t group_min_by_sort(const uint64_t* keys, const uint32_t* vals, uint64_
   uint32_t* rep = (uint32_t*)p;
   const uint32_t nb = tiles_of(n, 256);
   sd_widen_vals<<<nb, 256, 0, s>>>(vals, n, vkey);
-  hipError_t e = radix_sort_pairs(vkey, nullptr, k2, order, n, 0, 32, gws, s);
+  // (spos is a permutation of the positions, so rep can be prefilled by the first sort)
+  hipError_t e = radix_sort_pairs(vkey, nullptr, k2, order, n, 0, 32, gws, s, rep);
   if (e != hipSuccess) return e;
   sd_gather_keys<<<nb, 256, 0, s>>>(keys, order, n, k2);
   e = radix_sort_pairs(k2, order, skeys, spos, n, 0, 64, gws, s);
   if (e != hipSuccess) return e;
-  e = group_sorted(skeys, spos, n, rep, d_objects, gws, s);
+  e = group_sorted(skeys, spos, n, rep, d_objects, gws, s, true);
   if (e != hipSuccess) return e;
   sd_gather_vals<<<nb, 256, 0, s>>>(vals, rep, n, out);
   return hipGetLastError();

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "sd_debug.h"
 #include "sd_links.h"
 
 namespace sdcas {
@@ -154,7 +155,7 @@ sd_links_decide(const uint8_t* __restrict__ state, const uint32_t* __restrict__ 
                 const uint32_t* __restrict__ starts, uint32_t nsteps, uint64_t reached,
                 uint32_t* __restrict__ step_out, uint32_t* __restrict__ object_out,
                 uint8_t* __restrict__ action_out, unsigned int* __restrict__ counts, bool seeded,
-                const uint64_t* __restrict__ keys, PreEvents ev) {
+                const uint64_t* __restrict__ keys, PreEvents ev, uint32_t chunk) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t i0 = i - (threadIdx.x & 63u);  // the wave's first row
   uint32_t step = SD_LINKS_NO_STEP, object = SD_LINKS_NO_OBJECT;
@@ -174,6 +175,14 @@ sd_links_decide(const uint8_t* __restrict__ state, const uint32_t* __restrict__ 
     } else {
       uint32_t v = rep[i];
       const uint32_t r = seeded ? v & ~LINKS_ROW_FLAG : v;  // the key's first row
+      // INVARIANT (both uses below: pre_min_of's bound = starts[step + 1], and the CREATED
+      // test r >= starts[step]): a HASHED row is never a re-queried cursor row — only a row
+      // that stays orphan (an error, or an empty file with no cas_id) is the last row of one
+      // step and the first of the next (starts[k] == starts[k-1] + chunk - 1).  If "stays
+      // orphan" ever grows to include hashed rows, both tests misclassify such rows; the
+      // debug build checks it for this row.
+      SD_DBG_CHECK(!(step > 0 && (uint32_t)i == starts[step] && starts[step] + 1u == starts[step - 1] + chunk),
+                   "links: hashed row %u is the re-queried first row of step %u", (uint32_t)i, step);
       if (ev.m) {  // a pre-existing Object its step or an earlier one saw
         const uint32_t bound = step + 1 < nsteps ? starts[step + 1] : 0xFFFFFFFFu;
         v = min(v, pre_min_of(ev, keys[i], bound));
@@ -536,13 +545,15 @@ hipError_t links_decide(const uint8_t* state, const uint32_t* rep, uint64_t n,
                         uint32_t* step_out, uint32_t* object_out, uint8_t* action_out,
                         uint32_t* counts, bool seeded, const uint64_t* keys,
                         const uint64_t* ekeys, const uint32_t* erows, const uint64_t* T,
-                        const uint32_t* filter, uint64_t m, hipStream_t s) {
+                        const uint32_t* filter, uint64_t m, uint32_t chunk, hipStream_t s) {
   if (n == 0) return hipSuccess;
   PreEvents ev{ekeys, erows, T, filter, m};
   sd_links_decide<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(
       state, rep, n, starts, nsteps, reached, step_out, object_out, action_out, counts, seeded,
-      keys, ev);
+      keys, ev, chunk);
   return hipGetLastError();
 }
+
+SD_DBG_ACCESSOR(sd_dbg_violations_links)
 
 }  // namespace sdcas

@@ -3,7 +3,7 @@
 // Makefile: libsd_hip_cas_debug.so).  A violated invariant prints one line from the device
 // and counts itself in a per-translation-unit device counter; sd_cas_debug_violations()
 // (debug library only, not part of the ABI header) sums the counters, and the GPU test
-// suite run against the debug library (tools/gpu_r3_debug.sh) fails the test after which
+// suite run against the debug library (tools/gpu_r6_final.sh <tag> suite) fails the test after which
 // any counter moved.  Counting instead of trapping keeps a violation from faulting the GPU.
 #ifndef SD_DEBUG_H
 #define SD_DEBUG_H

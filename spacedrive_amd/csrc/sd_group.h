@@ -12,10 +12,11 @@ size_t group_workspace_bytes(uint64_t n);
 
 // Stable LSD sort of (keys, vals) on bits [begin_bit, end_bit).  vals_in == nullptr means
 // vals = 0..n-1.  Results land in (keys_out, vals_out).  keys_in is not modified;
-// `ws` must hold sort_workspace_bytes(n).  n < 2^32.
+// `ws` must hold sort_workspace_bytes(n).  n < 2^32.  iota_out (vals_in == nullptr only):
+// iota_out[i] = i is written by the first pass as well (group_sorted's rep_prefilled).
 hipError_t radix_sort_pairs(const uint64_t* keys_in, const uint32_t* vals_in, uint64_t* keys_out,
                             uint32_t* vals_out, uint64_t n, int begin_bit, int end_bit,
-                            void* ws, hipStream_t stream);
+                            void* ws, hipStream_t stream, uint32_t* iota_out = nullptr);
 
 // Canonical grouping: rep[i] = min{ j : keys[j] == keys[i] }; *d_objects = #distinct keys
 // (written on the device).  ws must hold group_workspace_bytes(n).
@@ -28,9 +29,11 @@ size_t group_min_sorted_workspace_bytes(uint64_t n);
 hipError_t group_min_by_sort(const uint64_t* keys, const uint32_t* vals, uint64_t n, uint32_t* out,
                              uint64_t* d_objects, void* ws, hipStream_t stream);
 
-// Group already-sorted pairs (keys ascending, vals = original idx, stable).
+// Group already-sorted pairs (keys ascending, vals = original idx, stable): rep[v] = the val
+// of v's run head.  rep_prefilled: rep[v] == v already holds for every val (vals a
+// permutation of 0..n-1 and rep laid down by the iota sort), so heads are not stored.
 hipError_t group_sorted(const uint64_t* skeys, const uint32_t* svals, uint64_t n, uint32_t* rep,
-                        uint64_t* d_objects, void* ws, hipStream_t stream);
+                        uint64_t* d_objects, void* ws, hipStream_t stream, bool rep_prefilled = false);
 
 // Device-wide exclusive scan of m <= 4096^2 u32 (partial: >= m/4096 + 1 u32 of scratch).
 // total (optional, device): the sum of in[] in u64 — exact even where the u32 scan wraps.

@@ -43,12 +43,13 @@ namespace sdcas {
 uint32_t sd_dbg_violations_group_hash();
 uint32_t sd_dbg_violations_group();
 uint32_t sd_dbg_violations_checksum();
+uint32_t sd_dbg_violations_links();
 }  // namespace sdcas
 // debug library only (libsd_hip_cas_debug.so, not in the ABI header): invariant violations
 // counted by the device checks of sd_debug.h since the library was loaded
 extern "C" uint64_t sd_cas_debug_violations(void) {
   return (uint64_t)sd_dbg_violations_group_hash() + sd_dbg_violations_group() +
-         sd_dbg_violations_checksum();
+         sd_dbg_violations_checksum() + sd_dbg_violations_links();
 }
 #endif
 
@@ -123,6 +124,12 @@ int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
     // the whole key array) run on K1G output — uniform BLAKE3 keys never reach the real bound
     const char* f = getenv("SD_CAS_TEST_TABLE_FILL");
     c->test_table_fill = f && *f ? (uint32_t)strtoul(f, nullptr, 10) : 0u;
+    //  results stay exact with it set, but every fused grouping then takes the
+    // slow overflow paths: never silent
+    if (c->test_table_fill)
+      fprintf(stderr, "sd_hip_cas: SD_CAS_TEST_TABLE_FILL=%u (test knob): the fused grouping's "
+              "region tables overflow at %u distinct keys (exact, much slower)\n",
+              c->test_table_fill, c->test_table_fill);
   }
   sd_cas_set_latency_threshold(c, SD_CAS_THRESHOLD_DEFAULT, SD_CAS_THRESHOLD_DEFAULT);
   sd_cas_set_chunkpar_split(c, SD_CAS_THRESHOLD_DEFAULT, SD_CAS_THRESHOLD_DEFAULT);
@@ -704,7 +711,7 @@ int sd_cas_identifier_links_ex_dev(sd_cas_ctx* c, const uint64_t* d_keys, const 
   HIP_TRY(c, hipMemsetAsync(counts, 0, std::max<size_t>(nsteps, 1) * 8, s));
   HIP_TRY(c, links_decide(d_state, rep, n, starts, (uint32_t)nsteps, reached, d_step, d_object,
                           d_action, counts, seeded, d_keys, orphans, minrow, hkeys, filter, n_ev,
-                          s));
+                          (uint32_t)chunk, s));
   std::vector<uint32_t> hc(2 * std::max<size_t>(nsteps, 1));
   HIP_TRY(c, hipMemcpyAsync(hc.data(), counts, hc.size() * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));

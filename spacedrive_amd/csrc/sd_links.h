@@ -40,7 +40,7 @@ hipError_t links_decide(const uint8_t* state, const uint32_t* rep, uint64_t n,
                         uint32_t* step_out, uint32_t* object_out, uint8_t* action_out,
                         uint32_t* counts, bool seeded, const uint64_t* keys,
                         const uint64_t* ekeys, const uint32_t* erows, const uint64_t* T,
-                        const uint32_t* filter, uint64_t m, hipStream_t s);
+                        const uint32_t* filter, uint64_t m, uint32_t chunk, hipStream_t s);
 // *d_bad (u64, zeroed by the caller) += 1 per wave holding an id >= LINKS_ROW_FLAG (none_ok:
 // SD_LINKS_NO_OBJECT allowed)
 hipError_t links_check_ids(const uint32_t* ids, uint64_t n, bool none_ok, uint64_t* d_bad,

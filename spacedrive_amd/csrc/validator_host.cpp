@@ -325,11 +325,25 @@ int sd_cas_checksums_dev(sd_cas_ctx* c, const void* d_arena, uint64_t arena_byte
   return SD_CAS_OK;
 }
 
-// file_checksum over many paths.  Windows of up to CK_WIN bytes / CK_WIN_FILES files in
-// index order, double-buffered: the pool reads window w (one slot of up128(st_size + 1) per
-// file: the spare byte shows EOF, so a file that grew since stat fills its slot and is
-// redone by the streaming path) into one pinned slot while the GPU copies and hashes window
-// w-1 from the other.  Pinned slot layout: offs | lens | digests | data.
+// A/B knobs of the file path below (tools/build_variant.sh + tools/patch_define.py)
+#ifndef SD_CK_PIECE_KB
+#define SD_CK_PIECE_KB 1024
+#endif
+#ifndef SD_CK_COPY_MB
+#define SD_CK_COPY_MB 8
+#endif
+
+// file_checksum over many paths.  The batch files are laid out in windows of up to CK_WIN
+// bytes / CK_WIN_FILES files in index order (one slot of up128(st_size + 1) per file: the
+// spare byte shows EOF, so a file that grew since stat fills its slot and is redone by the
+// streaming path), windows rotating over CK_SLOTS pinned + device slots.  Round 6: the files
+// are read as PIECES of <= CK_PIECE bytes (1 MiB reads into the pinned slot run ~18 % faster
+// host-side than one whole-file pread, profiles/r05/official_c/probe_pread.log) taken from ONE
+// queue over the whole job by up to 15 pool threads; this thread pumps: every finished
+// prefix of the current window (>= CK_COPY bytes) goes to HBM on the copy stream as it
+// lands, a finished window gets its header, K3b and its digests back on the compute stream,
+// and a window whose digests are back frees its slot for the readers.  Pinned and device
+// slot layout: offs | lens | digests | data.
 int sd_cas_file_checksums(sd_cas_ctx* c, const char* const* paths, size_t n, char* out_hex,
                           int32_t* status) {
   if (!c) return SD_CAS_EINVAL;
@@ -339,9 +353,13 @@ int sd_cas_file_checksums(sd_cas_ctx* c, const char* const* paths, size_t n, cha
   constexpr uint64_t CK_WIN = 128ull << 20;  // data bytes per window
   constexpr uint64_t CK_BIG = CK_WIN / 2;    // larger files stream on their own (64 MiB segments)
   constexpr size_t CK_WIN_FILES = 32768;
+  constexpr uint64_t CK_PIECE = (uint64_t)SD_CK_PIECE_KB << 10;  // read unit (a file's last piece takes the rest)
+  constexpr uint64_t CK_COPY = (uint64_t)SD_CK_COPY_MB << 20;     // H2D unit of a window's landed prefix
+  constexpr int CK_SLOTS = 3;
   constexpr size_t HDR = CK_WIN_FILES * (8 + 8 + 32);
   constexpr size_t SLOT = HDR + CK_WIN + 256;
   enum : uint8_t { K_BATCH = 0, K_STREAM = 1, K_ERROR = 2 };
+  SdTrace tr(c->trace, "file_checksums", n);
   std::vector<uint64_t> fsize(n, 0);
   std::vector<uint8_t> kind(n, K_BATCH);
   for (size_t i = 0; i < n; i++) { status[i] = 0; out_hex[65 * i] = 0; }
@@ -357,132 +375,235 @@ int sd_cas_file_checksums(sd_cas_ctx* c, const char* const* paths, size_t n, cha
       }
     });
   }
-  // windows: [w0, w1) file ranges in index order
-  std::vector<size_t> wstart{0};
+  tr.mark("stat");
+  // members (batch files) in index order, grouped into windows; each member's slot offset
+  // and capacity; its pieces in slot byte order (so a prefix of pieces is a prefix of bytes)
+  std::vector<size_t> mfile, wmem{0}, wpiece{0};
+  std::vector<uint64_t> moff, mcap, wbytes;
+  struct Piece { uint32_t mem; uint32_t win; uint64_t off, len; };
+  std::vector<Piece> pieces;
   {
     uint64_t bytes = 0;
-    size_t files = 0;
     for (size_t i = 0; i < n; i++) {
       if (kind[i] != K_BATCH) continue;
       const uint64_t need = up128(fsize[i] + 1);
+      const size_t files = mfile.size() - wmem.back();
       if (files && (bytes + need > CK_WIN || files == CK_WIN_FILES)) {
-        wstart.push_back(i);
+        wbytes.push_back(bytes);
+        wmem.push_back(mfile.size());
+        wpiece.push_back(pieces.size());
         bytes = 0;
-        files = 0;
       }
+      const uint32_t k = (uint32_t)mfile.size();
+      mfile.push_back(i);
+      moff.push_back(bytes);
+      mcap.push_back(need);
+      const uint64_t np = std::max<uint64_t>(1, need / CK_PIECE);
+      for (uint64_t j = 0; j < np; j++)
+        pieces.push_back({k, (uint32_t)(wmem.size() - 1), j * CK_PIECE,
+                          j + 1 < np ? CK_PIECE : need - j * CK_PIECE});
       bytes += need;
-      files++;
     }
-    wstart.push_back(n);
+    if (mfile.size() > wmem.back()) {
+      wbytes.push_back(bytes);
+      wmem.push_back(mfile.size());
+      wpiece.push_back(pieces.size());
+    }
   }
-  const size_t nw = wstart.size() - 1;
-  int rc = ensure_pinned(c, 2 * SLOT);
-  if (rc) return rc;
-  if ((rc = ensure(c, c->staging, 2 * SLOT))) return rc;
-  if ((rc = ensure(c, c->ws, checksum_batch_workspace_bytes(CK_WIN_FILES, CK_WIN)))) return rc;
-  hipStream_t s = c->stream;
-  hipEvent_t done[2] = {nullptr, nullptr};
-  for (int b = 0; b < 2; b++)
+  const size_t nw = wbytes.size(), nm = mfile.size(), np = pieces.size();
+  int rc = SD_CAS_OK;
+  if (nw) {
+    if ((rc = ensure_pinned(c, CK_SLOTS * SLOT))) return rc;
+    if ((rc = ensure(c, c->staging, CK_SLOTS * SLOT))) return rc;
+    if ((rc = ensure(c, c->ws, checksum_batch_workspace_bytes(CK_WIN_FILES, CK_WIN)))) return rc;
+  }
+  hipStream_t s = c->stream, cs = c->copy;
+  hipEvent_t done[CK_SLOTS] = {}, landed = nullptr;
+  auto destroy_events = [&]() {
+    for (int b = 0; b < CK_SLOTS; b++)
+      if (done[b]) (void)hipEventDestroy(done[b]);
+    if (landed) (void)hipEventDestroy(landed);
+  };
+  for (int b = 0; b < CK_SLOTS && nw; b++)
     if (hipEventCreateWithFlags(&done[b], hipEventDisableTiming) != hipSuccess) {
-      if (done[0]) (void)hipEventDestroy(done[0]);
+      destroy_events();
       return fail(c, SD_CAS_EHIP, "file_checksums: event create");
     }
-  std::vector<size_t> members[2];  // file index of each batch entry of the window in a slot
+  if (nw && hipEventCreateWithFlags(&landed, hipEventDisableTiming) != hipSuccess) {
+    destroy_events();
+    return fail(c, SD_CAS_EHIP, "file_checksums: event create");
+  }
+  // per member: bytes read, read error, and a read that a local regular file never gives (a
+  // short piece before the file's last, or data after a short read)
+  std::unique_ptr<std::atomic<uint64_t>[]> mgot(new std::atomic<uint64_t>[nm]);
+  std::unique_ptr<std::atomic<int>[]> merr(new std::atomic<int>[nm]);
+  std::unique_ptr<std::atomic<uint8_t>[]> mirr(new std::atomic<uint8_t>[nm]);
+  std::unique_ptr<std::atomic<uint8_t>[]> fin(new std::atomic<uint8_t>[np]);
+  for (size_t k = 0; k < nm; k++) { mgot[k].store(0); merr[k].store(0); mirr[k].store(0); }
+  for (size_t p = 0; p < np; p++) fin[p].store(0, std::memory_order_relaxed);
+  std::atomic<size_t> next{0};
+  std::atomic<size_t> freed{0};  // windows [0, freed) have their digests back: their slots are free
+  std::atomic<bool> abort{false};
+  auto slot_free = [&](uint32_t w) { return w < freed.load(std::memory_order_acquire) + CK_SLOTS; };
+  auto read_piece = [&](size_t p) {
+    const Piece& pc = pieces[p];
+    const size_t i = mfile[pc.mem];
+    char* dst = (char*)c->pinned + (size_t)(pc.win % CK_SLOTS) * SLOT + HDR + moff[pc.mem] + pc.off;
+    int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
+    if (fd < 0) {
+      merr[pc.mem].store(errno);
+      return;
+    }
+    uint64_t got = 0;
+    bool was_short = false;
+    while (got < pc.len) {
+      ssize_t r = pread(fd, dst + got, pc.len - got, (off_t)(pc.off + got));
+      if (r < 0 && errno == EINTR) continue;
+      if (r < 0) { merr[pc.mem].store(errno); break; }
+      if (r == 0) break;  // EOF
+      if (was_short) mirr[pc.mem].store(1);  // data after a short read: not a local file
+      if ((uint64_t)r < pc.len - got) was_short = true;
+      got += (uint64_t)r;
+    }
+    close(fd);
+    if (got < pc.len && pc.off + pc.len < mcap[pc.mem]) mirr[pc.mem].store(1);  // ended before its last piece
+    mgot[pc.mem].fetch_add(got);
+  };
+  auto spin = []() {
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#else
+    std::this_thread::yield();
+#endif
+  };
+  auto worker = [&]() {
+    for (size_t p; !abort.load(std::memory_order_relaxed) && (p = next.fetch_add(1)) < np;) {
+      // a piece of window w waits for window w - CK_SLOTS to free the slot
+      while (!slot_free(pieces[p].win) && !abort.load(std::memory_order_relaxed)) std::this_thread::yield();
+      if (abort.load(std::memory_order_relaxed)) break;
+      read_piece(p);
+      fin[p].store(1, std::memory_order_release);
+    }
+  };
   static const char* hx = "0123456789abcdef";
-  auto emit = [&](int b) {  // the window in slot b is complete: digests -> hex
-    const uint8_t* dg = (const uint8_t*)c->pinned + (size_t)b * SLOT + CK_WIN_FILES * 16;
-    for (size_t k = 0; k < members[b].size(); k++) {
-      char* o = out_hex + 65 * members[b][k];
-      for (int j = 0; j < 32; j++) { o[2 * j] = hx[dg[32 * k + j] >> 4]; o[2 * j + 1] = hx[dg[32 * k + j] & 15]; }
+  auto emit = [&](size_t w) {  // window w's digests are back in its pinned slot: -> hex
+    const uint8_t* dg = (const uint8_t*)c->pinned + (size_t)(w % CK_SLOTS) * SLOT + CK_WIN_FILES * 16;
+    for (size_t k = wmem[w]; k < wmem[w + 1]; k++) {
+      const uint8_t* d = dg + 32 * (k - wmem[w]);
+      char* o = out_hex + 65 * mfile[k];
+      for (int j = 0; j < 32; j++) { o[2 * j] = hx[d[j] >> 4]; o[2 * j + 1] = hx[d[j] & 15]; }
       o[64] = 0;
     }
-    members[b].clear();
   };
-  bool pending[2] = {false, false};
   uint32_t* d_bad = (uint32_t*)(c->d_scalar + 6);
-  {
-    hipError_t e = sd_ws_acquire(c, s);
-    if (e == hipSuccess) e = hipMemsetAsync(d_bad, 0, 4, s);
-    if (e != hipSuccess) rc = fail(c, SD_CAS_EHIP, "file_checksums: %s", hipGetErrorString(e));
-  }
-  for (size_t w = 0; w < nw && rc == SD_CAS_OK; w++) {
-    const int b = (int)(w & 1);
-    if (pending[b]) {  // slot b's previous window: copied, hashed and its digests back
-      if (hipEventSynchronize(done[b]) != hipSuccess) { rc = fail(c, SD_CAS_EHIP, "file_checksums: sync"); break; }
-      emit(b);
-      pending[b] = false;
+  size_t ncopies = 0;
+  double stall_us = 0;
+  // the pump (this thread): copies, window launches, retirement; reads a piece when idle
+  auto pump = [&]() {
+    size_t wc = 0, issued = 0, retired = 0, ready = 0;
+    uint64_t sent = 0;
+    auto hipfail = [&](hipError_t e, const char* what) {
+      rc = fail(c, SD_CAS_EHIP, "file_checksums %s: %s", what, hipGetErrorString(e));
+      abort.store(true);
+    };
+    {
+      hipError_t e = sd_ws_acquire(c, s);
+      if (e == hipSuccess) e = hipMemsetAsync(d_bad, 0, 4, s);
+      if (e != hipSuccess) { hipfail(e, "setup"); return; }
     }
-    char* pin = (char*)c->pinned + (size_t)b * SLOT;
-    uint64_t* h_offs = (uint64_t*)pin;
-    uint64_t* h_lens = h_offs + CK_WIN_FILES;
-    char* data = pin + HDR;
-    std::vector<size_t>& mem = members[b];
-    std::vector<uint64_t> cap;
-    uint64_t o = 0;
-    for (size_t i = wstart[w]; i < wstart[w + 1]; i++) {
-      if (kind[i] != K_BATCH) continue;
-      h_offs[mem.size()] = o;
-      cap.push_back(up128(fsize[i] + 1));
-      o += cap.back();
-      mem.push_back(i);
-    }
-    const size_t m = mem.size();
-    if (m == 0) continue;
-    std::atomic<size_t> next{0};
-    c->pool.run(std::max(1u, std::min(16u, (unsigned)((m + 3) / 4))), [&]() {
-      for (size_t k; (k = next.fetch_add(1)) < m;) {
-        const size_t i = mem[k];
-        int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
-        if (fd < 0) { status[i] = -errno; kind[i] = K_ERROR; h_lens[k] = 0; continue; }
-        uint64_t got = 0;
-        bool was_short = false, irregular = false;
-        while (got < cap[k]) {
-          ssize_t r = pread(fd, data + h_offs[k] + got, cap[k] - got, (off_t)got);
-          if (r < 0 && errno == EINTR) continue;
-          if (r < 0) { status[i] = -errno; kind[i] = K_ERROR; break; }
-          if (r == 0) break;  // EOF
-          if (was_short) irregular = true;  // data after a short read: not a local file
-          if ((uint64_t)r < cap[k] - got) was_short = true;
-          got += (uint64_t)r;
+    while (retired < nw && rc == SD_CAS_OK) {
+      bool progress = false;
+      if (retired < issued) {  // the oldest window in flight: digests back?
+        const hipError_t q = hipEventQuery(done[retired % CK_SLOTS]);
+        if (q == hipSuccess) {
+          emit(retired);
+          freed.store(++retired, std::memory_order_release);
+          continue;
         }
-        close(fd);
-        // grew past its slot, or read unlike a local regular file (a short read before the
-        // end, or an end before st_size): sd_cas_file_checksum afterwards, which reads such
-        // a file exactly as hash.rs:15-21 does (1 MiB reads, stop at the first short one)
-        if (kind[i] == K_BATCH && (got == cap[k] || irregular || got < fsize[i])) kind[i] = K_STREAM;
-        h_lens[k] = kind[i] == K_BATCH ? got : 0;
+        if (q != hipErrorNotReady) { hipfail(q, "window sync"); break; }
       }
-    });
-    // entries that failed or grew are hashed as empty buffers and ignored
-    hipError_t e = hipMemcpyAsync((char*)c->staging.p + (size_t)b * SLOT, pin, CK_WIN_FILES * 16,
-                                  hipMemcpyHostToDevice, s);
-    if (e == hipSuccess)
-      e = hipMemcpyAsync((char*)c->staging.p + (size_t)b * SLOT + HDR, data, o, hipMemcpyHostToDevice, s);
-    char* dbase = (char*)c->staging.p + (size_t)b * SLOT;
-    if (e == hipSuccess)
-      e = checksum_batch_device((const uint8_t*)(dbase + HDR), o, (const uint64_t*)dbase,
-                                (const uint64_t*)dbase + CK_WIN_FILES, m,
-                                (uint32_t*)(dbase + CK_WIN_FILES * 16), d_bad, c->ws.p, s);
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(pin + CK_WIN_FILES * 16, dbase + CK_WIN_FILES * 16, m * 32,
-                         hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipEventRecord(done[b], s);
-    if (e != hipSuccess) { rc = fail(c, SD_CAS_EHIP, "file_checksums window: %s", hipGetErrorString(e)); break; }
-    pending[b] = true;
+      if (wc < nw) {
+        const size_t b = wc % CK_SLOTS;
+        char* pin = (char*)c->pinned + b * SLOT;
+        char* dev = (char*)c->staging.p + b * SLOT;
+        while (ready < wpiece[wc + 1] && fin[ready].load(std::memory_order_acquire)) ++ready;
+        const bool complete = ready == wpiece[wc + 1];
+        const uint64_t hi = complete ? wbytes[wc] : moff[pieces[ready].mem] + pieces[ready].off;
+        if (hi > sent && (hi - sent >= CK_COPY || complete)) {
+          const hipError_t e = hipMemcpyAsync(dev + HDR + sent, pin + HDR + sent, hi - sent, hipMemcpyHostToDevice, cs);
+          if (e != hipSuccess) { hipfail(e, "copy"); break; }
+          sent = hi;
+          ++ncopies;
+          progress = true;
+        }
+        if (complete && sent == wbytes[wc]) {
+          // every piece of the window has landed: decide each member, header, K3b, digests back
+          uint64_t* h_offs = (uint64_t*)pin;
+          uint64_t* h_lens = h_offs + CK_WIN_FILES;
+          const size_t m = wmem[wc + 1] - wmem[wc];
+          for (size_t k = wmem[wc]; k < wmem[wc + 1]; k++) {
+            const size_t i = mfile[k], j = k - wmem[wc];
+            h_offs[j] = moff[k];
+            h_lens[j] = 0;  // failed or redone entries are hashed as empty buffers and ignored
+            if (int er = merr[k].load()) { status[i] = -er; kind[i] = K_ERROR; continue; }
+            const uint64_t got = mgot[k].load();
+            // grew past its slot, or read unlike a local regular file (a short read before
+            // the end, or an end before st_size): sd_cas_file_checksum afterwards, which reads
+            // such a file exactly as hash.rs:15-21 does (1 MiB reads, stop at the first short one)
+            if (got == mcap[k] || mirr[k].load() || got < fsize[i]) { kind[i] = K_STREAM; continue; }
+            h_lens[j] = got;
+          }
+          hipError_t e = hipMemcpyAsync(dev, pin, CK_WIN_FILES * 16, hipMemcpyHostToDevice, cs);
+          if (e == hipSuccess) e = hipEventRecord(landed, cs);
+          if (e == hipSuccess) e = hipStreamWaitEvent(s, landed, 0);
+          if (e == hipSuccess)
+            e = checksum_batch_device((const uint8_t*)(dev + HDR), wbytes[wc], (const uint64_t*)dev,
+                                      (const uint64_t*)dev + CK_WIN_FILES, m,
+                                      (uint32_t*)(dev + CK_WIN_FILES * 16), d_bad, c->ws.p, s);
+          if (e == hipSuccess)
+            e = hipMemcpyAsync(pin + CK_WIN_FILES * 16, dev + CK_WIN_FILES * 16, m * 32, hipMemcpyDeviceToHost, s);
+          if (e == hipSuccess) e = hipEventRecord(done[b], s);
+          if (e != hipSuccess) { hipfail(e, "window"); break; }
+          ++issued;
+          ++wc;
+          sent = 0;
+          continue;
+        }
+      }
+      if (progress) continue;
+      // nothing to copy or retire: read a piece too (a 16th reader) if its slot is free
+      // (only a piece whose slot is free now: this thread is the one that frees slots)
+      size_t p = next.load(std::memory_order_relaxed);
+      if (p < np && slot_free(pieces[p].win) && next.compare_exchange_strong(p, p + 1)) {
+        read_piece(p);
+        fin[p].store(1, std::memory_order_release);
+      } else {
+        const auto t0 = std::chrono::steady_clock::now();
+        spin();
+        if (tr.on) stall_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+      }
+    }
+  };
+  if (nw) {
+    c->pool.run2(std::max(1u, std::min(15u, (unsigned)((np + 1) / 2))), worker, pump);
+    tr.mark("windows");
+    tr.note("windows", (double)nw);
+    tr.note("pieces", (double)np);
+    tr.note("copies", (double)ncopies);
+    tr.note("pump_idle_us", stall_us);
+    uint32_t bad = 0;
+    if (rc == SD_CAS_OK) {
+      hipError_t e = hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      if (e != hipSuccess) rc = fail(c, SD_CAS_EHIP, "file_checksums: %s", hipGetErrorString(e));
+      else if (bad) rc = fail(c, SD_CAS_EHIP, "file_checksums: batch work list overflow");
+    }
+    (void)sd_ws_release(c, s);
+    // a failed call leaves nothing in flight that reads the pinned slots
+    (void)hipStreamSynchronize(cs);
+    (void)hipStreamSynchronize(s);
   }
-  uint32_t bad = 0;
-  if (rc == SD_CAS_OK) {
-    hipError_t e = hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) rc = fail(c, SD_CAS_EHIP, "file_checksums: %s", hipGetErrorString(e));
-    else if (bad) rc = fail(c, SD_CAS_EHIP, "file_checksums: batch work list overflow");
-  }
-  (void)sd_ws_release(c, s);
-  (void)hipStreamSynchronize(s);
-  for (int b = 0; b < 2; b++) {
-    if (rc == SD_CAS_OK && pending[b]) emit(b);
-    (void)hipEventDestroy(done[b]);
-  }
+  destroy_events();
   if (rc) return rc;
   // big files and files that grew: the streaming path, one at a time (after the windows:
   // it reuses the pinned and device staging)
@@ -494,6 +615,7 @@ int sd_cas_file_checksums(sd_cas_ctx* c, const char* const* paths, size_t n, cha
     if (r == SD_CAS_EIO) { status[i] = -(err_no ? err_no : EIO); o[0] = 0; continue; }
     if (r) return r;
   }
+  tr.mark("streamed");
   for (size_t i = 0; i < n; i++)
     if (status[i]) out_hex[65 * i] = 0;
   return SD_CAS_OK;

@@ -504,6 +504,57 @@ def test_group_methods_and_deep_plans(eng, oracle, method, target, n):
         eng.set_group_method()
 
 
+def test_lsd_group_runs_across_tiles(eng, oracle):
+    """The LSD grouping's runs kernel (round 6: heads + rep in one pass, a run entering a tile
+    found by a galloping lower bound): runs that end exactly at, one before and one after the
+    4,096-key tile boundaries, runs spanning many tiles, one key everywhere, 0 and 2^64-1,
+    hot keys among uniform ones — through sd_cas_group_dev (SD_CAS_GROUP_SORT: rep laid down
+    by the iota sort, only duplicates stored), the public sort_pairs + group_sorted pair
+    (every rep stored) and sd_cas_group_min_dev (two sorts), each vs the canonical grouping."""
+    rng = np.random.default_rng(61)
+    T = 4096
+    counts = [T, T, 1, T - 1, 2 * T, 3, T - 2, 1, 1, 5 * T + 7, 17, T + 1, 40 * T, 2, 9]
+    tiled = np.repeat(rng.integers(0, 2 ** 64, len(counts), dtype=np.uint64), counts)
+    hot = np.concatenate([rng.integers(0, 2 ** 64, 300_000, dtype=np.uint64),
+                          np.full(70_000, 0x1234, dtype=np.uint64),
+                          np.full(9_000, 2 ** 64 - 1, dtype=np.uint64), np.zeros(5000, dtype=np.uint64)])
+    pool = rng.integers(0, 2 ** 64, 700, dtype=np.uint64)
+    cases = {
+        "tile-aligned runs": tiled[rng.permutation(len(tiled))],
+        "tile-aligned runs, input sorted": np.sort(tiled),
+        "one key": np.full(3 * T * 25 + 5, 0xABCDEF, dtype=np.uint64),
+        "hot keys": hot[rng.permutation(len(hot))],
+        "few keys, long runs": pool[rng.integers(0, len(pool), 1_000_003)],
+        "30% dups at a tile multiple": None,
+    }
+    u = rng.integers(0, 2 ** 64, 7 * T * 10 // 10, dtype=np.uint64)
+    cases["30% dups at a tile multiple"] = np.concatenate([u, u[rng.integers(0, len(u), 10 * T - len(u))]])
+    for name, keys in cases.items():
+        n = len(keys)
+        orep, oobj = oracle.group_canonical(keys)
+        eng.set_group_method(eng.GROUP_SORT)
+        try:
+            rep = torch.full((n,), -7, dtype=torch.int32, device="cuda")
+            objects = eng.group(dev64(keys), rep)
+            assert objects == oobj, name
+            assert (rep.cpu().numpy().astype(np.uint32) == orep).all(), name
+            vals = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+            out = torch.empty(n, dtype=torch.int32, device="cuda")
+            objects = eng.group_min(dev64(keys), torch.from_numpy(vals.view(np.int32)).cuda(), out)
+            uniq, inv = np.unique(keys, return_inverse=True)
+            mins = np.full(len(uniq), 0xFFFFFFFF, dtype=np.uint32)
+            np.minimum.at(mins, inv, vals)
+            assert objects == len(uniq) and (out.cpu().numpy().view(np.uint32) == mins[inv]).all(), name
+        finally:
+            eng.set_group_method()
+        ko = torch.empty(n, dtype=torch.int64, device="cuda")
+        vo = torch.empty(n, dtype=torch.int32, device="cuda")
+        eng.sort_pairs(dev64(keys), None, ko, vo)
+        rep2 = torch.full((n,), -7, dtype=torch.int32, device="cuda")
+        assert eng.group_sorted(ko, vo, rep2) == oobj, name
+        assert (rep2.cpu().numpy().astype(np.uint32) == orep).all(), name
+
+
 @pytest.mark.parametrize("quanta", [1, 2, 3])
 def test_hash_group_fused_vs_standalone(eng, oracle, quanta):
     """sd_cas_hash_group_sampled_dev (K1G: K1 with the grouping partition in its epilogue, then
@@ -1350,6 +1401,44 @@ def test_file_checksums_many_small_files(eng, oracle, tmp_path):
     finally:
         for p in paths:
             os.unlink(p)
+        os.rmdir(root)
+
+
+def test_file_checksums_pieces_and_slot_rotation(eng, oracle):
+    """Round 6 piece queue of sd_cas_file_checksums: files read as 1 MiB pieces (the last piece
+    takes the rest, incl. the EOF probe byte), lengths at every piece-count boundary, ~700 MB
+    so the windows rotate over the three pinned slots twice, missing paths between, and the
+    same files again (a second call reuses the grown staging) — every digest vs the oracle."""
+    d = "/dev/shm" if os.path.isdir("/dev/shm") else "/tmp"
+    root = os.path.join(d, f"sdcas_pieces_{os.getpid()}")
+    os.makedirs(root)
+    rng = np.random.default_rng(16)
+    M = 1 << 20
+    sizes = [k * M + e for k in (1, 2, 3) for e in (-129, -128, -127, -1, 0, 1, 127, 128)]
+    sizes += [int(x) for x in rng.integers(M // 2, 3 * M, 400)]
+    rng.shuffle(sizes)
+    paths = []
+    try:
+        for i, L in enumerate(sizes):
+            p = os.path.join(root, f"{i}")
+            with open(p, "wb") as fh:
+                fh.write(rng.integers(0, 256, int(L), dtype=np.uint8).tobytes())
+            paths.append(p)
+            if i % 97 == 5:
+                paths.append(os.path.join(root, f"missing{i}"))
+        assert sum(sizes) > 5 * (128 << 20)
+        want = {p: oracle.file_checksum(p) for p in paths if "missing" not in p}
+        for _ in range(2):
+            digests, errs = eng.file_checksums(paths)
+            for p, g, e in zip(paths, digests, errs):
+                if "missing" in p:
+                    assert g is None and e == 2
+                else:
+                    assert e == 0 and g == want[p], p
+    finally:
+        for p in paths:
+            if os.path.exists(p):
+                os.unlink(p)
         os.rmdir(root)
 
 

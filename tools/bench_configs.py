@@ -32,6 +32,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 THREADS = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+DROPIN_PASSES = int(os.environ.get("SD_CONFIG1_PASSES", "1"))
 
 
 def emit(d):
@@ -55,10 +56,15 @@ def config1(eng, orc, n_files: int, root: str):
         keys, errs = eng.generate_cas_keys_from_paths(paths, sizes)
         gpu_cold = time.perf_counter() - t  # includes growing the pinned staging once
         assert not errs.any()
-        t = time.perf_counter()
-        keys2, _ = eng.generate_cas_keys_from_paths(paths, sizes)
-        gpu = time.perf_counter() - t
-        assert (keys2 == keys).all()
+        # round 6: several timed passes of the drop-in call, median reported
+        # (one pass per run gave 629 k-854 k files/s across runs)
+        passes = []
+        for _ in range(max(1, DROPIN_PASSES)):
+            t = time.perf_counter()
+            keys2, _ = eng.generate_cas_keys_from_paths(paths, sizes)
+            passes.append(time.perf_counter() - t)
+            assert (keys2 == keys).all()
+        gpu = float(np.median(passes))
         t = time.perf_counter()
         want = [orc.generate_cas_id(p, int(s)) for p, s in zip(paths, sizes)]
         cpu1 = time.perf_counter() - t
@@ -121,6 +127,7 @@ def config1(eng, orc, n_files: int, root: str):
         emit({"config": 1, "files": n_files, "bytes_on_disk": total, "cpu_official_c": official,
               "small_fraction": float((sizes <= 102400).mean()),
               "gpu_dropin_files_per_s": n_files / gpu, "gpu_s": gpu, "gpu_s_first_call": gpu_cold,
+              "gpu_dropin_passes_files_per_s": [round(n_files / x) for x in passes],
               "job_step_100_ms": {k: round(v, 3) for k, v in step.items()},
               "job_step_100_ms_median": {k: round(v, 3) for k, v in step_med.items()},
               "cpu_step_100_ms": {k: {a: round(b, 3) for a, b in v.items()} for k, v in cpu_step.items()},

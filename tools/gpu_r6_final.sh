@@ -1,13 +1,13 @@
 #!/bin/bash
-# Round-5 evidence pass: GPU suite (release, then the debug build's invariant checks), smoke,
-# headline bench (fused chain at N=1, live rocm-smi power in the line), the --gpus 8 one-GPU
-# rehearsal, BASELINE configs 1-4, the validator shapes, the link emission forms, rocprofv3
-# kernel stats of the bench and PMC passes on K1G (HBM bytes).
+# Round-6 evidence pass: GPU suite (release, then the debug build's invariant checks), smoke,
+# headline bench (fused chain at N=1, live rocm-smi power in the line), the --gpus 2 / 4 / 8
+# one-GPU rehearsals, BASELINE configs 1-4, the validator shapes and file path, the link
+# emission forms, rocprofv3 kernel stats of the bench and PMC passes on K1G (HBM bytes).
 # Usage: <tag> [skip-suite | suite]   (suite: the suites and smoke only; two calls fit gpurun)
 # Each GPU step has its own time limit; stop at the first failure.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-OUT=$R/gpurun_out/${1:-r5_final}
+OUT=$R/gpurun_out/${1:-r6_final}
 mkdir -p $OUT
 cd $R
 if [ "$2" != "skip-suite" ]; then
@@ -21,9 +21,11 @@ if [ "$2" != "skip-suite" ]; then
 fi
 timeout -k 10 400 python3 -u bench.py --steps 20 --warmup 3 > $OUT/bench.log 2>&1 || { echo BENCH_FAIL; tail -20 $OUT/bench.log; exit 1; }
 tail -1 $OUT/bench.log | cut -c1-300
+SD_BENCH_ONE_DEVICE=1 SD_CPU_BASELINE_THREADS=16 timeout -k 10 500 python3 -u bench.py --gpus 2 --steps 10 --warmup 2 --files-per-gpu 262144 --e2e-files 1048576 > $OUT/bench_n2_rehearsal.log 2>&1 || { echo REH2_FAIL; tail -20 $OUT/bench_n2_rehearsal.log; exit 1; }
+SD_BENCH_ONE_DEVICE=1 SD_CPU_BASELINE_THREADS=16 timeout -k 10 500 python3 -u bench.py --gpus 4 --steps 10 --warmup 2 --files-per-gpu 131072 --e2e-files 1048576 > $OUT/bench_n4_rehearsal.log 2>&1 || { echo REH4_FAIL; tail -20 $OUT/bench_n4_rehearsal.log; exit 1; }
 SD_BENCH_ONE_DEVICE=1 SD_CPU_BASELINE_THREADS=16 timeout -k 10 500 python3 -u bench.py --gpus 8 --steps 10 --warmup 2 --files-per-gpu 65536 --e2e-files 524288 > $OUT/bench_n8_rehearsal.log 2>&1 || { echo REH_FAIL; tail -20 $OUT/bench_n8_rehearsal.log; exit 1; }
-timeout -k 10 600 python3 -u tools/bench_configs.py --config 2 --config 3e --config 4 --config 1 > $OUT/configs.log 2>&1 || { echo CONFIGS_FAIL; tail -20 $OUT/configs.log; exit 1; }
-timeout -k 10 300 python3 -u tools/prof_checksums.py --paths 2000 > $OUT/validator.log 2>&1 || { echo VALIDATOR_FAIL; tail -20 $OUT/validator.log; exit 1; }
+SD_CONFIG1_PASSES=7 timeout -k 10 600 python3 -u tools/bench_configs.py --config 2 --config 3e --config 4 --config 1 > $OUT/configs.log 2>&1 || { echo CONFIGS_FAIL; tail -20 $OUT/configs.log; exit 1; }
+timeout -k 10 300 python3 -u tools/prof_checksums.py --paths 2000 --path-runs 6 > $OUT/validator.log 2>&1 || { echo VALIDATOR_FAIL; tail -20 $OUT/validator.log; exit 1; }
 timeout -k 10 300 python3 -u tools/prof_links.py > $OUT/links.log 2>&1 || { echo LINKS_FAIL; tail -20 $OUT/links.log; exit 1; }
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench --output-format csv -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu-baseline --sustain-seconds 0 --e2e-files 0 > $OUT/bench_prof.log 2>&1 || { echo PROF_FAIL; exit 1; }

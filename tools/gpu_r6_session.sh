@@ -1,0 +1,95 @@
+#!/bin/bash
+# Round-6 focused GPU session.  Usage: <tag> <step>...  Steps (each under its own time limit,
+# stop at the first failure):
+#   valtests   the validator / path GPU tests
+#   valab      validator file path A/B: the in-tree library vs tools/ablib/val_r5.so (round 5's
+#              whole-file pread windows), interleaved, 2,000 tmpfs files, 6 passes each
+#   valab2     the same over several builds: in-tree + $VAL_VARIANTS (tools/ablib/<name>.so)
+#   h2d        tools/h2d_sizes.py: H2D rate by transfer size, one and two streams
+#   mmapprobe  tools/probe_mmap_reg (needs it built): tmpfs files mapped + hipHostRegister'ed, DMA'd
+#              straight to HBM, vs the pread copy
+#   config1    BASELINE config 1 with 7 timed drop-in passes, twice, then one traced pass
+#   reh2 reh4  the one-GPU rehearsals of the N = 2 / N = 4 bench lines
+#   sorttests  the sort / grouping / link GPU tests
+#   sortab     LSD grouping at 12.5 M keys: in-tree vs $SORT_VARIANTS (default sort_r5: round
+#              5's group.hip), 3 interleaved rounds, then a rocprofv3 kernel trace of the new one
+#   sortpmc    tools/gpu_r6_pmc_sort.sh (HBM bytes per key of hash / lsd / lsdapi)
+#   power      tools/power_split.py (needs tools/ubench_k1 built): where K1's random-content power goes
+#   stress     randomised parity: grouping with the forced LSD path every iteration, link
+#              emission vs the replay, the path gather + validator file path vs the C oracle
+#   suite      the whole GPU suite (release)
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/${1:-r6}
+shift
+mkdir -p $OUT
+cd $R
+for step in "$@"; do
+  case $step in
+    valtests)
+      timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "checksum or from_paths" > $OUT/pytest_validator.log 2>&1 || { echo VALTESTS_FAIL; tail -30 $OUT/pytest_validator.log; exit 1; }
+      tail -1 $OUT/pytest_validator.log ;;
+    valab)
+      for k in 1 2; do
+        timeout -k 10 300 python3 -u tools/prof_checksums.py --no-device --paths 2000 --path-runs 6 > $OUT/val_new_$k.log 2>&1 || { echo VALAB_FAIL; tail -20 $OUT/val_new_$k.log; exit 1; }
+        SD_HIP_CAS_LIB=$R/tools/ablib/val_r5.so timeout -k 10 300 python3 -u tools/prof_checksums.py --no-device --paths 2000 --path-runs 6 > $OUT/val_r5_$k.log 2>&1 || { echo VALAB_FAIL; tail -20 $OUT/val_r5_$k.log; exit 1; }
+      done
+      SD_CAS_TRACE=1 timeout -k 10 300 python3 -u tools/prof_checksums.py --no-device --paths 2000 --path-runs 4 > $OUT/val_new_trace.log 2>&1 || { echo VALAB_FAIL; exit 1; }
+      grep -h '"files"' $OUT/val_*_[12].log | cut -c1-400 ;;
+    valab2)
+      for k in $(seq 1 ${VAL_ROUNDS:-2}); do
+        for v in intree ${VAL_VARIANTS:-val_r5}; do
+          lib=""; [ $v != intree ] && lib=$R/tools/ablib/$v.so
+          SD_HIP_CAS_LIB=$lib timeout -k 10 300 python3 -u tools/prof_checksums.py --no-device --paths 2000 --path-runs 6 > $OUT/val2_${v}_$k.log 2>&1 || { echo VALAB2_FAIL; tail -20 $OUT/val2_${v}_$k.log; exit 1; }
+        done
+      done ;;
+    h2d)
+      timeout -k 10 200 python3 -u tools/h2d_sizes.py > $OUT/h2d_sizes.log 2>&1 || { echo H2D_FAIL; tail -20 $OUT/h2d_sizes.log; exit 1; } ;;
+    mmapprobe)
+      timeout -k 10 300 tools/probe_mmap_reg 15 > $OUT/probe_mmap_reg.log 2>&1 || { echo MMAP_FAIL; tail -20 $OUT/probe_mmap_reg.log; exit 1; }
+      cat $OUT/probe_mmap_reg.log ;;
+    config1)
+      for k in 1 2; do
+        SD_CONFIG1_PASSES=7 timeout -k 10 300 python3 -u tools/bench_configs.py --config 1 > $OUT/config1_$k.log 2>&1 || { echo CONFIG1_FAIL; tail -20 $OUT/config1_$k.log; exit 1; }
+      done
+      SD_CAS_TRACE=1 SD_CONFIG1_PASSES=7 timeout -k 10 300 python3 -u tools/bench_configs.py --config 1 > $OUT/config1_trace.log 2>&1 || { echo CONFIG1_FAIL; exit 1; }
+      grep -h '"config"' $OUT/config1_[12].log | cut -c1-600 ;;
+    reh2)
+      SD_BENCH_ONE_DEVICE=1 SD_CPU_BASELINE_THREADS=16 timeout -k 10 500 python3 -u bench.py --gpus 2 --steps 10 --warmup 2 --files-per-gpu 262144 --e2e-files 1048576 > $OUT/bench_n2_rehearsal.log 2>&1 || { echo REH2_FAIL; tail -20 $OUT/bench_n2_rehearsal.log; exit 1; }
+      tail -1 $OUT/bench_n2_rehearsal.log | cut -c1-300 ;;
+    reh4)
+      SD_BENCH_ONE_DEVICE=1 SD_CPU_BASELINE_THREADS=16 timeout -k 10 500 python3 -u bench.py --gpus 4 --steps 10 --warmup 2 --files-per-gpu 131072 --e2e-files 1048576 > $OUT/bench_n4_rehearsal.log 2>&1 || { echo REH4_FAIL; tail -20 $OUT/bench_n4_rehearsal.log; exit 1; }
+      tail -1 $OUT/bench_n4_rehearsal.log | cut -c1-300 ;;
+    sorttests)
+      timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "sort or group or links or identifier" > $OUT/pytest_sort.log 2>&1 || { echo SORTTESTS_FAIL; tail -30 $OUT/pytest_sort.log; exit 1; }
+      tail -1 $OUT/pytest_sort.log ;;
+    sortab)
+      for k in 1 2 3; do
+        timeout -k 10 200 python3 -u tools/bench_group.py 1310720 12500000 > $OUT/group_new_$k.log 2>&1 || { echo SORTAB_FAIL; tail -20 $OUT/group_new_$k.log; exit 1; }
+        for v in ${SORT_VARIANTS:-sort_r5}; do
+          SD_HIP_CAS_LIB=$R/tools/ablib/$v.so timeout -k 10 200 python3 -u tools/bench_group.py --only lsd 12500000 > $OUT/group_${v}_$k.log 2>&1 || { echo SORTAB_FAIL; tail -20 $OUT/group_${v}_$k.log; exit 1; }
+        done
+      done
+      grep -h '"keys": 12500000' $OUT/group_*_[123].log | cut -c1-300
+      cd /tmp && export TMPDIR=/tmp
+      timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/sortprof -o run --output-format csv -- python3 $R/tools/bench_group.py --only lsd 12500000 > $OUT/sortprof.log 2>&1 || { echo SORTPROF_FAIL; exit 1; }
+      cd $R ;;
+    sortpmc)
+      bash tools/gpu_r6_pmc_sort.sh ${OUT#$R/gpurun_out/}/pmc || { echo SORTPMC_FAIL; exit 1; } ;;
+    power)
+      timeout -k 10 400 python3 -u tools/power_split.py --seconds 6 --rounds 2 > $OUT/power_split.log 2>&1 || { echo POWER_FAIL; tail -20 $OUT/power_split.log; exit 1; }
+      tail -1 $OUT/power_split.log ;;
+    stress)
+      timeout -k 10 300 python3 -u tools/stress_parity.py --seconds 150 --lsd-every 1 > $OUT/stress_parity_lsd.log 2>&1 || { echo STRESS_FAIL; tail -5 $OUT/stress_parity_lsd.log; exit 1; }
+      tail -1 $OUT/stress_parity_lsd.log | cut -c1-300
+      timeout -k 10 240 python3 -u tools/stress_links.py --seconds 90 > $OUT/stress_links.log 2>&1 || { echo STRESS_FAIL; tail -5 $OUT/stress_links.log; exit 1; }
+      tail -1 $OUT/stress_links.log | cut -c1-300
+      timeout -k 10 240 python3 -u tools/stress_paths.py --checksums --seconds 90 > $OUT/stress_paths.log 2>&1 || { echo STRESS_FAIL; tail -5 $OUT/stress_paths.log; exit 1; }
+      tail -1 $OUT/stress_paths.log | cut -c1-300 ;;
+    suite)
+      timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -30 $OUT/pytest_gpu.log; exit 1; }
+      tail -1 $OUT/pytest_gpu.log ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo SESSION_OK

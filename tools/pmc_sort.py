@@ -1,15 +1,15 @@
 #!/usr/bin/env python3
-"""HBM bytes per key of the two Object-grouping methods at 12.5 M keys (config 4's rank share)
-from the rocprofv3 --pmc passes of tools/gpu_r5_pmc_sort.sh: per method (one process each,
-tools/bench_group.py --only hash|lsd, `chain_calls` chains per process), the FETCH_SIZE /
-WRITE_SIZE of every sd_* dispatch summed and divided by chain_calls x keys.  gfx950
-correction (MI355X_MICROARCH.md, HBM/rocprofv3): FETCH_SIZE reports half the bytes of a wide
-coalesced read, so it is doubled; both are in KiB.  Algorithmic bytes per key: hash chain
-68 B (bench.group_bytes_per_key, two-level region chain); LSD sort as implemented (group.hip):
-8 passes x (upsweep reads the 8-B key + scatter reads and writes key + 4-B idx = 32 B) +
-run heads (read 8) + emit (read 12, write the 4-B rep) = 280 B; SURVEY §8(d)'s model of a
-sort without a separate histogram read (8 x 24 + 16 = 208 B) is reported beside it.
-Usage: pmc_sort.py <out dir>   (expects <out>/{hash,lsd}_{fetch,write,hit}/ and *.log)"""
+"""HBM bytes per key of the Object-grouping methods at 12.5 M keys (config 4's rank share)
+from the rocprofv3 --pmc passes of tools/gpu_r6_pmc_sort.sh: per method (one process each,
+tools/bench_group.py --only hash|lsd|lsdapi, `chain_calls` chains per process), the
+FETCH_SIZE / WRITE_SIZE of every sd_* dispatch summed and divided by chain_calls x keys.
+gfx950 correction (MI355X_MICROARCH.md, HBM/rocprofv3): FETCH_SIZE reports half the bytes of
+a wide coalesced read, so it is doubled; both are in KiB.  Algorithmic bytes per key (ALGO
+below): hash chain 68 B (bench.group_bytes_per_key, two-level region chain); the LSD sort as
+implemented (group.hip): 8 passes x (upsweep reads the 8-B key + scatter reads and writes key
++ 4-B idx = 32 B), then the runs kernel; SURVEY §8(d)'s model of a sort without a separate
+histogram read (8 x 24 + 16 = 208 B) is reported beside it.
+Usage: pmc_sort.py <out dir>   (expects <out>/<method>_{fetch,write,hit}/ and *.log)"""
 import csv
 import glob
 import json
@@ -18,8 +18,13 @@ import sys
 from collections import defaultdict
 
 KEYS = 12_500_000
-ALGO = {"hash": 68, "lsd": 8 * 32 + 8 + 16}
-SURVEY_MODEL = {"hash": None, "lsd": 208}
+# round 6: "lsd" = the product's LSD grouping (sd_cas_group_dev, SD_CAS_GROUP_SORT): 8 passes x
+# 32 B + rep[i] = i laid down by the first pass (4) + the runs kernel reading the sorted pairs
+# (12) + one 4-B rep store per key that is not its run's head ((n - objects) / n x 4, added
+# below); "lsdapi" = sd_cas_sort_pairs_dev + sd_cas_group_sorted_dev (every rep stored: 272)
+ALGO = {"hash": 68, "lsd": 8 * 32 + 4 + 12, "lsdapi": 8 * 32 + 12 + 4}
+SURVEY_MODEL = {"hash": None, "lsd": 208, "lsdapi": 208}
+METHODS = ("hash", "lsd", "lsdapi")
 
 
 def counters(d):
@@ -38,12 +43,16 @@ def counters(d):
 def main():
     out = sys.argv[1]
     res = {"keys": KEYS, "correction": "FETCH_SIZE x 2 (gfx950), KiB -> bytes x 1024"}
-    for m in ("hash", "lsd"):
-        chains = None
+    for m in METHODS:
+        if not os.path.exists(os.path.join(out, f"{m}_fetch.log")):
+            continue
+        chains, objects = None, None
         with open(os.path.join(out, f"{m}_fetch.log")) as fh:
             for line in fh:
                 if line.startswith("{"):
                     chains = json.loads(line)["chain_calls"]
+                    objects = json.loads(line).get("objects")
+        algo = ALGO[m] + (4 * (KEYS - objects) / KEYS if m == "lsd" and objects else 0)
         fetch, fc = counters(os.path.join(out, f"{m}_fetch"))
         write, _ = counters(os.path.join(out, f"{m}_write"))
         hit, _ = counters(os.path.join(out, f"{m}_hit"))
@@ -59,8 +68,8 @@ def main():
             tot_r += r
             tot_w += w
         res[m] = {"chain_calls": chains, "measured_b_per_key": tot_r + tot_w, "read_b_per_key": tot_r,
-                  "write_b_per_key": tot_w, "algorithmic_b_per_key": ALGO[m],
-                  "measured_over_algorithmic": (tot_r + tot_w) / ALGO[m],
+                  "write_b_per_key": tot_w, "algorithmic_b_per_key": algo,
+                  "measured_over_algorithmic": (tot_r + tot_w) / algo,
                   "survey_model_b_per_key": SURVEY_MODEL[m], "kernels": per_kernel}
     print(json.dumps(res, indent=1))
 

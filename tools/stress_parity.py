@@ -66,6 +66,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=180)
     ap.add_argument("--max-n", type=int, default=4_000_000)
     ap.add_argument("--seed", type=int, default=2026)
+    ap.add_argument("--lsd-every", type=int, default=4, help="forced LSD grouping every k-th iteration")
     ap.add_argument("--validator", action="store_true",
                     help="also stress sd_cas_checksums_dev: random batches of ragged buffers vs the oracle")
     ap.add_argument("--fused", action="store_true",
@@ -96,7 +97,9 @@ def main():
         dk = torch.from_numpy(keys.view(np.int64)).cuda()
         res = {"it": it, "n": n, "pattern": pattern}
         # grouping (hash; every 4th iteration the LSD path)
-        method = 2 if it % 4 == 3 else 0
+        # the forced LSD path every 4th iteration (--lsd-every 1: every iteration; a pattern
+        # per iteration still cycles through all four)
+        method = 2 if it % a.lsd_every == a.lsd_every - 1 else 0
         eng.set_group_method(method)
         rep = torch.empty(n, dtype=torch.int32, device="cuda")
         objects = eng.group(dk, rep)

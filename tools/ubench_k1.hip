@@ -3,9 +3,12 @@
 // L2-resident window, or broadcast (every lane the same file), plus the compute-only loop,
 // each with the shader clock measured inside the kernel (s_memtime / s_memrealtime).
 // Build: hipcc --offload-arch=gfx950 -O3 -I spacedrive_amd/csrc -I include -o tools/ubench_k1 tools/ubench_k1.hip
+// `ubench_k1 sustain <mode> <data> <seconds>` runs one variant back to back (tools/power_split.py).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "../spacedrive_amd/csrc/cas_hash.hip"
 
@@ -38,23 +41,25 @@ __device__ __forceinline__ void load_pair(const uint4* __restrict__ q, uint32_t 
   }
 }
 
-// the product's sdcas::cas_lane_sampled with the loader swapped
+// the product's sdcas::cas_lane_sampled (cas_hash.hip, round 5's loop: both lines loaded at
+// the iteration start) with the loader swapped — rebased in round 6: the round-5
+// LINE / QUAD / non-temporal rows in profiles/r05/valu_power*/ubench_k1.txt were measured
+// with the older loop that prefetched a pair across the back edge
 template <bool NT = false, int L = LAYOUT_ROW, int BLK = 256>
 __device__ __forceinline__ uint64_t cas_lane_sampled(const uint4* __restrict__ q, uint64_t size,
                                                      sdcas::LdsStack<BLK>& stk) {
   using namespace sdcas;
   uint32_t c0 = (uint32_t)size, c1 = (uint32_t)(size >> 32);
   uint4 A[8], B[8];
-  load_pair<NT, L>(q, 0, A);
   uint32_t cv[8];
   for (uint32_t c = 0; c < SAMPLED_CHUNKS; ++c) {
     set_iv(cv);
 #pragma unroll 1
     for (uint32_t pp = 0; pp < 4; ++pp) {
       const uint32_t P = 8u * c + 2u * pp;
+      load_pair<NT, L>(q, P, A);
       load_pair<NT, L>(q, P + 1, B);
       compress_pair(cv, A, c0, c1, c, pp == 0 ? (uint32_t)CHUNK_START : 0u, 0u);
-      if (P + 2 < SAMPLED_PAIRS) load_pair<NT, L>(q, P + 2, A);
       compress_pair(cv, B, c0, c1, c, 0u, pp == 3 ? (uint32_t)CHUNK_END : 0u);
     }
     uint32_t total = c + 1;
@@ -136,6 +141,24 @@ __global__ void __launch_bounds__(256) k_compress(uint32_t* out, uint32_t seed, 
   }
 }
 
+// compute-only with a CONSTANT message (the cv chain still evolves): the ALU share of the
+// random-content power cost (tools/power_split.py)
+__global__ void __launch_bounds__(256) k_compress_const(uint32_t* out, uint32_t seed, uint64_t* clk) {
+  uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t cv[8];
+  sdcas::set_iv(cv);
+  uint32_t m[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) m[i] = seed;
+  for (int i = 0; i < 953; ++i) sdcas::compress(cv, m, (uint32_t)i, 0u, 64u, 0u);
+  out[blockIdx.x * 256 + threadIdx.x] = cv[0] ^ cv[7];
+  uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) {
+    atomicAdd((unsigned long long*)&clk[0], (unsigned long long)(t1 - t0));
+    atomicAdd((unsigned long long*)&clk[1], (unsigned long long)(r1 - r0));
+  }
+}
+
 __global__ void fill_random(uint32_t* p, uint64_t nwords, uint32_t seed) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nwords;
        i += (uint64_t)gridDim.x * blockDim.x) {
@@ -146,7 +169,73 @@ __global__ void fill_random(uint32_t* p, uint64_t nwords, uint32_t seed) {
   }
 }
 
-int main() {
+static int launch(int mode, const uint8_t* content, uint64_t stride, const uint64_t* sizes, uint64_t n,
+                  uint64_t* keys, uint32_t* out, uint64_t* clk) {
+  const uint32_t blocks = (uint32_t)(n / 256);
+  switch (mode) {
+    case 0: k1_variant<0><<<blocks, 256>>>(content, stride, sizes, n, keys, clk); break;
+    case 1: k1_variant<1><<<blocks, 256>>>(content, stride, sizes, n, keys, clk); break;
+    case 2: k1_variant<2><<<blocks, 256>>>(content, stride, sizes, n, keys, clk); break;
+    case 3: k_compress<<<blocks, 256>>>(out, 1u, clk); break;
+    case 4: k1_variant<4><<<blocks, 256>>>(content, stride, sizes, n, keys, clk); break;
+    case 5: k1_variant<5><<<blocks, 256>>>(content, stride, sizes, n, keys, clk); break;
+    case 6: k1_variant<6><<<blocks, 256>>>(content, stride, sizes, n, keys, clk); break;
+    case 7: k_compress_const<<<blocks, 256>>>(out, 0x5a5a5a5au, clk); break;
+    default: return 1;
+  }
+  return 0;
+}
+
+// `ubench_k1 sustain <mode> <data> <seconds>`: one variant back to back for <seconds>
+// (data 0: constant 0x5a bytes, 1: random, 2: zero), one JSON line with the rate and the
+// in-kernel clock of the last second — tools/power_split.py samples rocm-smi beside it.
+static int sustain(int mode, int data, double seconds) {
+  const uint64_t n = 1310720, stride = 57344;
+  uint8_t* content;
+  uint64_t *sizes, *keys, *clk;
+  uint32_t* out;
+  CHECK(hipMalloc(&content, n * stride));
+  CHECK(hipMalloc(&sizes, n * 8));
+  CHECK(hipMalloc(&keys, n * 8));
+  CHECK(hipMalloc(&clk, 16));
+  CHECK(hipMalloc(&out, n * 4));
+  CHECK(hipMemset(content, data == 2 ? 0 : 0x5a, n * stride));
+  CHECK(hipMemset(sizes, 0x11, n * 8));
+  if (data == 1) fill_random<<<4096, 256>>>((uint32_t*)content, n * stride / 4, 7u);
+  CHECK(hipDeviceSynchronize());
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  double t_all = 0, t_late = 0, cyc = 0, real = 0;
+  uint64_t launches = 0, late = 0;
+  while (t_all < seconds * 1e3) {
+    CHECK(hipMemset(clk, 0, 16));
+    CHECK(hipEventRecord(a, 0));
+    if (launch(mode, content, stride, sizes, n, keys, out, clk)) return 2;
+    CHECK(hipEventRecord(b, 0));
+    CHECK(hipEventSynchronize(b));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    t_all += ms;
+    ++launches;
+    if (t_all > 1e3) {  // after a 1 s settle
+      uint64_t h[2];
+      CHECK(hipMemcpy(h, clk, 16, hipMemcpyDeviceToHost));
+      t_late += ms;
+      ++late;
+      cyc += (double)h[0];
+      real += (double)h[1];
+    }
+  }
+  printf("{\"mode\": %d, \"data\": %d, \"launches\": %llu, \"files_per_s\": %.1f, "
+         "\"kernel_ms_mean\": %.4f, \"clock_ghz\": %.4f}\n",
+         mode, data, (unsigned long long)launches, late ? n * late / (t_late * 1e-3) : 0.0,
+         late ? t_late / late : 0.0, real > 0 ? cyc / real * 0.1 : 0.0);
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc == 5 && !strcmp(argv[1], "sustain")) return sustain(atoi(argv[2]), atoi(argv[3]), atof(argv[4]));
   const uint64_t n = 1310720, stride = 57344;
   uint8_t* content;
   uint64_t *sizes, *keys, *clk;
