@@ -332,6 +332,12 @@ int sd_cas_checksums_dev(sd_cas_ctx* c, const void* d_arena, uint64_t arena_byte
 #ifndef SD_CK_COPY_MB
 #define SD_CK_COPY_MB 8
 #endif
+#ifndef SD_CK_PUMP_READS  // the pump thread also reads pieces when it has nothing to issue
+#define SD_CK_PUMP_READS 1
+#endif
+#ifndef SD_CK_COPY_STREAMS  // copies alternate over this many streams (1 or 2)
+#define SD_CK_COPY_STREAMS 1
+#endif
 
 // file_checksum over many paths.  The batch files are laid out in windows of up to CK_WIN
 // bytes / CK_WIN_FILES files in index order (one slot of up128(st_size + 1) per file: the
@@ -530,7 +536,8 @@ int sd_cas_file_checksums(sd_cas_ctx* c, const char* const* paths, size_t n, cha
         const bool complete = ready == wpiece[wc + 1];
         const uint64_t hi = complete ? wbytes[wc] : moff[pieces[ready].mem] + pieces[ready].off;
         if (hi > sent && (hi - sent >= CK_COPY || complete)) {
-          const hipError_t e = hipMemcpyAsync(dev + HDR + sent, pin + HDR + sent, hi - sent, hipMemcpyHostToDevice, cs);
+          hipStream_t xs = (SD_CK_COPY_STREAMS > 1 && (ncopies & 1)) ? c->copy2 : cs;
+          const hipError_t e = hipMemcpyAsync(dev + HDR + sent, pin + HDR + sent, hi - sent, hipMemcpyHostToDevice, xs);
           if (e != hipSuccess) { hipfail(e, "copy"); break; }
           sent = hi;
           ++ncopies;
@@ -553,7 +560,12 @@ int sd_cas_file_checksums(sd_cas_ctx* c, const char* const* paths, size_t n, cha
             if (got == mcap[k] || mirr[k].load() || got < fsize[i]) { kind[i] = K_STREAM; continue; }
             h_lens[j] = got;
           }
-          hipError_t e = hipMemcpyAsync(dev, pin, CK_WIN_FILES * 16, hipMemcpyHostToDevice, cs);
+          hipError_t e = hipSuccess;
+          if (SD_CK_COPY_STREAMS > 1) {  // the header copy (on cs) after copy2's pieces too
+            e = hipEventRecord(landed, c->copy2);
+            if (e == hipSuccess) e = hipStreamWaitEvent(cs, landed, 0);
+          }
+          if (e == hipSuccess) e = hipMemcpyAsync(dev, pin, CK_WIN_FILES * 16, hipMemcpyHostToDevice, cs);
           if (e == hipSuccess) e = hipEventRecord(landed, cs);
           if (e == hipSuccess) e = hipStreamWaitEvent(s, landed, 0);
           if (e == hipSuccess)
@@ -574,7 +586,7 @@ int sd_cas_file_checksums(sd_cas_ctx* c, const char* const* paths, size_t n, cha
       // nothing to copy or retire: read a piece too (a 16th reader) if its slot is free
       // (only a piece whose slot is free now: this thread is the one that frees slots)
       size_t p = next.load(std::memory_order_relaxed);
-      if (p < np && slot_free(pieces[p].win) && next.compare_exchange_strong(p, p + 1)) {
+      if (SD_CK_PUMP_READS && p < np && slot_free(pieces[p].win) && next.compare_exchange_strong(p, p + 1)) {
         read_piece(p);
         fin[p].store(1, std::memory_order_release);
       } else {
@@ -601,6 +613,7 @@ int sd_cas_file_checksums(sd_cas_ctx* c, const char* const* paths, size_t n, cha
     (void)sd_ws_release(c, s);
     // a failed call leaves nothing in flight that reads the pinned slots
     (void)hipStreamSynchronize(cs);
+    (void)hipStreamSynchronize(c->copy2);
     (void)hipStreamSynchronize(s);
   }
   destroy_events();

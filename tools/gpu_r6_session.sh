@@ -8,6 +8,7 @@
 #   h2d        tools/h2d_sizes.py: H2D rate by transfer size, one and two streams
 #   mmapprobe  tools/probe_mmap_reg (needs it built): tmpfs files mapped + hipHostRegister'ed, DMA'd
 #              straight to HBM, vs the pread copy
+#   probe      tools/probe_pread (needs it built) twice: the file path's reads by destination form
 #   config1    BASELINE config 1 with 7 timed drop-in passes, twice, then one traced pass
 #   reh2 reh4  the one-GPU rehearsals of the N = 2 / N = 4 bench lines
 #   sorttests  the sort / grouping / link GPU tests
@@ -17,6 +18,8 @@
 #   power      tools/power_split.py (needs tools/ubench_k1 built): where K1's random-content power goes
 #   stress     randomised parity: grouping with the forced LSD path every iteration, link
 #              emission vs the replay, the path gather + validator file path vs the C oracle
+#   powerab    K1 on random content, product layout vs the 64-file LINE / QUAD tiled layouts,
+#              10 s sustained each, 3 rounds (the HBM-energy lever)
 #   suite      the whole GPU suite (release)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
@@ -48,6 +51,11 @@ for step in "$@"; do
     mmapprobe)
       timeout -k 10 300 tools/probe_mmap_reg 15 > $OUT/probe_mmap_reg.log 2>&1 || { echo MMAP_FAIL; tail -20 $OUT/probe_mmap_reg.log; exit 1; }
       cat $OUT/probe_mmap_reg.log ;;
+    probe)
+      for k in 1 2; do
+        timeout -k 10 300 tools/probe_pread 15 $R/spacedrive_amd/libsd_hip_cas.so > $OUT/probe_pread_$k.log 2>&1 || { echo PROBE_FAIL; tail -20 $OUT/probe_pread_$k.log; exit 1; }
+      done
+      cat $OUT/probe_pread_*.log ;;
     config1)
       for k in 1 2; do
         SD_CONFIG1_PASSES=7 timeout -k 10 300 python3 -u tools/bench_configs.py --config 1 > $OUT/config1_$k.log 2>&1 || { echo CONFIG1_FAIL; tail -20 $OUT/config1_$k.log; exit 1; }
@@ -79,6 +87,9 @@ for step in "$@"; do
     power)
       timeout -k 10 400 python3 -u tools/power_split.py --seconds 6 --rounds 2 > $OUT/power_split.log 2>&1 || { echo POWER_FAIL; tail -20 $OUT/power_split.log; exit 1; }
       tail -1 $OUT/power_split.log ;;
+    powerab)
+      timeout -k 10 400 python3 -u tools/power_split.py --seconds 10 --rounds 3 --variants k1_rand,k1_line_rand,k1_quad_rand > $OUT/power_layout_ab.log 2>&1 || { echo POWERAB_FAIL; tail -20 $OUT/power_layout_ab.log; exit 1; }
+      cat $OUT/power_layout_ab.log | cut -c1-250 ;;
     stress)
       timeout -k 10 300 python3 -u tools/stress_parity.py --seconds 150 --lsd-every 1 > $OUT/stress_parity_lsd.log 2>&1 || { echo STRESS_FAIL; tail -5 $OUT/stress_parity_lsd.log; exit 1; }
       tail -1 $OUT/stress_parity_lsd.log | cut -c1-300

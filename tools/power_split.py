@@ -10,7 +10,8 @@ per file = (median power - idle power) / rate, after a 1 s settle.
   comp_rand / comp_const compute-only, 953 compressions per lane, message evolving / constant
 Splits (J per file, dynamic): HBM + fabric beyond L2 = k1_rand - l2_rand; on-chip toggling of
 random vs constant data = l2_rand - l2_const; the HBM share of the random-content cost =
-(k1_rand - k1_const) - (l2_rand - l2_const).  Two interleaved rounds.
+(k1_rand - k1_const) - (l2_rand - l2_const).  Two interleaved rounds.  --variants
+k1_rand,k1_line_rand,k1_quad_rand: the A/B of a layout with DRAM row locality.
 Usage: power_split.py [--seconds S] [--bin tools/ubench_k1]"""
 import argparse
 import json
@@ -23,7 +24,11 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from clock_probe import smi_sample  # noqa: E402
 
 VARIANTS = {"k1_rand": (0, 1), "k1_const": (0, 0), "l2_rand": (1, 1), "l2_const": (1, 0),
-            "comp_rand": (3, 1), "comp_const": (7, 1)}
+            "comp_rand": (3, 1), "comp_const": (7, 1),
+            # --variants: the HBM-energy A/B — 64-file tiled layouts, so a wave's loads of one
+            # iteration hit consecutive lines (DRAM row locality) instead of 64 files' rows
+            "k1_line_rand": (5, 1), "k1_quad_rand": (6, 1)}
+DEFAULT = ["k1_rand", "k1_const", "l2_rand", "l2_const", "comp_rand", "comp_const"]
 
 
 def run(binary, name, seconds):
@@ -54,13 +59,14 @@ def main():
     ap.add_argument("--seconds", type=float, default=6.0)
     ap.add_argument("--bin", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "ubench_k1"))
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--variants", default=",".join(DEFAULT))
     a = ap.parse_args()
     idle = [smi_sample()[0] for _ in range(5)]
     idle_w = sorted(x for x in idle if x is not None)[len(idle) // 2]
     print(json.dumps({"idle_power_w": idle_w, "idle_samples": idle}), flush=True)
     res = {}
     for r in range(a.rounds):
-        for name in VARIANTS:
+        for name in a.variants.split(","):
             line = run(a.bin, name, a.seconds)
             line["round"] = r
             print(json.dumps(line), flush=True)

@@ -9,10 +9,13 @@
 //   pinned+dma the "pinned" form while the GPU copies another 128 MB pinned buffer to HBM
 //             back to back (the file path double-buffers: window w is read while w-1 crosses)
 //   product   sd_cas_file_checksums (include/sd_hip_cas.h) on the same files, from C
+//   malloc1m / thp1m (round 6)  1 MiB preads into the malloc'd window / into a window of
+//             transparent huge pages registered with hipHostRegister
 // Build: hipcc --offload-arch=gfx950 -O2 -o tools/probe_pread tools/probe_pread.cpp -lpthread
 #include <hip/hip_runtime.h>
 #include <dlfcn.h>
 #include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <pthread.h>
 #include <unistd.h>
@@ -107,12 +110,30 @@ int main(int argc, char** argv) {
   memset(mwin, 0, (128u << 20) + (8u << 20));
   char* pwin = nullptr;
   if (hipHostMalloc((void**)&pwin, (128u << 20) + (8u << 20), hipHostMallocDefault) != hipSuccess) return 1;
-  const char* names[] = {"scratch", "malloc", "pinned", "pinned1m"};
-  char* wins[] = {nullptr, mwin, pwin, pwin};
-  for (int m = 0; m < 4; m++) {
-    run(m, wins[m], T);
+  // round 6: the same 1 MiB preads into a window of transparent huge pages (anonymous mmap +
+  // MADV_HUGEPAGE, touched, then hipHostRegister'ed: DMA-able like the pinned staging) — does
+  // the destination's page size bound the kernel's copy?
+  const size_t tw = (128u << 20) + (8u << 20);
+  char* thp = (char*)mmap(nullptr, tw, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (thp == MAP_FAILED) return 1;
+  (void)madvise(thp, tw, MADV_HUGEPAGE);
+  memset(thp, 0, tw);
+  const bool thp_reg = hipHostRegister(thp, tw, hipHostRegisterDefault) == hipSuccess;
+  long anon_huge_kb = -1;
+  if (FILE* f = fopen("/proc/self/smaps_rollup", "r")) {
+    char line[256];
+    while (fgets(line, sizeof line, f))
+      if (!strncmp(line, "AnonHugePages:", 14)) anon_huge_kb = atol(line + 14);
+    fclose(f);
+  }
+  printf("{\"thp_window\": true, \"registered\": %s, \"anon_huge_kb\": %ld}\n", thp_reg ? "true" : "false", anon_huge_kb);
+  const char* names[] = {"scratch", "malloc", "pinned", "pinned1m", "malloc1m", "thp1m"};
+  char* wins[] = {nullptr, mwin, pwin, pwin, mwin, thp};
+  const int modes[] = {0, 1, 2, 3, 3, 3};
+  for (int m = 0; m < 6; m++) {
+    run(modes[m], wins[m], T);
     double best = 1e9;
-    for (int r = 0; r < 3; r++) best = std::min(best, run(m, wins[m], T));
+    for (int r = 0; r < 3; r++) best = std::min(best, run(modes[m], wins[m], T));
     printf("{\"form\": \"%s\", \"threads\": %d, \"gb_per_s\": %.2f}\n", names[m], T, total / best / 1e9);
     fflush(stdout);
   }
