@@ -3,8 +3,12 @@
 // part of the public ABI.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <pthread.h>
+#include <sched.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -27,6 +31,16 @@ struct DevBuf {
 // returns when all are done; fn pulls work items itself (atomic cursor).
 class HostPool {
  public:
+  // Round 6: the pool's threads may be confined to a CPU set — the CPUs of the GPU's NUMA
+  // node (sd_cas_ctx_create), so the gather's page-cache copies and the pinned staging stay
+  // on the socket whose PCIe root the DMA reads from.  Empty = the process's own mask.
+  void set_cpus(const cpu_set_t& cpus, int ncpus) {
+    std::lock_guard<std::mutex> g(mu_);
+    cpus_ = cpus;
+    ncpus_ = ncpus;
+    for (auto& t : th_) (void)pthread_setaffinity_np(t.native_handle(), sizeof cpus_, &cpus_);
+  }
+  int bound_cpus() const { return ncpus_; }
   ~HostPool() {
     {
       std::lock_guard<std::mutex> g(mu_);
@@ -42,7 +56,10 @@ class HostPool {
   // `workers` pool threads run fn while the caller runs caller_fn; returns when all are done
   void run2(unsigned workers, const std::function<void()>& fn, const std::function<void()>& caller_fn) {
     std::unique_lock<std::mutex> lk(mu_);
-    while (th_.size() < workers) th_.emplace_back([this] { loop(); });
+    while (th_.size() < workers) {
+      th_.emplace_back([this] { loop(); });
+      if (ncpus_) (void)pthread_setaffinity_np(th_.back().native_handle(), sizeof cpus_, &cpus_);
+    }
     fn_ = &fn;
     want_ = workers;
     pending_ = workers;
@@ -78,6 +95,8 @@ class HostPool {
   unsigned want_ = 0, pending_ = 0;
   uint64_t gen_ = 0;
   bool stop_ = false;
+  cpu_set_t cpus_{};
+  int ncpus_ = 0;
 };
 
 struct sd_cas_ctx {
@@ -143,6 +162,7 @@ struct sd_cas_ctx {
   // 100-file job step ~10 us)
   hipEvent_t gather_done[2] = {nullptr, nullptr};
   bool trace = false;  // SD_CAS_TRACE=1: per-phase host timestamps of host-buffer calls on stderr
+  int numa_node = -1;  // the GPU's NUMA node (sysfs), -1 unknown; pool bound to it unless SD_CAS_POOL_NUMA=0
   uint32_t test_table_fill = 0;  // SD_CAS_TEST_TABLE_FILL (tests): region tables' overflow bound
   std::string err;
 };
@@ -179,6 +199,15 @@ struct SdTrace {
             std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
   }
 };
+
+// the NUMA node holding the page at p (get_mempolicy MPOL_F_NODE | MPOL_F_ADDR), -1 unknown
+// (trace output only)
+inline int sd_page_node(const void* p) {
+  int node = -1;
+  if (!p || syscall(SYS_get_mempolicy, &node, nullptr, 0UL, p, 3UL /* MPOL_F_NODE|MPOL_F_ADDR */) != 0)
+    return -1;
+  return node;
+}
 
 inline int sd_fail(sd_cas_ctx* c, int code, const char* fmt, ...) {
   if (c) {

@@ -11,6 +11,7 @@
 //     for the path variant), copied with hipMemcpyAsync on the side stream, and hashed
 //     on the compute stream after an event hand-off;
 //   - no CPU hashing anywhere: every digest comes from the HIP kernels.
+#include <ctype.h>
 #include <errno.h>
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
@@ -67,6 +68,50 @@ int sd_cas_abi_version(void) { return SD_CAS_ABI_VERSION; }
 
 // why the calling thread's last sd_cas_ctx_create failed: sd_cas_last_error(NULL)
 static thread_local std::string g_ctx_create_err;
+
+// The gather pool's CPUs: the GPU's NUMA node (its PCI device's sysfs numa_node and the node's
+// cpulist), intersected with the CPUs this process may use.  On a two-socket host a reader on
+// the far socket copies page-cache bytes across the socket link into staging that the DMA then
+// reads back across it again; round 6 measured the file path bimodal between processes (~52 vs
+// ~40 GB/s, profiles/r06/validator/) before binding.  SD_CAS_POOL_NUMA=0 leaves the pool
+// unbound (A/B); nothing is bound when the node or its CPUs cannot be read.
+static void bind_pool_to_gpu_node(sd_cas_ctx* c) {
+  const char* e = getenv("SD_CAS_POOL_NUMA");
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof bus, c->device) != hipSuccess) return;
+  for (char* q = bus; *q; ++q) *q = (char)tolower(*q);
+  char path[160];
+  snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
+  FILE* f = fopen(path, "r");
+  int node = -1;
+  if (f) {
+    if (fscanf(f, "%d", &node) != 1) node = -1;
+    fclose(f);
+  }
+  c->numa_node = node;
+  if (node < 0 || (e && strcmp(e, "0") == 0)) return;
+  snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+  f = fopen(path, "r");
+  if (!f) return;
+  char list[4096] = {0};
+  const bool got = fgets(list, sizeof list, f) != nullptr;
+  fclose(f);
+  if (!got) return;
+  cpu_set_t allowed, cpus;
+  CPU_ZERO(&cpus);
+  if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return;
+  int n = 0;
+  for (char* q = list; *q && *q != '\n';) {  // "0-63,128-191"
+    char* end;
+    long a = strtol(q, &end, 10), b = a;
+    if (end == q) break;
+    if (*end == '-') b = strtol(end + 1, &end, 10);
+    for (long cpu = a; cpu <= b && cpu < CPU_SETSIZE; ++cpu)
+      if (CPU_ISSET(cpu, &allowed)) { CPU_SET(cpu, &cpus); ++n; }
+    q = *end == ',' ? end + 1 : end;
+  }
+  if (n >= 2) c->pool.set_cpus(cpus, n);
+}
 
 int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
   if (!out) return SD_CAS_EINVAL;
@@ -131,6 +176,10 @@ int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
               "region tables overflow at %u distinct keys (exact, much slower)\n",
               c->test_table_fill, c->test_table_fill);
   }
+  bind_pool_to_gpu_node(c);
+  if (c->trace)
+    fprintf(stderr, "sd_cas_trace ctx device=%d numa_node=%d pool_cpus=%d\n", device, c->numa_node,
+            c->pool.bound_cpus());
   sd_cas_set_latency_threshold(c, SD_CAS_THRESHOLD_DEFAULT, SD_CAS_THRESHOLD_DEFAULT);
   sd_cas_set_chunkpar_split(c, SD_CAS_THRESHOLD_DEFAULT, SD_CAS_THRESHOLD_DEFAULT);
   *out = c;

@@ -9,6 +9,8 @@
 #   mmapprobe  tools/probe_mmap_reg (needs it built): tmpfs files mapped + hipHostRegister'ed, DMA'd
 #              straight to HBM, vs the pread copy
 #   probe      tools/probe_pread (needs it built) twice: the file path's reads by destination form
+#   numa       the gather pool bound to the GPU's NUMA node (default) vs unbound (SD_CAS_POOL_NUMA=0):
+#              the validator file path (3 rounds) and config 1 (2 rounds)
 #   config1    BASELINE config 1 with 7 timed drop-in passes, twice, then one traced pass
 #   reh2 reh4  the one-GPU rehearsals of the N = 2 / N = 4 bench lines
 #   sorttests  the sort / grouping / link GPU tests
@@ -56,6 +58,19 @@ for step in "$@"; do
         timeout -k 10 300 tools/probe_pread 15 $R/spacedrive_amd/libsd_hip_cas.so > $OUT/probe_pread_$k.log 2>&1 || { echo PROBE_FAIL; tail -20 $OUT/probe_pread_$k.log; exit 1; }
       done
       cat $OUT/probe_pread_*.log ;;
+    numa)
+      for k in 1 2 3; do
+        for m in 1 0; do
+          SD_CAS_POOL_NUMA=$m timeout -k 10 300 python3 -u tools/prof_checksums.py --no-device --paths 2000 --path-runs 6 > $OUT/valnuma${m}_$k.log 2>&1 || { echo NUMA_FAIL; tail -20 $OUT/valnuma${m}_$k.log; exit 1; }
+        done
+      done
+      for k in 1 2; do
+        for m in 1 0; do
+          SD_CAS_POOL_NUMA=$m SD_CONFIG1_PASSES=7 timeout -k 10 300 python3 -u tools/bench_configs.py --config 1 > $OUT/config1numa${m}_$k.log 2>&1 || { echo NUMA_FAIL; tail -20 $OUT/config1numa${m}_$k.log; exit 1; }
+        done
+      done
+      SD_CAS_TRACE=1 timeout -k 10 120 python3 -u -c "from spacedrive_amd import CasEngine; CasEngine(0)" > $OUT/numa_ctx.log 2>&1 || { echo NUMA_FAIL; exit 1; }
+      cat $OUT/numa_ctx.log ;;
     config1)
       for k in 1 2; do
         SD_CONFIG1_PASSES=7 timeout -k 10 300 python3 -u tools/bench_configs.py --config 1 > $OUT/config1_$k.log 2>&1 || { echo CONFIG1_FAIL; tail -20 $OUT/config1_$k.log; exit 1; }
