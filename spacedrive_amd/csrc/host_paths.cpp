@@ -339,6 +339,9 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
 #ifndef SD_PATHS_ZERO_COPY
 #define SD_PATHS_ZERO_COPY 0
 #endif
+#ifndef SD_PATHS_CALLER_READS
+#define SD_PATHS_CALLER_READS 0
+#endif
 #ifndef SD_PATHS_STREAM_CHUNK_KB
 #define SD_PATHS_STREAM_CHUNK_KB 512
 #endif
@@ -456,7 +459,12 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
       }
     };
     if (!streamed) {
-      c->pool.run(std::max(1u, std::min(16u, (unsigned)((m + 7) / 8))), worker);
+      const unsigned k = std::max(1u, std::min(16u, (unsigned)((m + 7) / 8)));
+      // (round 6) the readers are all pool threads — bound to the GPU's NUMA node, see
+      // sd_cas_ctx_create — and the calling thread only waits; SD_PATHS_CALLER_READS 1: the
+      // calling thread reads too (round 5)
+      if (SD_PATHS_CALLER_READS || k == 1) c->pool.run(k, worker);
+      else c->pool.run2(k, worker, []() {});
       return SD_CAS_OK;
     }
     // streamed: this thread pumps the copies, up to 15 pool threads read (~7 files each for

@@ -11,6 +11,7 @@
 #   probe      tools/probe_pread (needs it built) twice: the file path's reads by destination form
 #   numa       the gather pool bound to the GPU's NUMA node (default) vs unbound (SD_CAS_POOL_NUMA=0):
 #              the validator file path (3 rounds) and config 1 (2 rounds)
+#   c1ab       config 1 on the in-tree build vs $C1_VARIANTS (tools/ablib/<name>.so), 3 rounds
 #   config1    BASELINE config 1 with 7 timed drop-in passes, twice, then one traced pass
 #   reh2 reh4  the one-GPU rehearsals of the N = 2 / N = 4 bench lines
 #   sorttests  the sort / grouping / link GPU tests
@@ -71,6 +72,13 @@ for step in "$@"; do
       done
       SD_CAS_TRACE=1 timeout -k 10 120 python3 -u -c "from spacedrive_amd import CasEngine; CasEngine(0)" > $OUT/numa_ctx.log 2>&1 || { echo NUMA_FAIL; exit 1; }
       cat $OUT/numa_ctx.log ;;
+    c1ab)
+      for k in 1 2 3; do
+        for v in intree ${C1_VARIANTS:-paths_caller}; do
+          lib=""; [ $v != intree ] && lib=$R/tools/ablib/$v.so
+          SD_HIP_CAS_LIB=$lib SD_CONFIG1_PASSES=7 timeout -k 10 300 python3 -u tools/bench_configs.py --config 1 > $OUT/c1_${v}_$k.log 2>&1 || { echo C1AB_FAIL; tail -20 $OUT/c1_${v}_$k.log; exit 1; }
+        done
+      done ;;
     config1)
       for k in 1 2; do
         SD_CONFIG1_PASSES=7 timeout -k 10 300 python3 -u tools/bench_configs.py --config 1 > $OUT/config1_$k.log 2>&1 || { echo CONFIG1_FAIL; tail -20 $OUT/config1_$k.log; exit 1; }
