@@ -110,7 +110,9 @@ static void bind_pool_to_gpu_node(sd_cas_ctx* c) {
       if (CPU_ISSET(cpu, &allowed)) { CPU_SET(cpu, &cpus); ++n; }
     q = *end == ',' ? end + 1 : end;
   }
-  if (n >= 2) c->pool.set_cpus(cpus, n);
+  // bind only where the node offers the pool's 16 threads a CPU each (a process confined to a
+  // few of the node's CPUs keeps its own placement)
+  if (n >= 16) c->pool.set_cpus(cpus, n);
 }
 
 int sd_cas_ctx_create(int device, sd_cas_ctx** out) {

@@ -1442,6 +1442,33 @@ def test_file_checksums_pieces_and_slot_rotation(eng, oracle):
         os.rmdir(root)
 
 
+def test_host_pool_numa_modes_agree(eng, oracle, monkeypatch, tmp_path):
+    """Round 6: the host gather pool is bound to the GPU's NUMA node unless SD_CAS_POOL_NUMA=0
+    (read at context creation).  A context of each mode gives the same validator digests and
+    cas_ids for the same files (the sampled and whole-file gather, the piece queue), equal
+    to the oracle."""
+    from spacedrive_amd import CasEngine
+    rng = np.random.default_rng(17)
+    sizes = [0, 5, 1 << 20, (1 << 20) + 1, 3 << 20] + [int(x) for x in rng.integers(1, 400_000, 60)]
+    paths = []
+    for i, L in enumerate(sizes):
+        p = tmp_path / f"n{i}"
+        p.write_bytes(rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+        paths.append(str(p))
+    want_sums = [oracle.file_checksum(p) for p in paths]
+    got = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("SD_CAS_POOL_NUMA", mode)
+        e = CasEngine(0)
+        sums, errs = e.file_checksums(paths)
+        assert not errs.any() and sums == want_sums, mode
+        keys, kerr = e.generate_cas_keys_from_paths(paths[1:], np.array(sizes[1:], dtype=np.int64))
+        assert not kerr.any(), mode
+        got[mode] = keys
+    assert (got["1"] == got["0"]).all()
+    assert [f"{k:016x}" for k in got["1"]] == [oracle.generate_cas_id(p, s) for p, s in zip(paths[1:], sizes[1:])]
+
+
 def test_synth_matches_oracle_generator(eng, oracle):
     n, seed = 64, 12345
     content = torch.empty((n, SAMPLED_CONTENT_LEN), dtype=torch.uint8, device="cuda")
