@@ -79,7 +79,7 @@ static void bind_pool_to_gpu_node(sd_cas_ctx* c) {
   const char* e = getenv("SD_CAS_POOL_NUMA");
   char bus[64] = {0};
   if (hipDeviceGetPCIBusId(bus, sizeof bus, c->device) != hipSuccess) return;
-  for (char* q = bus; *q; ++q) *q = (char)tolower(*q);
+  for (char* q = bus; *q; ++q) *q = (char)tolower((unsigned char)*q);
   char path[160];
   snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
   FILE* f = fopen(path, "r");
