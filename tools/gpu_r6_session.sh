@@ -23,6 +23,7 @@
 #              emission vs the replay, the path gather + validator file path vs the C oracle
 #   powerab    K1 on random content, product layout vs the 64-file LINE / QUAD tiled layouts,
 #              10 s sustained each, 3 rounds (the HBM-energy lever)
+#   sortstall  SQ stall / instruction counters of the LSD grouping's kernels (two rocprofv3 --pmc passes)
 #   suite      the whole GPU suite (release)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
@@ -120,6 +121,13 @@ for step in "$@"; do
       tail -1 $OUT/stress_links.log | cut -c1-300
       timeout -k 10 240 python3 -u tools/stress_paths.py --checksums --seconds 90 > $OUT/stress_paths.log 2>&1 || { echo STRESS_FAIL; tail -5 $OUT/stress_paths.log; exit 1; }
       tail -1 $OUT/stress_paths.log | cut -c1-300 ;;
+    sortstall)
+      i=0
+      for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT" "SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE GRBM_COUNT"; do
+        i=$((i+1))
+        (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $grp -d $OUT/sortstall/p$i -o run --output-format csv -- python3 $R/tools/bench_group.py --only lsd 12500000 > $OUT/sortstall_p$i.log 2>&1) || { echo "SORTSTALL_FAIL $i"; tail -5 $OUT/sortstall_p$i.log; exit 1; }
+      done
+      python3 tools/pmc_summarize.py $OUT/sortstall > $OUT/sortstall.json && echo SORTSTALL_OK ;;
     suite)
       timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -30 $OUT/pytest_gpu.log; exit 1; }
       tail -1 $OUT/pytest_gpu.log ;;
