@@ -24,6 +24,7 @@
 #   powerab    K1 on random content, product layout vs the 64-file LINE / QUAD tiled layouts,
 #              10 s sustained each, 3 rounds (the HBM-energy lever)
 #   sortstall  SQ stall / instruction counters of the LSD grouping's kernels (two rocprofv3 --pmc passes)
+#   stresslong longer randomised stress on the final code (~15 min)
 #   suite      the whole GPU suite (release)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
@@ -128,6 +129,12 @@ for step in "$@"; do
         (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $grp -d $OUT/sortstall/p$i -o run --output-format csv -- python3 $R/tools/bench_group.py --only lsd 12500000 > $OUT/sortstall_p$i.log 2>&1) || { echo "SORTSTALL_FAIL $i"; tail -5 $OUT/sortstall_p$i.log; exit 1; }
       done
       python3 tools/pmc_summarize.py $OUT/sortstall > $OUT/sortstall.json && echo SORTSTALL_OK ;;
+    stresslong)
+      timeout -k 10 420 python3 -u tools/stress_parity.py --seconds 300 --lsd-every 2 --validator > $OUT/stress_parity_long.log 2>&1 || { echo STRESS_FAIL; tail -5 $OUT/stress_parity_long.log; exit 1; }
+      timeout -k 10 300 python3 -u tools/stress_parity.py --seconds 200 --fused --seed 77 > $OUT/stress_fused_long.log 2>&1 || { echo STRESS_FAIL; tail -5 $OUT/stress_fused_long.log; exit 1; }
+      timeout -k 10 300 python3 -u tools/stress_links.py --seconds 180 --seed 11 > $OUT/stress_links_long.log 2>&1 || { echo STRESS_FAIL; tail -5 $OUT/stress_links_long.log; exit 1; }
+      timeout -k 10 300 python3 -u tools/stress_paths.py --checksums --seconds 180 --seed 2031 > $OUT/stress_paths_long.log 2>&1 || { echo STRESS_FAIL; tail -5 $OUT/stress_paths_long.log; exit 1; }
+      for f in stress_parity_long stress_fused_long stress_links_long stress_paths_long; do tail -1 $OUT/$f.log | cut -c1-200; done ;;
     suite)
       timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -30 $OUT/pytest_gpu.log; exit 1; }
       tail -1 $OUT/pytest_gpu.log ;;
