@@ -62,7 +62,10 @@ def main():
     ap.add_argument("--variants", default=",".join(DEFAULT))
     a = ap.parse_args()
     idle = [smi_sample()[0] for _ in range(5)]
-    idle_w = sorted(x for x in idle if x is not None)[len(idle) // 2]
+    seen = sorted(x for x in idle if x is not None)
+    if not seen:
+        raise SystemExit("rocm-smi gave no power reading")
+    idle_w = seen[len(seen) // 2]
     print(json.dumps({"idle_power_w": idle_w, "idle_samples": idle}), flush=True)
     res = {}
     for r in range(a.rounds):
