@@ -25,6 +25,7 @@
 #              10 s sustained each, 3 rounds (the HBM-energy lever)
 #   sortstall  SQ stall / instruction counters of the LSD grouping's kernels (two rocprofv3 --pmc passes)
 #   stresslong longer randomised stress on the final code (~15 min)
+#   repeat     the default `python bench.py` and the validator file path twice, on another box
 #   suite      the whole GPU suite (release)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
@@ -135,6 +136,12 @@ for step in "$@"; do
       timeout -k 10 300 python3 -u tools/stress_links.py --seconds 180 --seed 11 > $OUT/stress_links_long.log 2>&1 || { echo STRESS_FAIL; tail -5 $OUT/stress_links_long.log; exit 1; }
       timeout -k 10 300 python3 -u tools/stress_paths.py --checksums --seconds 180 --seed 2031 > $OUT/stress_paths_long.log 2>&1 || { echo STRESS_FAIL; tail -5 $OUT/stress_paths_long.log; exit 1; }
       for f in stress_parity_long stress_fused_long stress_links_long stress_paths_long; do tail -1 $OUT/$f.log | cut -c1-200; done ;;
+    repeat)
+      timeout -k 10 400 python3 -u bench.py > $OUT/bench_default.log 2>&1 || { echo BENCH_FAIL; tail -20 $OUT/bench_default.log; exit 1; }
+      tail -1 $OUT/bench_default.log | cut -c1-200
+      for k in 1 2; do
+        timeout -k 10 300 python3 -u tools/prof_checksums.py --no-device --paths 2000 --path-runs 6 > $OUT/validator_paths_$k.log 2>&1 || { echo VAL_FAIL; tail -20 $OUT/validator_paths_$k.log; exit 1; }
+      done ;;
     suite)
       timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -30 $OUT/pytest_gpu.log; exit 1; }
       tail -1 $OUT/pytest_gpu.log ;;
