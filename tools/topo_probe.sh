@@ -1,3 +1,7 @@
+#!/bin/bash
+# The GPU box's CPU / NUMA topology, the visible GPU's NUMA node and PCI bus, and this
+# process's CPU / memory masks (round 6: why the host gather pool is bound to the GPU's node;
+# profiles/r06/validator/box_topology.txt).  Usage (on the box): bash tools/topo_probe.sh
 set -o pipefail
 mkdir -p gpurun_out/topo
 {
