@@ -26,6 +26,8 @@
 #   sortstall  SQ stall / instruction counters of the LSD grouping's kernels (two rocprofv3 --pmc passes)
 #   stresslong longer randomised stress on the final code (~15 min)
 #   repeat     the default `python bench.py` and the validator file path twice, on another box
+#   valshapes  the validator file path on 20,000 small files, 150 files of 16-60 MiB, and 40 files
+#              of 128-192 MiB (streamed one by one)
 #   suite      the whole GPU suite (release)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
@@ -142,6 +144,11 @@ for step in "$@"; do
       for k in 1 2; do
         timeout -k 10 300 python3 -u tools/prof_checksums.py --no-device --paths 2000 --path-runs 6 > $OUT/validator_paths_$k.log 2>&1 || { echo VAL_FAIL; tail -20 $OUT/validator_paths_$k.log; exit 1; }
       done ;;
+    valshapes)
+      timeout -k 10 400 python3 -u tools/prof_checksums.py --no-device --paths 20000 --path-kib 16 256 --path-runs 4 > $OUT/validator_small_files.log 2>&1 || { echo VALSHAPES_FAIL; tail -20 $OUT/validator_small_files.log; exit 1; }
+      timeout -k 10 400 python3 -u tools/prof_checksums.py --no-device --paths 150 --path-kib 16384 61440 --path-runs 4 > $OUT/validator_large_files.log 2>&1 || { echo VALSHAPES_FAIL; tail -20 $OUT/validator_large_files.log; exit 1; }
+      timeout -k 10 400 python3 -u tools/prof_checksums.py --no-device --paths 40 --path-kib 131072 196608 --path-runs 3 > $OUT/validator_streamed_files.log 2>&1 || { echo VALSHAPES_FAIL; tail -20 $OUT/validator_streamed_files.log; exit 1; }
+      grep -h '"files"' $OUT/validator_*_files.log | cut -c1-300 ;;
     suite)
       timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -30 $OUT/pytest_gpu.log; exit 1; }
       tail -1 $OUT/pytest_gpu.log ;;

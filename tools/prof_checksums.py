@@ -10,7 +10,7 @@ engine's stream; every digest of a sample checked against the oracle.  Library s
   small16k .. small256k  16,384 .. 262,144 buffers of U(0, 16) KiB (batch-size sweep)
   docs64  262,144 buffers of U(1, 64) KiB
   skew64k / skew1m  mostly U(0, 4) KiB with 8 % U(96, 128) KiB / 3 % U(64, 128) KiB
-Paths (--paths N): N files of U(0.25, 4) MiB on /dev/shm through sd_cas_file_checksums vs
+Paths (--paths N): N files of U(0.25, 4) MiB (--path-kib LO HI) on /dev/shm through sd_cas_file_checksums vs
 the oracle's file_checksum on 1 thread (hash.rs is single-threaded) and file-parallel on
 the host cores.
 """
@@ -100,11 +100,11 @@ def device_batch(eng, orc, name, iters):
             "parity_sample": len(idx), "parity": bool(ok), "k3_same_bytes": k3}
 
 
-def paths_run(eng, orc, n, root, nruns=3):
+def paths_run(eng, orc, n, root, nruns=3, lo_kb=256, hi_kb=4096):
     import numpy as np
     rng = np.random.default_rng(6)
     os.makedirs(root, exist_ok=True)
-    sizes = rng.integers(1 << 18, 4 << 20, n)
+    sizes = rng.integers(lo_kb << 10, hi_kb << 10, n)
     paths = []
     for i, L in enumerate(sizes):
         p = os.path.join(root, f"v{i}")
@@ -149,7 +149,7 @@ def paths_run(eng, orc, n, root, nruns=3):
         pass
     for p in paths:
         os.unlink(p)
-    return {"files": n, "bytes": total, "gpu_s": gpu_s, "gpu_s_runs": runs, "gpu_gb_per_s": total / gpu_s / 1e9,
+    return {"files": n, "size_kib": [lo_kb, hi_kb], "bytes": total, "gpu_s": gpu_s, "gpu_s_runs": runs, "gpu_gb_per_s": total / gpu_s / 1e9,
             "gpu_files_per_s": n / gpu_s,
             "cold_first_pass_gb_per_s": total / runs[0] / 1e9,
             "warm_median_gb_per_s": total / warm[len(warm) // 2] / 1e9, "cpu_1thread_gb_per_s": total / cpu1_s / 1e9,
@@ -164,6 +164,8 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--paths", type=int, default=0)
     ap.add_argument("--path-runs", type=int, default=3)
+    ap.add_argument("--path-kib", type=int, nargs=2, default=[256, 4096], metavar=("LO", "HI"),
+                    help="file sizes U(LO, HI) KiB (default: the 2,000-file set's U(0.25, 4) MiB)")
     ap.add_argument("--no-device", action="store_true", help="paths only")
     ap.add_argument("--root", default="/dev/shm/sdcas_validator")
     a = ap.parse_args()
@@ -173,7 +175,7 @@ def main():
     for name in [] if a.no_device else a.shape or ["photos", "docs", "small", "one"]:
         print(json.dumps(device_batch(eng, orc, name, a.iters)), flush=True)
     if a.paths:
-        print(json.dumps(paths_run(eng, orc, a.paths, a.root, a.path_runs)), flush=True)
+        print(json.dumps(paths_run(eng, orc, a.paths, a.root, a.path_runs, a.path_kib[0], a.path_kib[1])), flush=True)
 
 
 if __name__ == "__main__":
