@@ -37,6 +37,24 @@ using namespace sdcas;
 #define ensure sd_ensure
 #define ensure_pinned sd_ensure_pinned
 
+// A/B knobs of the file paths below (tools/build_variant.sh + tools/patch_define.py)
+#ifndef SD_CK_PIECE_KB
+#define SD_CK_PIECE_KB 1024
+#endif
+#ifndef SD_CK_COPY_MB
+#define SD_CK_COPY_MB 8
+#endif
+#ifndef SD_CK_PUMP_READS  // the pump thread also reads pieces when it has nothing to issue
+#define SD_CK_PUMP_READS 1
+#endif
+#ifndef SD_CK_PUMP_ON_POOL  // the pump on a pool thread (1) or on the calling thread (0)
+#define SD_CK_PUMP_ON_POOL 1
+#endif
+#ifndef SD_CK_COPY_STREAMS  // copies alternate over this many streams (1 or 2)
+#define SD_CK_COPY_STREAMS 2
+#endif
+
+
 extern "C" {
 
 // ---- file_checksum --------------------------------------------------------------------
@@ -75,14 +93,17 @@ int sd_cas_checksum_dev(sd_cas_ctx* c, const void* d_data, uint64_t len, uint8_t
 // read on anything that returns short reads before its end (procfs seq_files give about one
 // page per read, FIFOs and FUSE/network mounts whatever is ready).
 // Two read modes, one result:
-//   * parallel (regular files): the file streams through two pinned segment buffers of up
-//     to 64 MiB (a segment = one complete 65,536-chunk subtree, hashed on the GPU while the
-//     pool reads the next one with pread pieces) until a segment comes back short; st_size
-//     only sizes the buffers (a file that outgrows its first buffer is re-read with full-size
-//     segments).  A regular file whose reads show it is not read like a local file — a short
-//     pread followed by more data, or an end before st_size — is redone sequentially;
+//   * pieces (regular files; round 6, file_checksum_pieces): the file is planned from st_size
+//     as 64 MiB segments (a segment = one complete 65,536-chunk subtree) rotating over three
+//     pinned + device slots; 1 MiB pieces from one queue are read by the pool (bound to the
+//     GPU's NUMA node) while a pump on a pool thread copies every landed prefix to HBM over
+//     two copy streams and hashes each complete segment (K3) into its subtree CV — the
+//     validator job's piece queue (sd_cas_file_checksums) for one file.  A regular file whose
+//     reads show it is not read like a local file — a short pread before the planned end,
+//     data in the probe byte past st_size (it grew), an end before st_size — is redone
+//     sequentially;
 //   * sequential (everything else, and those redos): hash.rs's loop literally, 1 MiB read()s
-//     from the start, stopping after the first short one, into the same segment pipeline.
+//     from the start, stopping after the first short one, through two pinned segment buffers.
 // The segment CVs are merged on the GPU (pair-and-promote, ROOT on the last parent); a file
 // of one segment is hashed with ROOT inside the segment.
 static int cv_capacity(sd_cas_ctx* c, DevBuf& cvb, size_t need_cvs, hipStream_t s) {
@@ -103,6 +124,290 @@ static int cv_capacity(sd_cas_ctx* c, DevBuf& cvb, size_t need_cvs, hipStream_t 
   return SD_CAS_OK;
 }
 
+// The pieces mode of file_checksum (see above).  Returns SD_CAS_OK with the digest in
+// digest[32], SD_CAS_OK with *go_seq set (redo with hash.rs's sequential reads), or an error
+// (*err_no = the failed read's errno).
+static int file_checksum_pieces(sd_cas_ctx* c, int fd, uint64_t st_size, const char* path,
+                                uint8_t digest[32], int* err_no, bool* go_seq) {
+  constexpr uint64_t SEG = 64ull << 20;  // 65,536 chunks: a complete left subtree
+  constexpr uint64_t PIECE = (uint64_t)SD_CK_PIECE_KB << 10;
+  constexpr uint64_t COPY = (uint64_t)SD_CK_COPY_MB << 20;
+  constexpr int SLOTS = 3;
+  *go_seq = false;
+  const uint64_t total = st_size + 1;  // + the probe byte: data there means the file grew
+  const uint64_t nplan = (total + SEG - 1) / SEG;
+  const uint64_t nreal = std::max<uint64_t>(1, (st_size + SEG - 1) / SEG);  // segments holding data
+  const uint64_t cap = std::min<uint64_t>(SEG, ((total + 4095) / 4096) * 4096);
+  const size_t sb = up256(cap + 16);
+  hipStream_t s = c->stream, cs = c->copy;
+  int rc = SD_CAS_OK;
+  if ((rc = ensure_pinned(c, SLOTS * sb)) || (rc = ensure(c, c->staging, SLOTS * sb))) return rc;
+  if ((rc = ensure(c, c->ws, std::max(checksum_workspace_bytes(cap), checksum_workspace_bytes(1 << 20)))))
+    return rc;
+  const size_t red_ws = 2 * up256((nreal + 255) / 256 * 32) + 512;  // reduce_cvs_device's ping-pong
+  if (nreal > 1 && (rc = ensure(c, c->ws, red_ws))) return rc;
+  if ((rc = cv_capacity(c, c->cvbuf, nreal, s))) return rc;
+  struct Piece { uint32_t seg; uint64_t off, len; };  // off: from the segment's start
+  std::vector<Piece> pieces;
+  std::vector<size_t> spiece{0};
+  for (uint64_t k = 0; k < nplan; k++) {
+    const uint64_t len = std::min(SEG, total - k * SEG);
+    const uint64_t np = std::max<uint64_t>(1, len / PIECE);
+    for (uint64_t j = 0; j < np; j++)
+      pieces.push_back({(uint32_t)k, j * PIECE, j + 1 < np ? PIECE : len - j * PIECE});
+    spiece.push_back(pieces.size());
+  }
+  const size_t np = pieces.size();
+  hipEvent_t done[SLOTS] = {}, landed = nullptr;
+  auto destroy_events = [&]() {
+    for (int b = 0; b < SLOTS; b++)
+      if (done[b]) (void)hipEventDestroy(done[b]);
+    if (landed) (void)hipEventDestroy(landed);
+  };
+  for (int b = 0; b < SLOTS; b++)
+    if (hipEventCreateWithFlags(&done[b], hipEventDisableTiming) != hipSuccess) {
+      destroy_events();
+      return fail(c, SD_CAS_EHIP, "file_checksum: event create");
+    }
+  if (hipEventCreateWithFlags(&landed, hipEventDisableTiming) != hipSuccess) {
+    destroy_events();
+    return fail(c, SD_CAS_EHIP, "file_checksum: event create");
+  }
+  std::unique_ptr<std::atomic<uint8_t>[]> fin(new std::atomic<uint8_t>[np]);
+  std::unique_ptr<std::atomic<uint64_t>[]> sgot(new std::atomic<uint64_t>[nplan]);
+  for (size_t p = 0; p < np; p++) fin[p].store(0, std::memory_order_relaxed);
+  for (uint64_t k = 0; k < nplan; k++) sgot[k].store(0);
+  std::atomic<int> rd_err{0};
+  std::atomic<bool> irregular{false}, abort{false};
+  std::atomic<size_t> next{0}, freed{0};
+  auto slot_free = [&](uint32_t k) { return k < freed.load(std::memory_order_acquire) + SLOTS; };
+  auto read_piece = [&](size_t p) {
+    const Piece& pc = pieces[p];
+    char* dst = (char*)c->pinned + (size_t)(pc.seg % SLOTS) * sb + pc.off;
+    const uint64_t foff = (uint64_t)pc.seg * SEG + pc.off;
+    uint64_t got = 0;
+    bool was_short = false;
+    while (got < pc.len) {
+      ssize_t r = pread(fd, dst + got, pc.len - got, (off_t)(foff + got));
+      if (r < 0 && errno == EINTR) continue;
+      if (r < 0) { rd_err.store(errno); abort.store(true); break; }
+      if (r == 0) break;  // EOF
+      if (was_short) irregular.store(true);  // data after a short read
+      if ((uint64_t)r < pc.len - got) was_short = true;
+      got += (uint64_t)r;
+    }
+    if (got < pc.len && foff + pc.len < total) irregular.store(true);  // ended before the planned end
+    sgot[pc.seg].fetch_add(got);
+  };
+  auto worker = [&]() {
+    for (size_t p; !abort.load(std::memory_order_relaxed) && (p = next.fetch_add(1)) < np;) {
+      while (!slot_free(pieces[p].seg) && !abort.load(std::memory_order_relaxed)) std::this_thread::yield();
+      if (abort.load(std::memory_order_relaxed)) break;
+      read_piece(p);
+      fin[p].store(1, std::memory_order_release);
+    }
+  };
+  // the pump: copies landed prefixes, hashes complete segments, frees slots; reads when idle
+  auto pump = [&]() {
+    size_t kc = 0, issued = 0, retired = 0, ready = 0, ncopies = 0;
+    uint64_t sent = 0;
+    auto hipfail = [&](hipError_t e, const char* what) {
+      rc = fail(c, SD_CAS_EHIP, "file_checksum %s: %s", what, hipGetErrorString(e));
+      abort.store(true);
+    };
+    if (hipError_t e = hipSetDevice(c->device); e != hipSuccess) { hipfail(e, "setup"); return; }
+    if (hipError_t e = sd_ws_acquire(c, s); e != hipSuccess) { hipfail(e, "setup"); return; }
+    while (retired < nplan && rc == SD_CAS_OK && !abort.load()) {
+      if (retired < issued) {
+        const hipError_t q = hipEventQuery(done[retired % SLOTS]);
+        if (q == hipSuccess) {
+          freed.store(++retired, std::memory_order_release);
+          continue;
+        }
+        if (q != hipErrorNotReady) { hipfail(q, "segment sync"); break; }
+      }
+      bool progress = false;
+      if (kc < nplan) {
+        const size_t b = kc % SLOTS;
+        char* pin = (char*)c->pinned + b * sb;
+        char* dev = (char*)c->staging.p + b * sb;
+        while (ready < spiece[kc + 1] && fin[ready].load(std::memory_order_acquire)) ++ready;
+        const bool complete = ready == spiece[kc + 1];
+        const uint64_t want = kc < nreal ? std::min(SEG, st_size - kc * SEG) : 0;  // bytes to hash
+        const uint64_t hi = complete ? want : std::min(want, pieces[ready].off);
+        if (hi > sent && (hi - sent >= COPY || complete)) {
+          hipStream_t xs = (SD_CK_COPY_STREAMS > 1 && (ncopies & 1)) ? c->copy2 : cs;
+          const uint64_t hi16 = complete ? up16(hi) : hi;  // (K3 reads to the 16-B round-up)
+          const hipError_t e = hipMemcpyAsync(dev + sent, pin + sent, hi16 - sent, hipMemcpyHostToDevice, xs);
+          if (e != hipSuccess) { hipfail(e, "copy"); break; }
+          sent = hi16;
+          ++ncopies;
+          progress = true;
+        }
+        if (complete && sent >= want) {
+          // the segment must hold exactly its planned bytes (the probe byte none)
+          const uint64_t got = sgot[kc].load(), planned = std::min(SEG, total - kc * SEG);
+          if (irregular.load() || got != (kc + 1 == nplan ? planned - 1 : planned)) {
+            *go_seq = true;
+            abort.store(true);
+            break;
+          }
+          hipError_t e = hipSuccess;
+          if (kc < nreal) {
+            if (SD_CK_COPY_STREAMS > 1) {
+              e = hipEventRecord(landed, c->copy2);
+              if (e == hipSuccess) e = hipStreamWaitEvent(s, landed, 0);
+            }
+            if (e == hipSuccess) e = hipEventRecord(landed, cs);
+            if (e == hipSuccess) e = hipStreamWaitEvent(s, landed, 0);
+            if (e == hipSuccess)
+              e = checksum_device((const uint8_t*)dev, want, (kc * SEG) >> 10, nreal == 1,
+                                  (uint32_t*)c->cvbuf.p + 8 * kc, c->ws.p, s);
+          }
+          if (e == hipSuccess) e = hipEventRecord(done[b], s);
+          if (e != hipSuccess) { hipfail(e, "segment"); break; }
+          ++issued;
+          ++kc;
+          sent = 0;
+          continue;
+        }
+      }
+      if (progress) continue;
+      size_t p = next.load(std::memory_order_relaxed);
+      if (SD_CK_PUMP_READS && p < np && slot_free(pieces[p].seg) && next.compare_exchange_strong(p, p + 1)) {
+        read_piece(p);
+        fin[p].store(1, std::memory_order_release);
+      } else {
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#else
+        std::this_thread::yield();
+#endif
+      }
+    }
+  };
+  std::atomic<bool> pump_taken{false};
+  const std::function<void()> pool_fn = [&]() {
+    if (!pump_taken.exchange(true)) pump(); else worker();
+  };
+  c->pool.run2(std::max(2u, std::min(16u, (unsigned)np + 1)), pool_fn, []() {});
+  if (rc == SD_CAS_OK && !*go_seq) {
+    if (int e = rd_err.load()) {
+      if (err_no) *err_no = e;
+      rc = fail(c, SD_CAS_EIO, "read(%s): %s", path, strerror(e));
+    }
+  }
+  if (rc == SD_CAS_OK && !*go_seq) {
+    uint32_t* d_out = (uint32_t*)c->d_scalar;
+    hipError_t e = nreal == 1 ? hipMemcpyAsync(d_out, c->cvbuf.p, 32, hipMemcpyDeviceToDevice, s)
+                              : reduce_cvs_device((uint32_t*)c->cvbuf.p, nreal, d_out, c->ws.p, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(digest, d_out, 32, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) rc = fail(c, SD_CAS_EHIP, "checksum reduce: %s", hipGetErrorString(e));
+  }
+  (void)sd_ws_release(c, s);
+  // nothing in flight may still read the pinned slots or write the CVs
+  (void)hipStreamSynchronize(cs);
+  (void)hipStreamSynchronize(c->copy2);
+  (void)hipStreamSynchronize(s);
+  destroy_events();
+  return rc;
+}
+
+// The sequential mode of file_checksum: hash.rs:15-21 literally — 1 MiB read()s in order,
+// stop after the first short one — through two pinned 64 MiB segment buffers (segment k is
+// hashed on the GPU while the next one is read).
+static int file_checksum_seq(sd_cas_ctx* c, int fd, const char* path, uint8_t digest[32], int* err_no) {
+  constexpr uint64_t SEG = 64ull << 20;
+  constexpr uint64_t BLOCK_LEN = 1ull << 20;  // hash.rs:9
+  static_assert(SEG % BLOCK_LEN == 0, "a segment holds whole hash.rs reads");
+  hipStream_t s = c->stream;
+  const size_t sb = up256(SEG + 16);
+  int rc = SD_CAS_OK;
+  if ((rc = ensure_pinned(c, 2 * sb)) || (rc = ensure(c, c->staging, 2 * sb))) return rc;
+  if ((rc = ensure(c, c->ws, checksum_workspace_bytes(SEG)))) return rc;
+  hipEvent_t done[2] = {nullptr, nullptr};
+  for (int i = 0; i < 2; i++)
+    if (hipEventCreateWithFlags(&done[i], hipEventDisableTiming) != hipSuccess) {
+      for (int k = 0; k < i; k++) (void)hipEventDestroy(done[k]);
+      return fail(c, SD_CAS_EHIP, "file_checksum: event create");
+    }
+  char* pin[2] = {(char*)c->pinned, (char*)c->pinned + sb};
+  char* dev[2] = {(char*)c->staging.p, (char*)c->staging.p + sb};
+  bool stopped = false;  // the first short read has happened
+  auto read_seg = [&](char* dst) -> int64_t {
+    if (stopped) return 0;
+    uint64_t got = 0;
+    while (got < SEG) {
+      ssize_t r = read(fd, dst + got, BLOCK_LEN);
+      if (r < 0 && errno == EINTR) continue;
+      if (r < 0) return -(int64_t)errno;
+      got += (uint64_t)r;
+      if ((uint64_t)r != BLOCK_LEN) { stopped = true; break; }
+    }
+    return (int64_t)got;
+  };
+  // segment k is dispatched once it is known whether it is the only one (k == 0 waits for
+  // segment 1's read); ROOT sits inside it only then
+  auto dispatch = [&](uint64_t sgi, uint64_t len, bool only) -> int {
+    const int b = (int)(sgi & 1);
+    int r2 = cv_capacity(c, c->cvbuf, sgi + 1, s);
+    if (r2) return r2;
+    hipError_t e = hipMemcpyAsync(dev[b], pin[b], up16(len), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+      e = checksum_device((const uint8_t*)dev[b], len, (sgi * SEG) >> 10, only,
+                          (uint32_t*)c->cvbuf.p + 8 * sgi, c->ws.p, s);
+    if (e == hipSuccess) e = hipEventRecord(done[b], s);
+    if (e != hipSuccess) return fail(c, SD_CAS_EHIP, "checksum segment: %s", hipGetErrorString(e));
+    return SD_CAS_OK;
+  };
+  auto io_fail = [&](int64_t neg) {
+    if (err_no) *err_no = (int)-neg;
+    return fail(c, SD_CAS_EIO, "read(%s): %s", path, strerror((int)-neg));
+  };
+  if (hipError_t e = sd_ws_acquire(c, s); e != hipSuccess) {
+    (void)hipEventDestroy(done[0]);
+    (void)hipEventDestroy(done[1]);
+    return fail(c, SD_CAS_EHIP, "file_checksum: %s", hipGetErrorString(e));
+  }
+  uint64_t nseg = 1;
+  const int64_t len0 = read_seg(pin[0]);
+  if (len0 < 0) {
+    rc = io_fail(len0);
+  } else if ((uint64_t)len0 < SEG) {
+    rc = dispatch(0, (uint64_t)len0, true);
+  } else {  // a full first segment: more may follow
+    for (uint64_t sgi = 1;; sgi++) {
+      const int b = (int)(sgi & 1);
+      if (sgi >= 2 && hipEventSynchronize(done[b]) != hipSuccess) { rc = fail(c, SD_CAS_EHIP, "checksum: segment sync"); break; }
+      const int64_t ln = read_seg(pin[b]);
+      if (ln < 0) { rc = io_fail(ln); break; }
+      if (sgi == 1 && (rc = dispatch(0, (uint64_t)len0, ln == 0))) break;  // segment 0: the only one?
+      if (ln == 0) { nseg = sgi; break; }
+      if ((rc = dispatch(sgi, (uint64_t)ln, false))) break;
+      if ((uint64_t)ln < SEG) { nseg = sgi + 1; break; }
+    }
+  }
+  if (rc == SD_CAS_OK) {
+    uint32_t* d_out = (uint32_t*)c->d_scalar;
+    hipError_t e = hipSuccess;
+    // reduce_cvs_device ping-pongs ceil(nseg / 256) CVs per level through ws
+    if (nseg > 1) rc = ensure(c, c->ws, 2 * up256((nseg + 255) / 256 * 32) + 512);
+    if (rc == SD_CAS_OK) {
+      if (nseg == 1) e = hipMemcpyAsync(d_out, c->cvbuf.p, 32, hipMemcpyDeviceToDevice, s);
+      else e = reduce_cvs_device((uint32_t*)c->cvbuf.p, nseg, d_out, c->ws.p, s);
+      if (e == hipSuccess) e = hipMemcpyAsync(digest, d_out, 32, hipMemcpyDeviceToHost, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      if (e != hipSuccess) rc = fail(c, SD_CAS_EHIP, "checksum reduce: %s", hipGetErrorString(e));
+    }
+  }
+  (void)hipStreamSynchronize(s);  // no segment copy may still read the pinned buffers
+  (void)sd_ws_release(c, s);
+  (void)hipEventDestroy(done[0]);
+  (void)hipEventDestroy(done[1]);
+  return rc;
+}
+
 int sd_cas_file_checksum(sd_cas_ctx* c, const char* path, char out_hex[65], int* err_no) {
   if (!c || !path || !out_hex) return SD_CAS_EINVAL;
   if (err_no) *err_no = 0;
@@ -118,175 +423,18 @@ int sd_cas_file_checksum(sd_cas_ctx* c, const char* path, char out_hex[65], int*
     close(fd);
     return fail(c, SD_CAS_EIO, "fstat(%s): %s", path, strerror(errno));
   }
-  const uint64_t SEG = 64ull << 20;  // 65,536 chunks: a complete left subtree
-  constexpr uint64_t PIECE = 4ull << 20;  // pool read unit (one reader tops out near 5-10 GB/s)
-  constexpr uint64_t BLOCK_LEN = 1ull << 20;  // hash.rs:9
-  static_assert((64ull << 20) % BLOCK_LEN == 0, "a segment holds whole hash.rs reads");
-  bool seq = !S_ISREG(st.st_mode);
-  // segment capacity: the whole file plus room to see EOF, capped at one subtree (the
-  // sequential mode reads whole 1 MiB blocks: full segments)
-  uint64_t cap = seq ? SEG : std::min<uint64_t>(SEG, (((uint64_t)st.st_size + 1 + 4095) / 4096) * 4096);
-  hipStream_t s = c->stream;
-  int rc = SD_CAS_OK;
-  hipEvent_t done[2] = {nullptr, nullptr};
-  for (int i = 0; i < 2; i++)
-    if (hipEventCreateWithFlags(&done[i], hipEventDisableTiming) != hipSuccess) {
-      close(fd);
-      for (int k = 0; k < i; k++) (void)hipEventDestroy(done[k]);
-      return fail(c, SD_CAS_EHIP, "file_checksum: event create");
-    }
-  bool irregular = false;  // parallel mode saw reads that a local regular file never gives
-  bool seq_stopped = false;  // sequential mode: the first short read has happened
-  // parallel: read segment `sgi` into dst with pread pieces; its length (< cap at EOF) or -errno
-  auto read_seg_par = [&](uint64_t sgi, char* dst) -> int64_t {
-    const uint64_t off = sgi * cap;
-    const uint64_t npieces = (cap + PIECE - 1) / PIECE;
-    std::atomic<uint64_t> next{0}, eof{cap}, data_end{0};
-    std::atomic<int> rd_err{0};
-    std::atomic<bool> short_then_more{false};
-    c->pool.run((unsigned)std::min<uint64_t>(8, npieces), [&]() {
-      for (uint64_t p; (p = next.fetch_add(1)) < npieces && !rd_err.load();) {
-        const uint64_t p0 = p * PIECE, pn = std::min(PIECE, cap - p0);
-        if (p0 >= eof.load()) break;
-        uint64_t got = 0;
-        bool was_short = false;
-        while (got < pn) {
-          ssize_t r = pread(fd, dst + p0 + got, pn - got, (off_t)(off + p0 + got));
-          if (r < 0 && errno == EINTR) continue;
-          if (r < 0) { rd_err.store(errno); break; }
-          if (r == 0) break;
-          if (was_short) short_then_more.store(true);  // data after a short read
-          if ((uint64_t)r < pn - got) was_short = true;
-          got += (uint64_t)r;
-        }
-        if (got) {
-          uint64_t cur = data_end.load();
-          while (p0 + got > cur && !data_end.compare_exchange_weak(cur, p0 + got)) {}
-        }
-        if (got < pn) {  // eof = min(eof, p0 + got)
-          uint64_t cur = eof.load();
-          while (p0 + got < cur && !eof.compare_exchange_weak(cur, p0 + got)) {}
-        }
-      }
-    });
-    if (int e = rd_err.load()) return -(int64_t)e;
-    // bytes past the first end (a short piece whose successor still had data)
-    if (short_then_more.load() || data_end.load() > eof.load()) irregular = true;
-    return (int64_t)eof.load();
-  };
-  // sequential: hash.rs:15-21 — 1 MiB read()s in order, stop after the first short one
-  auto read_seg_seq = [&](char* dst) -> int64_t {
-    if (seq_stopped) return 0;
-    uint64_t got = 0;
-    while (got < cap) {
-      ssize_t r = read(fd, dst + got, BLOCK_LEN);
-      if (r < 0 && errno == EINTR) continue;
-      if (r < 0) return -(int64_t)errno;
-      got += (uint64_t)r;
-      if ((uint64_t)r != BLOCK_LEN) { seq_stopped = true; break; }
-    }
-    return (int64_t)got;
-  };
-  auto read_seg = [&](uint64_t sgi, char* dst) -> int64_t {
-    return seq ? read_seg_seq(dst) : read_seg_par(sgi, dst);
-  };
   uint8_t digest[32];
-  for (int attempt = 0; attempt < 3; attempt++) {
-    const size_t sb = up256(cap + 16);
-    if ((rc = ensure_pinned(c, 2 * sb)) || (rc = ensure(c, c->staging, 2 * sb))) break;
-    if ((rc = ensure(c, c->ws, std::max(checksum_workspace_bytes(cap), checksum_workspace_bytes(1 << 20)))))
-      break;
-    char* pin[2] = {(char*)c->pinned, (char*)c->pinned + sb};
-    char* dev[2] = {(char*)c->staging.p, (char*)c->staging.p + sb};
-    if (hipError_t e = sd_ws_acquire(c, s); e != hipSuccess) {
-      rc = fail(c, SD_CAS_EHIP, "file_checksum: %s", hipGetErrorString(e));
-      break;
+  int rc = SD_CAS_OK;
+  bool seq = !S_ISREG(st.st_mode);
+  if (!seq) {  // a regular file: the pieces mode, redone sequentially if it reads irregularly
+    rc = file_checksum_pieces(c, fd, (uint64_t)st.st_size, path, digest, err_no, &seq);
+    if (rc == SD_CAS_OK && seq && lseek(fd, 0, SEEK_SET) != 0) {
+      if (err_no) *err_no = errno;
+      rc = fail(c, SD_CAS_EIO, "lseek(%s): %s", path, strerror(errno));
     }
-    // segment k is dispatched once it is known whether it is the only one (k == 0 waits for
-    // segment 1's read); ROOT sits inside it only then
-    auto dispatch = [&](uint64_t sgi, uint64_t len, bool only) -> int {
-      const int b = (int)(sgi & 1);
-      int r2 = cv_capacity(c, c->cvbuf, sgi + 1, s);
-      if (r2) return r2;
-      hipError_t e = hipMemcpyAsync(dev[b], pin[b], up16(len), hipMemcpyHostToDevice, s);
-      if (e == hipSuccess)
-        e = checksum_device((const uint8_t*)dev[b], len, (sgi * cap) >> 10, only,
-                            (uint32_t*)c->cvbuf.p + 8 * sgi, c->ws.p, s);
-      if (e == hipSuccess) e = hipEventRecord(done[b], s);
-      if (e != hipSuccess) return fail(c, SD_CAS_EHIP, "checksum segment: %s", hipGetErrorString(e));
-      return SD_CAS_OK;
-    };
-    auto io_fail = [&](int64_t neg) {
-      if (err_no) *err_no = (int)-neg;
-      return fail(c, SD_CAS_EIO, "read(%s): %s", path, strerror((int)-neg));
-    };
-    enum { DONE, GROW, GO_SEQ } next = DONE;
-    uint64_t nseg = 1, total = 0;
-    int64_t len0 = read_seg(0, pin[0]);
-    if (len0 < 0) {
-      rc = io_fail(len0);
-    } else if (irregular) {
-      next = GO_SEQ;
-    } else if ((uint64_t)len0 == cap && cap < SEG) {
-      next = GROW;  // grew past the buffer
-    } else if ((uint64_t)len0 < cap) {
-      total = (uint64_t)len0;
-      rc = dispatch(0, (uint64_t)len0, true);
-    } else {  // a full first segment: more may follow
-      total = (uint64_t)len0;
-      for (uint64_t sgi = 1;; sgi++) {
-        const int b = (int)(sgi & 1);
-        if (sgi >= 2 && hipEventSynchronize(done[b]) != hipSuccess) { rc = fail(c, SD_CAS_EHIP, "checksum: segment sync"); break; }
-        const int64_t ln = read_seg(sgi, pin[b]);
-        if (ln < 0) { rc = io_fail(ln); break; }
-        if (irregular) { next = GO_SEQ; break; }
-        total += (uint64_t)ln;
-        if (sgi == 1) {  // segment 0 is the only one iff nothing follows it
-          if ((rc = dispatch(0, (uint64_t)len0, ln == 0))) break;
-        }
-        if (ln == 0) { nseg = sgi; break; }
-        if ((rc = dispatch(sgi, (uint64_t)ln, false))) break;
-        if ((uint64_t)ln < cap) { nseg = sgi + 1; break; }
-      }
-    }
-    // a regular file that ended before its st_size (it shrank, or a read came back short at
-    // a piece boundary): redo it the way hash.rs reads
-    if (rc == SD_CAS_OK && next == DONE && !seq && total < (uint64_t)st.st_size) next = GO_SEQ;
-    if (rc == SD_CAS_OK && next == DONE) {
-      uint32_t* d_out = (uint32_t*)c->d_scalar;
-      hipError_t e = hipSuccess;
-      // reduce_cvs_device ping-pongs ceil(nseg / 256) CVs per level through ws
-      const size_t red_ws = 2 * up256((nseg + 255) / 256 * 32) + 512;
-      if (nseg > 1) rc = ensure(c, c->ws, red_ws);
-      if (rc == SD_CAS_OK) {
-        if (nseg == 1) e = hipMemcpyAsync(d_out, c->cvbuf.p, 32, hipMemcpyDeviceToDevice, s);
-        else e = reduce_cvs_device((uint32_t*)c->cvbuf.p, nseg, d_out, c->ws.p, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(digest, d_out, 32, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) rc = fail(c, SD_CAS_EHIP, "checksum reduce: %s", hipGetErrorString(e));
-      }
-    }
-    (void)hipStreamSynchronize(s);  // no segment copy may still read the pinned buffers
-    (void)sd_ws_release(c, s);
-    if (rc != SD_CAS_OK || next == DONE) break;
-    if (next == GROW) {
-      cap = SEG;
-    } else {  // GO_SEQ: from the start, hash.rs's reads
-      seq = true;
-      cap = SEG;
-      irregular = false;
-      if (lseek(fd, 0, SEEK_SET) != 0) {
-        if (err_no) *err_no = errno;
-        rc = fail(c, SD_CAS_EIO, "lseek(%s): %s", path, strerror(errno));
-        break;
-      }
-    }
-    if (attempt == 2) rc = fail(c, SD_CAS_EIO, "file_checksum(%s): no stable read", path);
   }
+  if (rc == SD_CAS_OK && seq) rc = file_checksum_seq(c, fd, path, digest, err_no);
   close(fd);
-  (void)hipStreamSynchronize(s);
-  (void)hipEventDestroy(done[0]);
-  (void)hipEventDestroy(done[1]);
   if (rc) return rc;
   static const char* hx = "0123456789abcdef";
   for (int i = 0; i < 32; i++) { out_hex[2 * i] = hx[digest[i] >> 4]; out_hex[2 * i + 1] = hx[digest[i] & 15]; }
@@ -324,23 +472,6 @@ int sd_cas_checksums_dev(sd_cas_ctx* c, const void* d_arena, uint64_t arena_byte
                                       : "the buffers' subtrees exceed arena_bytes' bound (overlapping buffers?)");
   return SD_CAS_OK;
 }
-
-// A/B knobs of the file path below (tools/build_variant.sh + tools/patch_define.py)
-#ifndef SD_CK_PIECE_KB
-#define SD_CK_PIECE_KB 1024
-#endif
-#ifndef SD_CK_COPY_MB
-#define SD_CK_COPY_MB 8
-#endif
-#ifndef SD_CK_PUMP_READS  // the pump thread also reads pieces when it has nothing to issue
-#define SD_CK_PUMP_READS 1
-#endif
-#ifndef SD_CK_PUMP_ON_POOL  // the pump on a pool thread (1) or on the calling thread (0)
-#define SD_CK_PUMP_ON_POOL 1
-#endif
-#ifndef SD_CK_COPY_STREAMS  // copies alternate over this many streams (1 or 2)
-#define SD_CK_COPY_STREAMS 2
-#endif
 
 // file_checksum over many paths.  The batch files are laid out in windows of up to CK_WIN
 // bytes / CK_WIN_FILES files in index order (one slot of up128(st_size + 1) per file: the

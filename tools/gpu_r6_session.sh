@@ -28,6 +28,8 @@
 #   repeat     the default `python bench.py` and the validator file path twice, on another box
 #   valshapes  the validator file path on 20,000 small files, 150 files of 16-60 MiB, and 40 files
 #              of 128-192 MiB (streamed one by one)
+#   streamab   the streamed single-file path (40 files of 128-192 MiB; one 4 GiB file): in-tree vs
+#              $STREAM_VARIANTS, 2 rounds
 #   suite      the whole GPU suite (release)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
@@ -149,6 +151,15 @@ for step in "$@"; do
       timeout -k 10 400 python3 -u tools/prof_checksums.py --no-device --paths 150 --path-kib 16384 61440 --path-runs 4 > $OUT/validator_large_files.log 2>&1 || { echo VALSHAPES_FAIL; tail -20 $OUT/validator_large_files.log; exit 1; }
       timeout -k 10 400 python3 -u tools/prof_checksums.py --no-device --paths 40 --path-kib 131072 196608 --path-runs 3 > $OUT/validator_streamed_files.log 2>&1 || { echo VALSHAPES_FAIL; tail -20 $OUT/validator_streamed_files.log; exit 1; }
       grep -h '"files"' $OUT/validator_*_files.log | cut -c1-300 ;;
+    streamab)
+      for k in 1 2; do
+        for v in intree ${STREAM_VARIANTS:-stream_old}; do
+          lib=""; [ $v != intree ] && lib=$R/tools/ablib/$v.so
+          SD_HIP_CAS_LIB=$lib timeout -k 10 400 python3 -u tools/prof_checksums.py --no-device --paths 40 --path-kib 131072 196608 --path-runs 4 > $OUT/streamed_${v}_$k.log 2>&1 || { echo STREAMAB_FAIL; tail -20 $OUT/streamed_${v}_$k.log; exit 1; }
+          SD_HIP_CAS_LIB=$lib timeout -k 10 400 python3 -u tools/prof_checksums.py --no-device --paths 1 --path-kib 4194304 4194305 --path-runs 4 > $OUT/onefile_${v}_$k.log 2>&1 || { echo STREAMAB_FAIL; tail -20 $OUT/onefile_${v}_$k.log; exit 1; }
+        done
+      done
+      grep -h '"files"' $OUT/streamed_*.log $OUT/onefile_*.log | cut -c1-200 ;;
     suite)
       timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -30 $OUT/pytest_gpu.log; exit 1; }
       tail -1 $OUT/pytest_gpu.log ;;
