@@ -30,6 +30,7 @@
 #              of 128-192 MiB (streamed one by one)
 #   streamab   the streamed single-file path (40 files of 128-192 MiB; one 4 GiB file): in-tree vs
 #              $STREAM_VARIANTS, 2 rounds
+#   smalltrace the validator file path on 20,000 small files with SD_CAS_TRACE=1
 #   suite      the whole GPU suite (release)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
@@ -160,6 +161,9 @@ for step in "$@"; do
         done
       done
       grep -h '"files"' $OUT/streamed_*.log $OUT/onefile_*.log | cut -c1-200 ;;
+    smalltrace)
+      SD_CAS_TRACE=1 timeout -k 10 400 python3 -u tools/prof_checksums.py --no-device --paths 20000 --path-kib 16 256 --path-runs 4 > $OUT/small_trace.log 2>&1 || { echo SMALLTRACE_FAIL; tail -20 $OUT/small_trace.log; exit 1; }
+      grep sd_cas_trace $OUT/small_trace.log | grep "n=20000" | cut -c1-300 ;;
     suite)
       timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -30 $OUT/pytest_gpu.log; exit 1; }
       tail -1 $OUT/pytest_gpu.log ;;
