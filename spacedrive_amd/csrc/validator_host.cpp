@@ -124,40 +124,64 @@ static int cv_capacity(sd_cas_ctx* c, DevBuf& cvb, size_t need_cvs, hipStream_t 
   return SD_CAS_OK;
 }
 
-// The pieces mode of file_checksum (see above).  Returns SD_CAS_OK with the digest in
-// digest[32], SD_CAS_OK with *go_seq set (redo with hash.rs's sequential reads), or an error
-// (*err_no = the failed read's errno).
-static int file_checksum_pieces(sd_cas_ctx* c, int fd, uint64_t st_size, const char* path,
-                                uint8_t digest[32], int* err_no, bool* go_seq) {
+// The pieces mode of file_checksum (see above), over one or many files in ONE queue: every
+// file is planned from its st_size (+ one probe byte) as 64 MiB segments; the segments of all
+// files, in file order, rotate over three pinned + device slots, and their 1 MiB pieces are
+// read by the pool while the pump copies landed prefixes (two copy streams), hashes each
+// complete segment (K3 at its chunk offset, ROOT inside for a one-segment file) and, after a
+// file's last segment, reduces its CVs into its digest — so a validator job's large files
+// stream back to back with no per-file fill and drain.  fds: the files' open descriptors, or
+// nullptr (each piece opens its file).  Per file: digests[32 j], errs[j] = the errno of a
+// failed open/read (0 otherwise), go_seq[j] = 1 when its reads were irregular (a short pread
+// before its planned end, data in the probe byte, an end before st_size): redo with hash.rs's
+// sequential reads.  Returns SD_CAS_OK or a HIP / allocation error.
+static int file_checksums_pieces(sd_cas_ctx* c, const char* const* paths, const int* fds,
+                                 const uint64_t* sizes, size_t nf, uint8_t* digests, int* errs,
+                                 uint8_t* go_seq) {
   constexpr uint64_t SEG = 64ull << 20;  // 65,536 chunks: a complete left subtree
   constexpr uint64_t PIECE = (uint64_t)SD_CK_PIECE_KB << 10;
   constexpr uint64_t COPY = (uint64_t)SD_CK_COPY_MB << 20;
   constexpr int SLOTS = 3;
-  *go_seq = false;
-  const uint64_t total = st_size + 1;  // + the probe byte: data there means the file grew
-  const uint64_t nplan = (total + SEG - 1) / SEG;
-  const uint64_t nreal = std::max<uint64_t>(1, (st_size + SEG - 1) / SEG);  // segments holding data
-  const uint64_t cap = std::min<uint64_t>(SEG, ((total + 4095) / 4096) * 4096);
+  if (nf == 0) return SD_CAS_OK;
+  struct Seg { uint32_t file; uint64_t k, len, want; };  // len: planned bytes, want: bytes to hash
+  struct Piece { uint32_t seg; uint64_t off, len; };     // off: from the segment's start
+  std::vector<Seg> segs;
+  std::vector<uint64_t> nreal(nf), cvbase(nf + 1, 0);
+  uint64_t maxtotal = 0, maxreal = 1;
+  for (size_t j = 0; j < nf; j++) {
+    const uint64_t total = sizes[j] + 1;  // + the probe byte: data there means the file grew
+    const uint64_t nplan = (total + SEG - 1) / SEG;
+    nreal[j] = std::max<uint64_t>(1, (sizes[j] + SEG - 1) / SEG);  // segments holding data
+    cvbase[j + 1] = cvbase[j] + nreal[j];
+    maxtotal = std::max(maxtotal, total);
+    maxreal = std::max(maxreal, nreal[j]);
+    for (uint64_t k = 0; k < nplan; k++)
+      segs.push_back({(uint32_t)j, k, std::min(SEG, total - k * SEG),
+                      k < nreal[j] ? std::min(SEG, sizes[j] - std::min(sizes[j], k * SEG)) : 0});
+    errs[j] = 0;
+    go_seq[j] = 0;
+  }
+  std::vector<Piece> pieces;
+  std::vector<size_t> spiece{0};
+  for (size_t g = 0; g < segs.size(); g++) {
+    const uint64_t np = std::max<uint64_t>(1, segs[g].len / PIECE);
+    for (uint64_t q = 0; q < np; q++)
+      pieces.push_back({(uint32_t)g, q * PIECE, q + 1 < np ? PIECE : segs[g].len - q * PIECE});
+    spiece.push_back(pieces.size());
+  }
+  const size_t ns = segs.size(), np = pieces.size();
+  const uint64_t cap = std::min<uint64_t>(SEG, ((maxtotal + 4095) / 4096) * 4096);
   const size_t sb = up256(cap + 16);
+  const uint64_t ncv = cvbase[nf];
   hipStream_t s = c->stream, cs = c->copy;
   int rc = SD_CAS_OK;
   if ((rc = ensure_pinned(c, SLOTS * sb)) || (rc = ensure(c, c->staging, SLOTS * sb))) return rc;
-  if ((rc = ensure(c, c->ws, std::max(checksum_workspace_bytes(cap), checksum_workspace_bytes(1 << 20)))))
+  if ((rc = ensure(c, c->ws, std::max({checksum_workspace_bytes(cap), checksum_workspace_bytes(1 << 20),
+                                        2 * up256((maxreal + 255) / 256 * 32) + 512}))))
     return rc;
-  const size_t red_ws = 2 * up256((nreal + 255) / 256 * 32) + 512;  // reduce_cvs_device's ping-pong
-  if (nreal > 1 && (rc = ensure(c, c->ws, red_ws))) return rc;
-  if ((rc = cv_capacity(c, c->cvbuf, nreal, s))) return rc;
-  struct Piece { uint32_t seg; uint64_t off, len; };  // off: from the segment's start
-  std::vector<Piece> pieces;
-  std::vector<size_t> spiece{0};
-  for (uint64_t k = 0; k < nplan; k++) {
-    const uint64_t len = std::min(SEG, total - k * SEG);
-    const uint64_t np = std::max<uint64_t>(1, len / PIECE);
-    for (uint64_t j = 0; j < np; j++)
-      pieces.push_back({(uint32_t)k, j * PIECE, j + 1 < np ? PIECE : len - j * PIECE});
-    spiece.push_back(pieces.size());
-  }
-  const size_t np = pieces.size();
+  if ((rc = cv_capacity(c, c->cvbuf, ncv + nf, s))) return rc;  // CVs, then the digests
+  uint32_t* d_cv = (uint32_t*)c->cvbuf.p;
+  uint32_t* d_dig = d_cv + 8 * ncv;
   hipEvent_t done[SLOTS] = {}, landed = nullptr;
   auto destroy_events = [&]() {
     for (int b = 0; b < SLOTS; b++)
@@ -174,29 +198,37 @@ static int file_checksum_pieces(sd_cas_ctx* c, int fd, uint64_t st_size, const c
     return fail(c, SD_CAS_EHIP, "file_checksum: event create");
   }
   std::unique_ptr<std::atomic<uint8_t>[]> fin(new std::atomic<uint8_t>[np]);
-  std::unique_ptr<std::atomic<uint64_t>[]> sgot(new std::atomic<uint64_t>[nplan]);
+  std::unique_ptr<std::atomic<uint64_t>[]> sgot(new std::atomic<uint64_t>[ns]);
+  std::unique_ptr<std::atomic<int>[]> ferr(new std::atomic<int>[nf]);
+  std::unique_ptr<std::atomic<uint8_t>[]> firr(new std::atomic<uint8_t>[nf]);
   for (size_t p = 0; p < np; p++) fin[p].store(0, std::memory_order_relaxed);
-  for (uint64_t k = 0; k < nplan; k++) sgot[k].store(0);
-  std::atomic<int> rd_err{0};
-  std::atomic<bool> irregular{false}, abort{false};
+  for (size_t g = 0; g < ns; g++) sgot[g].store(0);
+  for (size_t j = 0; j < nf; j++) { ferr[j].store(0); firr[j].store(0); }
+  std::atomic<bool> abort{false};
   std::atomic<size_t> next{0}, freed{0};
-  auto slot_free = [&](uint32_t k) { return k < freed.load(std::memory_order_acquire) + SLOTS; };
+  auto slot_free = [&](uint32_t g) { return g < freed.load(std::memory_order_acquire) + SLOTS; };
   auto read_piece = [&](size_t p) {
     const Piece& pc = pieces[p];
+    const Seg& sg = segs[pc.seg];
+    const uint32_t j = sg.file;
+    if (ferr[j].load(std::memory_order_relaxed) || firr[j].load(std::memory_order_relaxed)) return;
     char* dst = (char*)c->pinned + (size_t)(pc.seg % SLOTS) * sb + pc.off;
-    const uint64_t foff = (uint64_t)pc.seg * SEG + pc.off;
+    const uint64_t foff = sg.k * SEG + pc.off;
+    int fd = fds ? fds[j] : open(paths[j], O_RDONLY | O_CLOEXEC);
+    if (fd < 0) { ferr[j].store(errno); return; }
     uint64_t got = 0;
     bool was_short = false;
     while (got < pc.len) {
       ssize_t r = pread(fd, dst + got, pc.len - got, (off_t)(foff + got));
       if (r < 0 && errno == EINTR) continue;
-      if (r < 0) { rd_err.store(errno); abort.store(true); break; }
+      if (r < 0) { ferr[j].store(errno); break; }
       if (r == 0) break;  // EOF
-      if (was_short) irregular.store(true);  // data after a short read
+      if (was_short) firr[j].store(1);  // data after a short read
       if ((uint64_t)r < pc.len - got) was_short = true;
       got += (uint64_t)r;
     }
-    if (got < pc.len && foff + pc.len < total) irregular.store(true);  // ended before the planned end
+    if (!fds) close(fd);
+    if (got < pc.len && foff + pc.len < sizes[j] + 1) firr[j].store(1);  // ended before the planned end
     sgot[pc.seg].fetch_add(got);
   };
   auto worker = [&]() {
@@ -207,7 +239,8 @@ static int file_checksum_pieces(sd_cas_ctx* c, int fd, uint64_t st_size, const c
       fin[p].store(1, std::memory_order_release);
     }
   };
-  // the pump: copies landed prefixes, hashes complete segments, frees slots; reads when idle
+  std::vector<uint8_t> fok(nf, 1);  // (pump only) every segment of the file so far as planned
+  // the pump: copies landed prefixes, hashes complete segments and finished files, frees slots
   auto pump = [&]() {
     size_t kc = 0, issued = 0, retired = 0, ready = 0, ncopies = 0;
     uint64_t sent = 0;
@@ -217,7 +250,7 @@ static int file_checksum_pieces(sd_cas_ctx* c, int fd, uint64_t st_size, const c
     };
     if (hipError_t e = hipSetDevice(c->device); e != hipSuccess) { hipfail(e, "setup"); return; }
     if (hipError_t e = sd_ws_acquire(c, s); e != hipSuccess) { hipfail(e, "setup"); return; }
-    while (retired < nplan && rc == SD_CAS_OK && !abort.load()) {
+    while (retired < ns && rc == SD_CAS_OK) {
       if (retired < issued) {
         const hipError_t q = hipEventQuery(done[retired % SLOTS]);
         if (q == hipSuccess) {
@@ -227,14 +260,14 @@ static int file_checksum_pieces(sd_cas_ctx* c, int fd, uint64_t st_size, const c
         if (q != hipErrorNotReady) { hipfail(q, "segment sync"); break; }
       }
       bool progress = false;
-      if (kc < nplan) {
+      if (kc < ns) {
+        const Seg& sg = segs[kc];
         const size_t b = kc % SLOTS;
         char* pin = (char*)c->pinned + b * sb;
         char* dev = (char*)c->staging.p + b * sb;
         while (ready < spiece[kc + 1] && fin[ready].load(std::memory_order_acquire)) ++ready;
         const bool complete = ready == spiece[kc + 1];
-        const uint64_t want = kc < nreal ? std::min(SEG, st_size - kc * SEG) : 0;  // bytes to hash
-        const uint64_t hi = complete ? want : std::min(want, pieces[ready].off);
+        const uint64_t hi = complete ? sg.want : std::min(sg.want, pieces[ready].off);
         if (hi > sent && (hi - sent >= COPY || complete)) {
           hipStream_t xs = (SD_CK_COPY_STREAMS > 1 && (ncopies & 1)) ? c->copy2 : cs;
           const uint64_t hi16 = complete ? up16(hi) : hi;  // (K3 reads to the 16-B round-up)
@@ -244,16 +277,13 @@ static int file_checksum_pieces(sd_cas_ctx* c, int fd, uint64_t st_size, const c
           ++ncopies;
           progress = true;
         }
-        if (complete && sent >= want) {
+        if (complete && sent >= sg.want) {
+          const uint32_t j = sg.file;
+          const bool last = sg.k + 1 == (sizes[j] + SEG) / SEG;  // (sizes[j] + 1 + SEG - 1) / SEG segments
           // the segment must hold exactly its planned bytes (the probe byte none)
-          const uint64_t got = sgot[kc].load(), planned = std::min(SEG, total - kc * SEG);
-          if (irregular.load() || got != (kc + 1 == nplan ? planned - 1 : planned)) {
-            *go_seq = true;
-            abort.store(true);
-            break;
-          }
+          if (ferr[j].load() || firr[j].load() || sgot[kc].load() != (last ? sg.len - 1 : sg.len)) fok[j] = 0;
           hipError_t e = hipSuccess;
-          if (kc < nreal) {
+          if (fok[j] && sg.k < nreal[j]) {
             if (SD_CK_COPY_STREAMS > 1) {
               e = hipEventRecord(landed, c->copy2);
               if (e == hipSuccess) e = hipStreamWaitEvent(s, landed, 0);
@@ -261,9 +291,12 @@ static int file_checksum_pieces(sd_cas_ctx* c, int fd, uint64_t st_size, const c
             if (e == hipSuccess) e = hipEventRecord(landed, cs);
             if (e == hipSuccess) e = hipStreamWaitEvent(s, landed, 0);
             if (e == hipSuccess)
-              e = checksum_device((const uint8_t*)dev, want, (kc * SEG) >> 10, nreal == 1,
-                                  (uint32_t*)c->cvbuf.p + 8 * kc, c->ws.p, s);
+              e = checksum_device((const uint8_t*)dev, sg.want, (sg.k * SEG) >> 10, nreal[j] == 1,
+                                  d_cv + 8 * (cvbase[j] + sg.k), c->ws.p, s);
           }
+          if (e == hipSuccess && fok[j] && last)  // the file's digest
+            e = nreal[j] == 1 ? hipMemcpyAsync(d_dig + 8 * j, d_cv + 8 * cvbase[j], 32, hipMemcpyDeviceToDevice, s)
+                              : reduce_cvs_device(d_cv + 8 * cvbase[j], nreal[j], d_dig + 8 * j, c->ws.p, s);
           if (e == hipSuccess) e = hipEventRecord(done[b], s);
           if (e != hipSuccess) { hipfail(e, "segment"); break; }
           ++issued;
@@ -290,20 +323,11 @@ static int file_checksum_pieces(sd_cas_ctx* c, int fd, uint64_t st_size, const c
   const std::function<void()> pool_fn = [&]() {
     if (!pump_taken.exchange(true)) pump(); else worker();
   };
-  c->pool.run2(std::max(2u, std::min(16u, (unsigned)np + 1)), pool_fn, []() {});
-  if (rc == SD_CAS_OK && !*go_seq) {
-    if (int e = rd_err.load()) {
-      if (err_no) *err_no = e;
-      rc = fail(c, SD_CAS_EIO, "read(%s): %s", path, strerror(e));
-    }
-  }
-  if (rc == SD_CAS_OK && !*go_seq) {
-    uint32_t* d_out = (uint32_t*)c->d_scalar;
-    hipError_t e = nreal == 1 ? hipMemcpyAsync(d_out, c->cvbuf.p, 32, hipMemcpyDeviceToDevice, s)
-                              : reduce_cvs_device((uint32_t*)c->cvbuf.p, nreal, d_out, c->ws.p, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(digest, d_out, 32, hipMemcpyDeviceToHost, s);
+  c->pool.run2(std::max(2u, std::min(16u, (unsigned)std::min<size_t>(np + 1, 16))), pool_fn, []() {});
+  if (rc == SD_CAS_OK) {
+    hipError_t e = hipMemcpyAsync(digests, d_dig, nf * 32, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) rc = fail(c, SD_CAS_EHIP, "checksum reduce: %s", hipGetErrorString(e));
+    if (e != hipSuccess) rc = fail(c, SD_CAS_EHIP, "checksum digests: %s", hipGetErrorString(e));
   }
   (void)sd_ws_release(c, s);
   // nothing in flight may still read the pinned slots or write the CVs
@@ -311,6 +335,24 @@ static int file_checksum_pieces(sd_cas_ctx* c, int fd, uint64_t st_size, const c
   (void)hipStreamSynchronize(c->copy2);
   (void)hipStreamSynchronize(s);
   destroy_events();
+  for (size_t j = 0; j < nf; j++) {
+    errs[j] = ferr[j].load();
+    go_seq[j] = !errs[j] && !fok[j];
+  }
+  return rc;
+}
+
+// One file (sd_cas_file_checksum): the queue above with its open descriptor.
+static int file_checksum_pieces(sd_cas_ctx* c, int fd, uint64_t st_size, const char* path,
+                                uint8_t digest[32], int* err_no, bool* go_seq) {
+  int err = 0;
+  uint8_t seq = 0;
+  int rc = file_checksums_pieces(c, &path, &fd, &st_size, 1, digest, &err, &seq);
+  *go_seq = rc == SD_CAS_OK && seq;
+  if (rc == SD_CAS_OK && err) {
+    if (err_no) *err_no = err;
+    rc = fail(c, SD_CAS_EIO, "read(%s): %s", path, strerror(err));
+  }
   return rc;
 }
 
@@ -505,7 +547,7 @@ int sd_cas_file_checksums(sd_cas_ctx* c, const char* const* paths, size_t n, cha
   enum : uint8_t { K_BATCH = 0, K_STREAM = 1, K_ERROR = 2 };
   SdTrace tr(c->trace, "file_checksums", n);
   std::vector<uint64_t> fsize(n, 0);
-  std::vector<uint8_t> kind(n, K_BATCH);
+  std::vector<uint8_t> kind(n, K_BATCH), big(n, 0);  // big: a regular file over CK_BIG
   for (size_t i = 0; i < n; i++) { status[i] = 0; out_hex[65 * i] = 0; }
   {  // stat pass
     std::atomic<size_t> next{0};
@@ -516,6 +558,7 @@ int sd_cas_file_checksums(sd_cas_ctx* c, const char* const* paths, size_t n, cha
         fsize[i] = (uint64_t)st.st_size;
         // not a regular file (FIFO, device, ...): hash.rs's sequential reads, streamed
         if (fsize[i] > CK_BIG || !S_ISREG(st.st_mode)) kind[i] = K_STREAM;
+        big[i] = fsize[i] > CK_BIG && S_ISREG(st.st_mode);
       }
     });
   }
@@ -768,8 +811,34 @@ int sd_cas_file_checksums(sd_cas_ctx* c, const char* const* paths, size_t n, cha
   }
   destroy_events();
   if (rc) return rc;
-  // big files and files that grew: the streaming path, one at a time (after the windows:
-  // it reuses the pinned and device staging)
+  // big regular files: 64 MiB segments of all of them in one piece queue, back to back (after
+  // the windows: it reuses the pinned and device staging)
+  {
+    std::vector<size_t> bi;
+    std::vector<const char*> bp;
+    std::vector<uint64_t> bs;
+    for (size_t i = 0; i < n; i++)
+      if (kind[i] == K_STREAM && big[i]) { bi.push_back(i); bp.push_back(paths[i]); bs.push_back(fsize[i]); }
+    if (!bi.empty()) {
+      std::vector<uint8_t> dg(32 * bi.size()), gs(bi.size());
+      std::vector<int> er(bi.size());
+      if ((rc = file_checksums_pieces(c, bp.data(), nullptr, bs.data(), bi.size(), dg.data(), er.data(),
+                                      gs.data())))
+        return rc;
+      for (size_t k = 0; k < bi.size(); k++) {
+        const size_t i = bi[k];
+        if (er[k]) { status[i] = -er[k]; kind[i] = K_ERROR; continue; }
+        if (gs[k]) continue;  // read irregularly (or changed since stat): the path below
+        char* o = out_hex + 65 * i;
+        for (int j = 0; j < 32; j++) { o[2 * j] = hx[dg[32 * k + j] >> 4]; o[2 * j + 1] = hx[dg[32 * k + j] & 15]; }
+        o[64] = 0;
+        kind[i] = K_BATCH;
+      }
+    }
+  }
+  tr.mark("big");
+  // everything else off the windows — files that grew or read irregularly there, files that
+  // changed since stat, non-regular files: sd_cas_file_checksum, one at a time
   for (size_t i = 0; i < n; i++) {
     if (kind[i] != K_STREAM) continue;
     char* o = out_hex + 65 * i;

@@ -1442,6 +1442,43 @@ def test_file_checksums_pieces_and_slot_rotation(eng, oracle):
         os.rmdir(root)
 
 
+def test_file_checksums_big_files_one_queue(eng, oracle):
+    """Round 6: regular files over 64 MiB go through ONE piece queue of 64 MiB segments (all
+    files back to back), and sd_cas_file_checksum through the same queue for one file —
+    sizes at segment multiples (a probe-only last segment), one byte either side, the empty
+    file, small files between them (the windows), every digest vs the oracle; then the same
+    big files one at a time through file_checksum."""
+    d = "/dev/shm" if os.path.isdir("/dev/shm") else "/tmp"
+    root = os.path.join(d, f"sdcas_big_{os.getpid()}")
+    os.makedirs(root)
+    rng = np.random.default_rng(19)
+    M = 1 << 20
+    sizes = [64 * M + 1, 5 * M, 128 * M, 0, 128 * M + 1, 3, 192 * M - 1, 65 * M, 64 * M]
+    paths = []
+    try:
+        block = rng.integers(0, 256, 8 * M, dtype=np.uint8)
+        for i, L in enumerate(sizes):
+            p = os.path.join(root, f"b{i}")
+            with open(p, "wb") as fh:
+                left, k = L, 0
+                while left:  # distinct bytes per file and per 8 MiB block
+                    n = min(left, 8 * M)
+                    fh.write((block[:n] ^ np.uint8((i * 31 + k) & 255)).tobytes())
+                    left -= n
+                    k += 1
+            paths.append(p)
+        want = [oracle.file_checksum(p) for p in paths]
+        got, errs = eng.file_checksums(paths)
+        assert not errs.any() and got == want
+        for p, w in zip(paths, want):
+            if os.path.getsize(p) >= 64 * M:
+                assert eng.file_checksum(p) == w, p
+    finally:
+        for p in paths:
+            os.unlink(p)
+        os.rmdir(root)
+
+
 def test_host_pool_numa_modes_agree(eng, oracle, monkeypatch, tmp_path):
     """Round 6: the host gather pool is bound to the GPU's NUMA node unless SD_CAS_POOL_NUMA=0
     (read at context creation).  A context of each mode gives the same validator digests and
