@@ -3,14 +3,18 @@
 // part of the public ABI.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <dirent.h>
 #include <pthread.h>
 #include <sched.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <functional>
@@ -41,6 +45,20 @@ class HostPool {
     for (auto& t : th_) (void)pthread_setaffinity_np(t.native_handle(), sizeof cpus_, &cpus_);
   }
   int bound_cpus() const { return ncpus_; }
+  // Round 6: each pool thread may start by unsharing the process's descriptor table
+  // (unshare(CLONE_FILES): a private copy of the table as it is then).  The readers open and
+  // close a file per item, and with one shared table every open / close takes the same
+  // table lock: 16 readers of config 1's mix gathered 575 k files/s shared and 745-775 k
+  // private (tools/probe_gather.cpp, profiles/r06/gather/).  The rule this imposes: a pool
+  // thread only uses descriptors it opened itself (or that existed when it started: the HIP
+  // runtime's) — no task may hand a pool thread a descriptor opened elsewhere.  Set before
+  // the first run (threads start lazily); SD_CAS_POOL_PRIVATE_FDS=0 keeps the shared table.
+  // The copy would also keep every other descriptor of the process alive in this thread (a
+  // pipe's write end: its reader never sees EOF; a socket the application closed: its peer
+  // never sees the close), so the thread then closes all of its copies except 0-2, the HIP
+  // runtime's device nodes (/dev/kfd, /dev/dri/*) and anonymous-inode descriptors.
+  void set_private_fds(bool on) { private_fds_ = on; }
+  int private_threads() const { return nprivate_.load(); }
   ~HostPool() {
     {
       std::lock_guard<std::mutex> g(mu_);
@@ -73,7 +91,32 @@ class HostPool {
   }
 
  private:
+  static void keep_only_device_fds() {
+    DIR* d = opendir("/proc/thread-self/fd");
+    if (!d) return;
+    const int self = dirfd(d);
+    std::vector<int> drop;
+    char path[64], link[256];
+    while (dirent* e = readdir(d)) {
+      if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
+      const int fd = atoi(e->d_name);
+      if (fd == self || fd <= 2) continue;  // stdin/out/err stay (logging from a pool thread)
+      snprintf(path, sizeof path, "/proc/thread-self/fd/%d", fd);
+      const ssize_t n = readlink(path, link, sizeof link - 1);
+      if (n < 0) continue;
+      link[n] = 0;
+      if (!strcmp(link, "/dev/kfd") || !strncmp(link, "/dev/dri/", 9) || !strncmp(link, "anon_inode:", 11))
+        continue;
+      drop.push_back(fd);
+    }
+    closedir(d);
+    for (int fd : drop) close(fd);
+  }
   void loop() {
+    if (private_fds_ && unshare(CLONE_FILES) == 0) {
+      keep_only_device_fds();
+      nprivate_.fetch_add(1);
+    }
     uint64_t seen = 0;
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
@@ -97,6 +140,8 @@ class HostPool {
   bool stop_ = false;
   cpu_set_t cpus_{};
   int ncpus_ = 0;
+  bool private_fds_ = false;
+  std::atomic<int> nprivate_{0};
 };
 
 struct sd_cas_ctx {

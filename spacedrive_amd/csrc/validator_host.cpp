@@ -130,14 +130,15 @@ static int cv_capacity(sd_cas_ctx* c, DevBuf& cvb, size_t need_cvs, hipStream_t 
 // read by the pool while the pump copies landed prefixes (two copy streams), hashes each
 // complete segment (K3 at its chunk offset, ROOT inside for a one-segment file) and, after a
 // file's last segment, reduces its CVs into its digest — so a validator job's large files
-// stream back to back with no per-file fill and drain.  fds: the files' open descriptors, or
-// nullptr (each piece opens its file).  Per file: digests[32 j], errs[j] = the errno of a
-// failed open/read (0 otherwise), go_seq[j] = 1 when its reads were irregular (a short pread
-// before its planned end, data in the probe byte, an end before st_size): redo with hash.rs's
-// sequential reads.  Returns SD_CAS_OK or a HIP / allocation error.
-static int file_checksums_pieces(sd_cas_ctx* c, const char* const* paths, const int* fds,
-                                 const uint64_t* sizes, size_t nf, uint8_t* digests, int* errs,
-                                 uint8_t* go_seq) {
+// stream back to back with no per-file fill and drain.  Each piece opens its file by path on
+// the pool thread that reads it (the pool's threads have private descriptor tables,
+// HostPool::set_private_fds: a descriptor opened on the calling thread is not theirs).  Per
+// file: digests[32 j], errs[j] = the errno of a failed open/read (0 otherwise), go_seq[j] = 1
+// when its reads were irregular (a short pread before its planned end, data in the probe byte,
+// an end before st_size): redo with hash.rs's sequential reads.  Returns SD_CAS_OK or a HIP /
+// allocation error.
+static int file_checksums_pieces(sd_cas_ctx* c, const char* const* paths, const uint64_t* sizes,
+                                 size_t nf, uint8_t* digests, int* errs, uint8_t* go_seq) {
   constexpr uint64_t SEG = 64ull << 20;  // 65,536 chunks: a complete left subtree
   constexpr uint64_t PIECE = (uint64_t)SD_CK_PIECE_KB << 10;
   constexpr uint64_t COPY = (uint64_t)SD_CK_COPY_MB << 20;
@@ -214,7 +215,7 @@ static int file_checksums_pieces(sd_cas_ctx* c, const char* const* paths, const 
     if (ferr[j].load(std::memory_order_relaxed) || firr[j].load(std::memory_order_relaxed)) return;
     char* dst = (char*)c->pinned + (size_t)(pc.seg % SLOTS) * sb + pc.off;
     const uint64_t foff = sg.k * SEG + pc.off;
-    int fd = fds ? fds[j] : open(paths[j], O_RDONLY | O_CLOEXEC);
+    const int fd = open(paths[j], O_RDONLY | O_CLOEXEC);
     if (fd < 0) { ferr[j].store(errno); return; }
     uint64_t got = 0;
     bool was_short = false;
@@ -227,7 +228,7 @@ static int file_checksums_pieces(sd_cas_ctx* c, const char* const* paths, const 
       if ((uint64_t)r < pc.len - got) was_short = true;
       got += (uint64_t)r;
     }
-    if (!fds) close(fd);
+    close(fd);
     if (got < pc.len && foff + pc.len < sizes[j] + 1) firr[j].store(1);  // ended before the planned end
     sgot[pc.seg].fetch_add(got);
   };
@@ -342,12 +343,14 @@ static int file_checksums_pieces(sd_cas_ctx* c, const char* const* paths, const 
   return rc;
 }
 
-// One file (sd_cas_file_checksum): the queue above with its open descriptor.
-static int file_checksum_pieces(sd_cas_ctx* c, int fd, uint64_t st_size, const char* path,
+// One file (sd_cas_file_checksum): the queue above over its path (the readers open it
+// themselves; a file replaced since the caller's open reads irregularly or not — the same
+// race the batch path's per-piece opens have, and hash.rs's reads have no defined answer to).
+static int file_checksum_pieces(sd_cas_ctx* c, uint64_t st_size, const char* path,
                                 uint8_t digest[32], int* err_no, bool* go_seq) {
   int err = 0;
   uint8_t seq = 0;
-  int rc = file_checksums_pieces(c, &path, &fd, &st_size, 1, digest, &err, &seq);
+  int rc = file_checksums_pieces(c, &path, &st_size, 1, digest, &err, &seq);
   *go_seq = rc == SD_CAS_OK && seq;
   if (rc == SD_CAS_OK && err) {
     if (err_no) *err_no = err;
@@ -469,7 +472,7 @@ int sd_cas_file_checksum(sd_cas_ctx* c, const char* path, char out_hex[65], int*
   int rc = SD_CAS_OK;
   bool seq = !S_ISREG(st.st_mode);
   if (!seq) {  // a regular file: the pieces mode, redone sequentially if it reads irregularly
-    rc = file_checksum_pieces(c, fd, (uint64_t)st.st_size, path, digest, err_no, &seq);
+    rc = file_checksum_pieces(c, (uint64_t)st.st_size, path, digest, err_no, &seq);
     if (rc == SD_CAS_OK && seq && lseek(fd, 0, SEEK_SET) != 0) {
       if (err_no) *err_no = errno;
       rc = fail(c, SD_CAS_EIO, "lseek(%s): %s", path, strerror(errno));
@@ -822,7 +825,7 @@ int sd_cas_file_checksums(sd_cas_ctx* c, const char* const* paths, size_t n, cha
     if (!bi.empty()) {
       std::vector<uint8_t> dg(32 * bi.size()), gs(bi.size());
       std::vector<int> er(bi.size());
-      if ((rc = file_checksums_pieces(c, bp.data(), nullptr, bs.data(), bi.size(), dg.data(), er.data(),
+      if ((rc = file_checksums_pieces(c, bp.data(), bs.data(), bi.size(), dg.data(), er.data(),
                                       gs.data())))
         return rc;
       for (size_t k = 0; k < bi.size(); k++) {

@@ -1506,6 +1506,64 @@ def test_host_pool_numa_modes_agree(eng, oracle, monkeypatch, tmp_path):
     assert [f"{k:016x}" for k in got["1"]] == [oracle.generate_cas_id(p, s) for p, s in zip(paths[1:], sizes[1:])]
 
 
+def test_host_pool_private_fds(eng, oracle, monkeypatch, tmp_path):
+    """Round 6: the pool's threads start on private descriptor tables (HostPool::
+    set_private_fds, SD_CAS_POOL_PRIVATE_FDS; read at context creation) and keep only 0-2 and
+    the HIP runtime's device descriptors of the copy.  Both modes give the oracle's digests and
+    cas_ids — the validator's batch windows, its queue of files over 64 MiB, the single-file
+    pieces mode (its readers open the file themselves) and the sampled / whole-file gather — and
+    a pipe the caller closes after the pool started still reaches EOF (the copies are dropped)."""
+    import os
+    import select
+    from spacedrive_amd import CasEngine
+    rng = np.random.default_rng(23)
+    sizes = [1, 4096, 100 * 1024, 100 * 1024 + 1, 3 << 20, (64 << 20) + 4097] + \
+        [int(x) for x in rng.integers(1, 600_000, 40)]
+    paths = []
+    for i, L in enumerate(sizes):
+        p = tmp_path / f"p{i}"
+        p.write_bytes(rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+        paths.append(str(p))
+    want_sums = [oracle.file_checksum(p) for p in paths]
+    want_ids = [oracle.generate_cas_id(p, s) for p, s in zip(paths, sizes)]
+
+    def tasks_without(fd):
+        n = 0
+        for t in os.listdir("/proc/self/task"):
+            try:
+                if str(fd) not in os.listdir(f"/proc/self/task/{t}/fd"):
+                    n += 1
+            except OSError:
+                pass
+        return n
+
+    for mode in ("1", "0"):
+        monkeypatch.setenv("SD_CAS_POOL_PRIVATE_FDS", mode)
+        r, w = os.pipe()
+        try:
+            before = tasks_without(r)
+            e = CasEngine(0)
+            sums, errs = e.file_checksums(paths)
+            assert not errs.any() and sums == want_sums, mode
+            assert e.file_checksum(paths[4]) == want_sums[4], mode
+            keys, kerr = e.generate_cas_keys_from_paths(paths, np.array(sizes, dtype=np.int64))
+            assert not kerr.any(), mode
+            assert [f"{k:016x}" for k in keys] == want_ids, mode
+            keys100, _ = e.generate_cas_keys_from_paths(paths[:30], np.array(sizes[:30], dtype=np.int64))
+            assert [f"{k:016x}" for k in keys100] == want_ids[:30], mode
+            if mode == "1":  # the new pool's threads hold no copy of the caller's pipe
+                assert tasks_without(r) > before
+            os.close(w)
+            w = -1
+            ready, _, _ = select.select([r], [], [], 10.0)
+            assert ready and os.read(r, 1) == b"", mode  # EOF: no thread holds the write end
+            del e
+        finally:
+            os.close(r)
+            if w >= 0:
+                os.close(w)
+
+
 def test_synth_matches_oracle_generator(eng, oracle):
     n, seed = 64, 12345
     content = torch.empty((n, SAMPLED_CONTENT_LEN), dtype=torch.uint8, device="cuda")

@@ -41,7 +41,7 @@ cd $R
 for step in "$@"; do
   case $step in
     valtests)
-      timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "checksum or from_paths" > $OUT/pytest_validator.log 2>&1 || { echo VALTESTS_FAIL; tail -30 $OUT/pytest_validator.log; exit 1; }
+      timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "checksum or from_paths or host_pool" > $OUT/pytest_validator.log 2>&1 || { echo VALTESTS_FAIL; tail -30 $OUT/pytest_validator.log; exit 1; }
       tail -1 $OUT/pytest_validator.log ;;
     valab)
       for k in 1 2; do
@@ -67,6 +67,19 @@ for step in "$@"; do
         timeout -k 10 300 tools/probe_pread 15 $R/spacedrive_amd/libsd_hip_cas.so > $OUT/probe_pread_$k.log 2>&1 || { echo PROBE_FAIL; tail -20 $OUT/probe_pread_$k.log; exit 1; }
       done
       cat $OUT/probe_pread_*.log ;;
+    fdsab)
+      # the pool's private descriptor tables (SD_CAS_POOL_PRIVATE_FDS=1, the default) vs the
+      # shared table: config 1 (the drop-in gather), the 2,000-file validator set, 20,000 small
+      # files, interleaved
+      for k in 1 2; do
+        for m in 1 0; do
+          SD_CAS_POOL_PRIVATE_FDS=$m SD_CONFIG1_PASSES=7 timeout -k 10 300 python3 -u tools/bench_configs.py --config 1 > $OUT/config1fds${m}_$k.log 2>&1 || { echo FDSAB_FAIL; tail -20 $OUT/config1fds${m}_$k.log; exit 1; }
+          SD_CAS_POOL_PRIVATE_FDS=$m timeout -k 10 300 python3 -u tools/prof_checksums.py --no-device --paths 2000 --path-runs 6 > $OUT/valfds${m}_$k.log 2>&1 || { echo FDSAB_FAIL; tail -20 $OUT/valfds${m}_$k.log; exit 1; }
+          SD_CAS_POOL_PRIVATE_FDS=$m timeout -k 10 300 python3 -u tools/prof_checksums.py --no-device --paths 20000 --path-kib 16 256 --path-runs 4 > $OUT/smallfds${m}_$k.log 2>&1 || { echo FDSAB_FAIL; tail -20 $OUT/smallfds${m}_$k.log; exit 1; }
+        done
+      done
+      grep -h '"gpu_dropin_files_per_s"' $OUT/config1fds*.log | python3 -c "import sys,json; [print(json.loads(l).get('gpu_dropin_passes_files_per_s'), json.loads(l)['job_step_100_ms_median']) for l in sys.stdin]"
+      grep -h '"files"' $OUT/valfds*.log $OUT/smallfds*.log | cut -c1-220 ;;
     numa)
       for k in 1 2 3; do
         for m in 1 0; do
