@@ -55,8 +55,9 @@ class HostPool {
   // the first run (threads start lazily); SD_CAS_POOL_PRIVATE_FDS=0 keeps the shared table.
   // The copy would also keep every other descriptor of the process alive in this thread (a
   // pipe's write end: its reader never sees EOF; a socket the application closed: its peer
-  // never sees the close), so the thread then closes all of its copies except 0-2, the HIP
-  // runtime's device nodes (/dev/kfd, /dev/dri/*) and anonymous-inode descriptors.
+  // never sees the close; a dmabuf: its memory), so the thread then closes all of its copies
+  // except 0-2 and what the HIP runtime holds — /dev/kfd, /dev/dri/renderD*, one eventfd
+  // (tools/fd_list.py on the box: nothing else after HIP init, a context and a gather).
   void set_private_fds(bool on) { private_fds_ = on; }
   int private_threads() const { return nprivate_.load(); }
   ~HostPool() {
@@ -105,7 +106,7 @@ class HostPool {
       const ssize_t n = readlink(path, link, sizeof link - 1);
       if (n < 0) continue;
       link[n] = 0;
-      if (!strcmp(link, "/dev/kfd") || !strncmp(link, "/dev/dri/", 9) || !strncmp(link, "anon_inode:", 11))
+      if (!strcmp(link, "/dev/kfd") || !strncmp(link, "/dev/dri/", 9) || !strcmp(link, "anon_inode:[eventfd]"))
         continue;
       drop.push_back(fd);
     }
