@@ -291,24 +291,38 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
   // (mod.rs:34), up to SMALL_BATCH_FILES files and SMALL_BATCH_BYTES staged — is one window:
   // cutting its ~4 MB in two added a second H2D/hash/D2H chain and its serial tail
   // (0.36-0.41 -> 0.48-0.52 ms per step).
+  // Round 6: the last windows TAPER — a window's target is at most half of what remains — so
+  // the call's un-overlapped tail (the last full window's H2D + hash after the gather ends;
+  // gather and H2D run at about the same rate) shrinks to about two small windows' copies
+  // (SD_PATHS_TAPER 0: equal windows, round 5)
+#ifndef SD_PATHS_TAPER
+#define SD_PATHS_TAPER 1
+#endif
   constexpr size_t GATHER_WINDOW = 2048;
   constexpr size_t SMALL_BATCH_FILES = 2048;
   constexpr uint64_t SMALL_BATCH_BYTES = 16ull << 20;
+  constexpr uint64_t MIN_WINDOW_BYTES = 2ull << 20;
   std::vector<size_t> wstart{0};
   {
     uint64_t total = 0;
     for (size_t i = 0; i < n; i++) total += up128(lens[i]);
     const bool one_window = n <= SMALL_BATCH_FILES && total <= SMALL_BATCH_BYTES;
     const uint64_t target = one_window ? SMALL_BATCH_BYTES
-                                       : std::min<uint64_t>(64ull << 20, std::max<uint64_t>(2ull << 20, total / 12));
-    uint64_t bytes = 0;
+                                       : std::min<uint64_t>(64ull << 20, std::max<uint64_t>(MIN_WINDOW_BYTES, total / 12));
+    auto window_target = [&](uint64_t remaining) {
+      return one_window || !SD_PATHS_TAPER ? target
+                                           : std::min(target, std::max(MIN_WINDOW_BYTES, remaining / 2));
+    };
+    uint64_t bytes = 0, left = total, want = window_target(left);
     for (size_t i = 0; i < n; i++) {
       const size_t files = i - wstart.back();
-      if (files && (files == GATHER_WINDOW || bytes + up128(lens[i]) > target)) {
+      if (files && (files == GATHER_WINDOW || bytes + up128(lens[i]) > want)) {
         wstart.push_back(i);
         bytes = 0;
+        want = window_target(left);
       }
       bytes += up128(lens[i]);
+      left -= up128(lens[i]);
     }
     wstart.push_back(n);
   }
