@@ -114,7 +114,9 @@ class HostPool {
     for (int fd : drop) close(fd);
   }
   void loop() {
-    if (private_fds_ && unshare(CLONE_FILES) == 0) {
+    // private only where the copy can be swept (/proc mounted); closing a copy never releases
+    // the application's POSIX locks (their owner is the table they were taken through)
+    if (private_fds_ && access("/proc/thread-self/fd", R_OK) == 0 && unshare(CLONE_FILES) == 0) {
       keep_only_device_fds();
       nprivate_.fetch_add(1);
     }

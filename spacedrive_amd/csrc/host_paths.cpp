@@ -611,6 +611,8 @@ static int cas_ids_from_paths(sd_cas_ctx* c, const char* const* paths, const uin
   }
   for (size_t w = nw >= 2 ? nw - 2 : 0; w < nw && rc == 0; w++) rc = finish(w);
   tr.mark("wait");
+  tr.note("windows", (double)nw);
+  tr.note("private_threads", (double)c->pool.private_threads());
   if (rc) {
     // a failed call leaves nothing in flight: its pulls (copy streams) and an early
     // whole-file hash (copy2) would otherwise still read the staging, or write keys into it,
