@@ -12,7 +12,9 @@
 //             hipMemcpyAsync on one of 2 streams before the thread reuses it (event-gated)
 //   unshared  the window form, each reader first calling unshare(CLONE_FILES): a private
 //             descriptor table, so open/close stop sharing the process's table lock
-// argv: T files [sweep] — with "sweep", the window and unshared forms at T = 1, 2, 4, 8, 16.
+//   openat    the unshared form, each reader opening the files by name relative to its own
+//             descriptor of their directory (openat): no absolute-path walk from "/"
+// argv: T files [sweep] — with "sweep", the window, unshared and openat forms at T = 1..16.
 // Build: hipcc --offload-arch=gfx950 -O2 -o tools/probe_gather tools/probe_gather.cpp -lpthread
 #include <hip/hip_runtime.h>
 #include <fcntl.h>
@@ -38,8 +40,10 @@ static std::vector<uint64_t> sizes;
 static constexpr uint64_t MIN_FILE = 100 * 1024, CONTENT = 57344, RING = 2u << 20, QUARTER = RING / 4;
 
 // one file's cas.rs reads into dst; returns bytes written
-static uint64_t read_item(size_t i, char* dst) {
-  const int fd = open(paths[i].c_str(), O_RDONLY | O_CLOEXEC);
+static std::vector<std::string> names;  // the files' names in their directory
+static uint64_t read_item(size_t i, char* dst, int dirfd = -1) {
+  const int fd = dirfd >= 0 ? openat(dirfd, names[i].c_str(), O_RDONLY | O_CLOEXEC)
+                            : open(paths[i].c_str(), O_RDONLY | O_CLOEXEC);
   if (fd < 0) return 0;
   struct stat st;
   uint64_t offs[5], lns[5];
@@ -76,21 +80,23 @@ struct Shared {
   char* dev;       // T rings on the device
   hipStream_t st[2];
   std::mutex mu;
+  const char* dir;
 };
 struct Arg { Shared* s; int t; };
 
 static void* worker(void* p) {
   Arg* a = (Arg*)p;
   Shared* s = a->s;
-  if (s->mode == 4 && unshare(CLONE_FILES) != 0) perror("unshare");
+  if ((s->mode == 4 || s->mode == 5) && unshare(CLONE_FILES) != 0) perror("unshare");
+  const int dirfd = s->mode == 5 ? open(s->dir, O_RDONLY | O_DIRECTORY | O_CLOEXEC) : -1;
   char* ring = s->rings ? s->rings + (size_t)a->t * RING : nullptr;
   hipEvent_t ev[4] = {};
   if (s->mode == 3)
     for (auto& e : ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   uint64_t pos = 0;  // ring fill position (bytes since start)
   for (size_t i; (i = s->next.fetch_add(1)) < s->i1;) {
-    if (s->mode <= 1 || s->mode == 4) {
-      read_item(i, s->win + (*s->offs)[i - s->i0]);
+    if (s->mode <= 1 || s->mode >= 4) {
+      read_item(i, s->win + (*s->offs)[i - s->i0], dirfd);
       continue;
     }
     // ring: the file's content at the fill position (wrapping to the ring start when the
@@ -119,6 +125,7 @@ static void* worker(void* p) {
   }
   if (s->mode == 3)
     for (auto& e : ev) { (void)hipEventSynchronize(e); (void)hipEventDestroy(e); }
+  if (dirfd >= 0) close(dirfd);
   return nullptr;
 }
 
@@ -166,6 +173,7 @@ int main(int argc, char** argv) {
     if (!f || fwrite(buf.data(), 1, n, f) != n) return 1;
     fclose(f);
     paths.push_back(p);
+    names.push_back("f" + std::to_string(i));
     sizes.push_back(n);
     staged += n <= MIN_FILE ? n : CONTENT;
   }
@@ -173,6 +181,7 @@ int main(int argc, char** argv) {
   char* pwin = nullptr;
   Shared s;
   s.T = T;
+  s.dir = root;
   if (hipHostMalloc((void**)&pwin, 40u << 20, hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void**)&s.rings, (size_t)T * RING, hipHostMallocDefault) != hipSuccess ||
       hipMalloc((void**)&s.dev, (size_t)T * RING) != hipSuccess ||
@@ -182,16 +191,16 @@ int main(int argc, char** argv) {
   std::fill(mwin, mwin + (40u << 20), 0);
   std::fill(pwin, pwin + (40u << 20), 0);
   std::fill(s.rings, s.rings + (size_t)T * RING, 0);
-  const char* names[] = {"window", "malloc", "ring", "ring+h2d", "unshared"};
-  char* wins[] = {pwin, mwin, nullptr, nullptr, pwin};
+  const char* forms[] = {"window", "malloc", "ring", "ring+h2d", "unshared", "openat"};
+  char* wins[] = {pwin, mwin, nullptr, nullptr, pwin, pwin};
   const bool sweep = argc > 3 && std::string(argv[3]) == "sweep";
   std::vector<std::pair<int, int>> plan;  // (threads, mode)
   for (int round = 0; round < 2; round++)
     if (sweep)
       for (int t : {1, 2, 4, 8, 16})
-        for (int m : {0, 4}) plan.push_back({t, m});
+        for (int m : {0, 4, 5}) plan.push_back({t, m});
     else
-      for (int m = 0; m < 5; m++) plan.push_back({T, m});
+      for (int m = 0; m < 6; m++) plan.push_back({T, m});
   for (size_t pi = 0; pi < plan.size(); pi++) {
       const int m = plan[pi].second, round = (int)(pi * 2 / plan.size());
       s.T = plan[pi].first;
@@ -201,7 +210,7 @@ int main(int argc, char** argv) {
       std::sort(ts.begin(), ts.end());
       printf("{\"form\": \"%s\", \"round\": %d, \"threads\": %d, \"files\": %d, \"staged_mb\": %.1f, "
              "\"median_s\": %.5f, \"files_per_s\": %.0f, \"gb_per_s\": %.2f}\n",
-             names[m], round, s.T, N, staged / 1e6, ts[2], N / ts[2], staged / ts[2] / 1e9);
+             forms[m], round, s.T, N, staged / 1e6, ts[2], N / ts[2], staged / ts[2] / 1e9);
       fflush(stdout);
     }
   for (auto& p : paths) unlink(p.c_str());
