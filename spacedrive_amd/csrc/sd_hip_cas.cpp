@@ -179,14 +179,13 @@ int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
               c->test_table_fill, c->test_table_fill);
   }
   bind_pool_to_gpu_node(c);
-  {  // the pool's readers on private descriptor tables (HostPool::set_private_fds)
-    const char* e = getenv("SD_CAS_POOL_PRIVATE_FDS");
-    c->pool.set_private_fds(!(e && e[0] == '0'));
-  }
+  // the pool's readers on private descriptor tables (HostPool::set_private_fds)
+  const char* pf = getenv("SD_CAS_POOL_PRIVATE_FDS");
+  const bool private_fds = !(pf && pf[0] == '0');
+  c->pool.set_private_fds(private_fds);
   if (c->trace)
     fprintf(stderr, "sd_cas_trace ctx device=%d numa_node=%d pool_cpus=%d private_fds=%d\n", device,
-            c->numa_node, c->pool.bound_cpus(), !(getenv("SD_CAS_POOL_PRIVATE_FDS") &&
-                                                  getenv("SD_CAS_POOL_PRIVATE_FDS")[0] == '0'));
+            c->numa_node, c->pool.bound_cpus(), (int)private_fds);
   sd_cas_set_latency_threshold(c, SD_CAS_THRESHOLD_DEFAULT, SD_CAS_THRESHOLD_DEFAULT);
   sd_cas_set_chunkpar_split(c, SD_CAS_THRESHOLD_DEFAULT, SD_CAS_THRESHOLD_DEFAULT);
   *out = c;
