@@ -2246,6 +2246,14 @@ def test_sampled_host_pipeline(eng, oracle):
         for batch in [0, 1, 999, 1024, 5000]:
             got = eng.hash_sampled_host(pinned, sizes, batch_files=batch)
             assert (got == want).all(), batch
+        # the ring form (bench e2e, config 3): 5,000 files cycling through the first 777 rows;
+        # each batch's two halves cross on the two copy streams and wrap the ring mid-half
+        ring = 777
+        want_ring = want[:ring][np.arange(n) % ring]
+        sizes_ring = sizes[:ring][np.arange(n) % ring]
+        for batch in [1, 333, 1000, 4999]:
+            got = eng.hash_sampled_host_ring(pinned.ctypes.data, ring, sizes_ring, batch_files=batch)
+            assert (got == want_ring).all(), batch
     finally:
         eng.free_pinned(pinned)
     # pageable memory works too (synchronous copies)

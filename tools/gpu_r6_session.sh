@@ -80,6 +80,19 @@ for step in "$@"; do
       done
       grep -h '"gpu_dropin_files_per_s"' $OUT/config1fds*.log | python3 -c "import sys,json; [print(json.loads(l).get('gpu_dropin_passes_files_per_s'), json.loads(l)['job_step_100_ms_median']) for l in sys.stdin]"
       grep -h '"files"' $OUT/valfds*.log $OUT/smallfds*.log | cut -c1-220 ;;
+    hostab)
+      # config 3 as worded (pinned host memory -> HBM -> K1): session 23's build split each
+      # batch's copy in two halves over the two copy streams; hcs1 = one stream (the kept
+      # form: no difference, the split is in git history), interleaved
+      timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread -k "sampled_host" > $OUT/pytest_host.log 2>&1 || { echo HOSTAB_FAIL; tail -30 $OUT/pytest_host.log; exit 1; }
+      tail -1 $OUT/pytest_host.log
+      for k in 1 2 3; do
+        for v in intree hcs1; do
+          lib=""; [ $v != intree ] && lib=$R/tools/ablib/$v.so
+          SD_HIP_CAS_LIB=$lib timeout -k 10 300 python3 -u tools/bench_configs.py --config 3e > $OUT/c3e_${v}_$k.log 2>&1 || { echo HOSTAB_FAIL; tail -20 $OUT/c3e_${v}_$k.log; exit 1; }
+        done
+      done
+      grep -h '"3-e2e"' $OUT/c3e_*.log | cut -c1-200 ;;
     numa)
       for k in 1 2 3; do
         for m in 1 0; do
