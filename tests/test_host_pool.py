@@ -1,7 +1,8 @@
 """The host gather pool (spacedrive_amd/csrc/ctx_internal.h HostPool: the persistent workers
 behind every path gather) exercised on the CPU: 4,000 calls with random worker counts, back to
 back and across pauses that park the workers; every item processed exactly once, the caller's
-share run once, no deadlock (the run is under a time limit)."""
+share run once, no deadlock (the run is under a time limit); the threads' private descriptor
+tables (round 6): no copy of the caller's pipe, own files readable, the pipe's EOF intact."""
 import os
 import subprocess
 
